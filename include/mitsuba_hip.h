@@ -1,0 +1,282 @@
+/*
+ * mitsuba_hip.h — C-ABI of the MI355X-native (gfx950) wavefront backend for the
+ * `path` / `volpath` / `prb` integrator loop of ksalesin/mitsuba3-nasa.
+ *
+ * This is the drop-in boundary.  Plain C types only: no HIP,
+ * no torch, no C++ in the signatures.  Every entry point returns an `int`
+ * status (MH_OK == 0); on failure `mh_last_error()` returns a thread-local,
+ * human-readable message whose text mirrors the reference's `Throw(...)`
+ * messages where one exists.  No C++ exception ever crosses this boundary.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference checkout):
+ *
+ *   mh_scene_create / mh_scene_destroy
+ *       Scene::Scene + accel_init_gpu (OptiX GAS/IAS build)
+ *       src/render/scene.cpp:22-96, src/render/scene_optix.inl:304-547
+ *   mh_scene_update_texture / mh_scene_update_rgb
+ *       SceneParameters.update -> Scene::parameters_changed
+ *       src/python/python/util.py:292-350, src/render/scene.cpp:481-529
+ *   mh_render
+ *       SamplingIntegrator::render (JIT branch)        src/render/integrator.cpp:276-390
+ *       ADIntegrator.render (prb primal)               src/python/python/ad/integrators/common.py:47-111
+ *       (the film is left un-developed: RGBW, i.e. `develop=False` + Film storage)
+ *   mh_develop
+ *       HDRFilm::develop (JIT branch)                  src/films/hdrfilm.cpp:304-405
+ *   mh_render_backward
+ *       RBIntegrator.render_backward                   src/python/python/ad/integrators/common.py:828-983
+ *       (+ PRBIntegrator.sample adjoint mode           src/python/python/ad/integrators/prb.py:59-257)
+ *   mh_trace_closest / mh_trace_shadow
+ *       Scene::ray_intersect_preliminary_gpu / ray_test_gpu (the OptiX slot)
+ *       src/render/scene_optix.inl:592-721, include/mitsuba/render/optix/common.h:43-58
+ *
+ * Units / conventions: all matrices are row-major float[16] (4x4) or
+ * float[12] (3x4 affine, last row implicitly 0 0 0 1) and equal the
+ * reference's `Transform4f::matrix`.  Images are (height, width, channels),
+ * channel-fastest, float32.
+ */
+#ifndef MITSUBA_HIP_H
+#define MITSUBA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MH_ABI_VERSION 1u
+#define MH_INVALID 0xffffffffu
+
+/* ----------------------------------------------------------------------- */
+/* Status codes                                                             */
+/* ----------------------------------------------------------------------- */
+enum {
+    MH_OK = 0,
+    MH_ERR_INVALID_ARGUMENT = 1,
+    MH_ERR_HIP = 2,
+    MH_ERR_OUT_OF_MEMORY = 3,
+    MH_ERR_UNSUPPORTED = 4,
+    MH_ERR_NO_DEVICE = 5
+};
+
+/* ----------------------------------------------------------------------- */
+/* Plugin type tags (names follow the reference plugin names)               */
+/* ----------------------------------------------------------------------- */
+enum { MH_SHAPE_RECTANGLE = 0, MH_SHAPE_MESH = 1 };           /* rectangle.cpp, mesh.cpp (cube.cpp) */
+enum { MH_BSDF_DIFFUSE = 0, MH_BSDF_NULL = 1 };               /* diffuse.cpp, null.cpp */
+enum { MH_TEX_RGB = 0, MH_TEX_BITMAP = 1 };                   /* srgb.cpp, bitmap.cpp */
+enum { MH_EMITTER_AREA = 0, MH_EMITTER_CONSTANT = 1, MH_EMITTER_DIRECTIONAL = 2 };
+enum { MH_RFILTER_BOX = 0, MH_RFILTER_GAUSSIAN = 1 };         /* box.cpp, gaussian.cpp */
+enum { MH_MEDIUM_HETEROGENEOUS = 0, MH_MEDIUM_HOMOGENEOUS = 1 };
+enum { MH_PHASE_ISOTROPIC = 0, MH_PHASE_HG = 1 };
+enum { MH_INTEGRATOR_PATH = 0, MH_INTEGRATOR_VOLPATH = 1, MH_INTEGRATOR_PRB = 2 };
+
+/* Flags for mh_render / mh_render_backward / mh_trace_*                   */
+enum {
+    MH_FLAG_DEVICE_POINTERS = 1u << 0,  /* in/out buffers are device pointers on the scene's device */
+    MH_FLAG_ACCUMULATE      = 1u << 1,  /* mh_render: add into `film_rgbw` instead of overwriting */
+    MH_FLAG_NO_SYNC         = 1u << 2   /* do not synchronise the stream before returning */
+};
+
+/* ----------------------------------------------------------------------- */
+/* Flattened scene description (host memory; copied by mh_scene_create)     */
+/* ----------------------------------------------------------------------- */
+typedef struct mh_shape {
+    uint32_t type;              /* MH_SHAPE_* */
+    uint32_t bsdf;              /* index into bsdfs[] */
+    uint32_t emitter;           /* index into emitters[] or MH_INVALID */
+    uint32_t interior_medium;   /* index into media[] or MH_INVALID */
+    uint32_t exterior_medium;   /* index into media[] or MH_INVALID */
+    uint32_t face_offset;       /* meshes: first face in faces[] */
+    uint32_t face_count;        /* meshes: #triangles; rectangles: 1 */
+    uint32_t vertex_offset;     /* meshes: first vertex in positions[]/normals[]/texcoords[] */
+    uint32_t vertex_count;
+    uint32_t has_normals;       /* meshes: per-vertex normals present */
+    uint32_t has_texcoords;     /* meshes: per-vertex uvs present */
+    uint32_t pad0;
+    float to_world[12];         /* rectangles: Transform4f::matrix (3x4) */
+    float to_object[12];        /* rectangles: inverse of to_world (3x4) */
+    float frame_s[3];           /* rectangles: m_frame (rectangle.cpp:115-126) */
+    float frame_t[3];
+    float frame_n[3];
+    float inv_area;             /* rectangles: m_inv_surface_area */
+} mh_shape;
+
+typedef struct mh_texture {
+    uint32_t type;              /* MH_TEX_* */
+    uint32_t width, height;     /* bitmap resolution */
+    uint32_t channels;          /* bitmap: 1 or 3 */
+    uint64_t data_offset;       /* bitmap: first float in texels[] (row-major, channel fastest) */
+    uint32_t filter;            /* bitmap: 0 nearest, 1 bilinear */
+    uint32_t wrap;              /* bitmap: 0 repeat, 1 mirror, 2 clamp */
+    float value[3];             /* rgb: SRGBReflectanceSpectrum::m_value */
+    float to_uv[6];             /* bitmap: ScalarTransform3f (2x3 row-major) */
+    float pad1;
+} mh_texture;
+
+typedef struct mh_bsdf {
+    uint32_t type;              /* MH_BSDF_* */
+    uint32_t reflectance;       /* diffuse: index into textures[] */
+} mh_bsdf;
+
+typedef struct mh_emitter {
+    uint32_t type;              /* MH_EMITTER_* */
+    uint32_t shape;             /* area: index into shapes[] (rectangles only) */
+    uint32_t pad0, pad1;
+    float radiance[3];          /* area / constant: radiance; directional: irradiance */
+    float direction[3];         /* directional: world-space propagation direction (normalised) */
+    float scene_center[3];      /* constant / directional: bounding sphere of the scene */
+    float scene_radius;
+} mh_emitter;
+
+typedef struct mh_medium {
+    uint32_t type;              /* MH_MEDIUM_* */
+    uint32_t phase;             /* MH_PHASE_* */
+    float g;                    /* HG asymmetry */
+    float scale;                /* sigma_t scale */
+    float albedo[3];            /* constant single-scattering albedo */
+    float sigma_t_const;        /* homogeneous: sigma_t (before scale) */
+    uint32_t grid_res[3];       /* heterogeneous: sigma_t grid resolution (x, y, z) */
+    uint32_t pad0;
+    uint64_t grid_offset;       /* heterogeneous: first float in grid_data[] (z-major: x fastest) */
+    float grid_to_local[12];    /* world -> grid-local [0,1]^3 (3x4) */
+    float bbox_min[3];          /* world-space AABB of the grid */
+    float bbox_max[3];
+    float max_density;          /* max(grid) — the global majorant is scale * max_density */
+    float pad1;
+} mh_medium;
+
+typedef struct mh_sensor {
+    float to_world[16];         /* PerspectiveCamera m_to_world */
+    float sample_to_camera[16]; /* m_sample_to_camera (perspective.cpp:174-184) */
+    float near_clip, far_clip;
+    uint32_t width, height;     /* film size == crop size (crop_offset = 0) */
+    uint32_t rfilter;           /* MH_RFILTER_* */
+    float rfilter_radius;       /* gaussian: 4 * stddev */
+    float filter_coeff[10];     /* gaussian: scaled Remez coefficients (gaussian.cpp:57-89) */
+    uint32_t sample_count;      /* sampler.sample_count */
+    uint32_t sampler_seed;      /* sampler base seed ('seed' property, default 0) */
+    uint32_t medium;            /* camera medium index or MH_INVALID */
+    uint32_t pad0;
+} mh_sensor;
+
+typedef struct mh_scene_desc {
+    uint32_t abi_version;       /* must be MH_ABI_VERSION */
+    uint32_t pad0;
+    mh_sensor sensor;
+    uint32_t n_shapes, n_bsdfs, n_textures, n_emitters, n_media, n_vertices, n_faces, pad1;
+    const mh_shape   *shapes;
+    const mh_bsdf    *bsdfs;
+    const mh_texture *textures;
+    const mh_emitter *emitters;
+    const mh_medium  *media;
+    const float      *positions;   /* n_vertices * 3 (world space) */
+    const float      *normals;     /* n_vertices * 3 or NULL */
+    const float      *texcoords;   /* n_vertices * 2 or NULL */
+    const uint32_t   *faces;       /* n_faces * 3, shape-local vertex indices */
+    const float      *texels;      /* bitmap data */
+    uint64_t          n_texels;
+    const float      *grid_data;   /* volume grid data */
+    uint64_t          n_grid;
+    uint32_t          environment; /* index of the environment emitter (constant) or MH_INVALID */
+    uint32_t          pad2;
+} mh_scene_desc;
+
+typedef struct mh_integrator {
+    uint32_t type;              /* MH_INTEGRATOR_* */
+    uint32_t max_depth;         /* -1 (infinite) is passed as 0xffffffff */
+    uint32_t rr_depth;
+    uint32_t hide_emitters;
+} mh_integrator;
+
+/* Per-call render statistics (device counters; deterministic at fixed seed) */
+typedef struct mh_stats {
+    uint64_t samples;           /* W*H*spp processed */
+    uint64_t rays_closest;      /* closest-hit traversals */
+    uint64_t rays_shadow;       /* shadow (any-hit) traversals */
+    uint64_t bounces;           /* active lane-bounces */
+    double   ms_total;          /* wall time of the call (host clock, ms) */
+    double   ms_kernel;         /* device time of the dominant kernel (hipEvents, ms) */
+} mh_stats;
+
+typedef struct mh_scene mh_scene;   /* opaque; owns all device buffers */
+
+/* ----------------------------------------------------------------------- */
+/* Entry points                                                             */
+/* ----------------------------------------------------------------------- */
+const char *mh_last_error(void);
+uint32_t    mh_abi_version(void);
+int         mh_device_count(int *count);
+
+/* Scene lifetime. `device` is a HIP ordinal; `stream` a hipStream_t, or NULL
+   to let the scene create (and own) a non-blocking stream.  set_stream(NULL)
+   selects the device's default (null) stream. */
+int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scene **out);
+int mh_scene_destroy(mh_scene *scene);
+int mh_scene_set_stream(mh_scene *scene, void *stream);
+
+/* Parameter updates (traverse()/update() of 'x.reflectance.value' / '.data'). */
+int mh_scene_update_rgb(mh_scene *scene, uint32_t texture, const float value[3]);
+int mh_scene_update_texture(mh_scene *scene, uint32_t texture, const float *data, uint64_t n_floats);
+
+/*
+ * Forward render into an un-developed RGBW film (H*W*4 floats).
+ *   seed      : render seed (Integrator::render `seed`)
+ *   spp       : samples per pixel (0 = sensor sample_count)
+ *   spp_begin/spp_end : sample-slab [begin, end) of every pixel rendered by this call
+ *               (multi-GPU sample-slab sharding); pass 0, 0 for all.
+ *   film_rgbw : output (host or device pointer per flags)
+ */
+int mh_render(mh_scene *scene, const mh_integrator *integrator, uint32_t seed, uint32_t spp,
+              uint32_t spp_begin, uint32_t spp_end, float *film_rgbw, uint32_t flags,
+              mh_stats *stats);
+
+/*
+ * Per-sample outputs of the integrator (the value `sample()` returns per lane,
+ * path.cpp:283-286 / prb.py:253-257) and the splat position, for sample-level
+ * parity tests.  out = 5 SoA planes of n = W*H*(spp_end-spp_begin) floats:
+ * L.r, L.g, L.b, pos.x, pos.y, lane order idx = pixel * S + s.  Single pass only.
+ */
+int mh_render_samples(mh_scene *scene, const mh_integrator *integrator, uint32_t seed,
+                      uint32_t spp, uint32_t spp_begin, uint32_t spp_end, float *out,
+                      uint32_t flags);
+
+/* RGBW film -> RGB image (H*W*3): rgb / (w == 0 ? 1 : w). */
+int mh_develop(mh_scene *scene, const float *film_rgbw, float *image_rgb, uint32_t flags);
+
+/*
+ * Reverse-mode derivative of render(): accumulates d(loss)/d(param) for each
+ * listed texture parameter into grads[k] (3 floats for MH_TEX_RGB, W*H*C for
+ * MH_TEX_BITMAP).  `grad_in` is d(loss)/d(image), H*W*3.
+ *   weights_rgbw (optional, device flag applies): the per-pixel filter-weight
+ *   image W of the backward pass; pass NULL to compute it in-call.  Multi-GPU
+ *   callers compute the W image per slab with mh_prb_weights, all-reduce it
+ *   and pass it in.
+ */
+int mh_prb_weights(mh_scene *scene, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+                   uint32_t spp_end, float *weights, uint32_t flags);
+int mh_render_backward(mh_scene *scene, const mh_integrator *integrator, uint32_t seed,
+                       uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
+                       const float *grad_in, const float *weights, uint32_t n_params,
+                       const uint32_t *param_textures, float *const *grads, uint32_t flags,
+                       mh_stats *stats);
+
+/*
+ * Ray-query sub-boundary (the OptiX slot).  Rays are SoA: ray[0..6][n] =
+ * o.x o.y o.z d.x d.y d.z maxt (mint = 0).  Hits: t (+inf on miss), u, v
+ * (prim_uv), prim (prim_index; 0xffffffff for rectangles) and shape
+ * (shape index; 0xffffffff on miss) — the payload of scene_optix.inl:619-657.
+ */
+int mh_trace_closest(mh_scene *scene, uint64_t n, const float *rays, float *t, float *u,
+                     float *v, uint32_t *prim, uint32_t *shape, uint32_t flags, mh_stats *stats);
+int mh_trace_shadow(mh_scene *scene, uint64_t n, const float *rays, uint32_t *occluded,
+                    uint32_t flags, mh_stats *stats);
+
+/* BVH introspection (host): #nodes, #primitives, max depth. */
+int mh_scene_bvh_info(mh_scene *scene, uint32_t *n_nodes, uint32_t *n_prims, uint32_t *depth);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MITSUBA_HIP_H */

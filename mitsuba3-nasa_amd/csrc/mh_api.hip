@@ -1,0 +1,794 @@
+// mh_api.hip — C-ABI of the MI355X backend (include/mitsuba_hip.h).
+//
+// Host orchestration only: scene upload, BVH build, chunked launch of the
+// render / splat / develop / PRB kernels on the scene's HIP stream.  There is
+// no CPU fallback: every compute entry point requires a HIP device and fails
+// with MH_ERR_NO_DEVICE otherwise.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mh_device.hpp"
+#include "mh_internal.hpp"
+
+using namespace mh;
+
+namespace {
+
+thread_local std::string g_error;
+
+int set_error(int code, const std::string &msg) {
+    g_error = msg;
+    return code;
+}
+
+#define MH_HIP(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return set_error(MH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t alloc(size_t n) {
+        if (n <= bytes && ptr) return hipSuccess;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        if (n == 0) return hipSuccess;
+        hipError_t e = hipMalloc(&ptr, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }
+};
+
+uint32_t log2_exact(uint32_t v) {
+    for (uint32_t k = 0; k < 32; ++k)
+        if ((1u << k) == v) return k;
+    return 32;
+}
+
+template <typename T>
+hipError_t upload(DevBuf &b, const T *src, size_t count, hipStream_t st) {
+    size_t bytes = sizeof(T) * count;
+    if (bytes == 0) bytes = 16;  // keep a valid pointer
+    hipError_t e = b.alloc(bytes);
+    if (e != hipSuccess) return e;
+    if (src && count) return hipMemcpyAsync(b.ptr, src, sizeof(T) * count, hipMemcpyHostToDevice, st);
+    return hipMemsetAsync(b.ptr, 0, bytes, st);
+}
+
+}  // namespace
+
+struct mh_scene {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    DScene S{};
+    // device buffers
+    DevBuf nodes, prims, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
+        texcoords, faces, texels;
+    DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
+    // host mirrors (parameter updates)
+    std::vector<DTexture> h_textures;
+    uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0;
+    uint64_t n_texels = 0;
+    uint32_t bvh_nodes = 0, bvh_prims = 0, bvh_depth = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::vector<hipEvent_t> evpool;  // per-chunk timing events of mh_render
+};
+
+extern "C" {
+
+const char *mh_last_error(void) { return g_error.c_str(); }
+uint32_t mh_abi_version(void) { return MH_ABI_VERSION; }
+
+int mh_device_count(int *count) {
+    if (!count) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_device_count: count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return MH_OK;
+}
+
+static int require_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return set_error(MH_ERR_NO_DEVICE,
+                         "mitsuba_hip: no HIP device available (hip_ad_rgb requires an MI355X; "
+                         "there is no CPU fallback)");
+    if (device < 0 || device >= n)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: device index out of bounds");
+    return MH_OK;
+}
+
+
+int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scene **out) {
+    if (!desc || !out) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: NULL argument");
+    if (desc->abi_version != MH_ABI_VERSION)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: ABI version mismatch");
+    int rc = require_device(device);
+    if (rc) return rc;
+    const mh_sensor &sn = desc->sensor;
+    if (sn.width == 0 || sn.height == 0)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: film size must be positive");
+    for (uint32_t i = 0; i < desc->n_emitters; ++i) {
+        const mh_emitter &e = desc->emitters[i];
+        if (e.type == MH_EMITTER_AREA &&
+            (e.shape >= desc->n_shapes || desc->shapes[e.shape].type != MH_SHAPE_RECTANGLE))
+            return set_error(MH_ERR_UNSUPPORTED,
+                             "mh_scene_create: area emitters are supported on rectangles only");
+    }
+    MH_HIP(hipSetDevice(device));
+    mh_scene *s = new (std::nothrow) mh_scene();
+    if (!s) return set_error(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: out of host memory");
+    s->device = device;
+    if (stream) {
+        s->stream = (hipStream_t)stream;
+    } else {
+        if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete s;
+            return set_error(MH_ERR_HIP, "mh_scene_create: hipStreamCreate failed");
+        }
+        s->own_stream = true;
+    }
+    hipStream_t st = s->stream;
+    auto fail = [&](int code, const std::string &m) {
+        mh_scene_destroy(s);
+        return set_error(code, m);
+    };
+
+    // ---- primitives for the BVH (rectangles + mesh triangles) ----
+    std::vector<BuildPrim> bp;
+    for (uint32_t si = 0; si < desc->n_shapes; ++si) {
+        const mh_shape &sh = desc->shapes[si];
+        if (sh.type == MH_SHAPE_RECTANGLE) {
+            BuildPrim p{};
+            const float *m = sh.to_world;
+            for (int a = 0; a < 3; ++a) { p.lo[a] = INFINITY; p.hi[a] = -INFINITY; }
+            const float cs[4][2] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}};
+            for (auto &c : cs) {
+                for (int a = 0; a < 3; ++a) {
+                    float q = m[4 * a + 0] * c[0] + m[4 * a + 1] * c[1] + m[4 * a + 3];
+                    p.lo[a] = std::min(p.lo[a], q);
+                    p.hi[a] = std::max(p.hi[a], q);
+                }
+            }
+            memcpy(p.rec, sh.to_object, sizeof(float) * 12);
+            p.shape = si;
+            p.prim = MH_INVALID;
+            p.type = MH_SHAPE_RECTANGLE;
+            bp.push_back(p);
+        } else if (sh.type == MH_SHAPE_MESH) {
+            if ((uint64_t)sh.face_offset + sh.face_count > desc->n_faces ||
+                (uint64_t)sh.vertex_offset + sh.vertex_count > desc->n_vertices)
+                return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: mesh range out of bounds");
+            for (uint32_t f = 0; f < sh.face_count; ++f) {
+                const uint32_t *fi = desc->faces + 3ull * (sh.face_offset + f);
+                const float *v[3];
+                for (int k = 0; k < 3; ++k) {
+                    if (fi[k] >= sh.vertex_count)
+                        return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: face index out of bounds");
+                    v[k] = desc->positions + 3ull * (sh.vertex_offset + fi[k]);
+                }
+                BuildPrim p{};
+                for (int a = 0; a < 3; ++a) {
+                    p.lo[a] = std::min(v[0][a], std::min(v[1][a], v[2][a]));
+                    p.hi[a] = std::max(v[0][a], std::max(v[1][a], v[2][a]));
+                    p.rec[a] = v[0][a];
+                    p.rec[4 + a] = v[1][a] - v[0][a];  // e1 (mesh.h:437)
+                    p.rec[8 + a] = v[2][a] - v[0][a];  // e2
+                }
+                p.shape = si;
+                p.prim = f;
+                p.type = MH_SHAPE_MESH;
+                bp.push_back(p);
+            }
+        } else {
+            return fail(MH_ERR_UNSUPPORTED, "mh_scene_create: unknown shape type");
+        }
+    }
+    BvhOut bvh;
+    build_bvh(bp, bvh);
+    s->bvh_nodes = bvh.n_nodes;
+    s->bvh_prims = bvh.n_prims;
+    s->bvh_depth = bvh.depth;
+    if (upload(s->nodes, bvh.nodes.data(), bvh.nodes.size(), st) != hipSuccess ||
+        upload(s->prims, bvh.prims.data(), bvh.prims.size(), st) != hipSuccess)
+        return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: BVH upload failed");
+
+    // ---- shading-time records ----
+    std::vector<DShape> shapes(desc->n_shapes);
+    for (uint32_t i = 0; i < desc->n_shapes; ++i) {
+        const mh_shape &a = desc->shapes[i];
+        DShape &b = shapes[i];
+        memset(&b, 0, sizeof(b));
+        b.type = a.type; b.bsdf = a.bsdf; b.emitter = a.emitter; b.face_offset = a.face_offset;
+        b.vertex_offset = a.vertex_offset; b.has_normals = a.has_normals; b.has_texcoords = a.has_texcoords;
+        if (a.bsdf >= desc->n_bsdfs) return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: bsdf index out of bounds");
+        memcpy(b.to_world, a.to_world, sizeof(b.to_world));
+        memcpy(b.frame_s, a.frame_s, 12);
+        memcpy(b.frame_t, a.frame_t, 12);
+        memcpy(b.frame_n, a.frame_n, 12);
+        b.inv_area = a.inv_area;
+    }
+    std::vector<uint32_t> btype(desc->n_bsdfs), btex(desc->n_bsdfs);
+    for (uint32_t i = 0; i < desc->n_bsdfs; ++i) {
+        btype[i] = desc->bsdfs[i].type;
+        btex[i] = desc->bsdfs[i].reflectance;
+        if (btype[i] == MH_BSDF_DIFFUSE && btex[i] >= desc->n_textures)
+            return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: texture index out of bounds");
+    }
+    s->h_textures.resize(desc->n_textures);
+    for (uint32_t i = 0; i < desc->n_textures; ++i) {
+        const mh_texture &a = desc->textures[i];
+        DTexture &b = s->h_textures[i];
+        memset(&b, 0, sizeof(b));
+        b.type = a.type; b.width = a.width; b.height = a.height; b.channels = a.channels;
+        b.data_offset = a.data_offset; b.filter = a.filter; b.wrap = a.wrap;
+        memcpy(b.value, a.value, 12);
+        memcpy(b.to_uv, a.to_uv, 24);
+        if (a.type == MH_TEX_BITMAP &&
+            a.data_offset + (uint64_t)a.width * a.height * a.channels > desc->n_texels)
+            return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: bitmap data out of bounds");
+    }
+    std::vector<DEmitter> ems(desc->n_emitters);
+    for (uint32_t i = 0; i < desc->n_emitters; ++i) {
+        memset(&ems[i], 0, sizeof(DEmitter));
+        ems[i].type = desc->emitters[i].type;
+        ems[i].shape = desc->emitters[i].shape;
+        memcpy(ems[i].radiance, desc->emitters[i].radiance, 12);
+        memcpy(ems[i].direction, desc->emitters[i].direction, 12);
+    }
+    s->n_textures = desc->n_textures;
+    s->n_bsdfs = desc->n_bsdfs;
+    s->n_shapes = desc->n_shapes;
+    s->n_texels = desc->n_texels;
+    bool ok = upload(s->shapes, shapes.data(), shapes.size(), st) == hipSuccess &&
+              upload(s->bsdf_type, btype.data(), btype.size(), st) == hipSuccess &&
+              upload(s->bsdf_tex, btex.data(), btex.size(), st) == hipSuccess &&
+              upload(s->textures, s->h_textures.data(), s->h_textures.size(), st) == hipSuccess &&
+              upload(s->emitters, ems.data(), ems.size(), st) == hipSuccess &&
+              upload(s->positions, desc->positions, 3ull * desc->n_vertices, st) == hipSuccess &&
+              upload(s->normals, desc->normals, desc->normals ? 3ull * desc->n_vertices : 0, st) == hipSuccess &&
+              upload(s->texcoords, desc->texcoords, desc->texcoords ? 2ull * desc->n_vertices : 0, st) == hipSuccess &&
+              upload(s->faces, desc->faces, 3ull * desc->n_faces, st) == hipSuccess &&
+              upload(s->texels, desc->texels, desc->n_texels, st) == hipSuccess &&
+              s->counters.alloc(64) == hipSuccess;
+    if (!ok) return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: device upload failed");
+
+    DScene &S = s->S;
+    S.nodes = s->nodes.as<Node>();
+    S.prims = s->prims.as<Prim>();
+    S.shapes = s->shapes.as<DShape>();
+    S.bsdf_type = s->bsdf_type.as<uint32_t>();
+    S.bsdf_tex = s->bsdf_tex.as<uint32_t>();
+    S.textures = s->textures.as<DTexture>();
+    S.emitters = s->emitters.as<DEmitter>();
+    S.positions = s->positions.as<float>();
+    S.normals = s->normals.as<float>();
+    S.texcoords = s->texcoords.as<float>();
+    S.faces = s->faces.as<uint32_t>();
+    S.texels = s->texels.as<float>();
+    S.n_nodes = bvh.n_nodes;
+    S.n_prims = bvh.n_prims;
+    S.n_emitters = desc->n_emitters;
+    S.environment = desc->environment;
+    S.stack_size = bvh.depth + 2;
+    const size_t bvh_bytes = bvh.nodes.size() + bvh.prims.size();
+    S.lds_bytes_bvh = bvh_bytes <= 32768 ? (uint32_t)bvh_bytes : 0u;  // stage into LDS when small
+    if ((size_t)S.stack_size * 256 * 4 + S.lds_bytes_bvh > 65536)
+        return fail(MH_ERR_UNSUPPORTED, "mh_scene_create: BVH too deep for the LDS traversal stack");
+    memcpy(S.cam_to_world, sn.to_world, sizeof(S.cam_to_world));
+    memcpy(S.sample_to_camera, sn.sample_to_camera, sizeof(S.sample_to_camera));
+    S.near_clip = sn.near_clip;
+    S.far_clip = sn.far_clip;
+    S.width = sn.width;
+    S.height = sn.height;
+    S.rfilter = sn.rfilter;
+    S.rfilter_radius = sn.rfilter_radius;
+    memcpy(S.filter_coeff, sn.filter_coeff, sizeof(S.filter_coeff));
+    S.sampler_seed = sn.sampler_seed;
+    if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess)
+        return fail(MH_ERR_HIP, "mh_scene_create: hipEventCreate failed");
+    if (hipStreamSynchronize(st) != hipSuccess) return fail(MH_ERR_HIP, "mh_scene_create: upload sync failed");
+    *out = s;
+    return MH_OK;
+}
+
+int mh_scene_destroy(mh_scene *s) {
+    if (!s) return MH_OK;
+    (void)hipSetDevice(s->device);
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (DevBuf *b : {&s->nodes, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
+                      &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
+                      &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp})
+        b->release();
+    for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+    return MH_OK;
+}
+
+int mh_scene_set_stream(mh_scene *s, void *stream) {
+    if (!s) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_set_stream: NULL scene");
+    if (s->own_stream && s->stream == (hipStream_t)stream) return MH_OK;
+    if (s->own_stream && s->stream) {
+        (void)hipStreamSynchronize(s->stream);
+        (void)hipStreamDestroy(s->stream);
+    }
+    s->own_stream = false;
+    s->stream = (hipStream_t)stream;
+    return MH_OK;
+}
+
+int mh_scene_bvh_info(mh_scene *s, uint32_t *n_nodes, uint32_t *n_prims, uint32_t *depth) {
+    if (!s) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_bvh_info: NULL scene");
+    if (n_nodes) *n_nodes = s->bvh_nodes;
+    if (n_prims) *n_prims = s->bvh_prims;
+    if (depth) *depth = s->bvh_depth;
+    return MH_OK;
+}
+
+int mh_scene_update_rgb(mh_scene *s, uint32_t tex, const float value[3]) {
+    if (!s || !value) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_rgb: NULL argument");
+    if (tex >= s->n_textures || s->h_textures[tex].type != MH_TEX_RGB)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_rgb: not an rgb texture");
+    MH_HIP(hipSetDevice(s->device));
+    memcpy(s->h_textures[tex].value, value, 12);
+    MH_HIP(hipMemcpyAsync(s->textures.as<DTexture>() + tex, &s->h_textures[tex], sizeof(DTexture),
+                          hipMemcpyHostToDevice, s->stream));
+    MH_HIP(hipStreamSynchronize(s->stream));
+    return MH_OK;
+}
+
+int mh_scene_update_texture(mh_scene *s, uint32_t tex, const float *data, uint64_t n) {
+    if (!s || !data) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_texture: NULL argument");
+    if (tex >= s->n_textures || s->h_textures[tex].type != MH_TEX_BITMAP)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_texture: not a bitmap texture");
+    const DTexture &t = s->h_textures[tex];
+    if (n != (uint64_t)t.width * t.height * t.channels)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_texture: size mismatch");
+    MH_HIP(hipSetDevice(s->device));
+    MH_HIP(hipMemcpyAsync(s->texels.as<float>() + t.data_offset, data, n * 4, hipMemcpyHostToDevice,
+                          s->stream));
+    MH_HIP(hipStreamSynchronize(s->stream));
+    return MH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Render
+// ---------------------------------------------------------------------------
+struct Layout {
+    uint32_t W, H, spp, spp_pp, n_passes, s_begin, s_end;
+};
+
+static int make_layout(const mh_scene *s, uint32_t spp, uint32_t b, uint32_t e, Layout &L) {
+    L.W = s->S.width;
+    L.H = s->S.height;
+    L.spp = spp;
+    uint64_t wf = (uint64_t)L.W * L.H * spp, lim = 0xffffffffull;
+    L.spp_pp = spp;
+    L.n_passes = 1;
+    if (wf > lim) {  // integrator.cpp:281-295
+        L.spp_pp = spp / (uint32_t)((wf + lim - 1) / lim);
+        L.n_passes = spp / L.spp_pp;
+        if (L.spp_pp * L.n_passes != spp)
+            return set_error(MH_ERR_INVALID_ARGUMENT,
+                             "render(): sample_count should be a multiple of samples_per_wavefront!");
+    }
+    if (b == 0 && e == 0) e = L.spp_pp;
+    if (e > L.spp_pp || b >= e)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "render(): invalid sample slab [spp_begin, spp_end)");
+    L.s_begin = b;
+    L.s_end = e;
+    return MH_OK;
+}
+
+static LaneMap lane_map(const Layout &L, uint32_t pixel_begin) {
+    LaneMap m;
+    m.W = L.W;
+    m.spp_pp = L.spp_pp;
+    m.log_spp = log2_exact(L.spp_pp);
+    m.pixel_begin = pixel_begin;
+    m.S = L.s_end - L.s_begin;
+    m.s_begin = L.s_begin;
+    m.log_S = log2_exact(m.S);
+    return m;
+}
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+              uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
+    if (!s || !in || !film_rgbw) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: NULL argument");
+    if (in->type == MH_INTEGRATOR_VOLPATH)
+        return set_error(MH_ERR_UNSUPPORTED, "mh_render: 'volpath' is not available in this build");
+    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: unknown integrator");
+    if (in->rr_depth == 0)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
+    if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: spp must be > 0");
+    double t_start = now_ms();
+    Layout L;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    if (rc) return rc;
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const uint64_t n_px = (uint64_t)L.W * L.H;
+    float *film = film_rgbw;
+    if (!(flags & MH_FLAG_DEVICE_POINTERS)) {
+        MH_HIP(s->film_tmp.alloc(n_px * 16));
+        film = s->film_tmp.as<float>();
+    }
+    if (!(flags & MH_FLAG_ACCUMULATE) || !(flags & MH_FLAG_DEVICE_POINTERS)) {
+        if (!(flags & MH_FLAG_ACCUMULATE)) MH_HIP(hipMemsetAsync(film, 0, n_px * 16, st));
+        else MH_HIP(hipMemcpyAsync(film, film_rgbw, n_px * 16, hipMemcpyHostToDevice, st));
+    }
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    const uint32_t S_ = L.s_end - L.s_begin;
+    const uint64_t per_pixel = (uint64_t)S_ * L.n_passes;
+    const uint64_t max_samples = 1ull << 25;
+    uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
+    const uint64_t plane = (uint64_t)chunk_px * per_pixel;
+    MH_HIP(s->work.alloc(plane * 5 * sizeof(float)));
+    const bool fast_splat = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN &&
+                            s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
+    const int coalesce = L.spp_pp >= 4;
+    const uint32_t seed_value = s->S.sampler_seed + seed;
+    float kernel_ms = 0.f;
+    const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
+    while (s->evpool.size() < 2 * n_chunks) {
+        hipEvent_t e;
+        MH_HIP(hipEventCreate(&e));
+        s->evpool.push_back(e);
+    }
+    size_t chunk = 0;
+    for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
+        uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
+        LaneMap lm = lane_map(L, (uint32_t)p0);
+        uint64_t n = (uint64_t)npx * S_;
+        MH_HIP(hipEventRecord(s->evpool[2 * chunk], st));
+        MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
+                             s->counters.as<unsigned long long>(), st));
+        MH_HIP(hipEventRecord(s->evpool[2 * chunk + 1], st));
+        MH_HIP(launch_splat(s->S, lm, false, fast_splat, npx, L.n_passes, n, plane,
+                            s->work.as<float>(), film, seed_value, coalesce, st));
+    }
+    if (!(flags & MH_FLAG_DEVICE_POINTERS))
+        MH_HIP(hipMemcpyAsync(film_rgbw, film, n_px * 16, hipMemcpyDeviceToHost, st));
+    unsigned long long ctr[2] = {0, 0};
+    MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));  // the stats counters are read back
+    for (size_t c = 0; c < n_chunks; ++c) {
+        float ms = 0.f;
+        MH_HIP(hipEventElapsedTime(&ms, s->evpool[2 * c], s->evpool[2 * c + 1]));
+        kernel_ms += ms;
+    }
+    if (stats) {
+        stats->samples = n_px * per_pixel;
+        stats->rays_closest = ctr[0];
+        stats->rays_shadow = ctr[1];
+        stats->bounces = ctr[0];
+        stats->ms_total = now_ms() - t_start;
+        stats->ms_kernel = kernel_ms;
+    }
+    return MH_OK;
+}
+
+int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
+                      uint32_t spp_begin, uint32_t spp_end, float *out, uint32_t flags) {
+    if (!s || !in || !out) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: NULL argument");
+    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB)
+        return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: unsupported integrator");
+    if (spp == 0 || in->rr_depth == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: bad arguments");
+    Layout L;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    if (rc) return rc;
+    if (L.n_passes != 1) return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: single pass only");
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const uint64_t n = (uint64_t)L.W * L.H * (L.s_end - L.s_begin);
+    float *dst = out;
+    if (!(flags & MH_FLAG_DEVICE_POINTERS)) {
+        MH_HIP(s->tmp_a.alloc(n * 20));
+        dst = s->tmp_a.as<float>();
+    }
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    LaneMap lm = lane_map(L, 0);
+    MH_HIP(launch_render(s->S, *in, lm, s->S.sampler_seed + seed, 1, n, n, dst,
+                         s->counters.as<unsigned long long>(), st));
+    if (!(flags & MH_FLAG_DEVICE_POINTERS))
+        MH_HIP(hipMemcpyAsync(out, dst, n * 20, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+int mh_develop(mh_scene *s, const float *film_rgbw, float *image_rgb, uint32_t flags) {
+    if (!s || !film_rgbw || !image_rgb) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_develop: NULL argument");
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const uint64_t n_px = (uint64_t)s->S.width * s->S.height;
+    if (flags & MH_FLAG_DEVICE_POINTERS) {
+        MH_HIP(launch_develop(n_px, film_rgbw, image_rgb, st));
+        if (!(flags & MH_FLAG_NO_SYNC)) MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    }
+    MH_HIP(s->tmp_a.alloc(n_px * 16));
+    MH_HIP(s->tmp_b.alloc(n_px * 12));
+    MH_HIP(hipMemcpyAsync(s->tmp_a.ptr, film_rgbw, n_px * 16, hipMemcpyHostToDevice, st));
+    MH_HIP(launch_develop(n_px, s->tmp_a.as<float>(), s->tmp_b.as<float>(), st));
+    MH_HIP(hipMemcpyAsync(image_rgb, s->tmp_b.ptr, n_px * 12, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// PRB backward
+// ---------------------------------------------------------------------------
+int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
+                   float *weights, uint32_t flags) {
+    if (!s || !weights) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: NULL argument");
+    if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: spp must be > 0");
+    Layout L;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    if (rc) return rc;
+    if (L.n_passes != 1)
+        return set_error(MH_ERR_INVALID_ARGUMENT,
+                         "The total number of Monte Carlo samples required by this rendering task "
+                         "exceeds 2^32 = 4294967296. Please use fewer samples per pixel or render "
+                         "using multiple passes.");
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const uint64_t n_px = (uint64_t)L.W * L.H;
+    float *w = weights;
+    if (!(flags & MH_FLAG_DEVICE_POINTERS)) {
+        MH_HIP(s->weights_tmp.alloc(n_px * 4));
+        w = s->weights_tmp.as<float>();
+    }
+    if (!(flags & MH_FLAG_ACCUMULATE)) MH_HIP(hipMemsetAsync(w, 0, n_px * 4, st));
+    const bool fast = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN &&
+                      s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
+    LaneMap lm = lane_map(L, 0);
+    const uint32_t S_ = L.s_end - L.s_begin;
+    MH_HIP(launch_splat(s->S, lm, true, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w,
+                        s->S.sampler_seed + seed, L.spp_pp >= 4, st));
+    if (!(flags & MH_FLAG_DEVICE_POINTERS))
+        MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    return MH_OK;
+}
+
+int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
+                       uint32_t spp_begin, uint32_t spp_end, const float *grad_in,
+                       const float *weights, uint32_t n_params, const uint32_t *param_tex,
+                       float *const *grads, uint32_t flags, mh_stats *stats) {
+    if (!s || !in || !grad_in || (n_params && (!param_tex || !grads)))
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: NULL argument");
+    if (in->type != MH_INTEGRATOR_PRB)
+        return set_error(MH_ERR_UNSUPPORTED, "render_backward(): requires the 'prb' integrator");
+    if (in->rr_depth == 0)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
+    if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: spp must be > 0");
+    double t_start = now_ms();
+    Layout L;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    if (rc) return rc;
+    if (L.n_passes != 1)
+        return set_error(MH_ERR_INVALID_ARGUMENT,
+                         "The total number of Monte Carlo samples required by this rendering task "
+                         "exceeds 2^32 = 4294967296. Please use fewer samples per pixel or render "
+                         "using multiple passes.");
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const uint64_t n_px = (uint64_t)L.W * L.H;
+    const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
+
+    // ---- parameter slots ----
+    std::vector<int32_t> slot_of_tex(std::max<uint32_t>(s->n_textures, 1), -1);
+    std::vector<uint32_t> is_rgb(kMaxParams, 0);
+    std::vector<float *> bufs(kMaxParams, nullptr);
+    std::vector<size_t> counts(kMaxParams, 0);
+    std::vector<uint32_t> slot_of_param(n_params);
+    uint32_t n_rgb = 0, n_bmp = 0;
+    for (uint32_t k = 0; k < n_params; ++k) {
+        uint32_t t = param_tex[k];
+        if (t >= s->n_textures) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: texture index out of bounds");
+        if (slot_of_tex[t] >= 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: duplicate parameter");
+        const DTexture &tx = s->h_textures[t];
+        int slot;
+        if (tx.type == MH_TEX_RGB) {
+            if (n_rgb >= (uint32_t)kMaxRgbParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many rgb parameters");
+            slot = (int)n_rgb++;
+            is_rgb[slot] = 1;
+            counts[slot] = 3;
+        } else {
+            if (n_bmp >= (uint32_t)kMaxBitmapParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many bitmap parameters");
+            slot = kMaxRgbParams + (int)n_bmp++;
+            counts[slot] = (size_t)tx.width * tx.height * tx.channels;
+        }
+        slot_of_tex[t] = slot;
+        slot_of_param[k] = (uint32_t)slot;
+    }
+    // gradient buffers: device scratch, zeroed, accumulated into the caller's
+    size_t total = 0;
+    std::vector<size_t> off(kMaxParams, 0);
+    for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += counts[k]; }
+    MH_HIP(s->tmp_c.alloc(std::max<size_t>(total, 1) * 4));
+    MH_HIP(hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st));
+    for (int k = 0; k < kMaxParams; ++k) bufs[k] = counts[k] ? s->tmp_c.as<float>() + off[k] : nullptr;
+    // meta block: slot_of_tex | is_rgb | bufs
+    size_t meta_bytes = slot_of_tex.size() * 4 + kMaxParams * 4 + kMaxParams * 8 + 64;
+    std::vector<uint8_t> meta(meta_bytes, 0);
+    size_t o_slot = 0, o_isrgb = (slot_of_tex.size() * 4 + 15) / 16 * 16,
+           o_bufs = (o_isrgb + kMaxParams * 4 + 15) / 16 * 16;
+    memcpy(meta.data() + o_slot, slot_of_tex.data(), slot_of_tex.size() * 4);
+    memcpy(meta.data() + o_isrgb, is_rgb.data(), kMaxParams * 4);
+    memcpy(meta.data() + o_bufs, bufs.data(), kMaxParams * 8);
+    MH_HIP(s->grad_meta.alloc(meta_bytes));
+    MH_HIP(hipMemcpyAsync(s->grad_meta.ptr, meta.data(), meta_bytes, hipMemcpyHostToDevice, st));
+    GradArgs ga;
+    ga.slot_of_tex = reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_slot);
+    ga.is_rgb = reinterpret_cast<const uint32_t *>(s->grad_meta.as<uint8_t>() + o_isrgb);
+    ga.bufs = reinterpret_cast<float *const *>(s->grad_meta.as<uint8_t>() + o_bufs);
+    ga.n_rgb = n_rgb;
+
+    // ---- grad_in / weights on the device ----
+    const float *g_in = grad_in;
+    if (!dev) {
+        MH_HIP(s->tmp_d.alloc(n_px * 12));
+        MH_HIP(hipMemcpyAsync(s->tmp_d.ptr, grad_in, n_px * 12, hipMemcpyHostToDevice, st));
+        g_in = s->tmp_d.as<float>();
+    }
+    const float *w = weights;
+    if (!weights) {
+        MH_HIP(s->weights_tmp.alloc(n_px * 4));
+        MH_HIP(hipMemsetAsync(s->weights_tmp.ptr, 0, n_px * 4, st));
+        const bool fast = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN &&
+                          s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
+        Layout Lall = L;
+        Lall.s_begin = 0;
+        Lall.s_end = L.spp_pp;
+        LaneMap lmw = lane_map(Lall, 0);
+        MH_HIP(launch_splat(s->S, lmw, true, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
+                            s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st));
+        w = s->weights_tmp.as<float>();
+    } else if (!dev) {
+        MH_HIP(s->tmp_e.alloc(n_px * 4));
+        MH_HIP(hipMemcpyAsync(s->tmp_e.ptr, weights, n_px * 4, hipMemcpyHostToDevice, st));
+        w = s->tmp_e.as<float>();
+    }
+
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    LaneMap lm = lane_map(L, 0);
+    const uint64_t n = n_px * (L.s_end - L.s_begin);
+    MH_HIP(hipEventRecord(s->ev0, st));
+    MH_HIP(launch_prb_backward(s->S, *in, lm, s->S.sampler_seed + seed, n, L.spp_pp >= 4, g_in, w, ga,
+                               s->counters.as<unsigned long long>(), st));
+    MH_HIP(hipEventRecord(s->ev1, st));
+    // accumulate into the caller's gradient buffers
+    std::vector<float> host_tmp;
+    for (uint32_t k = 0; k < n_params; ++k) {
+        uint32_t slot = slot_of_param[k];
+        size_t c = counts[slot];
+        if (dev) {
+            MH_HIP(hipMemcpyAsync(grads[k], bufs[slot], c * 4, hipMemcpyDeviceToDevice, st));
+        } else {
+            host_tmp.resize(c);
+            MH_HIP(hipMemcpyAsync(host_tmp.data(), bufs[slot], c * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipStreamSynchronize(st));
+            for (size_t i = 0; i < c; ++i) grads[k][i] += host_tmp[i];
+        }
+    }
+    unsigned long long ctr[2] = {0, 0};
+    MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    if (stats) {
+        float ms = 0.f;
+        MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->samples = n;
+        stats->rays_closest = ctr[0];
+        stats->rays_shadow = ctr[1];
+        stats->bounces = ctr[0];
+        stats->ms_total = now_ms() - t_start;
+        stats->ms_kernel = ms;
+    }
+    return MH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Ray-query sub-boundary
+// ---------------------------------------------------------------------------
+static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, float *t, float *u,
+                      float *v, uint32_t *prim, uint32_t *shape, uint32_t *occ, uint32_t flags,
+                      mh_stats *stats) {
+    if (!s || (n && !rays)) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace: NULL argument");
+    if (n == 0) return MH_OK;
+    double t_start = now_ms();
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
+    const float *r = rays;
+    float *dt = t, *du = u, *dv = v;
+    uint32_t *dp = prim, *ds = shape, *doc = occ;
+    if (!dev) {
+        MH_HIP(s->tmp_a.alloc(n * 28));
+        MH_HIP(hipMemcpyAsync(s->tmp_a.ptr, rays, n * 28, hipMemcpyHostToDevice, st));
+        r = s->tmp_a.as<float>();
+        MH_HIP(s->tmp_b.alloc(n * 20));
+        float *base = s->tmp_b.as<float>();
+        dt = base; du = base + n; dv = base + 2 * n;
+        dp = reinterpret_cast<uint32_t *>(base + 3 * n);
+        ds = reinterpret_cast<uint32_t *>(base + 4 * n);
+        doc = reinterpret_cast<uint32_t *>(base);
+    }
+    // persistent grid: 8 workgroups of 256 lanes per CU
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+    uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 8);
+    MH_HIP(hipEventRecord(s->ev0, st));
+    MH_HIP(launch_trace(s->S, shadow, n, r, dt, du, dv, dp, ds, doc, grid, st));
+    MH_HIP(hipEventRecord(s->ev1, st));
+    if (!dev) {
+        if (shadow) {
+            MH_HIP(hipMemcpyAsync(occ, doc, n * 4, hipMemcpyDeviceToHost, st));
+        } else {
+            MH_HIP(hipMemcpyAsync(t, dt, n * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipMemcpyAsync(u, du, n * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipMemcpyAsync(v, dv, n * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipMemcpyAsync(prim, dp, n * 4, hipMemcpyDeviceToHost, st));
+            MH_HIP(hipMemcpyAsync(shape, ds, n * 4, hipMemcpyDeviceToHost, st));
+        }
+    }
+    if (!(flags & MH_FLAG_NO_SYNC) || !dev) MH_HIP(hipStreamSynchronize(st));
+    if (stats) {
+        MH_HIP(hipEventSynchronize(s->ev1));
+        float ms = 0.f;
+        MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->samples = 0;
+        stats->rays_closest = shadow ? 0 : n;
+        stats->rays_shadow = shadow ? n : 0;
+        stats->bounces = 0;
+        stats->ms_total = now_ms() - t_start;
+        stats->ms_kernel = ms;
+    }
+    return MH_OK;
+}
+
+int mh_trace_closest(mh_scene *s, uint64_t n, const float *rays, float *t, float *u, float *v,
+                     uint32_t *prim, uint32_t *shape, uint32_t flags, mh_stats *stats) {
+    if (n && (!t || !u || !v || !prim || !shape))
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace_closest: NULL output");
+    return trace_impl(s, false, n, rays, t, u, v, prim, shape, nullptr, flags, stats);
+}
+
+int mh_trace_shadow(mh_scene *s, uint64_t n, const float *rays, uint32_t *occluded, uint32_t flags,
+                    mh_stats *stats) {
+    if (n && !occluded) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace_shadow: NULL output");
+    return trace_impl(s, true, n, rays, nullptr, nullptr, nullptr, nullptr, nullptr, occluded, flags,
+                      stats);
+}
+
+}  // extern "C"

@@ -1,0 +1,225 @@
+// mh_device.hpp — gfx950 device-side data layout and per-lane math for the
+// `path` / `prb` / `volpath` hot path.  Compiled only by hipcc for gfx950.
+//
+// Numerics contract: built with -ffp-contract=off and
+// -fhip-fp32-correctly-rounded-divide-sqrt; an fma appears exactly where the
+// reference (or Dr.Jit 0.4.4's LLVM backend) emits dr::fmadd, rcp(x) = 1/x,
+// rsqrt(x) = sqrt(1/x), sincos = Cephes polynomial.  This makes every lane
+// bit-comparable with the CPU oracle (oracle/mh_oracle.c).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mitsuba_hip.h"
+
+namespace mh {
+
+#define MH_DEV __device__ __forceinline__
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kInvPi = 0.31830988618379067154f;
+constexpr float kRayEps = 1500.0f * 5.9604644775390625e-08f;  // core/math.h:18-23
+constexpr float kShadowEps = kRayEps * 10.0f;
+constexpr float kFloatMax = 3.40282346638528859812e+38f;      // dr::Largest<float>
+
+// ---------------------------------------------------------------------------
+// Device scene layout (HBM; the BVH + primitive records are staged into LDS)
+// ---------------------------------------------------------------------------
+struct alignas(16) Node {       // 64 B: two child boxes (Aila-Laine BVH2 layout)
+    float4 lo0, hi0, lo1, hi1;  // .w of lo = child index / first prim, .w of hi = leaf count (0 = inner)
+};
+
+struct alignas(16) Prim {       // 64 B primitive record
+    float4 a, b, c;             // triangle: v0, e1 = v1 - v0, e2 = v2 - v0; rectangle: to_object rows
+    uint4 info;                 // x: shape, y: prim index (face; ~0 for rectangles), z: type
+};
+
+struct DShape {                 // shading-time shape record
+    uint32_t type, bsdf, emitter, face_offset;
+    uint32_t vertex_offset, has_normals, has_texcoords, pad;
+    float to_world[12];
+    float frame_s[4], frame_t[4], frame_n[4];
+    float inv_area, pad1, pad2, pad3;
+};
+
+struct DTexture {
+    uint32_t type, width, height, channels;
+    uint64_t data_offset;
+    uint32_t filter, wrap;
+    float value[4];
+    float to_uv[8];
+};
+
+struct DEmitter {
+    uint32_t type, shape, pad0, pad1;
+    float radiance[4];
+    float direction[4];
+};
+
+struct DScene {                 // kernel argument (by value)
+    const Node *nodes;
+    const Prim *prims;
+    const DShape *shapes;
+    const uint32_t *bsdf_type;     // per bsdf
+    const uint32_t *bsdf_tex;      // per bsdf reflectance texture
+    const DTexture *textures;
+    const DEmitter *emitters;
+    const float *positions;        // float3 (packed)
+    const float *normals;
+    const float *texcoords;
+    const uint32_t *faces;
+    const float *texels;
+    uint32_t n_nodes, n_prims, n_emitters, environment;
+    uint32_t stack_size;           // BVH traversal stack entries per lane
+    uint32_t lds_bytes_bvh;        // bytes of nodes + prims staged into LDS
+    // sensor
+    float cam_to_world[16];
+    float sample_to_camera[16];
+    float near_clip, far_clip;
+    uint32_t width, height;
+    uint32_t rfilter;
+    float rfilter_radius;
+    float filter_coeff[10];
+    uint32_t sampler_seed;
+};
+
+// lane -> (pixel, sample) map of one render call (sample-slab aware)
+struct LaneMap {
+    uint32_t W, spp_pp, log_spp;  // log_spp == 32 -> integer division
+    uint32_t pixel_begin, S, s_begin, log_S;
+};
+
+// ---------------------------------------------------------------------------
+// fp32 vector helpers (Dr.Jit semantics)
+// ---------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+
+MH_DEV V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+MH_DEV V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+MH_DEV V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+MH_DEV V3 operator*(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+MH_DEV V3 operator*(V3 a, float s) { return V3{a.x * s, a.y * s, a.z * s}; }
+MH_DEV V3 operator-(V3 a) { return V3{-a.x, -a.y, -a.z}; }
+MH_DEV V3 vdiv(V3 a, float s) { return V3{a.x / s, a.y / s, a.z / s}; }
+// dr::fmadd(vector, scalar, vector)
+MH_DEV V3 fma3s(V3 a, float b, V3 c) {
+    return V3{__builtin_fmaf(a.x, b, c.x), __builtin_fmaf(a.y, b, c.y), __builtin_fmaf(a.z, b, c.z)};
+}
+MH_DEV V3 fma3(V3 a, V3 b, V3 c) {
+    return V3{__builtin_fmaf(a.x, b.x, c.x), __builtin_fmaf(a.y, b.y, c.y), __builtin_fmaf(a.z, b.z, c.z)};
+}
+// dr::dot: a.x*b.x then an fmadd chain
+MH_DEV float dot(V3 a, V3 b) {
+    return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+}
+// dr::cross: fmsub(a.y, b.z, a.z*b.y), ...
+MH_DEV V3 cross(V3 a, V3 b) {
+    return V3{__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
+              __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
+}
+MH_DEV float rcp(float x) { return 1.0f / x; }
+MH_DEV float rsqrt_(float x) { return __builtin_sqrtf(1.0f / x); }
+MH_DEV V3 normalize(V3 v) { return v * rsqrt_(dot(v, v)); }
+MH_DEV float norm(V3 v) { return __builtin_sqrtf(dot(v, v)); }
+MH_DEV float hmax(V3 v) { return fmaxf(fmaxf(v.x, v.y), v.z); }
+MH_DEV V3 ld3(const float *p) { return V3{p[0], p[1], p[2]}; }
+MH_DEV float mulsign(float a, float b) { return b >= 0.f ? a : -a; }
+MH_DEV float mulsign_neg(float a, float b) { return b >= 0.f ? -a : a; }
+MH_DEV bool isfinite_(float x) { return __builtin_fabsf(x) < __builtin_huge_valf(); }
+MH_DEV bool nonzero(V3 v) { return v.x != 0.f || v.y != 0.f || v.z != 0.f; }
+
+// Transform4f point / vector products (core/transform.h:104-141); 3x4 row-major
+MH_DEV V3 xf_point(const float *m, V3 p) {
+    return V3{__builtin_fmaf(m[2], p.z, __builtin_fmaf(m[1], p.y, __builtin_fmaf(m[0], p.x, m[3]))),
+              __builtin_fmaf(m[6], p.z, __builtin_fmaf(m[5], p.y, __builtin_fmaf(m[4], p.x, m[7]))),
+              __builtin_fmaf(m[10], p.z, __builtin_fmaf(m[9], p.y, __builtin_fmaf(m[8], p.x, m[11])))};
+}
+MH_DEV V3 xf_vector(const float *m, V3 v) {
+    return V3{__builtin_fmaf(m[2], v.z, __builtin_fmaf(m[1], v.y, m[0] * v.x)),
+              __builtin_fmaf(m[6], v.z, __builtin_fmaf(m[5], v.y, m[4] * v.x)),
+              __builtin_fmaf(m[10], v.z, __builtin_fmaf(m[9], v.y, m[8] * v.x))};
+}
+
+// ---------------------------------------------------------------------------
+// Cephes sincos (Dr.Jit 0.4.4 math.h sincos for JIT-LLVM float arrays)
+// ---------------------------------------------------------------------------
+MH_DEV float poly2(float x, float c0, float c1, float c2) {
+    float x2 = x * x;
+    return __builtin_fmaf(x2, c2, __builtin_fmaf(x, c1, c0));
+}
+MH_DEV void sincos_cephes(float x, float &s_out, float &c_out) {
+    float xa = __builtin_fabsf(x);
+    int32_t j = (int32_t)(xa * 1.2732395447351626862f);
+    j = (j + 1) & ~1;
+    float y = (float)j;
+    uint32_t sign_sin = ((uint32_t)j << 29) ^ __float_as_uint(x);
+    uint32_t sign_cos = (~(uint32_t)(j - 2)) << 29;
+    y = xa - y * 0.78515625f - y * 2.4187564849853515625e-4f - y * 3.77489497744594108e-8f;
+    float z = y * y;
+    if (xa == __builtin_huge_valf()) z = __uint_as_float(0xffffffffu);
+    float s = poly2(z, -1.6666654611e-1f, 8.3321608736e-3f, -1.9515295891e-4f) * z;
+    float c = poly2(z, 4.166664568298827e-2f, -1.388731625493765e-3f, 2.443315711809948e-5f) * z;
+    s = __builtin_fmaf(s, y, y);
+    c = __builtin_fmaf(c, z, __builtin_fmaf(z, -0.5f, 1.0f));
+    bool polymask = (j & 2) == 0;
+    float rs = polymask ? s : c, rc = polymask ? c : s;
+    s_out = __uint_as_float(__float_as_uint(rs) ^ (sign_sin & 0x80000000u));
+    c_out = __uint_as_float(__float_as_uint(rc) ^ (sign_cos & 0x80000000u));
+}
+
+// ---------------------------------------------------------------------------
+// TEA + PCG32 (core/random.h:77-90, render/sampler.cpp:115-134, [drjit] PCG32)
+// ---------------------------------------------------------------------------
+MH_DEV void tea4(uint32_t v0, uint32_t v1, uint32_t &o0, uint32_t &o1) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        sum += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    o0 = v0;
+    o1 = v1;
+}
+
+struct Pcg {
+    uint64_t state, inc;
+    MH_DEV uint32_t next() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dull + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((0u - rot) & 31u));
+    }
+    MH_DEV float next_float() { return __uint_as_float((next() >> 9) | 0x3f800000u) - 1.0f; }
+    MH_DEV void seed(uint32_t seed_value, uint32_t lane) {
+        uint32_t v0, v1;
+        tea4(seed_value, lane, v0, v1);
+        state = 0;
+        inc = ((uint64_t)v1 << 1) | 1u;
+        next();
+        state += (uint64_t)v0;
+        next();
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Gaussian reconstruction filter (rfilters/gaussian.cpp:94-97, [drjit] Estrin)
+// ---------------------------------------------------------------------------
+MH_DEV float estrin10(float x, const float *k) {
+    float c0 = __builtin_fmaf(x, k[1], k[0]), c1 = __builtin_fmaf(x, k[3], k[2]),
+          c2 = __builtin_fmaf(x, k[5], k[4]), c3 = __builtin_fmaf(x, k[7], k[6]),
+          c4 = __builtin_fmaf(x, k[9], k[8]);
+    float x2 = x * x;
+    float d0 = __builtin_fmaf(x2, c1, c0), d1 = __builtin_fmaf(x2, c3, c2);
+    float x4 = x2 * x2;
+    float e0 = __builtin_fmaf(x4, d1, d0);
+    float x8 = x4 * x4;
+    return __builtin_fmaf(x8, c4, e0);
+}
+MH_DEV float gaussian_eval(const float *coeff, float x) {
+    return fmaxf(estrin10(x * x, coeff), 0.f);
+}
+
+}  // namespace mh

@@ -1,0 +1,63 @@
+// mh_internal.hpp — declarations shared by the host API (mh_api.hip), the BVH
+// builder (mh_bvh.cpp) and the kernels (mh_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/mitsuba_hip.h"
+
+namespace mh {
+
+struct DScene;
+struct Node;
+struct Prim;
+struct LaneMap;
+
+using IntegratorParams = mh_integrator;
+
+constexpr int kMaxRgbParams = 4;     // constant-albedo gradient slots (register accumulators)
+constexpr int kMaxBitmapParams = 4;  // bitmap gradient slots (global atomics)
+constexpr int kMaxParams = kMaxRgbParams + kMaxBitmapParams;
+
+struct GradArgs {
+    const int32_t *slot_of_tex;  // device: texture -> slot or -1
+    float *const *bufs;          // device: slot -> gradient buffer
+    const uint32_t *is_rgb;      // device: slot -> 1 if rgb
+    uint32_t n_rgb;              // rgb slots are 0 .. n_rgb-1
+};
+
+// ---- BVH builder (host, binned SAH) --------------------------------------
+struct BuildPrim {
+    float lo[3], hi[3];   // world AABB
+    float rec[12];        // Prim a/b/c payload
+    uint32_t shape, prim, type;
+};
+struct BvhOut {
+    std::vector<uint8_t> nodes;  // sizeof(Node) * n_nodes
+    std::vector<uint8_t> prims;  // sizeof(Prim) * n_prims (reordered)
+    uint32_t n_nodes = 0, n_prims = 0, depth = 0;
+};
+void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out);
+
+// ---- kernel launchers (mh_kernels.hip) -------------------------------------
+size_t lds_bytes(const DScene &S, uint32_t block);
+hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *rays, float *t,
+                        float *u, float *v, uint32_t *prim, uint32_t *shape, uint32_t *occ,
+                        uint32_t grid, hipStream_t st);
+hipError_t launch_render(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                         uint32_t seed_value, uint32_t n_passes, uint64_t n, uint64_t plane,
+                         float *out, unsigned long long *counters, hipStream_t st);
+hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, bool fast,
+                        uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
+                        const float *in, float *film, uint32_t seed_value, int coalesce,
+                        hipStream_t st);
+hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st);
+hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                               uint32_t seed_value, uint64_t n, int coalesce,
+                               const float *grad_in, const float *weights, const GradArgs &ga,
+                               unsigned long long *counters, hipStream_t st);
+
+}  // namespace mh

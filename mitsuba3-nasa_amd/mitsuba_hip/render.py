@@ -1,0 +1,248 @@
+"""mi.render / traverse / render_backward on the hip_ad_rgb backend.
+
+Restates src/python/python/util.py:292-350 (traverse / SceneParameters),
+util.py:356-408 (_RenderOp) and util.py:512-625 (mi.render) with
+``torch.autograd`` standing in for Dr.Jit's AD graph: ``loss.backward()``
+drives RBIntegrator.render_backward exactly where ``dr.backward(loss)`` does in
+the reference.  Images and gradients live on the scene's HIP device as torch
+tensors (torch is plumbing here: device memory + streams).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import _abi as A
+from .scene import Integrator, Scene
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def sample_tea_32(v0: int, v1: int, rounds: int = 4):
+    """core/random.h:77-90"""
+    m = 0xFFFFFFFF
+    s = 0
+    v0 &= m
+    v1 &= m
+    for _ in range(rounds):
+        s = (s + 0x9E3779B9) & m
+        v0 = (v0 + ((((v1 << 4) & m) + 0xA341316C) ^ ((v1 + s) & m) ^ ((v1 >> 5) + 0xC8013EA4))) & m
+        v1 = (v1 + ((((v0 << 4) & m) + 0xAD90777D) ^ ((v0 + s) & m) ^ ((v0 >> 5) + 0x7E95761E))) & m
+    return v0, v1
+
+
+def _device_index(device) -> int:
+    torch = _torch()
+    if device is None:
+        if not torch.cuda.is_available():
+            raise A.MitsubaHipError("mitsuba_hip: no HIP device available (hip_ad_rgb has no CPU fallback)")
+        return torch.cuda.current_device()
+    return torch.device(device).index or 0
+
+
+def _ptr(t) -> C.c_void_p:
+    return C.c_void_p(t.data_ptr())
+
+
+class SceneParameters:
+    """util.py:13-290 (SceneParameters) restricted to the differentiable
+    texture parameters on the hot path ('<bsdf>.reflectance.value' and
+    '<bsdf>.reflectance.data')."""
+
+    def __init__(self, scene: Scene, device=None):
+        torch = _torch()
+        self.scene = scene
+        self._device = device
+        self._values = {}
+        self._kind = {}
+        for key, (kind, idx) in scene.params.items():
+            if kind == "rgb":
+                v = torch.tensor(list(scene.texture(idx).value), dtype=torch.float32)
+            elif kind == "bitmap":
+                t = scene.texture(idx)
+                v = torch.from_numpy(scene.texture_data(idx).reshape(t.height, t.width, t.channels).copy())
+            else:
+                continue
+            if device is not None:
+                v = v.to(device)
+            self._values[key] = v
+            self._kind[key] = (kind, idx)
+        self._dirty = set()
+
+    def keys(self):
+        return self._values.keys()
+
+    def items(self):
+        return self._values.items()
+
+    def __contains__(self, k):
+        return k in self._values
+
+    def __len__(self):
+        return len(self._values)
+
+    def __getitem__(self, k):
+        return self._values[k]
+
+    def __setitem__(self, k, v):
+        torch = _torch()
+        if k not in self._values:
+            raise KeyError(k)
+        old = self._values[k]
+        v = torch.as_tensor(v, dtype=torch.float32, device=old.device)
+        if v.shape != old.shape:
+            v = v.reshape(old.shape)
+        self._values[k] = v
+        self._dirty.add(k)
+
+    def texture_of(self, k) -> int:
+        return self._kind[k][1]
+
+    def update(self, values: Optional[Dict] = None):
+        """Push modified values into every device copy of the scene."""
+        if values:
+            for k, v in values.items():
+                self[k] = v
+        keys = list(self._dirty) if self._dirty else list(self._values.keys())
+        L = A.lib() if self.scene._handles else None
+        for k in keys:
+            kind, idx = self._kind[k]
+            arr = self._values[k].detach().float().cpu().contiguous().numpy().reshape(-1)
+            if kind == "rgb":
+                self.scene.texture(idx).value[:] = [float(x) for x in arr]
+                for h in self.scene._handles.values():
+                    A.check(L.mh_scene_update_rgb(h, idx, arr.ctypes.data_as(A.PF)))
+            else:
+                dst = self.scene.texture_data(idx)
+                dst[:] = arr
+                for h in self.scene._handles.values():
+                    A.check(L.mh_scene_update_texture(h, idx, arr.ctypes.data_as(A.PF), arr.size))
+        self._dirty.clear()
+        return [(k, None) for k in keys]
+
+    def __repr__(self):
+        return "SceneParameters[\n" + "".join(f"  {k}: {tuple(v.shape)}\n" for k, v in self._values.items()) + "]"
+
+
+def traverse(scene: Scene, device=None) -> SceneParameters:
+    return SceneParameters(scene, device)
+
+
+# ---------------------------------------------------------------------------
+# core entry points (C-ABI wrappers; all buffers stay on the device)
+# ---------------------------------------------------------------------------
+def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
+                spp_begin: int = 0, spp_end: int = 0, device=None, film=None, accumulate=False,
+                stats: Optional[A.Stats] = None):
+    """Integrator::render(develop=False): RGBW film (H, W, 4) on the device."""
+    torch = _torch()
+    dev = _device_index(device)
+    integrator = integrator or scene.integrator()
+    spp = spp or scene.sample_count()
+    h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
+    if film is None:
+        film = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device=f"cuda:{dev}")
+    flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_ACCUMULATE if accumulate else 0)
+    ic = integrator.c()
+    A.check(A.lib().mh_render(h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(film), flags,
+                              C.byref(stats) if stats is not None else None))
+    return film
+
+
+def develop(scene: Scene, film, device=None):
+    torch = _torch()
+    dev = film.device.index or 0
+    h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
+    out = torch.empty((scene.height, scene.width, 3), dtype=torch.float32, device=film.device)
+    A.check(A.lib().mh_develop(h, _ptr(film.contiguous()), _ptr(out), A.FLAG_DEVICE_POINTERS))
+    return out
+
+
+def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, device=None):
+    torch = _torch()
+    dev = _device_index(device)
+    h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
+    w = torch.empty((scene.height, scene.width), dtype=torch.float32, device=f"cuda:{dev}")
+    A.check(A.lib().mh_prb_weights(h, seed, spp, spp_begin, spp_end, _ptr(w), A.FLAG_DEVICE_POINTERS))
+    return w
+
+
+def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],
+                    integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
+                    spp_begin: int = 0, spp_end: int = 0, weights=None,
+                    stats: Optional[A.Stats] = None):
+    """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
+    Returns a list of gradient tensors (one per key, same shape as the param)."""
+    torch = _torch()
+    integrator = integrator or scene.integrator()
+    if integrator.type != "prb":
+        raise A.MitsubaHipError("render_backward(): requires the 'prb' integrator")
+    spp = spp or scene.sample_count()
+    dev = grad_in.device.index or 0
+    h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
+    grad_in = grad_in.to(torch.float32).contiguous()
+    tex = (C.c_uint32 * max(len(keys), 1))(*[params.texture_of(k) for k in keys])
+    outs = [torch.zeros(params[k].shape, dtype=torch.float32, device=grad_in.device) for k in keys]
+    ptrs = (C.c_void_p * max(len(keys), 1))(*[o.data_ptr() for o in outs])
+    ic = integrator.c()
+    A.check(A.lib().mh_render_backward(
+        h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(grad_in),
+        _ptr(weights) if weights is not None else None, len(keys), tex, ptrs,
+        A.FLAG_DEVICE_POINTERS, C.byref(stats) if stats is not None else None))
+    return outs
+
+
+# ---------------------------------------------------------------------------
+# mi.render with torch autograd (util.py:356-408, 512-625)
+# ---------------------------------------------------------------------------
+def _render_op():
+    torch = _torch()
+
+    class _RenderOp(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, scene, params, keys, integrator, seeds, spps, *values):
+            ctx.scene, ctx.params, ctx.keys, ctx.integrator = scene, params, keys, integrator
+            ctx.seeds, ctx.spps = seeds, spps
+            film = render_film(scene, integrator, seeds[0], spps[0])
+            return develop(scene, film)
+
+        @staticmethod
+        def backward(ctx, grad_out):
+            grads = render_backward(ctx.scene, ctx.params, grad_out, ctx.keys, ctx.integrator,
+                                    ctx.seeds[1], ctx.spps[1])
+            return (None, None, None, None, None, None, *grads)
+
+    return _RenderOp
+
+
+def render(scene: Scene, params: Optional[SceneParameters] = None, sensor: int = 0,
+           integrator: Optional[Integrator] = None, seed: int = 0, seed_grad: int = 0,
+           spp: int = 0, spp_grad: int = 0):
+    """mi.render (util.py:512-625): returns an (H, W, 3) torch tensor on the device."""
+    if sensor != 0:
+        raise A.MitsubaHipError("hip_ad_rgb: only sensor index 0 is supported")
+    if params is not None and not isinstance(params, SceneParameters):
+        raise A.MitsubaHipError("params should be an instance of mi.SceneParameter!")
+    integrator = integrator or scene.integrator()
+    if integrator is None:
+        raise A.MitsubaHipError("No integrator specified! Add an integrator in the scene "
+                                "description or provide an integrator directly as argument.")
+    spp = spp or scene.sample_count()
+    if spp_grad == 0:
+        spp_grad = spp
+    if seed_grad == 0:
+        seed_grad = sample_tea_32(seed, 1)[0]
+    elif seed_grad == seed:
+        raise A.MitsubaHipError("The primal and differential seed should be different to ensure "
+                                "unbiased gradient computation!")
+    keys = [k for k, v in params.items() if v.requires_grad] if params is not None else []
+    if not keys:
+        film = render_film(scene, integrator, seed, spp)
+        return develop(scene, film)
+    values = [params[k] for k in keys]
+    return _render_op().apply(scene, params, keys, integrator, (seed, seed_grad), (spp, spp_grad), *values)

@@ -1,0 +1,1484 @@
+/*
+ * mh_oracle.c — CPU restatement (plain C, scalar, fp32) of the reference's
+ * `path` / `prb` hot path with llvm_ad_rgb (JIT) semantics.
+ *
+ * TEST INFRASTRUCTURE ONLY (see mh_oracle.h).  Every function cites the
+ * reference file:line it restates (paths relative to /root/reference).
+ * Conventions that make the product bit-comparable:
+ *   - compiled with -ffp-contract=off; an explicit fmaf() appears exactly where
+ *     the reference (or Dr.Jit) calls dr::fmadd / fmsub / fnmadd;
+ *   - Dr.Jit 0.4.4 LLVM-backend lowering: rcp(x) = 1/x, rsqrt(x) = sqrt(1/x),
+ *     sqrt/div correctly rounded, sincos/log = Cephes polynomials.
+ */
+#include "mh_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Error reporting                                                          */
+/* ------------------------------------------------------------------------ */
+static __thread char g_err[512];
+const char *oracle_last_error(void) { return g_err; }
+static int fail(const char *msg) {
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Dr.Jit scalar primitives (LLVM backend lowering)                         */
+/* ------------------------------------------------------------------------ */
+#define PI_F      3.14159265358979323846f
+#define INV_PI_F  0.31830988618379067154f
+#define INV_4PI_F 0.07957747154594766788f
+/* include/mitsuba/core/math.h:18-23 with dr::Epsilon<float> = 2^-24 */
+#define RAY_EPS    (1500.0f * 5.9604644775390625e-08f)
+#define SHADOW_EPS (RAY_EPS * 10.0f)
+
+typedef struct { float x, y, z; } v3;
+
+static inline v3 V3(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vadd(v3 a, v3 b) { return V3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 vsub(v3 a, v3 b) { return V3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 vmul(v3 a, v3 b) { return V3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 vscale(v3 a, float s) { return V3(a.x * s, a.y * s, a.z * s); }
+static inline v3 vneg(v3 a) { return V3(-a.x, -a.y, -a.z); }
+static inline v3 vdivs(v3 a, float s) { return V3(a.x / s, a.y / s, a.z / s); }
+/* dr::fmadd(a, b, c) for a vector a, scalar b, vector c */
+static inline v3 vfma_s(v3 a, float b, v3 c) {
+    return V3(fmaf(a.x, b, c.x), fmaf(a.y, b, c.y), fmaf(a.z, b, c.z));
+}
+static inline v3 vfma(v3 a, v3 b, v3 c) {
+    return V3(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z));
+}
+/* dr::dot: a.x*b.x, then fmadd chain */
+static inline float vdot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+/* dr::cross: fmsub(a.y, b.z, a.z * b.y), ... */
+static inline v3 vcross(v3 a, v3 b) {
+    return V3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)),
+              fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static inline float rcpf_(float x) { return 1.0f / x; }
+static inline float rsqrtf_(float x) { return sqrtf(1.0f / x); }
+static inline v3 vnormalize(v3 v) { return vscale(v, rsqrtf_(vdot(v, v))); }
+static inline float vnorm(v3 v) { return sqrtf(vdot(v, v)); }
+static inline float vmax(v3 v) { return fmaxf(fmaxf(v.x, v.y), v.z); }
+static inline v3 vload(const float *p) { return V3(p[0], p[1], p[2]); }
+/* dr::mulsign for differentiable arrays: select(b >= 0, a, -a) */
+static inline float mulsign(float a, float b) { return b >= 0.f ? a : -a; }
+static inline float mulsign_neg(float a, float b) { return b >= 0.f ? -a : a; }
+static inline float signf_(float a) { return a >= 0.f ? 1.f : -1.f; }
+static inline int isfinitef_(float x) { return fabsf(x) < INFINITY; }
+static inline float safe_sqrtf(float x) { return sqrtf(fmaxf(x, 0.f)); }
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+/* Transform4f::operator*(Point) / transform_affine (core/transform.h:104-124),
+   matrix m is row-major 3x4 (affine) */
+static inline v3 xf_point(const float *m, v3 p) {
+    return V3(fmaf(m[2], p.z, fmaf(m[1], p.y, fmaf(m[0], p.x, m[3]))),
+              fmaf(m[6], p.z, fmaf(m[5], p.y, fmaf(m[4], p.x, m[7]))),
+              fmaf(m[10], p.z, fmaf(m[9], p.y, fmaf(m[8], p.x, m[11]))));
+}
+/* Transform4f::operator*(Vector) (core/transform.h:132-141) */
+static inline v3 xf_vector(const float *m, v3 v) {
+    return V3(fmaf(m[2], v.z, fmaf(m[1], v.y, m[0] * v.x)),
+              fmaf(m[6], v.z, fmaf(m[5], v.y, m[4] * v.x)),
+              fmaf(m[10], v.z, fmaf(m[9], v.y, m[8] * v.x)));
+}
+/* same with a 4x4 row-major matrix (only the top 3 rows used) */
+static inline v3 xf4_vector(const float *m, v3 v) {
+    return V3(fmaf(m[2], v.z, fmaf(m[1], v.y, m[0] * v.x)),
+              fmaf(m[6], v.z, fmaf(m[5], v.y, m[4] * v.x)),
+              fmaf(m[10], v.z, fmaf(m[9], v.y, m[8] * v.x)));
+}
+/* projective point transform (core/transform.h:118-124) */
+static inline v3 xf4_point_proj(const float *m, v3 p) {
+    float r[4];
+    for (int i = 0; i < 4; ++i)
+        r[i] = fmaf(m[4 * i + 2], p.z, fmaf(m[4 * i + 1], p.y, fmaf(m[4 * i + 0], p.x, m[4 * i + 3])));
+    return V3(r[0] / r[3], r[1] / r[3], r[2] / r[3]);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Cephes sincos / log as restated from Dr.Jit 0.4.4 include/drjit/math.h   */
+/* ------------------------------------------------------------------------ */
+static inline float poly2(float x, float c0, float c1, float c2) {
+    float x2 = x * x;
+    return fmaf(x2, c2, fmaf(x, c1, c0));
+}
+
+void oracle_sincos(float x, float *s_out, float *c_out) {
+    float xa = fabsf(x);
+    int32_t j = (int32_t)(xa * 1.2732395447351626862f);
+    j = (j + 1) & ~1;
+    float y = (float)j;
+    uint32_t sign_sin = ((uint32_t)j << 29) ^ f2u(x);
+    uint32_t sign_cos = (~(uint32_t)(j - 2)) << 29;
+    y = xa - y * 0.78515625f - y * 2.4187564849853515625e-4f - y * 3.77489497744594108e-8f;
+    float z = y * y;
+    if (xa == INFINITY)
+        z = u2f(0xffffffffu);
+    float s = poly2(z, -1.6666654611e-1f, 8.3321608736e-3f, -1.9515295891e-4f) * z;
+    float c = poly2(z, 4.166664568298827e-2f, -1.388731625493765e-3f, 2.443315711809948e-5f) * z;
+    s = fmaf(s, y, y);
+    c = fmaf(c, z, fmaf(z, -0.5f, 1.0f));
+    int polymask = (j & 2) == 0;
+    float rs = polymask ? s : c, rc = polymask ? c : s;
+    *s_out = u2f(f2u(rs) ^ (sign_sin & 0x80000000u));
+    *c_out = u2f(f2u(rc) ^ (sign_cos & 0x80000000u));
+}
+
+/* Cephes logf (frexp + rational polynomial), Dr.Jit 0.4.4 math.h `log` */
+float oracle_log(float x) {
+    if (!(x > 0.f)) {
+        if (x == 0.f) return -INFINITY;
+        return u2f(0xffffffffu); /* NaN */
+    }
+    if (x == INFINITY) return INFINITY;
+    /* frexp: mantissa in [0.5, 1) */
+    uint32_t bits = f2u(x);
+    int e;
+    float xm;
+    if ((bits & 0x7f800000u) == 0) { /* denormal */
+        xm = frexpf(x, &e);
+    } else {
+        e = (int)((bits >> 23) & 0xff) - 126;
+        xm = u2f((bits & 0x807fffffu) | 0x3f000000u);
+    }
+    if (xm < 0.70710678118654752440f) {
+        e -= 1;
+        xm = xm + xm - 1.0f;
+    } else {
+        xm = xm - 1.0f;
+    }
+    float z = xm * xm;
+    float y = 7.0376836292e-2f;
+    y = fmaf(y, xm, -1.1514610310e-1f);
+    y = fmaf(y, xm, 1.1676998740e-1f);
+    y = fmaf(y, xm, -1.2420140846e-1f);
+    y = fmaf(y, xm, 1.4249322787e-1f);
+    y = fmaf(y, xm, -1.6668057665e-1f);
+    y = fmaf(y, xm, 2.0000714765e-1f);
+    y = fmaf(y, xm, -2.4999993993e-1f);
+    y = fmaf(y, xm, 3.3333331174e-1f);
+    y = y * xm * z;
+    float fe = (float)e;
+    y = fmaf(fe, -2.12194440e-4f, y);
+    y = fmaf(z, -0.5f, y);
+    float r = xm + y;
+    r = fmaf(fe, 0.693359375f, r);
+    return r;
+}
+
+/* ------------------------------------------------------------------------ */
+/* TEA + PCG32 (include/mitsuba/core/random.h:77-140, sampler.cpp:115-134)  */
+/* ------------------------------------------------------------------------ */
+void oracle_tea32(uint32_t v0, uint32_t v1, int rounds, uint32_t *o0, uint32_t *o1) {
+    uint32_t sum = 0;
+    for (int i = 0; i < rounds; ++i) {
+        sum += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    *o0 = v0;
+    *o1 = v1;
+}
+
+float oracle_tea_float32(uint32_t v0, uint32_t v1, int rounds) {
+    uint32_t a, b;
+    oracle_tea32(v0, v1, rounds, &a, &b);
+    return u2f((b >> 9) | 0x3f800000u) - 1.0f;
+}
+
+double oracle_tea_float64(uint32_t v0, uint32_t v1, int rounds) {
+    uint32_t a, b;
+    oracle_tea32(v0, v1, rounds, &a, &b);
+    uint64_t v = (uint64_t)a | ((uint64_t)b << 32);
+    uint64_t bits = (v >> 12) | 0x3ff0000000000000ull;
+    double d;
+    memcpy(&d, &bits, 8);
+    return d - 1.0;
+}
+
+#define PCG32_MULT 0x5851f42d4c957f2dull
+typedef struct { uint64_t state, inc; } pcg32;
+
+static inline uint32_t pcg_next(pcg32 *r) {
+    uint64_t old = r->state;
+    r->state = old * PCG32_MULT + r->inc;
+    uint32_t xorshifted = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    uint32_t rot = (uint32_t)(old >> 59u);
+    return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+}
+/* [drjit] PCG32::seed(size, initstate, initseq) */
+static inline void pcg_seed(pcg32 *r, uint64_t initstate, uint64_t initseq) {
+    r->state = 0;
+    r->inc = (initseq << 1) | 1u;
+    pcg_next(r);
+    r->state += initstate;
+    pcg_next(r);
+}
+static inline float pcg_float(pcg32 *r) {
+    return u2f((pcg_next(r) >> 9) | 0x3f800000u) - 1.0f;
+}
+/* PCG32Sampler::seed (sampler.cpp:115-134): TEA(seed_value, lane) -> seed(v0, v1) */
+static inline void sampler_seed(pcg32 *r, uint32_t seed_value, uint32_t lane) {
+    uint32_t v0, v1;
+    oracle_tea32(seed_value, lane, 4, &v0, &v1);
+    pcg_seed(r, v0, v1);
+}
+
+void oracle_pcg32_stream(uint64_t initstate, uint64_t initseq, uint32_t n, uint32_t *out) {
+    pcg32 r;
+    pcg_seed(&r, initstate, initseq);
+    for (uint32_t i = 0; i < n; ++i) out[i] = pcg_next(&r);
+}
+
+void oracle_sampler_floats(uint32_t seed_value, uint32_t lane, uint32_t n, float *out) {
+    pcg32 r;
+    sampler_seed(&r, seed_value, lane);
+    for (uint32_t i = 0; i < n; ++i) out[i] = pcg_float(&r);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reconstruction filter: Gaussian (src/rfilters/gaussian.cpp:94-97)        */
+/* [drjit] estrin_impl over 10 coefficients                                 */
+/* ------------------------------------------------------------------------ */
+static inline float estrin10(float x, const float *k) {
+    float c0 = fmaf(x, k[1], k[0]), c1 = fmaf(x, k[3], k[2]), c2 = fmaf(x, k[5], k[4]),
+          c3 = fmaf(x, k[7], k[6]), c4 = fmaf(x, k[9], k[8]);
+    float x2 = x * x;
+    float d0 = fmaf(x2, c1, c0), d1 = fmaf(x2, c3, c2), d2 = c4;
+    float x4 = x2 * x2;
+    float e0 = fmaf(x4, d1, d0), e1 = d2;
+    float x8 = x4 * x4;
+    return fmaf(x8, e1, e0);
+}
+
+float oracle_gaussian_eval(const float coeff[10], float x) {
+    return fmaxf(estrin10(x * x, coeff), 0.f);
+}
+
+static inline float rfilter_eval(const mh_sensor *s, float x) {
+    if (s->rfilter == MH_RFILTER_GAUSSIAN)
+        return oracle_gaussian_eval(s->filter_coeff, x);
+    return (fabsf(x) <= 0.5f) ? 1.f : 0.f; /* box.cpp (unused: box takes the fast path) */
+}
+
+/* ------------------------------------------------------------------------ */
+/* ImageBlock::put (src/render/imageblock.cpp:174-532)                      */
+/* values[4] = R G B W; `film` is H x W x 4 (row range [row0, row0+rows))   */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    float *data;
+    uint32_t width, height; /* full film size */
+    int32_t row0;           /* first row stored in `data` */
+    uint32_t rows;          /* number of rows stored */
+} film_band;
+
+static inline void band_add(film_band *f, uint32_t x, uint32_t y, const float *vals, float w,
+                            int nch) {
+    int32_t r = (int32_t)y - f->row0;
+    if (r < 0 || r >= (int32_t)f->rows) return; /* caller sized the band to cover it */
+    float *p = f->data + ((size_t)r * f->width + x) * 4;
+    for (int k = 0; k < nch; ++k) p[k] += vals[k] * w;
+}
+
+static void splat(const mh_sensor *s, film_band *f, float px, float py, const float *vals,
+                  int coalesce) {
+    const uint32_t W = s->width, H = s->height;
+    if (s->rfilter == MH_RFILTER_BOX) {
+        /* fast special case for the box filter (imageblock.cpp:210-233) */
+        int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py);
+        uint32_t ux = (uint32_t)ix, uy = (uint32_t)iy;
+        if (ux < W && uy < H) band_add(f, ux, uy, vals, 1.0f, 4);
+        return;
+    }
+    const float radius = s->rfilter_radius;
+    if (coalesce) {
+        /* 2. coalesced, recorded-loop variant (imageblock.cpp:418-531) */
+        int32_t n = (int32_t)ceilf(radius - 0.5f);
+        int32_t count = 2 * n + 1;
+        int32_t pix = (int32_t)floorf(px) - n, piy = (int32_t)floorf(py) - n;
+        uint32_t x = (uint32_t)pix, y = (uint32_t)piy;
+        float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
+        for (int32_t ys = 0; ys < count; ++ys) {
+            float wy = rfilter_eval(s, rely + (float)ys);
+            int act1 = (y + (uint32_t)ys) < H;
+            for (int32_t xs = 0; xs < count; ++xs) {
+                float wx = rfilter_eval(s, relx + (float)xs);
+                float w = wx * wy;
+                if (act1 && (x + (uint32_t)xs) < W)
+                    band_add(f, x + (uint32_t)xs, y + (uint32_t)ys, vals, w, 4);
+            }
+        }
+    } else {
+        /* 1.2 non-coalesced, recorded-loop variant (imageblock.cpp:264-409) */
+        float pfx = px - 0.5f, pfy = py - 0.5f;
+        float p0x = pfx - radius, p0y = pfy - radius, p1x = pfx + radius, p1y = pfy + radius;
+        int32_t a0x = (int32_t)ceilf(p0x), a0y = (int32_t)ceilf(p0y);
+        int32_t a1x = (int32_t)floorf(p1x), a1y = (int32_t)floorf(p1y);
+        if (a0x < 0) a0x = 0;
+        if (a0y < 0) a0y = 0;
+        if (a1x > (int32_t)W - 1) a1x = (int32_t)W - 1;
+        if (a1y > (int32_t)H - 1) a1y = (int32_t)H - 1;
+        uint32_t u0x = (uint32_t)a0x, u0y = (uint32_t)a0y, u1x = (uint32_t)a1x, u1y = (uint32_t)a1y;
+        if (!(u0x <= u1x && u0y <= u1y)) return;
+        uint32_t count = (uint32_t)ceilf(2.f * radius);
+        float relx = (float)u0x - pfx, rely = (float)u0y - pfy;
+        for (uint32_t ys = 0; ys < count; ++ys) {
+            float wy = rfilter_eval(s, rely + (float)ys);
+            int act1 = (u0y + ys) <= u1y;
+            for (uint32_t xs = 0; xs < count; ++xs) {
+                float wx = rfilter_eval(s, relx + (float)xs);
+                float w = wx * wy;
+                if (act1 && (u0x + xs) <= u1x)
+                    band_add(f, u0x + xs, u0y + ys, vals, w, 4);
+            }
+        }
+    }
+}
+
+/* HDRFilm::develop (src/films/hdrfilm.cpp:349-405) */
+void oracle_develop(uint32_t w, uint32_t h, const float *film, float *rgb) {
+    size_t n = (size_t)w * h;
+    for (size_t i = 0; i < n; ++i) {
+        float W = film[4 * i + 3];
+        float d = (W == 0.f) ? 1.f : W;
+        for (int c = 0; c < 3; ++c) rgb[3 * i + c] = film[4 * i + c] / d;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Scene view                                                               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const mh_scene_desc *d;
+    float (*bbox)[6]; /* per shape AABB */
+} scene_view;
+
+static void shape_bbox(const mh_scene_desc *d, uint32_t i, float *bb) {
+    const mh_shape *sh = &d->shapes[i];
+    bb[0] = bb[1] = bb[2] = INFINITY;
+    bb[3] = bb[4] = bb[5] = -INFINITY;
+    if (sh->type == MH_SHAPE_RECTANGLE) {
+        static const float cs[4][2] = {{-1, -1}, {-1, 1}, {1, -1}, {1, 1}};
+        for (int k = 0; k < 4; ++k) {
+            v3 p = xf_point(sh->to_world, V3(cs[k][0], cs[k][1], 0.f));
+            float q[3] = {p.x, p.y, p.z};
+            for (int a = 0; a < 3; ++a) {
+                if (q[a] < bb[a]) bb[a] = q[a];
+                if (q[a] > bb[3 + a]) bb[3 + a] = q[a];
+            }
+        }
+    } else {
+        for (uint32_t v = 0; v < sh->vertex_count; ++v) {
+            const float *q = d->positions + 3 * (size_t)(sh->vertex_offset + v);
+            for (int a = 0; a < 3; ++a) {
+                if (q[a] < bb[a]) bb[a] = q[a];
+                if (q[a] > bb[3 + a]) bb[3 + a] = q[a];
+            }
+        }
+    }
+    /* conservative padding: the AABB is only a culling test */
+    for (int a = 0; a < 3; ++a) {
+        float e = 1e-4f * (fabsf(bb[a]) + fabsf(bb[3 + a]) + 1.f);
+        bb[a] -= e;
+        bb[3 + a] += e;
+    }
+}
+
+static int scene_view_init(scene_view *sv, const mh_scene_desc *d) {
+    if (!d || d->abi_version != MH_ABI_VERSION) return fail("scene: ABI version mismatch");
+    sv->d = d;
+    sv->bbox = (float (*)[6])malloc(sizeof(float) * 6 * (d->n_shapes ? d->n_shapes : 1));
+    if (!sv->bbox) return fail("out of memory");
+    for (uint32_t i = 0; i < d->n_shapes; ++i) shape_bbox(d, i, sv->bbox[i]);
+    return 0;
+}
+static void scene_view_free(scene_view *sv) { free(sv->bbox); }
+
+typedef struct { v3 o, d; float maxt; } ray3;
+
+static inline int bbox_hit(const float *bb, v3 o, v3 d, float maxt) {
+    float t0 = 0.f, t1 = maxt;
+    float os[3] = {o.x, o.y, o.z}, ds[3] = {d.x, d.y, d.z};
+    for (int a = 0; a < 3; ++a) {
+        float inv = 1.0f / ds[a];
+        float tn = (bb[a] - os[a]) * inv, tf = (bb[3 + a] - os[a]) * inv;
+        if (tn > tf) { float tmp = tn; tn = tf; tf = tmp; }
+        if (tn != tn) tn = -INFINITY; /* 0 * inf */
+        if (tf != tf) tf = INFINITY;
+        if (tn > t0) t0 = tn;
+        if (tf < t1) t1 = tf;
+    }
+    return t0 <= t1 * 1.000001f + 1e-6f;
+}
+
+/* Rectangle::ray_intersect_preliminary_impl (src/shapes/rectangle.cpp:446-470) */
+static inline int rect_intersect(const mh_shape *sh, const ray3 *r, float *t_out, float *u,
+                                 float *v) {
+    v3 o = xf_point(sh->to_object, r->o);
+    v3 d = xf_vector(sh->to_object, r->d);
+    float t = -o.z / d.z;
+    v3 local = vfma_s(d, t, o); /* Ray::operator() = fmadd(d, t, o) (core/ray.h:61) */
+    int hit = t >= 0.f && t <= r->maxt && fabsf(local.x) <= 1.f && fabsf(local.y) <= 1.f;
+    *t_out = t;
+    *u = local.x;
+    *v = local.y;
+    return hit;
+}
+
+/* Mesh::moeller_trumbore (include/mitsuba/render/mesh.h:430-453) */
+static inline int tri_intersect(v3 p0, v3 p1, v3 p2, const ray3 *r, float *t_out, float *uo,
+                                float *vo) {
+    v3 e1 = vsub(p1, p0), e2 = vsub(p2, p0);
+    v3 pvec = vcross(r->d, e2);
+    float inv_det = rcpf_(vdot(e1, pvec));
+    v3 tvec = vsub(r->o, p0);
+    float u = vdot(tvec, pvec) * inv_det;
+    int active = u >= 0.f && u <= 1.f;
+    v3 qvec = vcross(tvec, e1);
+    float v = vdot(r->d, qvec) * inv_det;
+    active = active && v >= 0.f && u + v <= 1.f;
+    float t = vdot(e2, qvec) * inv_det;
+    active = active && t >= 0.f && t <= r->maxt;
+    *t_out = t;
+    *uo = u;
+    *vo = v;
+    return active;
+}
+
+static inline v3 mesh_vertex(const mh_scene_desc *d, const mh_shape *sh, uint32_t local) {
+    return vload(d->positions + 3 * (size_t)(sh->vertex_offset + local));
+}
+
+typedef struct {
+    float t, u, v;
+    uint32_t prim, shape;
+} pi_rec;
+
+/* Scene::ray_intersect_preliminary (closest hit; scene.cpp:181-190) */
+static void trace_closest(const scene_view *sv, const ray3 *r, pi_rec *pi) {
+    const mh_scene_desc *d = sv->d;
+    pi->t = INFINITY;
+    pi->u = pi->v = 0.f;
+    pi->prim = MH_INVALID;
+    pi->shape = MH_INVALID;
+    ray3 rr = *r;
+    for (uint32_t s = 0; s < d->n_shapes; ++s) {
+        if (!bbox_hit(sv->bbox[s], r->o, r->d, r->maxt)) continue;
+        const mh_shape *sh = &d->shapes[s];
+        float t, u, v;
+        if (sh->type == MH_SHAPE_RECTANGLE) {
+            if (rect_intersect(sh, &rr, &t, &u, &v) && t < pi->t) {
+                pi->t = t; pi->u = u; pi->v = v; pi->prim = MH_INVALID; pi->shape = s;
+            }
+        } else {
+            for (uint32_t f = 0; f < sh->face_count; ++f) {
+                const uint32_t *fi = d->faces + 3 * (size_t)(sh->face_offset + f);
+                if (tri_intersect(mesh_vertex(d, sh, fi[0]), mesh_vertex(d, sh, fi[1]),
+                                  mesh_vertex(d, sh, fi[2]), &rr, &t, &u, &v) &&
+                    t < pi->t) {
+                    pi->t = t; pi->u = u; pi->v = v; pi->prim = f; pi->shape = s;
+                }
+            }
+        }
+    }
+}
+
+/* Scene::ray_test (any hit; scene.cpp:201-210) */
+static int trace_shadow(const scene_view *sv, const ray3 *r) {
+    const mh_scene_desc *d = sv->d;
+    for (uint32_t s = 0; s < d->n_shapes; ++s) {
+        if (!bbox_hit(sv->bbox[s], r->o, r->d, r->maxt)) continue;
+        const mh_shape *sh = &d->shapes[s];
+        float t, u, v;
+        if (sh->type == MH_SHAPE_RECTANGLE) {
+            if (rect_intersect(sh, r, &t, &u, &v)) return 1;
+        } else {
+            for (uint32_t f = 0; f < sh->face_count; ++f) {
+                const uint32_t *fi = d->faces + 3 * (size_t)(sh->face_offset + f);
+                if (tri_intersect(mesh_vertex(d, sh, fi[0]), mesh_vertex(d, sh, fi[1]),
+                                  mesh_vertex(d, sh, fi[2]), r, &t, &u, &v))
+                    return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+int oracle_trace_closest(const mh_scene_desc *desc, uint64_t n, const float *rays, float *t,
+                         float *u, float *v, uint32_t *prim, uint32_t *shape) {
+    scene_view sv;
+    if (scene_view_init(&sv, desc)) return 1;
+    for (uint64_t i = 0; i < n; ++i) {
+        ray3 r = {V3(rays[i], rays[n + i], rays[2 * n + i]),
+                  V3(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]), rays[6 * n + i]};
+        pi_rec pi;
+        trace_closest(&sv, &r, &pi);
+        t[i] = pi.t; u[i] = pi.u; v[i] = pi.v; prim[i] = pi.prim; shape[i] = pi.shape;
+    }
+    scene_view_free(&sv);
+    return 0;
+}
+
+int oracle_trace_shadow(const mh_scene_desc *desc, uint64_t n, const float *rays,
+                        uint32_t *occluded) {
+    scene_view sv;
+    if (scene_view_init(&sv, desc)) return 1;
+    for (uint64_t i = 0; i < n; ++i) {
+        ray3 r = {V3(rays[i], rays[n + i], rays[2 * n + i]),
+                  V3(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]), rays[6 * n + i]};
+        occluded[i] = (uint32_t)trace_shadow(&sv, &r);
+    }
+    scene_view_free(&sv);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* SurfaceInteraction                                                       */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int valid;
+    float t;
+    v3 p, n;             /* geometric */
+    v3 sh_s, sh_t, sh_n; /* shading frame */
+    v3 dp_du;
+    float uvx, uvy;
+    v3 wi;               /* local */
+    uint32_t shape, prim;
+} surf_int;
+
+/* coordinate_system (include/mitsuba/core/vector.h:116-136) */
+static inline void coordinate_system(v3 n, v3 *s, v3 *t) {
+    float sign = signf_(n.z), a = -rcpf_(sign + n.z), b = n.x * n.y * a;
+    *s = V3(mulsign(n.x * n.x * a, n.z) + 1.f, mulsign(b, n.z), mulsign_neg(n.x, n.z));
+    *t = V3(b, fmaf(n.y, n.y * a, sign), -n.y);
+}
+
+static inline v3 to_local(const surf_int *si, v3 v) {
+    return V3(vdot(v, si->sh_s), vdot(v, si->sh_t), vdot(v, si->sh_n));
+}
+/* Frame3f::to_world (include/mitsuba/core/frame.h:40-43) */
+static inline v3 to_world(const surf_int *si, v3 v) {
+    return vfma_s(si->sh_n, v.z, vfma_s(si->sh_t, v.y, vscale(si->sh_s, v.x)));
+}
+
+/* PreliminaryIntersection::compute_surface_interaction (interaction.h:731-757)
+   + Rectangle / Mesh::compute_surface_interaction (ad variant branch)
+   + finalize_surface_interaction (interaction.h:464-484)                  */
+static void compute_si(const mh_scene_desc *d, const ray3 *r, const pi_rec *pi, surf_int *si) {
+    memset(si, 0, sizeof(*si));
+    si->shape = pi->shape;
+    si->prim = pi->prim;
+    if (pi->shape == MH_INVALID || !(pi->t != INFINITY)) {
+        si->valid = 0;
+        si->t = INFINITY;
+        si->wi = vneg(r->d); /* world-space -d for invalid lanes */
+        return;
+    }
+    si->valid = 1;
+    si->t = pi->t;
+    const mh_shape *sh = &d->shapes[pi->shape];
+    if (sh->type == MH_SHAPE_RECTANGLE) {
+        /* rectangle.cpp:497-567 (IsDiff branch: p = ray(t)) */
+        si->p = vfma_s(r->d, pi->t, r->o);
+        si->n = vload(sh->frame_n);
+        si->sh_n = si->n;
+        si->dp_du = vload(sh->frame_s);
+        si->uvx = fmaf(pi->u, 0.5f, 0.5f);
+        si->uvy = fmaf(pi->v, 0.5f, 0.5f);
+    } else {
+        /* mesh.cpp:1368-1536 */
+        const uint32_t *fi = d->faces + 3 * (size_t)(sh->face_offset + pi->prim);
+        v3 p0 = mesh_vertex(d, sh, fi[0]), p1 = mesh_vertex(d, sh, fi[1]),
+           p2 = mesh_vertex(d, sh, fi[2]);
+        float b1 = pi->u, b2 = pi->v, b0 = 1.f - b1 - b2;
+        si->p = vfma_s(p0, b0, vfma_s(p1, b1, vscale(p2, b2)));
+        si->n = vnormalize(vcross(vsub(p1, p0), vsub(p2, p0)));
+        si->uvx = b1;
+        si->uvy = b2;
+        v3 dpdv;
+        coordinate_system(si->n, &si->dp_du, &dpdv);
+        v3 dp0 = vsub(p1, p0), dp1 = vsub(p2, p0);
+        if (sh->has_texcoords) {
+            const float *tc = d->texcoords;
+            size_t o = sh->vertex_offset;
+            float u0x = tc[2 * (o + fi[0])], u0y = tc[2 * (o + fi[0]) + 1];
+            float u1x = tc[2 * (o + fi[1])], u1y = tc[2 * (o + fi[1]) + 1];
+            float u2x = tc[2 * (o + fi[2])], u2y = tc[2 * (o + fi[2]) + 1];
+            si->uvx = fmaf(u2x, b2, fmaf(u1x, b1, u0x * b0));
+            si->uvy = fmaf(u2y, b2, fmaf(u1y, b1, u0y * b0));
+            float d0x = u1x - u0x, d0y = u1y - u0y, d1x = u2x - u0x, d1y = u2y - u0y;
+            float det = fmaf(d0x, d1y, -(d0y * d1x)), inv_det = rcpf_(det);
+            if (det != 0.f) {
+                si->dp_du = vscale(V3(fmaf(d1y, dp0.x, -(d0y * dp1.x)),
+                                      fmaf(d1y, dp0.y, -(d0y * dp1.y)),
+                                      fmaf(d1y, dp0.z, -(d0y * dp1.z))),
+                                   inv_det);
+            }
+        }
+        if (sh->has_normals) {
+            const float *nn = d->normals;
+            size_t o = sh->vertex_offset;
+            v3 n0 = vload(nn + 3 * (o + fi[0])), n1 = vload(nn + 3 * (o + fi[1])),
+               n2 = vload(nn + 3 * (o + fi[2]));
+            v3 n = vfma_s(n2, b2, vfma_s(n1, b1, vscale(n0, b0)));
+            float il = rsqrtf_(vdot(n, n));
+            si->sh_n = vscale(n, il);
+        } else {
+            si->sh_n = si->n;
+        }
+    }
+    /* initialize_sh_frame (interaction.h:245-255) */
+    si->sh_s = vnormalize(vfma_s(si->sh_n, -vdot(si->sh_n, si->dp_du), si->dp_du));
+    if (si->dp_du.x == 0.f && si->dp_du.y == 0.f && si->dp_du.z == 0.f) {
+        v3 tt;
+        coordinate_system(si->sh_n, &si->sh_s, &tt);
+    }
+    si->sh_t = vcross(si->sh_n, si->sh_s);
+    si->wi = to_local(si, vneg(r->d));
+}
+
+/* Interaction::offset_p (interaction.h:158-162) */
+static inline v3 offset_p(v3 p, v3 n, v3 d) {
+    float mag = (1.f + vmax(V3(fabsf(p.x), fabsf(p.y), fabsf(p.z)))) * RAY_EPS;
+    mag = mulsign(mag, vdot(n, d));
+    return vfma_s(n, mag, p);
+}
+/* Interaction::spawn_ray (interaction.h:133-136) */
+static inline ray3 spawn_ray(v3 p, v3 n, v3 d) {
+    ray3 r = {offset_p(p, n, d), d, FLT_MAX};
+    return r;
+}
+/* Interaction::spawn_ray_to (interaction.h:138-145) */
+static inline ray3 spawn_ray_to(v3 p, v3 n, v3 target) {
+    v3 o = offset_p(p, n, vsub(target, p));
+    v3 d = vsub(target, o);
+    float dist = vnorm(d);
+    d = vdivs(d, dist);
+    ray3 r = {o, d, dist * (1.f - SHADOW_EPS)};
+    return r;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Textures / BSDF / emitters                                               */
+/* ------------------------------------------------------------------------ */
+static inline int32_t wrap_index(int32_t i, int32_t res, uint32_t mode) {
+    if (mode == 2) return i < 0 ? 0 : (i >= res ? res - 1 : i);   /* clamp */
+    if (mode == 1) {                                               /* mirror */
+        int32_t p = 2 * res;
+        int32_t m = i % p;
+        if (m < 0) m += p;
+        return m < res ? m : p - 1 - m;
+    }
+    int32_t m = i % res;                                           /* repeat */
+    if (m < 0) m += res;
+    return m;
+}
+
+/* bitmap texture taps: [drjit] Texture2f::eval_nonaccel (bilinear / nearest)
+   at uv' = to_uv.transform_affine(si.uv) (src/textures/bitmap.cpp:696-710)  */
+typedef struct {
+    int n;             /* 1 (nearest) or 4 (bilinear) */
+    uint64_t idx[4];   /* float offset of channel 0: 00, 10, 01, 11 */
+    float w0x, w1x, w0y, w1y;
+} tex_taps;
+
+static void bitmap_taps(const mh_texture *tx, float uvx, float uvy, tex_taps *tp) {
+    const float *m = tx->to_uv;
+    float ux = fmaf(m[1], uvy, fmaf(m[0], uvx, m[2]));
+    float uy = fmaf(m[4], uvy, fmaf(m[3], uvx, m[5]));
+    int32_t W = (int32_t)tx->width, H = (int32_t)tx->height;
+    uint32_t C = tx->channels;
+    if (tx->filter == 0) {
+        int32_t ix = wrap_index((int32_t)floorf(ux * (float)W), W, tx->wrap);
+        int32_t iy = wrap_index((int32_t)floorf(uy * (float)H), H, tx->wrap);
+        tp->n = 1;
+        tp->idx[0] = tx->data_offset + ((uint64_t)iy * W + ix) * C;
+        tp->w0x = tp->w0y = 1.f;
+        tp->w1x = tp->w1y = 0.f;
+        return;
+    }
+    float fx = fmaf(ux, (float)W, -0.5f), fy = fmaf(uy, (float)H, -0.5f);
+    float flx = floorf(fx), fly = floorf(fy);
+    int32_t ix = (int32_t)flx, iy = (int32_t)fly;
+    tp->w1x = fx - flx;
+    tp->w1y = fy - fly;
+    tp->w0x = 1.f - tp->w1x;
+    tp->w0y = 1.f - tp->w1y;
+    int32_t x0 = wrap_index(ix, W, tx->wrap), x1 = wrap_index(ix + 1, W, tx->wrap);
+    int32_t y0 = wrap_index(iy, H, tx->wrap), y1 = wrap_index(iy + 1, H, tx->wrap);
+    tp->n = 4;
+    tp->idx[0] = tx->data_offset + ((uint64_t)y0 * W + x0) * C;
+    tp->idx[1] = tx->data_offset + ((uint64_t)y0 * W + x1) * C;
+    tp->idx[2] = tx->data_offset + ((uint64_t)y1 * W + x0) * C;
+    tp->idx[3] = tx->data_offset + ((uint64_t)y1 * W + x1) * C;
+}
+
+static v3 tex_eval(const mh_scene_desc *d, uint32_t tex, float uvx, float uvy) {
+    const mh_texture *tx = &d->textures[tex];
+    if (tx->type == MH_TEX_RGB) return vload(tx->value);
+    tex_taps tp;
+    bitmap_taps(tx, uvx, uvy, &tp);
+    float out[3];
+    for (int c = 0; c < 3; ++c) {
+        uint32_t cc = tx->channels == 3 ? (uint32_t)c : 0u;
+        if (tp.n == 1) {
+            out[c] = d->texels[tp.idx[0] + cc];
+        } else {
+            float f00 = d->texels[tp.idx[0] + cc], f10 = d->texels[tp.idx[1] + cc],
+                  f01 = d->texels[tp.idx[2] + cc], f11 = d->texels[tp.idx[3] + cc];
+            out[c] = fmaf(tp.w0y, fmaf(tp.w0x, f00, tp.w1x * f10),
+                          tp.w1y * fmaf(tp.w0x, f01, tp.w1x * f11));
+        }
+    }
+    return V3(out[0], out[1], out[2]);
+}
+
+/* Gradient sink: d(loss)/d(texture parameter) accumulators (double) */
+typedef struct {
+    uint32_t n_params;
+    const uint32_t *tex;
+    double **acc;
+} grad_sink;
+
+/* adjoint of tex_eval: scatter adj (= d loss / d rho) into the texels */
+static void tex_backward(const mh_scene_desc *d, uint32_t tex, float uvx, float uvy, v3 adj,
+                         grad_sink *g) {
+    for (uint32_t k = 0; k < g->n_params; ++k) {
+        if (g->tex[k] != tex) continue;
+        const mh_texture *tx = &d->textures[tex];
+        double *a = g->acc[k];
+        if (tx->type == MH_TEX_RGB) {
+            a[0] += adj.x; a[1] += adj.y; a[2] += adj.z;
+            continue;
+        }
+        tex_taps tp;
+        bitmap_taps(tx, uvx, uvy, &tp);
+        float av[3] = {adj.x, adj.y, adj.z};
+        float w[4];
+        if (tp.n == 1) {
+            w[0] = 1.f;
+        } else {
+            w[0] = tp.w0y * tp.w0x; w[1] = tp.w0y * tp.w1x;
+            w[2] = tp.w1y * tp.w0x; w[3] = tp.w1y * tp.w1x;
+        }
+        for (int j = 0; j < tp.n; ++j) {
+            uint64_t base = tp.idx[j] - tx->data_offset;
+            if (tx->channels == 3) {
+                for (int c = 0; c < 3; ++c) a[base + c] += (double)av[c] * (double)w[j];
+            } else {
+                a[base] += ((double)av[0] + av[1] + av[2]) * (double)w[j];
+            }
+        }
+    }
+}
+
+static inline uint32_t si_bsdf(const mh_scene_desc *d, const surf_int *si) {
+    return si->valid ? d->shapes[si->shape].bsdf : MH_INVALID;
+}
+static inline uint32_t si_emitter(const mh_scene_desc *d, const surf_int *si) {
+    return si->valid ? d->shapes[si->shape].emitter : d->environment;
+}
+
+/* SmoothDiffuse::eval_pdf (src/bsdfs/diffuse.cpp:160-180) */
+static inline void diffuse_eval_pdf(v3 rho, v3 wi, v3 wo, int active, v3 *val, float *pdf) {
+    float ci = wi.z, co = wo.z;
+    active = active && ci > 0.f && co > 0.f;
+    if (active) {
+        *val = vscale(vscale(rho, INV_PI_F), co);
+        *pdf = INV_PI_F * co;
+    } else {
+        *val = V3(0, 0, 0);
+        *pdf = 0.f;
+    }
+}
+
+/* warp.h:54-90 square_to_uniform_disk_concentric + warp.h:412-428 */
+void oracle_square_to_cosine_hemisphere(const float s[2], float out[3]) {
+    float x = fmaf(2.f, s[0], -1.f), y = fmaf(2.f, s[1], -1.f);
+    int is_zero = x == 0.f && y == 0.f, q13 = fabsf(x) < fabsf(y);
+    float r = q13 ? y : x, rp = q13 ? x : y;
+    float phi = ((0.25f * PI_F) * rp) / r;
+    if (q13) phi = (0.5f * PI_F) - phi;
+    if (is_zero) phi = 0.f;
+    float sn, cs;
+    oracle_sincos(phi, &sn, &cs);
+    float px = r * cs, py = r * sn;
+    float z = safe_sqrtf(1.f - fmaf(py, py, px * px));
+    out[0] = px; out[1] = py; out[2] = z;
+}
+
+typedef struct {
+    v3 wo;
+    float pdf, eta;
+    int sampled_delta, sampled_null;
+} bsdf_sample;
+
+/* SmoothDiffuse::sample (diffuse.cpp:101-125): weight = rho, masked */
+static inline void diffuse_sample(v3 rho, v3 wi, float s2x, float s2y, int active,
+                                  bsdf_sample *bs, v3 *weight) {
+    float s[2] = {s2x, s2y}, w[3];
+    oracle_square_to_cosine_hemisphere(s, w);
+    bs->wo = V3(w[0], w[1], w[2]);
+    bs->pdf = INV_PI_F * w[2];
+    bs->eta = 1.f;
+    bs->sampled_delta = 0;
+    bs->sampled_null = 0;
+    active = active && wi.z > 0.f;
+    *weight = (active && bs->pdf > 0.f) ? rho : V3(0, 0, 0);
+}
+
+void oracle_diffuse_eval_pdf(const float wi[3], const float wo[3], const float rho[3],
+                             float value[3], float *pdf) {
+    v3 v;
+    diffuse_eval_pdf(vload(rho), vload(wi), vload(wo), 1, &v, pdf);
+    value[0] = v.x; value[1] = v.y; value[2] = v.z;
+}
+
+/* mis_weight (path.cpp:300-305, common.py:1817-1825) */
+static inline float mis_weight(float a, float b) {
+    a = a * a;
+    b = b * b;
+    float w = a / (a + b);
+    return isfinitef_(w) ? w : 0.f;
+}
+
+typedef struct {
+    v3 p, n, d;
+    float dist, pdf;
+    int delta;
+} dir_sample;
+
+/* AreaLight::pdf_direction (area.cpp:170-200) + Shape::pdf_direction (shape.cpp:377-388) */
+static float area_pdf_direction(const mh_scene_desc *d, uint32_t em, const dir_sample *ds) {
+    const mh_emitter *e = &d->emitters[em];
+    if (e->type != MH_EMITTER_AREA) return 0.f;
+    float dp = vdot(ds->d, ds->n);
+    int active = dp < 0.f;
+    const mh_shape *sh = &d->shapes[e->shape];
+    float pdf = sh->inv_area, adp = fabsf(dp);
+    pdf *= (adp != 0.f) ? (ds->dist * ds->dist) / adp : 0.f;
+    return active ? pdf : 0.f;
+}
+
+/* AreaLight::sample_direction (area.cpp:118-168) -> Shape::sample_direction
+   (shape.cpp:358-375) -> Rectangle::sample_position (rectangle.cpp:166-180).
+   Returns the (masked) spectral weight radiance / pdf.                      */
+static v3 area_sample_direction(const mh_scene_desc *d, uint32_t em, v3 ref_p, float sx,
+                                float sy, dir_sample *ds) {
+    const mh_emitter *e = &d->emitters[em];
+    const mh_shape *sh = &d->shapes[e->shape];
+    ds->p = xf_point(sh->to_world, V3(sx * 2.f - 1.f, sy * 2.f - 1.f, 0.f));
+    ds->n = vload(sh->frame_n);
+    ds->pdf = sh->inv_area;
+    ds->delta = 0;
+    ds->d = vsub(ds->p, ref_p);
+    float dist2 = vdot(ds->d, ds->d);
+    ds->dist = sqrtf(dist2);
+    ds->d = vdivs(ds->d, ds->dist);
+    float dp = fabsf(vdot(ds->d, ds->n));
+    float x = dist2 / dp;
+    ds->pdf *= isfinitef_(x) ? x : 0.f;
+    int active = vdot(ds->d, ds->n) < 0.f && ds->pdf != 0.f;
+    if (!active) return V3(0, 0, 0);
+    return vdivs(vload(e->radiance), ds->pdf);
+}
+
+/* Scene::sample_emitter_direction, single emitter branch (scene.cpp:335-346),
+   test_visibility = true.  A shadow ray whose contribution is exactly zero
+   (back-facing light sample) is skipped: it cannot change the result.     */
+static v3 sample_emitter_direction(const scene_view *sv, const surf_int *si, float sx, float sy,
+                                   dir_sample *ds, uint64_t *n_shadow) {
+    const mh_scene_desc *d = sv->d;
+    memset(ds, 0, sizeof(*ds));
+    if (d->n_emitters == 0) return V3(0, 0, 0);
+    v3 spec = area_sample_direction(d, 0, si->p, sx, sy, ds);
+    if (ds->pdf != 0.f && (spec.x != 0.f || spec.y != 0.f || spec.z != 0.f)) {
+        ray3 r = spawn_ray_to(si->p, si->n, ds->p);
+        if (n_shadow) (*n_shadow)++;
+        if (trace_shadow(sv, &r)) {
+            spec = V3(0, 0, 0);
+            ds->pdf = 0.f;
+        }
+    }
+    return spec;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Camera: PerspectiveCamera::sample_ray_differential (perspective.cpp:240-281) */
+/* ------------------------------------------------------------------------ */
+static ray3 camera_ray(const mh_sensor *s, float ax, float ay) {
+    v3 near_p = xf4_point_proj(s->sample_to_camera, V3(ax + 0.f, ay + 0.f, 0.f));
+    v3 d = vnormalize(near_p);
+    ray3 r;
+    r.o = V3(s->to_world[3], s->to_world[7], s->to_world[11]);
+    r.d = xf4_vector(s->to_world, d);
+    float inv_z = rcpf_(d.z);
+    float near_t = s->near_clip * inv_z, far_t = s->far_clip * inv_z;
+    r.o = vadd(r.o, vscale(r.d, near_t));
+    r.maxt = far_t - near_t;
+    return r;
+}
+
+int oracle_camera_ray(const mh_scene_desc *desc, const float pos[2], float o[3], float d[3],
+                      float *maxt) {
+    ray3 r = camera_ray(&desc->sensor, pos[0], pos[1]);
+    o[0] = r.o.x; o[1] = r.o.y; o[2] = r.o.z;
+    d[0] = r.d.x; d[1] = r.d.y; d[2] = r.d.z;
+    *maxt = r.maxt;
+    return 0;
+}
+
+/* Emitter-hit MIS record: DirectionSample3f(scene, si, prev_si) (records.h:173-180) */
+static inline float emitter_hit_pdf(const mh_scene_desc *d, uint32_t em, const surf_int *si,
+                                    v3 prev_p) {
+    dir_sample ds;
+    ds.p = si->p;
+    ds.n = si->sh_n;
+    v3 rel = vsub(si->p, prev_p);
+    ds.dist = vnorm(rel);
+    ds.d = si->valid ? vdivs(rel, ds.dist) : vneg(si->wi);
+    ds.pdf = 0.f;
+    ds.delta = 0;
+    /* Scene::pdf_emitter_direction (scene.cpp:355-366): uniform pmf */
+    return area_pdf_direction(d, em, &ds) * (1.f / (float)d->n_emitters);
+}
+
+/* ------------------------------------------------------------------------ */
+/* PathIntegrator::sample, JIT semantics (src/integrators/path.cpp:95-287)  */
+/* counters: [0] closest rays, [1] shadow rays, [2] lane-bounces            */
+/* ------------------------------------------------------------------------ */
+static v3 path_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
+                      int *valid_out, uint64_t *counters) {
+    const mh_scene_desc *d = sv->d;
+    if (in->max_depth == 0) { *valid_out = 0; return V3(0, 0, 0); }
+    v3 throughput = V3(1, 1, 1), result = V3(0, 0, 0);
+    float eta = 1.f;
+    uint32_t depth = 0;
+    int valid_ray = !in->hide_emitters && d->environment != MH_INVALID;
+    v3 prev_p = V3(0, 0, 0);
+    float prev_bsdf_pdf = 1.f;
+    int prev_bsdf_delta = 1;
+    int active = 1;
+    while (active) {
+        pi_rec pi;
+        trace_closest(sv, &ray, &pi);
+        if (counters) { counters[0]++; counters[2]++; }
+        surf_int si;
+        compute_si(d, &ray, &pi, &si);
+
+        /* ---- direct emission (path.cpp:158-174) ---- */
+        uint32_t em = si_emitter(d, &si);
+        if (em != MH_INVALID) {
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(d, em, &si, prev_p);
+            float mis_bsdf = mis_weight(prev_bsdf_pdf, em_pdf);
+            v3 le = V3(0, 0, 0);
+            if (prev_bsdf_pdf > 0.f && si.valid && si.wi.z > 0.f) le = vload(d->emitters[em].radiance);
+            result = vfma(throughput, vscale(le, mis_bsdf), result);
+        }
+
+        int active_next = (depth + 1 < in->max_depth) && si.valid;
+        uint32_t b = si_bsdf(d, &si);
+        int smooth = b != MH_INVALID && d->bsdfs[b].type == MH_BSDF_DIFFUSE;
+        int active_em = active_next && smooth;
+
+        /* ---- emitter sampling (path.cpp:187-208) ---- */
+        float e0 = pcg_float(rng), e1 = pcg_float(rng);
+        dir_sample ds;
+        memset(&ds, 0, sizeof(ds));
+        v3 em_weight = V3(0, 0, 0), wo = V3(0, 0, 0);
+        if (active_em) {
+            em_weight = sample_emitter_direction(sv, &si, e0, e1, &ds,
+                                                 counters ? &counters[1] : NULL);
+            active_em = ds.pdf != 0.f;
+            wo = to_local(&si, ds.d);
+        }
+
+        /* ---- BSDF eval + sample (path.cpp:212-216) ---- */
+        float s1 = pcg_float(rng);
+        float s2x = pcg_float(rng), s2y = pcg_float(rng);
+        (void)s1;
+        v3 bsdf_val = V3(0, 0, 0), bsdf_weight = V3(0, 0, 0);
+        float bsdf_pdf = 0.f;
+        bsdf_sample bs;
+        memset(&bs, 0, sizeof(bs));
+        if (smooth) {
+            v3 rho = tex_eval(d, d->bsdfs[b].reflectance, si.uvx, si.uvy);
+            diffuse_eval_pdf(rho, si.wi, wo, 1, &bsdf_val, &bsdf_pdf);
+            diffuse_sample(rho, si.wi, s2x, s2y, 1, &bs, &bsdf_weight);
+        }
+
+        /* ---- emitter sampling contribution (path.cpp:220-230) ---- */
+        if (active_em) {
+            float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf);
+            result = vfma(throughput, vscale(vmul(bsdf_val, em_weight), mis_em), result);
+        }
+
+        /* ---- BSDF sampling, state update (path.cpp:234-262) ---- */
+        ray = spawn_ray(si.p, si.n, to_world(&si, bs.wo));
+        throughput = vmul(throughput, bsdf_weight);
+        eta *= bs.eta;
+        valid_ray = valid_ray || (si.valid && !bs.sampled_null);
+        prev_p = si.p;
+        prev_bsdf_pdf = bs.pdf;
+        prev_bsdf_delta = bs.sampled_delta;
+
+        /* ---- stopping criterion (path.cpp:266-280) ---- */
+        if (si.valid) depth += 1;
+        float tmax = vmax(throughput);
+        float rr_prob = fminf(tmax * (eta * eta), 0.95f);
+        int rr_active = depth >= in->rr_depth;
+        int rr_continue = pcg_float(rng) < rr_prob;
+        if (rr_active) throughput = vscale(throughput, rcpf_(rr_prob));
+        active = active_next && (!rr_active || rr_continue) && tmax != 0.f;
+    }
+    *valid_out = valid_ray;
+    return valid_ray ? result : V3(0, 0, 0);
+}
+
+/* ------------------------------------------------------------------------ */
+/* PRBIntegrator.sample (src/python/python/ad/integrators/prb.py:59-257)    */
+/* primal: grad == NULL; adjoint: grad != NULL, L_in = primal radiance      */
+/* ------------------------------------------------------------------------ */
+static v3 prb_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
+                     v3 dL, v3 L_in, grad_sink *grad, int *valid_out) {
+    const mh_scene_desc *d = sv->d;
+    const int primal = grad == NULL;
+    uint32_t depth = 0;
+    v3 L = primal ? V3(0, 0, 0) : L_in;
+    v3 beta = V3(1, 1, 1);
+    float eta = 1.f;
+    int active = 1;
+    v3 prev_p = V3(0, 0, 0);
+    float prev_bsdf_pdf = 1.f;
+    int prev_bsdf_delta = 1;
+    while (active) {
+        int active_next = active;
+        pi_rec pi;
+        trace_closest(sv, &ray, &pi);
+        surf_int si;
+        compute_si(d, &ray, &pi, &si);
+        uint32_t b = si_bsdf(d, &si);
+        int smooth = b != MH_INVALID && d->bsdfs[b].type == MH_BSDF_DIFFUSE;
+
+        if (in->hide_emitters && depth == 0 && !si.valid) active_next = 0;
+
+        /* ---- direct emission (prb.py:121-135) ---- */
+        uint32_t em = si_emitter(d, &si);
+        v3 Le = V3(0, 0, 0);
+        if (em != MH_INVALID) {
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(d, em, &si, prev_p);
+            float mis = mis_weight(prev_bsdf_pdf, em_pdf);
+            v3 le = V3(0, 0, 0);
+            if (active_next && si.valid && si.wi.z > 0.f) le = vload(d->emitters[em].radiance);
+            Le = vmul(vscale(beta, mis), le);
+        }
+
+        /* ---- emitter sampling (prb.py:139-163) ---- */
+        active_next = active_next && (depth + 1 < in->max_depth) && si.valid;
+        int active_em = active_next && smooth;
+        float e0 = pcg_float(rng), e1 = pcg_float(rng);
+        dir_sample ds;
+        memset(&ds, 0, sizeof(ds));
+        v3 em_weight = V3(0, 0, 0);
+        if (active_em) {
+            em_weight = sample_emitter_direction(sv, &si, e0, e1, &ds, NULL);
+            active_em = ds.pdf != 0.f;
+        }
+        v3 rho = V3(0, 0, 0);
+        if (smooth) rho = tex_eval(d, d->bsdfs[b].reflectance, si.uvx, si.uvy);
+        v3 wo_em = to_local(&si, ds.d);
+        v3 bsdf_value_em = V3(0, 0, 0);
+        float bsdf_pdf_em = 0.f;
+        diffuse_eval_pdf(rho, si.wi, wo_em, active_em, &bsdf_value_em, &bsdf_pdf_em);
+        float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
+        v3 beta_mis_em = vscale(beta, mis_em);
+        v3 Lr_dir = V3(0, 0, 0);
+        if (active_em) Lr_dir = vmul(vmul(beta_mis_em, bsdf_value_em), em_weight);
+
+        /* ---- detached BSDF sampling (prb.py:167-170) ---- */
+        float s1 = pcg_float(rng);
+        float s2x = pcg_float(rng), s2y = pcg_float(rng);
+        (void)s1;
+        bsdf_sample bs;
+        memset(&bs, 0, sizeof(bs));
+        v3 bsdf_weight = V3(0, 0, 0);
+        if (smooth && active_next) diffuse_sample(rho, si.wi, s2x, s2y, 1, &bs, &bsdf_weight);
+
+        /* ---- state update (prb.py:174-199) ---- */
+        L = primal ? vadd(vadd(L, Le), Lr_dir) : vsub(vsub(L, Le), Lr_dir);
+        ray = spawn_ray(si.p, si.n, to_world(&si, bs.wo));
+        eta *= bs.eta;
+        beta = vmul(beta, bsdf_weight);
+        prev_p = si.p;
+        prev_bsdf_pdf = bs.pdf;
+        prev_bsdf_delta = bs.sampled_delta;
+        float beta_max = vmax(beta);
+        active_next = active_next && beta_max != 0.f;
+        float rr_prob = fminf(beta_max * (eta * eta), 0.95f);
+        int rr_active = depth >= in->rr_depth;
+        if (rr_active) beta = vscale(beta, rcpf_(rr_prob));
+        int rr_continue = pcg_float(rng) < rr_prob;
+        active_next = active_next && (!rr_active || rr_continue);
+
+        /* ---- differential phase (prb.py:203-248) wrt the diffuse reflectance:
+           Lr_dir = ((beta*mis_em) * (rho/pi*cos_em)) * em_weight
+           Lr_ind = L * replace_grad(1, inv_det * (rho/pi*cos_ind))
+           adj(rho) = [(dL*em_weight)*(beta*mis_em)*cos_em]/pi
+                    + [((dL*L)*inv_det)*cos_ind]/pi                         */
+        if (!primal && smooth) {
+            v3 adj = V3(0, 0, 0);
+            if (active_em && si.wi.z > 0.f && wo_em.z > 0.f)
+                adj = vscale(vscale(vmul(vmul(dL, em_weight), beta_mis_em), wo_em.z), INV_PI_F);
+            v3 wo2 = to_local(&si, ray.d);
+            if (active_next && si.wi.z > 0.f && wo2.z > 0.f) {
+                v3 det = vscale(bsdf_weight, bs.pdf);
+                v3 inv = V3(det.x != 0.f ? rcpf_(det.x) : 0.f, det.y != 0.f ? rcpf_(det.y) : 0.f,
+                            det.z != 0.f ? rcpf_(det.z) : 0.f);
+                v3 a2 = vscale(vscale(vmul(vmul(dL, L), inv), wo2.z), INV_PI_F);
+                adj = vadd(adj, a2);
+            }
+            tex_backward(d, d->bsdfs[b].reflectance, si.uvx, si.uvy, adj, grad);
+        }
+
+        if (si.valid) depth += 1;
+        active = active_next;
+    }
+    *valid_out = depth != 0;
+    return primal ? L : dL;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Wavefront driver (integrator.cpp:276-390 / common.py:447-525)            */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    uint32_t W, H, spp, spp_pp, n_passes, log_spp; /* log_spp = 32 if not pow2 */
+} wf_layout;
+
+static void wf_init(const mh_sensor *s, uint32_t spp, wf_layout *L) {
+    L->W = s->width;
+    L->H = s->height;
+    L->spp = spp;
+    uint64_t wf = (uint64_t)L->W * L->H * spp, lim = 0xffffffffull;
+    L->spp_pp = spp;
+    L->n_passes = 1;
+    if (wf > lim) {
+        L->spp_pp = spp / (uint32_t)((wf + lim - 1) / lim);
+        L->n_passes = spp / L->spp_pp;
+    }
+    L->log_spp = 32;
+    for (uint32_t k = 0; k < 32; ++k)
+        if ((1u << k) == L->spp_pp) L->log_spp = k;
+}
+
+/* lane -> pixel (integrator.cpp:323-340) */
+static inline void lane_pixel(const wf_layout *L, uint32_t lane, uint32_t *px, uint32_t *py) {
+    uint32_t pixel = L->log_spp < 32 ? (lane >> L->log_spp) : (lane / L->spp_pp);
+    *py = pixel / L->W;
+    *px = pixel - L->W * *py;
+}
+
+static inline float inv_size(uint32_t n) { return 1.f / (float)n; }
+
+/* one sample of one lane: jitter, camera ray, integrator (render_sample,
+   integrator.cpp:1139-1240 / common.py:447-525).  Returns L and sample_pos. */
+static v3 lane_sample(const scene_view *sv, const mh_integrator *in, const wf_layout *L,
+                      pcg32 *rng, uint32_t lane, float *pos_out, int *valid_out,
+                      uint64_t *counters) {
+    const mh_sensor *s = &sv->d->sensor;
+    uint32_t px, py;
+    lane_pixel(L, lane, &px, &py);
+    float jx = pcg_float(rng), jy = pcg_float(rng);
+    float sx = (float)px + jx, sy = (float)py + jy;
+    float ax = fmaf(sx, inv_size(L->W), -0.f), ay = fmaf(sy, inv_size(L->H), -0.f);
+    ray3 r = camera_ray(s, ax, ay);
+    pos_out[0] = sx;
+    pos_out[1] = sy;
+    if (in->type == MH_INTEGRATOR_PRB)
+        return prb_sample(sv, in, rng, r, V3(0, 0, 0), V3(0, 0, 0), NULL, valid_out);
+    return path_sample(sv, in, rng, r, valid_out, counters);
+}
+
+int oracle_sample_range(const mh_scene_desc *desc, const mh_integrator *integ, uint32_t seed,
+                        uint32_t spp, uint64_t idx_begin, uint64_t idx_end, float *out_L,
+                        float *out_pos, uint32_t *out_valid) {
+    scene_view sv;
+    if (scene_view_init(&sv, desc)) return 1;
+    if (integ->type == MH_INTEGRATOR_VOLPATH) { scene_view_free(&sv); return fail("volpath: not in oracle yet"); }
+    if (spp == 0) spp = desc->sensor.sample_count;
+    wf_layout L;
+    wf_init(&desc->sensor, spp, &L);
+    if (L.n_passes != 1) { scene_view_free(&sv); return fail("oracle_sample_range: multi-pass not supported"); }
+    uint32_t seed_value = desc->sensor.sampler_seed + seed;
+    for (uint64_t i = idx_begin; i < idx_end; ++i) {
+        pcg32 rng;
+        sampler_seed(&rng, seed_value, (uint32_t)i);
+        float pos[2];
+        int valid;
+        v3 l = lane_sample(&sv, integ, &L, &rng, (uint32_t)i, pos, &valid, NULL);
+        uint64_t k = i - idx_begin;
+        out_L[3 * k] = l.x; out_L[3 * k + 1] = l.y; out_L[3 * k + 2] = l.z;
+        if (out_pos) { out_pos[2 * k] = pos[0]; out_pos[2 * k + 1] = pos[1]; }
+        if (out_valid) out_valid[k] = (uint32_t)valid;
+    }
+    scene_view_free(&sv);
+    return 0;
+}
+
+/* ---- threaded film renderer (row bands, deterministic merge) ---- */
+typedef enum { JOB_RENDER = 0, JOB_WEIGHTS = 1, JOB_BACKWARD = 2 } job_kind;
+
+typedef struct {
+    const scene_view *sv;
+    const mh_integrator *in;
+    const wf_layout *L;
+    job_kind kind;
+    uint32_t seed_value, spp_begin, spp_end;
+    uint32_t row_begin, row_end;
+    film_band band;            /* rows [row_begin-2, row_end+2) */
+    /* backward */
+    const float *grad_in, *weights;
+    grad_sink sink;
+    int err;
+} band_job;
+
+static uint32_t splat_margin(const mh_sensor *s) {
+    return s->rfilter == MH_RFILTER_BOX ? 0u : (uint32_t)ceilf(s->rfilter_radius) + 1u;
+}
+
+/* δL_i = sum_px grad_in[px] / W'[px] * w_i(px)   (common.py:936-947) */
+static v3 gather_dL(const mh_sensor *s, int coalesce, const float *grad_in, const float *weights,
+                    float px, float py) {
+    const uint32_t W = s->width, H = s->height;
+    double acc[3] = {0, 0, 0};
+    float out[3] = {0, 0, 0};
+    (void)acc;
+    if (s->rfilter == MH_RFILTER_BOX) {
+        int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py);
+        uint32_t ux = (uint32_t)ix, uy = (uint32_t)iy;
+        if (ux < W && uy < H) {
+            size_t p = (size_t)uy * W + ux;
+            float Wp = weights[p] == 0.f ? 1.f : weights[p];
+            for (int c = 0; c < 3; ++c) out[c] = grad_in[3 * p + c] / Wp;
+        }
+        return V3(out[0], out[1], out[2]);
+    }
+    const float radius = s->rfilter_radius;
+    if (coalesce) {
+        int32_t n = (int32_t)ceilf(radius - 0.5f), count = 2 * n + 1;
+        int32_t pix = (int32_t)floorf(px) - n, piy = (int32_t)floorf(py) - n;
+        uint32_t x = (uint32_t)pix, y = (uint32_t)piy;
+        float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
+        for (int32_t ys = 0; ys < count; ++ys) {
+            float wy = rfilter_eval(s, rely + (float)ys);
+            for (int32_t xs = 0; xs < count; ++xs) {
+                float wx = rfilter_eval(s, relx + (float)xs);
+                uint32_t xx = x + (uint32_t)xs, yy = y + (uint32_t)ys;
+                if (xx < W && yy < H) {
+                    size_t p = (size_t)yy * W + xx;
+                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
+                    float w = wy * wx;
+                    for (int c = 0; c < 3; ++c) out[c] += (grad_in[3 * p + c] / Wp) * w;
+                }
+            }
+        }
+    } else {
+        float pfx = px - 0.5f, pfy = py - 0.5f;
+        int32_t a0x = (int32_t)ceilf(pfx - radius), a0y = (int32_t)ceilf(pfy - radius);
+        int32_t a1x = (int32_t)floorf(pfx + radius), a1y = (int32_t)floorf(pfy + radius);
+        if (a0x < 0) a0x = 0;
+        if (a0y < 0) a0y = 0;
+        if (a1x > (int32_t)W - 1) a1x = (int32_t)W - 1;
+        if (a1y > (int32_t)H - 1) a1y = (int32_t)H - 1;
+        if (!(a0x <= a1x && a0y <= a1y)) return V3(0, 0, 0);
+        uint32_t count = (uint32_t)ceilf(2.f * radius);
+        float relx = (float)a0x - pfx, rely = (float)a0y - pfy;
+        for (uint32_t ys = 0; ys < count; ++ys) {
+            float wy = rfilter_eval(s, rely + (float)ys);
+            for (uint32_t xs = 0; xs < count; ++xs) {
+                float wx = rfilter_eval(s, relx + (float)xs);
+                uint32_t xx = (uint32_t)a0x + xs, yy = (uint32_t)a0y + ys;
+                if ((int32_t)xx <= a1x && (int32_t)yy <= a1y) {
+                    size_t p = (size_t)yy * W + xx;
+                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
+                    float w = wy * wx;
+                    for (int c = 0; c < 3; ++c) out[c] += (grad_in[3 * p + c] / Wp) * w;
+                }
+            }
+        }
+    }
+    return V3(out[0], out[1], out[2]);
+}
+
+static void *band_worker(void *arg) {
+    band_job *j = (band_job *)arg;
+    const wf_layout *L = j->L;
+    const mh_sensor *s = &j->sv->d->sensor;
+    int coalesce = L->spp_pp >= 4;
+    for (uint32_t py = j->row_begin; py < j->row_end; ++py) {
+        for (uint32_t px = 0; px < L->W; ++px) {
+            uint64_t pixel = (uint64_t)py * L->W + px;
+            for (uint32_t sidx = j->spp_begin; sidx < j->spp_end; ++sidx) {
+                uint32_t lane = (uint32_t)(pixel * L->spp_pp + sidx);
+                pcg32 rng;
+                sampler_seed(&rng, j->seed_value, lane);
+                for (uint32_t pass = 0; pass < L->n_passes; ++pass) {
+                    float pos[2];
+                    int valid;
+                    if (j->kind == JOB_RENDER) {
+                        v3 l = lane_sample(j->sv, j->in, L, &rng, lane, pos, &valid, NULL);
+                        float vals[4] = {l.x, l.y, l.z, 1.f};
+                        splat(s, &j->band, pos[0], pos[1], vals, coalesce);
+                    } else if (j->kind == JOB_WEIGHTS) {
+                        float jx = pcg_float(&rng), jy = pcg_float(&rng);
+                        float vals[4] = {0.f, 0.f, 0.f, 1.f};
+                        splat(s, &j->band, (float)px + jx, (float)py + jy, vals, coalesce);
+                    } else {
+                        /* render_backward (common.py:900-983) for one sample */
+                        float jx = pcg_float(&rng), jy = pcg_float(&rng);
+                        float sx = (float)px + jx, sy = (float)py + jy;
+                        ray3 r = camera_ray(s, fmaf(sx, inv_size(L->W), -0.f),
+                                            fmaf(sy, inv_size(L->H), -0.f));
+                        v3 dL = gather_dL(s, coalesce, j->grad_in, j->weights, sx, sy);
+                        pcg32 rng_primal = rng; /* sampler.clone() */
+                        v3 Lp = prb_sample(j->sv, j->in, &rng_primal, r, V3(0, 0, 0),
+                                           V3(0, 0, 0), NULL, &valid);
+                        prb_sample(j->sv, j->in, &rng, r, dL, Lp, &j->sink, &valid);
+                    }
+                }
+            }
+        }
+    }
+    return NULL;
+}
+
+static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kind kind,
+                     uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
+                     int n_threads, float *film, const float *grad_in, const float *weights,
+                     uint32_t n_params, const uint32_t *param_tex, float *const *grads) {
+    scene_view sv;
+    if (scene_view_init(&sv, desc)) return 1;
+    if (in && in->type == MH_INTEGRATOR_VOLPATH) { scene_view_free(&sv); return fail("volpath: not in oracle yet"); }
+    const mh_sensor *s = &desc->sensor;
+    if (spp == 0) spp = s->sample_count;
+    wf_layout L;
+    wf_init(s, spp, &L);
+    if (spp_end == 0 && spp_begin == 0) spp_end = L.spp_pp;
+    if (spp_end > L.spp_pp || spp_begin >= spp_end) { scene_view_free(&sv); return fail("invalid sample slab"); }
+    if (n_threads < 1) n_threads = 1;
+    if ((uint32_t)n_threads > L.H) n_threads = (int)L.H;
+    uint32_t margin = splat_margin(s);
+    band_job *jobs = (band_job *)calloc((size_t)n_threads, sizeof(band_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    int nch = kind == JOB_WEIGHTS ? 1 : 4;
+    (void)nch;
+    for (int t = 0; t < n_threads; ++t) {
+        band_job *j = &jobs[t];
+        j->sv = &sv; j->in = in; j->L = &L; j->kind = kind;
+        j->seed_value = s->sampler_seed + seed;
+        j->spp_begin = spp_begin; j->spp_end = spp_end;
+        j->row_begin = (uint32_t)((uint64_t)L.H * t / n_threads);
+        j->row_end = (uint32_t)((uint64_t)L.H * (t + 1) / n_threads);
+        j->grad_in = grad_in; j->weights = weights;
+        if (kind != JOB_BACKWARD) {
+            int32_t r0 = (int32_t)j->row_begin - (int32_t)margin;
+            if (r0 < 0) r0 = 0;
+            int32_t r1 = (int32_t)j->row_end + (int32_t)margin;
+            if (r1 > (int32_t)L.H) r1 = (int32_t)L.H;
+            j->band.width = L.W; j->band.height = L.H; j->band.row0 = r0;
+            j->band.rows = (uint32_t)(r1 - r0);
+            j->band.data = (float *)calloc((size_t)j->band.rows * L.W * 4, sizeof(float));
+        } else {
+            j->sink.n_params = n_params;
+            j->sink.tex = param_tex;
+            j->sink.acc = (double **)calloc(n_params ? n_params : 1, sizeof(double *));
+            for (uint32_t k = 0; k < n_params; ++k) {
+                const mh_texture *tx = &desc->textures[param_tex[k]];
+                size_t cnt = tx->type == MH_TEX_RGB ? 3 : (size_t)tx->width * tx->height * tx->channels;
+                j->sink.acc[k] = (double *)calloc(cnt, sizeof(double));
+            }
+        }
+        pthread_create(&th[t], NULL, band_worker, j);
+    }
+    for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
+    if (kind == JOB_BACKWARD) {
+        for (uint32_t k = 0; k < n_params; ++k) {
+            const mh_texture *tx = &desc->textures[param_tex[k]];
+            size_t cnt = tx->type == MH_TEX_RGB ? 3 : (size_t)tx->width * tx->height * tx->channels;
+            for (size_t c = 0; c < cnt; ++c) {
+                double sum = 0.0;
+                for (int t = 0; t < n_threads; ++t) sum += jobs[t].sink.acc[k][c];
+                grads[k][c] += (float)sum;
+            }
+        }
+        for (int t = 0; t < n_threads; ++t) {
+            for (uint32_t k = 0; k < n_params; ++k) free(jobs[t].sink.acc[k]);
+            free(jobs[t].sink.acc);
+        }
+    } else {
+        size_t npx = (size_t)L.W * L.H;
+        if (kind == JOB_RENDER) memset(film, 0, npx * 4 * sizeof(float));
+        else memset(film, 0, npx * sizeof(float));
+        for (int t = 0; t < n_threads; ++t) {
+            band_job *j = &jobs[t];
+            for (uint32_t r = 0; r < j->band.rows; ++r) {
+                size_t row = (size_t)(j->band.row0 + (int32_t)r);
+                for (uint32_t x = 0; x < L.W; ++x) {
+                    const float *src = j->band.data + ((size_t)r * L.W + x) * 4;
+                    if (kind == JOB_RENDER) {
+                        float *dst = film + (row * L.W + x) * 4;
+                        for (int c = 0; c < 4; ++c) dst[c] += src[c];
+                    } else {
+                        film[row * L.W + x] += src[3];
+                    }
+                }
+            }
+            free(j->band.data);
+        }
+    }
+    free(jobs);
+    free(th);
+    scene_view_free(&sv);
+    return 0;
+}
+
+int oracle_render(const mh_scene_desc *desc, const mh_integrator *integ, uint32_t seed,
+                  uint32_t spp, uint32_t spp_begin, uint32_t spp_end, int n_threads,
+                  float *film_rgbw) {
+    return run_bands(desc, integ, JOB_RENDER, seed, spp, spp_begin, spp_end, n_threads,
+                     film_rgbw, NULL, NULL, 0, NULL, NULL);
+}
+
+int oracle_prb_weights(const mh_scene_desc *desc, uint32_t seed, uint32_t spp,
+                       uint32_t spp_begin, uint32_t spp_end, int n_threads, float *weights) {
+    mh_integrator dummy = {MH_INTEGRATOR_PRB, 1, 1, 0};
+    return run_bands(desc, &dummy, JOB_WEIGHTS, seed, spp, spp_begin, spp_end, n_threads,
+                     weights, NULL, NULL, 0, NULL, NULL);
+}
+
+int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ,
+                           uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
+                           const float *grad_in, const float *weights, uint32_t n_params,
+                           const uint32_t *param_textures, float *const *grads, int n_threads) {
+    if (integ->type != MH_INTEGRATOR_PRB) return fail("render_backward: requires the 'prb' integrator");
+    const mh_sensor *s = &desc->sensor;
+    float *w_local = NULL;
+    if (!weights) {
+        w_local = (float *)malloc(sizeof(float) * s->width * s->height);
+        if (oracle_prb_weights(desc, seed, spp, 0, 0, n_threads, w_local)) { free(w_local); return 1; }
+        weights = w_local;
+    }
+    int rc = run_bands(desc, integ, JOB_BACKWARD, seed, spp, spp_begin, spp_end, n_threads, NULL,
+                       grad_in, weights, n_params, param_textures, grads);
+    free(w_local);
+    return rc;
+}
