@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s (pixels x spp / s), `path` forward + `prb` gradient,
+cornell_box 512x512 @ 256 spp per GPU (BASELINE.json configs[1] + [2]).
+
+One step = one forward `path` render (max_depth 8) of the rank's 256-spp
+sample slab + the RCCL all-reduce of its RGBW film + develop, then one PRB
+render_backward (max_depth 8) w.r.t. 'white.reflectance.value' with
+grad_in = d mean(image) = 1/(H*W*3): the rank's W-image slab is all-reduced,
+its gradient slab computed and all-reduced.
+
+Weak scaling: rank r renders samples [256 r, 256 r + 256) of every pixel of a
+512x512 @ 256*N spp render (sample-slab sharding); value = N*512*512*256 /
+max-over-ranks step time.  Inputs (the scene) are resident in HBM before the
+timed region; the timed region ends with the image and gradients on the
+device.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...   (the driver)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "mitsuba3-nasa_amd"), os.path.join(ROOT, "tests")]
+
+# MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--res", type=int, default=512)
+    p.add_argument("--spp", type=int, default=256, help="samples per pixel per GPU")
+    p.add_argument("--max-depth", type=int, default=8)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
+    p.add_argument("--fwd-only", action="store_true")
+    return p.parse_args()
+
+
+def cpu_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(n, cap, 64))
+
+
+def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
+    """Oracle (CPU restatement, kind 'port') on the box's host cores, on a
+    bounded sample of the same workload: the same scene/integrators at a
+    reduced spp chosen to fit ~budget_s of CPU work."""
+    import numpy as np
+    import oracle_py as O
+    threads = cpu_threads()
+    H, W = scene.height, scene.width
+    gi = np.full((H, W, 3), 1.0 / (H * W * 3), np.float32)
+    tex = [scene.params[key][1]]
+
+    def run(spp):
+        t0 = time.perf_counter()
+        O.render(scene, fwd, seed=0, spp=spp, threads=threads)
+        if not fwd_only:
+            O.render_backward(scene, prb, 1, spp, gi, tex, [(3,)], threads=threads)
+        return time.perf_counter() - t0
+
+    t1 = run(1)
+    spp = int(max(1, min(spp_gpu, budget_s / max(t1, 1e-3))))
+    spp = 1 << max(0, spp.bit_length() - 1)
+    if spp > 1:
+        t1 = run(spp)
+    rate = H * W * spp / t1 / 1e6
+    return {"value": round(rate, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"cornell_box {W}x{H} @ {spp} spp, path fwd" + ("" if fwd_only else " + prb grad")
+                      + f" (oracle/libmh_oracle.so, {threads} threads, {t1:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    dist_on = world > 1
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    import mitsuba_hip as mi
+    from mitsuba_hip import _abi as A
+    mi.set_variant("hip_ad_rgb")
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"] = args.res
+    d["sensor"]["film"]["height"] = args.res
+    scene = mi.load_dict(d)
+    fwd = mi.load_dict({"type": "path", "max_depth": args.max_depth})
+    prb = mi.load_dict({"type": "prb", "max_depth": args.max_depth})
+    params = mi.traverse(scene)
+    key = "white.reflectance.value"
+    H = W = args.res
+    spp_total = args.spp * world
+    s0, s1 = args.spp * rank, args.spp * (rank + 1)
+    grad_in = torch.full((H, W, 3), 1.0 / (H * W * 3), dtype=torch.float32, device=dev)
+    st_f, st_b = A.Stats(), A.Stats()
+    film = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+
+    def step(i):
+        mi.render_film(scene, fwd, seed=i, spp=spp_total, spp_begin=s0, spp_end=s1, film=film, stats=st_f)
+        if dist_on:
+            dist.all_reduce(film)
+        img = mi.develop(scene, film)
+        if args.fwd_only:
+            return img, None
+        seed_grad = mi.sample_tea_32(i, 1)[0]
+        w = mi.prb_weights(scene, seed_grad, spp_total, s0, s1)
+        if dist_on:
+            dist.all_reduce(w)
+        g = mi.render_backward(scene, params, grad_in, [key], prb, seed=seed_grad, spp=spp_total,
+                               spp_begin=s0, spp_end=s1, weights=w, stats=st_b)[0]
+        if dist_on:
+            dist.all_reduce(g)
+        return img, g
+
+    for i in range(args.warmup):
+        step(1000 + i)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    fwd_ms, bwd_ms = [], []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        img, g = step(i)
+        fwd_ms.append(st_f.ms_kernel)
+        bwd_ms.append(st_b.ms_kernel)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed / args.steps * 1e3
+    samples_step = world * H * W * args.spp
+    value = samples_step / (ms_step / 1e3) / 1e6
+
+    if rank == 0:
+        # ---- roofline of the dominant kernel (HIP events inside the C-ABI) ----
+        avg_f = sum(fwd_ms) / len(fwd_ms)
+        avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
+        n_local = H * W * args.spp
+        if avg_b > avg_f:
+            kname = "k_prb_backward"
+            # algorithmic HBM bytes per sample: dL gather of grad_in + W image
+            # (25 taps x 16 B, L2/MALL resident: counted once per pixel) -> DESIGN.md
+            bytes_launch = H * W * (12 + 4)
+            dur = avg_b
+        else:
+            kname = "k_render<path>"
+            # per sample: L (12 B) + sample position (8 B) written
+            bytes_launch = n_local * 20
+            dur = avg_f
+        achieved = bytes_launch / (dur / 1e3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get(kname)
+            except Exception:
+                traffic = None
+        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "kernel": kname, "kernel_ms": round(dur, 3)}
+        cpu = None
+        if not args.no_cpu:
+            cpu = cpu_baseline(scene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)
+        line = {
+            "metric": "Msamples/s (pixels×spp/s) fwd + PRB grad, cornell_box 512²; 1/2/4/8 GPU",
+            "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (cornell_box scene, seeded PCG32)",
+            "config": {"workload": f"cornell_box {W}x{H} @ {args.spp} spp/GPU: path fwd (max_depth {args.max_depth})"
+                                   + ("" if args.fwd_only else f" + prb backward wrt '{key}'"),
+                       "film": f"{W}x{H}", "spp_per_gpu": args.spp, "spp_total": spp_total,
+                       "parallelism": f"sample-slab x{world} + RCCL all-reduce"},
+            "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
+            "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
+            "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -208,6 +208,7 @@ def _render_op():
         def forward(ctx, scene, params, keys, integrator, seeds, spps, *values):
             ctx.scene, ctx.params, ctx.keys, ctx.integrator = scene, params, keys, integrator
             ctx.seeds, ctx.spps = seeds, spps
+            ctx.value_devices = [v.device for v in values]
             film = render_film(scene, integrator, seeds[0], spps[0])
             return develop(scene, film)
 
@@ -215,6 +216,7 @@ def _render_op():
         def backward(ctx, grad_out):
             grads = render_backward(ctx.scene, ctx.params, grad_out, ctx.keys, ctx.integrator,
                                     ctx.seeds[1], ctx.spps[1])
+            grads = [g.to(d) for g, d in zip(grads, ctx.value_devices)]
             return (None, None, None, None, None, None, *grads)
 
     return _RenderOp
