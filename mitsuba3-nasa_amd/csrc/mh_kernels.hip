@@ -16,737 +16,19 @@
 //   k_prb_weights       W image of render_backward (common.py:936-947).
 //   k_prb_backward      per-lane dL gather + PRB primal + adjoint replay with
 //                       wave/block-reduced gradient atomics (common.py:828-983).
-#include "mh_device.hpp"
-#include "mh_internal.hpp"
+#include "mh_shading.hpp"
 
 namespace mh {
-
-// ===========================================================================
-// BVH traversal (replaces OptiX; payload = scene_optix.inl:619-657)
-// ===========================================================================
-struct Hit {
-    float t, u, v;
-    uint32_t prim, shape;
-};
-
-struct RayT {
-    V3 o, d;
-    float maxt;
-};
-
-// Moeller-Trumbore (render/mesh.h:430-453), e1/e2 precomputed bit-identically
-MH_DEV bool tri_test(const Prim &p, const RayT &r, float &t, float &u, float &v) {
-    V3 v0 = v3(p.a.x, p.a.y, p.a.z), e1 = v3(p.b.x, p.b.y, p.b.z), e2 = v3(p.c.x, p.c.y, p.c.z);
-    V3 pvec = cross(r.d, e2);
-    float inv_det = rcp(dot(e1, pvec));
-    V3 tvec = r.o - v0;
-    u = dot(tvec, pvec) * inv_det;
-    bool active = u >= 0.f && u <= 1.f;
-    V3 qvec = cross(tvec, e1);
-    v = dot(r.d, qvec) * inv_det;
-    active = active && v >= 0.f && u + v <= 1.f;
-    t = dot(e2, qvec) * inv_det;
-    return active && t >= 0.f && t <= r.maxt;
-}
-
-// Rectangle::ray_intersect_preliminary_impl (shapes/rectangle.cpp:446-470)
-MH_DEV bool rect_test(const Prim &p, const RayT &r, float &t, float &u, float &v) {
-    const float m[12] = {p.a.x, p.a.y, p.a.z, p.a.w, p.b.x, p.b.y, p.b.z, p.b.w,
-                         p.c.x, p.c.y, p.c.z, p.c.w};
-    V3 o = xf_point(m, r.o), d = xf_vector(m, r.d);
-    t = -o.z / d.z;
-    V3 local = fma3s(d, t, o);
-    u = local.x;
-    v = local.y;
-    return t >= 0.f && t <= r.maxt && __builtin_fabsf(local.x) <= 1.f &&
-           __builtin_fabsf(local.y) <= 1.f;
-}
-
-MH_DEV bool prim_test(const Prim &p, const RayT &r, float &t, float &u, float &v) {
-    return p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, t, u, v) : tri_test(p, r, t, u, v);
-}
-
-// Slab test for both children; conservative (host pads every box).
-MH_DEV void box2(const Node &n, V3 inv, V3 ood, float tmax, bool &h0, bool &h1, float &t0,
-                 float &t1) {
-    float a0 = __builtin_fmaf(n.lo0.x, inv.x, -ood.x), b0 = __builtin_fmaf(n.hi0.x, inv.x, -ood.x);
-    float a1 = __builtin_fmaf(n.lo0.y, inv.y, -ood.y), b1 = __builtin_fmaf(n.hi0.y, inv.y, -ood.y);
-    float a2 = __builtin_fmaf(n.lo0.z, inv.z, -ood.z), b2 = __builtin_fmaf(n.hi0.z, inv.z, -ood.z);
-    float lo = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.f));
-    float hi = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), tmax));
-    h0 = lo <= hi;
-    t0 = lo;
-    a0 = __builtin_fmaf(n.lo1.x, inv.x, -ood.x); b0 = __builtin_fmaf(n.hi1.x, inv.x, -ood.x);
-    a1 = __builtin_fmaf(n.lo1.y, inv.y, -ood.y); b1 = __builtin_fmaf(n.hi1.y, inv.y, -ood.y);
-    a2 = __builtin_fmaf(n.lo1.z, inv.z, -ood.z); b2 = __builtin_fmaf(n.hi1.z, inv.z, -ood.z);
-    lo = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.f));
-    hi = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), tmax));
-    h1 = lo <= hi;
-    t1 = lo;
-}
-
-// Closest hit (Shadow = false) or any hit (Shadow = true).  `stk` points at
-// this lane's column of the LDS stack (entry k at stk[k * stride]).
-template <bool Shadow>
-MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32_t stride,
-                     const RayT &r, Hit &hit) {
-    V3 inv = v3(rcp(r.d.x), rcp(r.d.y), rcp(r.d.z));
-    V3 ood = r.o * inv;
-    float best = r.maxt;
-    hit.t = __builtin_huge_valf();
-    hit.u = hit.v = 0.f;
-    hit.prim = MH_INVALID;
-    hit.shape = MH_INVALID;
-    if (nodes == nullptr) return false;  // scene without primitives
-    uint32_t sp = 0;
-    uint32_t node = 0;
-    // a root that is itself a leaf is encoded as node 0 with lo0.w = first prim
-    while (true) {
-        const Node n = nodes[node];
-        bool h0, h1;
-        float t0, t1;
-        box2(n, inv, ood, best, h0, h1, t0, t1);
-        uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
-        uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
-        // leaves are tested immediately
-        if (h0 && n0) {
-            for (uint32_t i = 0; i < n0; ++i) {
-                const Prim p = prims[c0 + i];
-                float t, u, v;
-                if (prim_test(p, r, t, u, v) && (Shadow || t < hit.t)) {
-                    if (Shadow) return true;
-                    hit.t = t; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x;
-                    best = t;
-                }
-            }
-            h0 = false;
-        }
-        if (h1 && n1) {
-            for (uint32_t i = 0; i < n1; ++i) {
-                const Prim p = prims[c1 + i];
-                float t, u, v;
-                if (prim_test(p, r, t, u, v) && (Shadow || t < hit.t)) {
-                    if (Shadow) return true;
-                    hit.t = t; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x;
-                    best = t;
-                }
-            }
-            h1 = false;
-        }
-        if (h0 && h1) {
-            uint32_t near_c = c0, far_c = c1;
-            if (t1 < t0) { near_c = c1; far_c = c0; }
-            stk[sp * stride] = far_c;
-            ++sp;
-            node = near_c;
-        } else if (h0) {
-            node = c0;
-        } else if (h1) {
-            node = c1;
-        } else {
-            if (sp == 0) break;
-            --sp;
-            node = stk[sp * stride];
-        }
-    }
-    return hit.shape != MH_INVALID;
-}
-
-// LDS staging of the BVH (nodes then prims) — one copy per workgroup.
-struct LdsBvh {
-    const Node *nodes;
-    const Prim *prims;
-    uint32_t *stack;  // this lane's column
-    uint32_t stride;
-};
-
-MH_DEV LdsBvh stage_bvh(const DScene &S, uint4 *lds) {
-    LdsBvh b;
-    const uint32_t nq = S.lds_bytes_bvh / 16u;
-    if (nq) {
-        const uint4 *src_nodes = reinterpret_cast<const uint4 *>(S.nodes);
-        const uint4 *src_prims = reinterpret_cast<const uint4 *>(S.prims);
-        const uint32_t nq_nodes = S.n_nodes * 4u;
-        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x)
-            lds[i] = i < nq_nodes ? src_nodes[i] : src_prims[i - nq_nodes];
-        __syncthreads();
-        b.nodes = reinterpret_cast<const Node *>(lds);
-        b.prims = reinterpret_cast<const Prim *>(lds + nq_nodes);
-    } else {
-        b.nodes = S.n_prims ? S.nodes : nullptr;
-        b.prims = S.prims;
-    }
-    b.stack = reinterpret_cast<uint32_t *>(lds + nq) + threadIdx.x;
-    b.stride = blockDim.x;
-    return b;
-}
-
-// ===========================================================================
-// SurfaceInteraction (interaction.h:464-484,731-757; rectangle.cpp:497-567;
-// mesh.cpp:1368-1536) — ad-variant branch (p = ray(t) for rectangles)
-// ===========================================================================
-struct SI {
-    bool valid;
-    V3 p, n, s, t_, sn;  // geometric p/n; shading frame (s, t_, sn)
-    float uvx, uvy;
-    V3 wi;               // local
-    uint32_t shape;
-};
-
-// coordinate_system (core/vector.h:116-136)
-MH_DEV void coordinate_system(V3 n, V3 &s, V3 &t) {
-    float sign = n.z >= 0.f ? 1.f : -1.f, a = -rcp(sign + n.z), b = n.x * n.y * a;
-    s = v3(mulsign(n.x * n.x * a, n.z) + 1.f, mulsign(b, n.z), mulsign_neg(n.x, n.z));
-    t = v3(b, __builtin_fmaf(n.y, n.y * a, sign), -n.y);
-}
-
-MH_DEV V3 to_local(const SI &si, V3 v) { return v3(dot(v, si.s), dot(v, si.t_), dot(v, si.sn)); }
-MH_DEV V3 to_world(const SI &si, V3 v) {
-    return fma3s(si.sn, v.z, fma3s(si.t_, v.y, si.s * v.x));
-}
-
-MH_DEV V3 vtx(const DScene &S, uint32_t i) { return ld3(S.positions + 3ull * i); }
-
-MH_DEV void compute_si(const DScene &S, const RayT &r, const Hit &h, SI &si) {
-    si.shape = h.shape;
-    if (h.shape == MH_INVALID) {
-        si.valid = false;
-        si.wi = -r.d;
-        si.p = si.n = si.s = si.t_ = si.sn = v3(0, 0, 0);
-        si.uvx = si.uvy = 0.f;
-        return;
-    }
-    si.valid = true;
-    const DShape &sh = S.shapes[h.shape];
-    V3 dp_du;
-    if (sh.type == MH_SHAPE_RECTANGLE) {
-        si.p = fma3s(r.d, h.t, r.o);
-        si.n = ld3(sh.frame_n);
-        si.sn = si.n;
-        dp_du = ld3(sh.frame_s);
-        si.uvx = __builtin_fmaf(h.u, 0.5f, 0.5f);
-        si.uvy = __builtin_fmaf(h.v, 0.5f, 0.5f);
-    } else {
-        const uint32_t *fi = S.faces + 3ull * (sh.face_offset + h.prim);
-        const uint32_t i0 = sh.vertex_offset + fi[0], i1 = sh.vertex_offset + fi[1],
-                       i2 = sh.vertex_offset + fi[2];
-        V3 p0 = vtx(S, i0), p1 = vtx(S, i1), p2 = vtx(S, i2);
-        float b1 = h.u, b2 = h.v, b0 = 1.f - b1 - b2;
-        si.p = fma3s(p0, b0, fma3s(p1, b1, p2 * b2));
-        si.n = normalize(cross(p1 - p0, p2 - p0));
-        si.uvx = b1;
-        si.uvy = b2;
-        V3 dpdv;
-        coordinate_system(si.n, dp_du, dpdv);
-        if (sh.has_texcoords) {
-            const float *tc = S.texcoords;
-            float u0x = tc[2ull * i0], u0y = tc[2ull * i0 + 1], u1x = tc[2ull * i1],
-                  u1y = tc[2ull * i1 + 1], u2x = tc[2ull * i2], u2y = tc[2ull * i2 + 1];
-            si.uvx = __builtin_fmaf(u2x, b2, __builtin_fmaf(u1x, b1, u0x * b0));
-            si.uvy = __builtin_fmaf(u2y, b2, __builtin_fmaf(u1y, b1, u0y * b0));
-            float d0x = u1x - u0x, d0y = u1y - u0y, d1x = u2x - u0x, d1y = u2y - u0y;
-            float det = __builtin_fmaf(d0x, d1y, -(d0y * d1x)), inv_det = rcp(det);
-            V3 dp0 = p1 - p0, dp1 = p2 - p0;
-            if (det != 0.f)
-                dp_du = v3(__builtin_fmaf(d1y, dp0.x, -(d0y * dp1.x)),
-                           __builtin_fmaf(d1y, dp0.y, -(d0y * dp1.y)),
-                           __builtin_fmaf(d1y, dp0.z, -(d0y * dp1.z))) * inv_det;
-        }
-        if (sh.has_normals) {
-            V3 n0 = ld3(S.normals + 3ull * i0), n1 = ld3(S.normals + 3ull * i1),
-               n2 = ld3(S.normals + 3ull * i2);
-            V3 nn = fma3s(n2, b2, fma3s(n1, b1, n0 * b0));
-            si.sn = nn * rsqrt_(dot(nn, nn));
-        } else {
-            si.sn = si.n;
-        }
-    }
-    // initialize_sh_frame (interaction.h:245-255)
-    si.s = normalize(fma3s(si.sn, -dot(si.sn, dp_du), dp_du));
-    if (dp_du.x == 0.f && dp_du.y == 0.f && dp_du.z == 0.f) {
-        V3 tt;
-        coordinate_system(si.sn, si.s, tt);
-    }
-    si.t_ = cross(si.sn, si.s);
-    si.wi = to_local(si, -r.d);
-}
-
-// Interaction::offset_p / spawn_ray / spawn_ray_to (interaction.h:133-162)
-MH_DEV V3 offset_p(V3 p, V3 n, V3 d) {
-    float mag = (1.f + hmax(v3(__builtin_fabsf(p.x), __builtin_fabsf(p.y), __builtin_fabsf(p.z)))) * kRayEps;
-    mag = mulsign(mag, dot(n, d));
-    return fma3s(n, mag, p);
-}
-MH_DEV RayT spawn_ray(V3 p, V3 n, V3 d) { return RayT{offset_p(p, n, d), d, kFloatMax}; }
-MH_DEV RayT spawn_ray_to(V3 p, V3 n, V3 target) {
-    V3 o = offset_p(p, n, target - p);
-    V3 d = target - o;
-    float dist = norm(d);
-    d = vdiv(d, dist);
-    return RayT{o, d, dist * (1.f - kShadowEps)};
-}
-
-// ===========================================================================
-// Textures, diffuse BSDF, area emitter
-// ===========================================================================
-MH_DEV int32_t wrap_index(int32_t i, int32_t res, uint32_t mode) {
-    if (mode == 2) return i < 0 ? 0 : (i >= res ? res - 1 : i);
-    if (mode == 1) {
-        int32_t p = 2 * res, m = i % p;
-        if (m < 0) m += p;
-        return m < res ? m : p - 1 - m;
-    }
-    int32_t m = i % res;
-    if (m < 0) m += res;
-    return m;
-}
-
-struct Taps {
-    uint32_t n;
-    uint64_t idx[4];
-    float w0x, w1x, w0y, w1y;
-};
-
-// bitmap: [drjit] Texture2f::eval_nonaccel at to_uv * uv (textures/bitmap.cpp:696-710)
-MH_DEV void bitmap_taps(const DTexture &tx, float uvx, float uvy, Taps &tp) {
-    const float *m = tx.to_uv;
-    float ux = __builtin_fmaf(m[1], uvy, __builtin_fmaf(m[0], uvx, m[2]));
-    float uy = __builtin_fmaf(m[4], uvy, __builtin_fmaf(m[3], uvx, m[5]));
-    int32_t W = (int32_t)tx.width, H = (int32_t)tx.height;
-    uint32_t C = tx.channels;
-    if (tx.filter == 0) {
-        int32_t ix = wrap_index((int32_t)floorf(ux * (float)W), W, tx.wrap);
-        int32_t iy = wrap_index((int32_t)floorf(uy * (float)H), H, tx.wrap);
-        tp.n = 1;
-        tp.idx[0] = tx.data_offset + ((uint64_t)iy * W + ix) * C;
-        tp.w0x = tp.w0y = 1.f;
-        tp.w1x = tp.w1y = 0.f;
-        return;
-    }
-    float fx = __builtin_fmaf(ux, (float)W, -0.5f), fy = __builtin_fmaf(uy, (float)H, -0.5f);
-    float flx = floorf(fx), fly = floorf(fy);
-    int32_t ix = (int32_t)flx, iy = (int32_t)fly;
-    tp.w1x = fx - flx;
-    tp.w1y = fy - fly;
-    tp.w0x = 1.f - tp.w1x;
-    tp.w0y = 1.f - tp.w1y;
-    int32_t x0 = wrap_index(ix, W, tx.wrap), x1 = wrap_index(ix + 1, W, tx.wrap);
-    int32_t y0 = wrap_index(iy, H, tx.wrap), y1 = wrap_index(iy + 1, H, tx.wrap);
-    tp.n = 4;
-    tp.idx[0] = tx.data_offset + ((uint64_t)y0 * W + x0) * C;
-    tp.idx[1] = tx.data_offset + ((uint64_t)y0 * W + x1) * C;
-    tp.idx[2] = tx.data_offset + ((uint64_t)y1 * W + x0) * C;
-    tp.idx[3] = tx.data_offset + ((uint64_t)y1 * W + x1) * C;
-}
-
-MH_DEV V3 tex_eval(const DScene &S, uint32_t tex, float uvx, float uvy) {
-    const DTexture &tx = S.textures[tex];
-    if (tx.type == MH_TEX_RGB) return v3(tx.value[0], tx.value[1], tx.value[2]);
-    Taps tp;
-    bitmap_taps(tx, uvx, uvy, tp);
-    float out[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        uint32_t cc = tx.channels == 3 ? (uint32_t)c : 0u;
-        if (tp.n == 1) {
-            out[c] = S.texels[tp.idx[0] + cc];
-        } else {
-            float f00 = S.texels[tp.idx[0] + cc], f10 = S.texels[tp.idx[1] + cc],
-                  f01 = S.texels[tp.idx[2] + cc], f11 = S.texels[tp.idx[3] + cc];
-            out[c] = __builtin_fmaf(tp.w0y, __builtin_fmaf(tp.w0x, f00, tp.w1x * f10),
-                                    tp.w1y * __builtin_fmaf(tp.w0x, f01, tp.w1x * f11));
-        }
-    }
-    return v3(out[0], out[1], out[2]);
-}
-
-// SmoothDiffuse::eval_pdf (bsdfs/diffuse.cpp:160-180)
-MH_DEV void diffuse_eval_pdf(V3 rho, V3 wi, V3 wo, bool active, V3 &val, float &pdf) {
-    active = active && wi.z > 0.f && wo.z > 0.f;
-    val = active ? (rho * kInvPi) * wo.z : v3(0, 0, 0);
-    pdf = active ? kInvPi * wo.z : 0.f;
-}
-
-// warp.h:54-90 + warp.h:412-428
-MH_DEV V3 square_to_cosine_hemisphere(float sx, float sy) {
-    float x = __builtin_fmaf(2.f, sx, -1.f), y = __builtin_fmaf(2.f, sy, -1.f);
-    bool is_zero = x == 0.f && y == 0.f, q13 = __builtin_fabsf(x) < __builtin_fabsf(y);
-    float r = q13 ? y : x, rp = q13 ? x : y;
-    float phi = ((0.25f * kPi) * rp) / r;
-    if (q13) phi = (0.5f * kPi) - phi;
-    if (is_zero) phi = 0.f;
-    float sn, cs;
-    sincos_cephes(phi, sn, cs);
-    float px = r * cs, py = r * sn;
-    float z = __builtin_sqrtf(fmaxf(1.f - __builtin_fmaf(py, py, px * px), 0.f));
-    return v3(px, py, z);
-}
-
-// mis_weight (integrators/path.cpp:300-305)
-MH_DEV float mis_weight(float a, float b) {
-    a = a * a;
-    b = b * b;
-    float w = a / (a + b);
-    return isfinite_(w) ? w : 0.f;
-}
-
-struct DirS {
-    V3 p, n, d;
-    float dist, pdf;
-};
-
-// AreaLight::pdf_direction (emitters/area.cpp:170-200), Shape::pdf_direction (shape.cpp:377-388)
-MH_DEV float area_pdf_direction(const DScene &S, uint32_t em, const DirS &ds) {
-    const DEmitter &e = S.emitters[em];
-    if (e.type != MH_EMITTER_AREA) return 0.f;
-    float dp = dot(ds.d, ds.n);
-    float pdf = S.shapes[e.shape].inv_area, adp = __builtin_fabsf(dp);
-    pdf *= (adp != 0.f) ? (ds.dist * ds.dist) / adp : 0.f;
-    return dp < 0.f ? pdf : 0.f;
-}
-
-// emitter-hit MIS density: DirectionSample3f(scene, si, prev_si) (render/records.h:173-180)
-MH_DEV float emitter_hit_pdf(const DScene &S, uint32_t em, const SI &si, V3 prev_p) {
-    DirS ds;
-    ds.p = si.p;
-    ds.n = si.sn;
-    V3 rel = si.p - prev_p;
-    ds.dist = norm(rel);
-    ds.d = si.valid ? vdiv(rel, ds.dist) : -si.wi;
-    return area_pdf_direction(S, em, ds) * (1.f / (float)S.n_emitters);
-}
-
-// AreaLight::sample_direction -> Shape::sample_direction -> Rectangle::sample_position
-// (area.cpp:118-168, shape.cpp:358-375, rectangle.cpp:166-180)
-MH_DEV V3 area_sample_direction(const DScene &S, uint32_t em, V3 ref_p, float sx, float sy,
-                                DirS &ds) {
-    const DEmitter &e = S.emitters[em];
-    const DShape &sh = S.shapes[e.shape];
-    ds.p = xf_point(sh.to_world, v3(sx * 2.f - 1.f, sy * 2.f - 1.f, 0.f));
-    ds.n = ld3(sh.frame_n);
-    ds.pdf = sh.inv_area;
-    ds.d = ds.p - ref_p;
-    float dist2 = dot(ds.d, ds.d);
-    ds.dist = __builtin_sqrtf(dist2);
-    ds.d = vdiv(ds.d, ds.dist);
-    float dp = __builtin_fabsf(dot(ds.d, ds.n));
-    float x = dist2 / dp;
-    ds.pdf *= isfinite_(x) ? x : 0.f;
-    bool active = dot(ds.d, ds.n) < 0.f && ds.pdf != 0.f;
-    if (!active) return v3(0, 0, 0);
-    return vdiv(v3(e.radiance[0], e.radiance[1], e.radiance[2]), ds.pdf);
-}
-
-// Scene::sample_emitter_direction, single emitter (scene.cpp:335-346), with
-// the shadow test; a sample whose weight is exactly zero traces no shadow ray.
-MH_DEV V3 sample_emitter_direction(const DScene &S, const LdsBvh &B, const SI &si, float sx,
-                                   float sy, DirS &ds, uint32_t &n_shadow) {
-    V3 spec = area_sample_direction(S, 0, si.p, sx, sy, ds);
-    if (ds.pdf != 0.f && nonzero(spec)) {
-        RayT r = spawn_ray_to(si.p, si.n, ds.p);
-        Hit h;
-        ++n_shadow;
-        if (traverse<true>(B.nodes, B.prims, B.stack, B.stride, r, h)) {
-            spec = v3(0, 0, 0);
-            ds.pdf = 0.f;
-        }
-    }
-    return spec;
-}
-
-// PerspectiveCamera::sample_ray_differential (sensors/perspective.cpp:240-281)
-MH_DEV RayT camera_ray(const DScene &S, float ax, float ay) {
-    const float *m = S.sample_to_camera;
-    float r4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        r4[i] = __builtin_fmaf(m[4 * i + 2], 0.f,
-                               __builtin_fmaf(m[4 * i + 1], ay + 0.f, __builtin_fmaf(m[4 * i + 0], ax + 0.f, m[4 * i + 3])));
-    V3 near_p = v3(r4[0] / r4[3], r4[1] / r4[3], r4[2] / r4[3]);
-    V3 d = normalize(near_p);
-    const float *w = S.cam_to_world;
-    RayT r;
-    r.o = v3(w[3], w[7], w[11]);
-    r.d = v3(__builtin_fmaf(w[2], d.z, __builtin_fmaf(w[1], d.y, w[0] * d.x)),
-             __builtin_fmaf(w[6], d.z, __builtin_fmaf(w[5], d.y, w[4] * d.x)),
-             __builtin_fmaf(w[10], d.z, __builtin_fmaf(w[9], d.y, w[8] * d.x)));
-    float inv_z = rcp(d.z);
-    float near_t = S.near_clip * inv_z, far_t = S.far_clip * inv_z;
-    r.o = r.o + r.d * near_t;
-    r.maxt = far_t - near_t;
-    return r;
-}
-
-// ===========================================================================
-// Lane -> pixel mapping (integrator.cpp:323-340), sample-slab aware
-// ===========================================================================
-
-
-MH_DEV void lane_of(const LaneMap &m, uint64_t k, uint32_t &lane, uint32_t &px, uint32_t &py) {
-    uint32_t pl, sl;
-    if (m.log_S < 32) { pl = (uint32_t)(k >> m.log_S); sl = (uint32_t)(k & ((1u << m.log_S) - 1u)); }
-    else { pl = (uint32_t)(k / m.S); sl = (uint32_t)(k - (uint64_t)pl * m.S); }
-    uint32_t pixel = m.pixel_begin + pl;
-    lane = pixel * m.spp_pp + (m.s_begin + sl);
-    // recompute the reference's own mapping from the lane index
-    uint32_t pix2 = m.log_spp < 32 ? (lane >> m.log_spp) : (lane / m.spp_pp);
-    py = pix2 / m.W;
-    px = pix2 - m.W * py;
-}
-
-// wave-aggregated counter increment
-MH_DEV void wave_count(unsigned long long *ctr, uint32_t v) {
-    // sum across the wave with a butterfly, one atomic by the first active lane
-    uint32_t s = v;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if ((threadIdx.x & 63) == (uint32_t)__ffsll(__ballot(1)) - 1u && s)
-        atomicAdd(ctr, (unsigned long long)s);
-}
-
-// ===========================================================================
-// PathIntegrator::sample, JIT semantics (integrators/path.cpp:95-287)
-// ===========================================================================
-MH_DEV V3 path_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                      RayT ray, uint32_t &n_closest, uint32_t &n_shadow) {
-    if (in.max_depth == 0) return v3(0, 0, 0);
-    V3 throughput = v3(1, 1, 1), result = v3(0, 0, 0);
-    float eta = 1.f;
-    uint32_t depth = 0;
-    bool valid_ray = !in.hide_emitters && S.environment != MH_INVALID;
-    V3 prev_p = v3(0, 0, 0);
-    float prev_bsdf_pdf = 1.f;
-    bool prev_bsdf_delta = true;
-    bool active = true;
-    while (active) {
-        Hit h;
-        traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
-        ++n_closest;
-        SI si;
-        compute_si(S, ray, h, si);
-
-        // ---- direct emission (path.cpp:158-174)
-        uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
-        if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
-            float mis_bsdf = mis_weight(prev_bsdf_pdf, em_pdf);
-            V3 le = v3(0, 0, 0);
-            if (prev_bsdf_pdf > 0.f && si.valid && si.wi.z > 0.f)
-                le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
-            result = fma3(throughput, le * mis_bsdf, result);
-        }
-
-        bool active_next = (depth + 1 < in.max_depth) && si.valid;
-        uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
-        bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
-        bool active_em = active_next && smooth;
-
-        // ---- emitter sampling (path.cpp:187-208)
-        float e0 = rng.next_float(), e1 = rng.next_float();
-        DirS ds;
-        ds.pdf = 0.f;
-        ds.d = v3(0, 0, 0);
-        V3 em_weight = v3(0, 0, 0), wo = v3(0, 0, 0);
-        if (active_em) {
-            em_weight = sample_emitter_direction(S, B, si, e0, e1, ds, n_shadow);
-            active_em = ds.pdf != 0.f;
-            wo = to_local(si, ds.d);
-        }
-
-        // ---- BSDF eval + sample (path.cpp:212-216)
-        (void)rng.next_float();
-        float s2x = rng.next_float(), s2y = rng.next_float();
-        V3 bsdf_val = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0), bs_wo = v3(0, 0, 0);
-        float bsdf_pdf = 0.f, bs_pdf = 0.f, bs_eta = 0.f;
-        if (smooth) {
-            V3 rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
-            diffuse_eval_pdf(rho, si.wi, wo, true, bsdf_val, bsdf_pdf);
-            bs_wo = square_to_cosine_hemisphere(s2x, s2y);
-            bs_pdf = kInvPi * bs_wo.z;
-            bs_eta = 1.f;
-            bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
-        }
-
-        // ---- emitter sampling contribution (path.cpp:220-230)
-        if (active_em) {
-            float mis_em = mis_weight(ds.pdf, bsdf_pdf);
-            result = fma3(throughput, (bsdf_val * em_weight) * mis_em, result);
-        }
-
-        // ---- BSDF sampling + state update (path.cpp:234-262)
-        ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
-        throughput = throughput * bsdf_weight;
-        eta *= bs_eta;
-        valid_ray = valid_ray || si.valid;
-        prev_p = si.p;
-        prev_bsdf_pdf = bs_pdf;
-        prev_bsdf_delta = false;
-
-        // ---- stopping criterion (path.cpp:266-280)
-        if (si.valid) depth += 1;
-        float tmax = hmax(throughput);
-        float rr_prob = fminf(tmax * (eta * eta), 0.95f);
-        bool rr_active = depth >= in.rr_depth;
-        bool rr_continue = rng.next_float() < rr_prob;
-        if (rr_active) throughput = throughput * rcp(rr_prob);
-        active = active_next && (!rr_active || rr_continue) && tmax != 0.f;
-    }
-    return valid_ray ? result : v3(0, 0, 0);
-}
-
-// ===========================================================================
-// PRBIntegrator.sample (python/ad/integrators/prb.py:59-257)
-//   primal (Grad == false) or adjoint (Grad == true, L = primal radiance)
-// ===========================================================================
-struct GradCtx {
-    const int32_t *slot_of_tex;   // texture -> param slot or -1
-    float *const *bufs;           // per slot gradient buffer
-    const uint32_t *is_rgb;       // per slot
-    float acc[kMaxRgbParams][3];  // per-lane accumulators for rgb params
-};
-
-MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3 adj, GradCtx &g) {
-    int32_t k = g.slot_of_tex[tex];
-    if (k < 0) return;
-    const DTexture &tx = S.textures[tex];
-    if (g.is_rgb[k]) {
-#pragma unroll
-        for (int kk = 0; kk < kMaxRgbParams; ++kk)
-            if (kk == k) { g.acc[kk][0] += adj.x; g.acc[kk][1] += adj.y; g.acc[kk][2] += adj.z; }
-        return;
-    }
-    Taps tp;
-    bitmap_taps(tx, uvx, uvy, tp);
-    float *buf = g.bufs[k];
-    float w[4];
-    if (tp.n == 1) { w[0] = 1.f; }
-    else { w[0] = tp.w0y * tp.w0x; w[1] = tp.w0y * tp.w1x; w[2] = tp.w1y * tp.w0x; w[3] = tp.w1y * tp.w1x; }
-    for (uint32_t j = 0; j < tp.n; ++j) {
-        uint64_t base = tp.idx[j] - tx.data_offset;
-        if (tx.channels == 3) {
-            atomicAdd(buf + base + 0, adj.x * w[j]);
-            atomicAdd(buf + base + 1, adj.y * w[j]);
-            atomicAdd(buf + base + 2, adj.z * w[j]);
-        } else {
-            atomicAdd(buf + base, (adj.x + adj.y + adj.z) * w[j]);
-        }
-    }
-}
-
-template <bool Grad>
-MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                     RayT ray, V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow) {
-    uint32_t depth = 0;
-    if (!Grad) L = v3(0, 0, 0);
-    V3 beta = v3(1, 1, 1);
-    float eta = 1.f;
-    bool active = true;
-    V3 prev_p = v3(0, 0, 0);
-    float prev_bsdf_pdf = 1.f;
-    bool prev_bsdf_delta = true;
-    while (active) {
-        bool active_next = active;
-        Hit h;
-        traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
-        ++n_closest;
-        SI si;
-        compute_si(S, ray, h, si);
-        uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
-        bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
-        if (in.hide_emitters && depth == 0 && !si.valid) active_next = false;
-
-        // ---- direct emission (prb.py:121-135)
-        uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
-        V3 Le = v3(0, 0, 0);
-        if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
-            float mis = mis_weight(prev_bsdf_pdf, em_pdf);
-            V3 le = v3(0, 0, 0);
-            if (active_next && si.valid && si.wi.z > 0.f)
-                le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
-            Le = (beta * mis) * le;
-        }
-
-        // ---- emitter sampling (prb.py:139-163)
-        active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
-        bool active_em = active_next && smooth;
-        float e0 = rng.next_float(), e1 = rng.next_float();
-        DirS ds;
-        ds.pdf = 0.f;
-        ds.d = v3(0, 0, 0);
-        V3 em_weight = v3(0, 0, 0);
-        if (active_em) {
-            em_weight = sample_emitter_direction(S, B, si, e0, e1, ds, n_shadow);
-            active_em = ds.pdf != 0.f;
-        }
-        V3 rho = v3(0, 0, 0);
-        if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
-        V3 wo_em = to_local(si, ds.d);
-        V3 bsdf_value_em;
-        float bsdf_pdf_em;
-        diffuse_eval_pdf(rho, si.wi, wo_em, active_em, bsdf_value_em, bsdf_pdf_em);
-        float mis_em = mis_weight(ds.pdf, bsdf_pdf_em);
-        V3 beta_mis_em = beta * mis_em;
-        V3 Lr_dir = active_em ? (beta_mis_em * bsdf_value_em) * em_weight : v3(0, 0, 0);
-
-        // ---- detached BSDF sampling (prb.py:167-170)
-        (void)rng.next_float();
-        float s2x = rng.next_float(), s2y = rng.next_float();
-        V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
-        float bs_pdf = 0.f, bs_eta = 0.f;
-        if (smooth && active_next) {
-            bs_wo = square_to_cosine_hemisphere(s2x, s2y);
-            bs_pdf = kInvPi * bs_wo.z;
-            bs_eta = 1.f;
-            bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
-        }
-
-        // ---- state update (prb.py:174-199)
-        L = Grad ? (L - Le) - Lr_dir : (L + Le) + Lr_dir;
-        ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
-        eta *= bs_eta;
-        beta = beta * bsdf_weight;
-        prev_p = si.p;
-        prev_bsdf_pdf = bs_pdf;
-        prev_bsdf_delta = false;
-        float beta_max = hmax(beta);
-        active_next = active_next && beta_max != 0.f;
-        float rr_prob = fminf(beta_max * (eta * eta), 0.95f);
-        bool rr_active = depth >= in.rr_depth;
-        if (rr_active) beta = beta * rcp(rr_prob);
-        bool rr_continue = rng.next_float() < rr_prob;
-        active_next = active_next && (!rr_active || rr_continue);
-
-        // ---- differential phase (prb.py:203-248) wrt the diffuse reflectance
-        if (Grad && smooth) {
-            V3 adj = v3(0, 0, 0);
-            if (active_em && si.wi.z > 0.f && wo_em.z > 0.f)
-                adj = (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi;
-            V3 wo2 = to_local(si, ray.d);
-            if (active_next && si.wi.z > 0.f && wo2.z > 0.f) {
-                V3 det = bsdf_weight * bs_pdf;
-                V3 inv = v3(det.x != 0.f ? rcp(det.x) : 0.f, det.y != 0.f ? rcp(det.y) : 0.f,
-                            det.z != 0.f ? rcp(det.z) : 0.f);
-                adj = adj + (((dL * L) * inv) * wo2.z) * kInvPi;
-            }
-            tex_backward(S, S.bsdf_tex[b], si.uvx, si.uvy, adj, *g);
-        }
-
-        if (si.valid) depth += 1;
-        active = active_next;
-    }
-    return L;
-}
-
 // ===========================================================================
 // Kernels
 // ===========================================================================
-extern "C" __global__ void __launch_bounds__(256)
+template <bool InLds>
+__global__ void __launch_bounds__(256)
 k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__restrict__ t_out,
                 float *__restrict__ u_out, float *__restrict__ v_out, uint32_t *__restrict__ prim_out,
                 uint32_t *__restrict__ shape_out) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh(S, lds);
+    LdsBvh B = stage_bvh<InLds>(S, lds);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         RayT r;
@@ -763,10 +45,11 @@ k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__r
     }
 }
 
-extern "C" __global__ void __launch_bounds__(256)
+template <bool InLds>
+__global__ void __launch_bounds__(256)
 k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *__restrict__ occ) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh(S, lds);
+    LdsBvh B = stage_bvh<InLds>(S, lds);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         RayT r;
@@ -781,12 +64,12 @@ k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *_
 // Forward render of one chunk: lane k in [0, n) -> samples of every pass.
 // out planes (each `plane` floats apart): Lr, Lg, Lb, posx, posy; sample
 // (k, pass) stored at pass * n + k.
-template <bool Prb>
+template <bool Prb, bool InLds>
 __global__ void __launch_bounds__(256)
 k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_t n_passes,
          uint64_t n, uint64_t plane, float *__restrict__ out, unsigned long long *__restrict__ counters) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh(S, lds);
+    LdsBvh B = stage_bvh<InLds>(S, lds);
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t n_closest = 0, n_shadow = 0;
     if (k < n) {
@@ -1083,12 +366,13 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const f
     return v3(o0, o1, o2);
 }
 
+template <bool InLds>
 __global__ void __launch_bounds__(256)
 k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n,
                int coalesce, const float *__restrict__ grad_in, const float *__restrict__ weights,
                GradArgs ga, unsigned long long *__restrict__ counters) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh(S, lds);
+    LdsBvh B = stage_bvh<InLds>(S, lds);
     GradCtx g;
     g.slot_of_tex = ga.slot_of_tex;
     g.bufs = ga.bufs;
@@ -1147,8 +431,14 @@ hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *r
     uint32_t g = grid ? grid : blocks_for(n, bs);
     if (g == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
-    if (shadow) hipLaunchKernelGGL(k_trace_shadow, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
-    else hipLaunchKernelGGL(k_trace_closest, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape);
+    const bool lds = S.lds_bytes_bvh != 0;
+    if (shadow) {
+        if (lds) hipLaunchKernelGGL(k_trace_shadow<true>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
+        else hipLaunchKernelGGL(k_trace_shadow<false>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
+    } else {
+        if (lds) hipLaunchKernelGGL(k_trace_closest<true>, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape);
+        else hipLaunchKernelGGL(k_trace_closest<false>, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape);
+    }
     return hipGetLastError();
 }
 
@@ -1158,12 +448,12 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
     const uint32_t bs = 256;
     size_t sh = lds_bytes(S, bs);
     if (n == 0) return hipSuccess;
-    if (in.type == MH_INTEGRATOR_PRB)
-        hipLaunchKernelGGL(k_render<true>, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
-                           seed_value, n_passes, n, plane, out, counters);
-    else
-        hipLaunchKernelGGL(k_render<false>, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
-                           seed_value, n_passes, n, plane, out, counters);
+    const bool prb = in.type == MH_INTEGRATOR_PRB, lds = S.lds_bytes_bvh != 0;
+    const dim3 g(blocks_for(n, bs)), b(bs);
+    if (prb && lds) hipLaunchKernelGGL((k_render<true, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
+    else if (prb) hipLaunchKernelGGL((k_render<true, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
+    else if (lds) hipLaunchKernelGGL((k_render<false, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
+    else hipLaunchKernelGGL((k_render<false, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
     return hipGetLastError();
 }
 
@@ -1207,8 +497,12 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
     const uint32_t bs = 256;
     if (n == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
-    hipLaunchKernelGGL(k_prb_backward, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
-                       seed_value, n, coalesce, grad_in, weights, ga, counters);
+    if (S.lds_bytes_bvh)
+        hipLaunchKernelGGL(k_prb_backward<true>, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
+                           seed_value, n, coalesce, grad_in, weights, ga, counters);
+    else
+        hipLaunchKernelGGL(k_prb_backward<false>, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
+                           seed_value, n, coalesce, grad_in, weights, ga, counters);
     return hipGetLastError();
 }
 
