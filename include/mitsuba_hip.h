@@ -76,7 +76,9 @@ enum { MH_INTEGRATOR_PATH = 0, MH_INTEGRATOR_VOLPATH = 1, MH_INTEGRATOR_PRB = 2 
 enum {
     MH_FLAG_DEVICE_POINTERS = 1u << 0,  /* in/out buffers are device pointers on the scene's device */
     MH_FLAG_ACCUMULATE      = 1u << 1,  /* mh_render: add into `film_rgbw` instead of overwriting */
-    MH_FLAG_NO_SYNC         = 1u << 2   /* do not synchronise the stream before returning */
+    MH_FLAG_NO_SYNC         = 1u << 2,  /* do not synchronise the stream before returning */
+    MH_FLAG_MEGAKERNEL      = 1u << 3,  /* mh_render: force the per-lane megakernel */
+    MH_FLAG_WAVEFRONT       = 1u << 4   /* mh_render: force the wavefront (trace/shade/shadow) kernels */
 };
 
 /* ----------------------------------------------------------------------- */
@@ -198,6 +200,10 @@ typedef struct mh_stats {
     uint64_t bounces;           /* active lane-bounces */
     double   ms_total;          /* wall time of the call (host clock, ms) */
     double   ms_kernel;         /* device time of the dominant kernel (hipEvents, ms) */
+    double   ms_trace;          /* wavefront: device time of all k_wf_trace launches (ms) */
+    uint64_t n_trace_launches;  /* wavefront: number of k_wf_trace launches */
+    uint32_t mode;              /* 0 megakernel, 1 wavefront */
+    uint32_t pad0;
 } mh_stats;
 
 typedef struct mh_scene mh_scene;   /* opaque; owns all device buffers */

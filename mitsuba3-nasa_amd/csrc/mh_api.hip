@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -84,6 +85,7 @@ struct mh_scene {
     DevBuf nodes, prims, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
+    DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0;
@@ -319,7 +321,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -450,7 +452,19 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
     const uint32_t S_ = L.s_end - L.s_begin;
     const uint64_t per_pixel = (uint64_t)S_ * L.n_passes;
-    const uint64_t max_samples = 1ull << 25;
+    // execution mode: wavefront for `path` (single pass, bounded depth) unless forced
+    bool wavefront = in->type == MH_INTEGRATOR_PATH && L.n_passes == 1 && in->max_depth <= 64;
+    const char *env_mode = getenv("MH_MODE");
+    if (env_mode && !strcmp(env_mode, "mega")) wavefront = false;
+    if (flags & MH_FLAG_MEGAKERNEL) wavefront = false;
+    if ((flags & MH_FLAG_WAVEFRONT) && !wavefront)
+        return set_error(MH_ERR_UNSUPPORTED, "mh_render: the wavefront mode supports the single-pass "
+                                             "'path' integrator with max_depth <= 64");
+    uint64_t max_samples = 1ull << 25;
+    if (wavefront) {
+        const char *ec = getenv("MH_WF_CHUNK");
+        max_samples = ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 21);
+    }
     uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
     const uint64_t plane = (uint64_t)chunk_px * per_pixel;
     MH_HIP(s->work.alloc(plane * 5 * sizeof(float)));
@@ -458,34 +472,70 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                             s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
     const int coalesce = L.spp_pp >= 4;
     const uint32_t seed_value = s->S.sampler_seed + seed;
-    float kernel_ms = 0.f;
+    float kernel_ms = 0.f, trace_ms = 0.f;
     const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
-    while (s->evpool.size() < 2 * n_chunks) {
+    const uint32_t n_bounces = wavefront ? in->max_depth : 0;
+    const size_t ev_per_chunk = 2 + 2 * n_bounces;
+    while (s->evpool.size() < ev_per_chunk * n_chunks) {
         hipEvent_t e;
         MH_HIP(hipEventCreate(&e));
         s->evpool.push_back(e);
+    }
+    const size_t ctr_per_chunk = wavefront ? wf_counter_words(n_bounces) : 0;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+    if (wavefront) {
+        MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(plane)));
+        MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, ctr_per_chunk * n_chunks * 4)));
     }
     size_t chunk = 0;
     for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
         uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
         LaneMap lm = lane_map(L, (uint32_t)p0);
         uint64_t n = (uint64_t)npx * S_;
-        MH_HIP(hipEventRecord(s->evpool[2 * chunk], st));
-        MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
-                             s->counters.as<unsigned long long>(), st));
-        MH_HIP(hipEventRecord(s->evpool[2 * chunk + 1], st));
+        hipEvent_t *ev = &s->evpool[ev_per_chunk * chunk];
+        MH_HIP(hipEventRecord(ev[0], st));
+        if (wavefront) {
+            MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
+                                    s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
+                                    n_bounces, (uint32_t)cus * 8, ev + 2, st));
+        } else {
+            MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
+                                 s->counters.as<unsigned long long>(), st));
+        }
+        MH_HIP(hipEventRecord(ev[1], st));
         MH_HIP(launch_splat(s->S, lm, false, fast_splat, npx, L.n_passes, n, plane,
                             s->work.as<float>(), film, seed_value, coalesce, st));
     }
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(film_rgbw, film, n_px * 16, hipMemcpyDeviceToHost, st));
     unsigned long long ctr[2] = {0, 0};
-    MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> wctr;
+    if (wavefront) {
+        wctr.resize(ctr_per_chunk * n_chunks);
+        MH_HIP(hipMemcpyAsync(wctr.data(), s->wf_ctr.ptr, wctr.size() * 4, hipMemcpyDeviceToHost, st));
+    } else {
+        MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    }
     MH_HIP(hipStreamSynchronize(st));  // the stats counters are read back
     for (size_t c = 0; c < n_chunks; ++c) {
+        hipEvent_t *ev = &s->evpool[ev_per_chunk * c];
         float ms = 0.f;
-        MH_HIP(hipEventElapsedTime(&ms, s->evpool[2 * c], s->evpool[2 * c + 1]));
+        MH_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
         kernel_ms += ms;
+        for (uint32_t b = 0; b < n_bounces; ++b) {
+            MH_HIP(hipEventElapsedTime(&ms, ev[2 + 2 * b], ev[3 + 2 * b]));
+            trace_ms += ms;
+        }
+    }
+    if (wavefront) {
+        const size_t per_bounce = ctr_per_chunk / (n_bounces + 1), nseg = per_bounce / 32;
+        for (size_t c = 0; c < n_chunks; ++c)
+            for (uint32_t b = 0; b < n_bounces; ++b)
+                for (size_t sg = 0; sg < nseg; ++sg) {
+                    ctr[0] += wctr[ctr_per_chunk * c + per_bounce * b + 32 * sg + 0];
+                    ctr[1] += wctr[ctr_per_chunk * c + per_bounce * b + 32 * sg + 1];
+                }
     }
     if (stats) {
         stats->samples = n_px * per_pixel;
@@ -494,6 +544,9 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         stats->bounces = ctr[0];
         stats->ms_total = now_ms() - t_start;
         stats->ms_kernel = kernel_ms;
+        stats->ms_trace = trace_ms;
+        stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces : 0;
+        stats->mode = wavefront ? 1u : 0u;
     }
     return MH_OK;
 }
@@ -518,8 +571,19 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     }
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
     LaneMap lm = lane_map(L, 0);
-    MH_HIP(launch_render(s->S, *in, lm, s->S.sampler_seed + seed, 1, n, n, dst,
-                         s->counters.as<unsigned long long>(), st));
+    if (flags & MH_FLAG_WAVEFRONT) {
+        if (in->type != MH_INTEGRATOR_PATH || in->max_depth > 64)
+            return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: wavefront mode needs 'path', max_depth <= 64");
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+        MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(n)));
+        MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, 4 * (size_t)wf_counter_words(in->max_depth))));
+        MH_HIP(launch_wavefront(s->S, *in, lm, s->S.sampler_seed + seed, n, n, dst, s->wf_ws.ptr, n,
+                                s->wf_ctr.as<uint32_t>(), in->max_depth, (uint32_t)cus * 8, nullptr, st));
+    } else {
+        MH_HIP(launch_render(s->S, *in, lm, s->S.sampler_seed + seed, 1, n, n, dst,
+                             s->counters.as<unsigned long long>(), st));
+    }
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(out, dst, n * 20, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));

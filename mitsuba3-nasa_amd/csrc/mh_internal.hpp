@@ -54,6 +54,12 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, b
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
                         hipStream_t st);
+size_t wf_workspace_bytes(uint64_t cap);
+uint32_t wf_counter_words(uint32_t n_bounces);
+hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                            uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
+                            uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
+                            hipEvent_t *trace_ev, hipStream_t st);
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,

@@ -1,0 +1,346 @@
+// mh_wavefront.hip — wavefront (stream) execution of the `path` integrator:
+// PathIntegrator::sample (integrators/path.cpp:95-287) split at its two ray
+// queries into separate persistent kernels over structure-of-arrays state.
+//
+//   k_wf_raygen   render_sample prologue (integrator.cpp:1139-1176): TEA/PCG32
+//                 seeding, pixel jitter, perspective camera ray -> ray SoA
+//   k_wf_trace    Scene::ray_intersect (scene.cpp:181-190): SoA ray in, SoA
+//                 hit record out (t, u, v, prim, shape) — the OptiX slot
+//   k_wf_shade    one loop iteration of path.cpp:142-281 up to the NEE
+//                 visibility test: emission + MIS, light sample, BSDF sample,
+//                 spawn, Russian roulette; survivors are compacted into the
+//                 next queue, NEE candidates into the shadow queue (wave
+//                 ballot + one atomic per wave)
+//   k_wf_shadow   Scene::ray_test (scene.cpp:201-210) + the deferred
+//                 `result = fma(throughput, bsdf_val*em_weight*mis, result)`
+//
+// Every per-lane operation is the one the megakernel executes (same device
+// functions, same order), so results are bit-identical to k_render and the
+// CPU oracle.  Work is pulled by waves from an atomic head (no host sync
+// between bounces: queue counts stay on the device).
+#include <algorithm>
+
+#include "mh_shading.hpp"
+
+namespace mh {
+
+struct WfState {
+    float *ox, *oy, *oz, *dx, *dy, *dz, *mt;                   // next ray
+    float *ht, *hu, *hv;                                       // hit record
+    uint32_t *hp, *hs;
+    float *bx, *by, *bz, *eta, *ppx, *ppy, *ppz, *ppdf;        // throughput, eta, prev vertex
+    uint32_t *dep;                                             // depth
+    uint64_t *rng;                                             // PCG32 state (inc recomputed)
+    uint32_t *q0, *q1;                                         // path-id queues
+    uint32_t *sid;                                             // shadow queue
+    float *sox, *soy, *soz, *sdx, *sdy, *sdz, *smt, *sax, *say, *saz, *sbx, *sby, *sbz;
+};
+
+// Queues are split into kSeg statically partitioned segments (paths never
+// change segment).  Workgroup b serves segment b % kSeg, so a segment's state
+// stays on one XCD's L2 (blocks b, b+8, ... share an XCD) and every segment
+// has its own counters on a private 128-B line: no single-word atomic hot
+// spot (MI355X_MICROARCH.md "dequeue": one word saturates at ~88 ops/us).
+// Per bounce: kSeg x 32 uint32: [s*32 + 0] queue length, [s*32 + 1] shadow length.
+constexpr uint32_t kSeg = 64;
+constexpr uint32_t kCtrStride = kSeg * 32;
+
+static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+uint32_t wf_counter_words(uint32_t n_bounces) { return kCtrStride * (n_bounces + 1); }
+
+size_t wf_workspace_bytes(uint64_t cap) {
+    // 37 4-byte planes + 1 8-byte plane, each 256-B aligned; capacity padded
+    // to a whole number of segments
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    return 37 * align_up(cap * 4) + align_up(cap * 8);
+}
+
+static WfState carve(void *ws, uint64_t cap) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    uint8_t *p = reinterpret_cast<uint8_t *>(ws);
+    auto f = [&]() { float *r = reinterpret_cast<float *>(p); p += align_up(cap * 4); return r; };
+    auto u = [&]() { uint32_t *r = reinterpret_cast<uint32_t *>(p); p += align_up(cap * 4); return r; };
+    WfState w;
+    w.ox = f(); w.oy = f(); w.oz = f(); w.dx = f(); w.dy = f(); w.dz = f(); w.mt = f();
+    w.ht = f(); w.hu = f(); w.hv = f(); w.hp = u(); w.hs = u();
+    w.bx = f(); w.by = f(); w.bz = f(); w.eta = f(); w.ppx = f(); w.ppy = f(); w.ppz = f(); w.ppdf = f();
+    w.dep = u(); w.q0 = u(); w.q1 = u(); w.sid = u();
+    w.sox = f(); w.soy = f(); w.soz = f(); w.sdx = f(); w.sdy = f(); w.sdz = f(); w.smt = f();
+    w.sax = f(); w.say = f(); w.saz = f(); w.sbx = f(); w.sby = f(); w.sbz = f();
+    w.rng = reinterpret_cast<uint64_t *>(p);
+    return w;
+}
+
+MH_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// segment geometry of a launch: segment of this block, this wave's rank
+// among the segment's waves and the number of waves serving the segment
+struct SegIter {
+    uint32_t seg, wave, nwaves;
+};
+MH_DEV SegIter seg_iter() {
+    SegIter it;
+    it.seg = blockIdx.x % kSeg;
+    const uint32_t wpb = blockDim.x / 64u;
+    it.wave = (blockIdx.x / kSeg) * wpb + threadIdx.x / 64u;
+    it.nwaves = (gridDim.x / kSeg) * wpb;
+    return it;
+}
+__host__ __device__ inline uint32_t seg_len(uint64_t n) { return (uint32_t)((n + kSeg - 1) / kSeg); }
+
+// ballot-compacted append; must be reached by the whole wave
+MH_DEV uint32_t wave_append(uint32_t *count, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    const uint32_t tot = (uint32_t)__popcll(m);
+    uint32_t base = 0;
+    if (lane_id() == 0 && tot) base = atomicAdd(count, tot);
+    base = __builtin_amdgcn_readfirstlane(base);
+    const uint32_t off = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+    return base + off;
+}
+
+// inc of the lane's PCG32 stream (sampler.cpp:115-134), recomputed from TEA
+MH_DEV uint64_t pcg_inc(uint32_t seed_value, uint32_t lane) {
+    uint32_t v0, v1;
+    tea4(seed_value, lane, v0, v1);
+    return ((uint64_t)v1 << 1) | 1u;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_wf_raygen(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane, float *out,
+            WfState w, uint32_t *ctr) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < kSeg) {
+        const uint64_t L = seg_len(n), b = k * L;
+        ctr[k * 32] = b >= n ? 0u : (uint32_t)std::min<uint64_t>(L, n - b);
+    }
+    if (k >= n) return;
+    uint32_t lane, px, py;
+    lane_of(lm, k, lane, px, py);
+    Pcg rng;
+    rng.seed(seed_value, lane);
+    float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+    RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
+                        __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+    w.ox[k] = r.o.x; w.oy[k] = r.o.y; w.oz[k] = r.o.z;
+    w.dx[k] = r.d.x; w.dy[k] = r.d.y; w.dz[k] = r.d.z; w.mt[k] = r.maxt;
+    w.bx[k] = 1.f; w.by[k] = 1.f; w.bz[k] = 1.f; w.eta[k] = 1.f;
+    w.ppx[k] = 0.f; w.ppy[k] = 0.f; w.ppz[k] = 0.f; w.ppdf[k] = 1.f;
+    w.dep[k] = 0u;  // depth 0, prev_bsdf_delta = true on the first bounce
+    w.rng[k] = rng.state;
+    w.q0[k] = (uint32_t)k;  // segment s = ids [s*L, (s+1)*L) stored at [s*L, ...)
+    out[k] = 0.f; out[plane + k] = 0.f; out[2 * plane + k] = 0.f;
+    out[3 * plane + k] = sx; out[4 * plane + k] = sy;
+}
+
+template <bool InLds>
+__global__ void __launch_bounds__(256)
+k_wf_trace(DScene S, WfState w, const uint32_t *__restrict__ queue, uint32_t seg_cap, uint32_t *ctr) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t *q = queue + (size_t)it.seg * seg_cap;
+    for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
+        const uint32_t i = base + lane_id();
+        if (i < n) {
+            const uint32_t pid = q[i];
+            RayT r;
+            r.o = v3(w.ox[pid], w.oy[pid], w.oz[pid]);
+            r.d = v3(w.dx[pid], w.dy[pid], w.dz[pid]);
+            r.maxt = w.mt[pid];
+            Hit h;
+            traverse<false>(B.nodes, B.prims, B.stack, B.stride, r, h);
+            w.ht[pid] = h.t; w.hu[pid] = h.u; w.hv[pid] = h.v; w.hp[pid] = h.prim; w.hs[pid] = h.shape;
+        }
+    }
+}
+
+// one iteration of PathIntegrator::sample for every queued path
+__global__ void __launch_bounds__(256)
+k_wf_shade(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
+           float *out, WfState w, const uint32_t *__restrict__ queue, uint32_t *__restrict__ next_q,
+           uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t *qin = queue + (size_t)it.seg * seg_cap;
+    uint32_t *qout = next_q + (size_t)it.seg * seg_cap;
+    const size_t soff = (size_t)it.seg * seg_cap;  // shadow records of this segment
+    for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
+        const uint32_t i = base + lane_id();
+        bool alive = false, shadow = false;
+        uint32_t pid = 0;
+        RayT ray, sray;
+        V3 tp, a_nee, b_nee, prev_p;
+        float eta = 1.f, prev_pdf = 1.f;
+        uint32_t depth = 0;
+        Pcg rng;
+        if (i < n) {
+            pid = qin[i];
+            ray.o = v3(w.ox[pid], w.oy[pid], w.oz[pid]);
+            ray.d = v3(w.dx[pid], w.dy[pid], w.dz[pid]);
+            ray.maxt = w.mt[pid];
+            Hit h;
+            h.t = w.ht[pid]; h.u = w.hu[pid]; h.v = w.hv[pid]; h.prim = w.hp[pid]; h.shape = w.hs[pid];
+            tp = v3(w.bx[pid], w.by[pid], w.bz[pid]);
+            eta = w.eta[pid];
+            depth = w.dep[pid];
+            const bool prev_delta = depth == 0;  // only the camera vertex is a delta "bsdf" here
+            prev_p = v3(w.ppx[pid], w.ppy[pid], w.ppz[pid]);
+            prev_pdf = w.ppdf[pid];
+            uint32_t lane, px, py;
+            lane_of(lm, pid, lane, px, py);
+            rng.state = w.rng[pid];
+            rng.inc = pcg_inc(seed_value, lane);
+            SI si;
+            compute_si(S, ray, h, si);
+
+            // ---- direct emission (path.cpp:158-174)
+            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+            if (em != MH_INVALID) {
+                float em_pdf = prev_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+                float mis_bsdf = mis_weight(prev_pdf, em_pdf);
+                V3 le = v3(0, 0, 0);
+                if (prev_pdf > 0.f && si.valid && si.wi.z > 0.f)
+                    le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+                V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
+                L = fma3(tp, le * mis_bsdf, L);
+                out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
+            }
+            const bool active_next = (depth + 1 < in.max_depth) && si.valid;
+            const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
+            const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+            const bool active_em = active_next && smooth;
+
+            // ---- emitter sampling (path.cpp:187-208); visibility is deferred
+            float e0 = rng.next_float(), e1 = rng.next_float();
+            DirS ds;
+            ds.pdf = 0.f;
+            ds.d = v3(0, 0, 0);
+            V3 em_weight = v3(0, 0, 0), wo = v3(0, 0, 0);
+            if (active_em) {
+                em_weight = area_sample_direction(S, 0, si.p, e0, e1, ds);
+                if (ds.pdf != 0.f && nonzero(em_weight)) {
+                    shadow = true;
+                    sray = spawn_ray_to(si.p, si.n, ds.p);
+                }
+                wo = to_local(si, ds.d);
+            }
+
+            // ---- BSDF eval + sample (path.cpp:212-216)
+            (void)rng.next_float();
+            float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bsdf_val = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0), bs_wo = v3(0, 0, 0);
+            float bsdf_pdf = 0.f, bs_pdf = 0.f, bs_eta = 0.f;
+            if (smooth) {
+                V3 rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+                diffuse_eval_pdf(rho, si.wi, wo, true, bsdf_val, bsdf_pdf);
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                bs_eta = 1.f;
+                bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+            }
+            if (shadow) {  // (path.cpp:220-230), applied by k_wf_shadow if unoccluded
+                a_nee = tp;
+                b_nee = (bsdf_val * em_weight) * mis_weight(ds.pdf, bsdf_pdf);
+            }
+
+            // ---- BSDF sampling, state update, Russian roulette (path.cpp:234-280)
+            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+            tp = tp * bsdf_weight;
+            eta *= bs_eta;
+            prev_p = si.p;
+            prev_pdf = bs_pdf;
+            if (si.valid) depth += 1;
+            float tmax = hmax(tp);
+            float rr_prob = fminf(tmax * (eta * eta), 0.95f);
+            bool rr_active = depth >= in.rr_depth;
+            bool rr_continue = rng.next_float() < rr_prob;
+            if (rr_active) tp = tp * rcp(rr_prob);
+            alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
+        }
+        // compaction: survivors -> next queue, NEE candidates -> shadow queue
+        const uint32_t slot = wave_append(ctr_next + it.seg * 32, alive);
+        const uint32_t sslot = (uint32_t)soff + wave_append(ctr + it.seg * 32 + 1, shadow);
+        if (alive) {
+            qout[slot] = pid;
+            w.ox[pid] = ray.o.x; w.oy[pid] = ray.o.y; w.oz[pid] = ray.o.z;
+            w.dx[pid] = ray.d.x; w.dy[pid] = ray.d.y; w.dz[pid] = ray.d.z; w.mt[pid] = ray.maxt;
+            w.bx[pid] = tp.x; w.by[pid] = tp.y; w.bz[pid] = tp.z; w.eta[pid] = eta;
+            w.ppx[pid] = prev_p.x; w.ppy[pid] = prev_p.y; w.ppz[pid] = prev_p.z; w.ppdf[pid] = prev_pdf;
+            w.dep[pid] = depth;
+            w.rng[pid] = rng.state;
+        }
+        if (shadow) {
+            w.sid[sslot] = pid;
+            w.sox[sslot] = sray.o.x; w.soy[sslot] = sray.o.y; w.soz[sslot] = sray.o.z;
+            w.sdx[sslot] = sray.d.x; w.sdy[sslot] = sray.d.y; w.sdz[sslot] = sray.d.z; w.smt[sslot] = sray.maxt;
+            w.sax[sslot] = a_nee.x; w.say[sslot] = a_nee.y; w.saz[sslot] = a_nee.z;
+            w.sbx[sslot] = b_nee.x; w.sby[sslot] = b_nee.y; w.sbz[sslot] = b_nee.z;
+        }
+    }
+}
+
+template <bool InLds>
+__global__ void __launch_bounds__(256)
+k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, uint32_t *ctr) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
+        const uint32_t jj = base + lane_id();
+        const uint32_t j = it.seg * seg_cap + jj;
+        if (jj < n) {
+            RayT r;
+            r.o = v3(w.sox[j], w.soy[j], w.soz[j]);
+            r.d = v3(w.sdx[j], w.sdy[j], w.sdz[j]);
+            r.maxt = w.smt[j];
+            Hit h;
+            if (!traverse<true>(B.nodes, B.prims, B.stack, B.stride, r, h)) {
+                const uint32_t pid = w.sid[j];
+                V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
+                L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
+                out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host driver: one chunk of n <= capacity paths, all bounces queued on `st`
+// without host synchronisation.  trace_ev: optional event pairs bracketing
+// every k_wf_trace launch (roofline timing of the dominant kernel).
+// ---------------------------------------------------------------------------
+hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                            uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
+                            uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
+                            hipEvent_t *trace_ev, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    WfState w = carve(ws, cap);
+    hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_wf_raygen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
+                       seed_value, n, plane, out, w, ctr);
+    const size_t sh = lds_bytes(S, 256);
+    const bool lds = S.lds_bytes_bvh != 0;
+    const uint32_t seg_cap = seg_len(n);
+    grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
+    for (uint32_t b = 0; b < n_bounces; ++b) {
+        uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
+        uint32_t *q = (b & 1) ? w.q1 : w.q0, *qn = (b & 1) ? w.q0 : w.q1;
+        if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
+        if (lds) hipLaunchKernelGGL(k_wf_trace<true>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
+        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
+        if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
+        hipLaunchKernelGGL(k_wf_shade, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, plane, out,
+                           w, q, qn, seg_cap, c, cn);
+        if (lds) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(grid), dim3(256), sh, st, S, w, plane, out, seg_cap, c);
+        else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(grid), dim3(256), sh, st, S, w, plane, out, seg_cap, c);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mh

@@ -138,8 +138,9 @@ def traverse(scene: Scene, device=None) -> SceneParameters:
 # ---------------------------------------------------------------------------
 def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                 spp_begin: int = 0, spp_end: int = 0, device=None, film=None, accumulate=False,
-                stats: Optional[A.Stats] = None):
-    """Integrator::render(develop=False): RGBW film (H, W, 4) on the device."""
+                stats: Optional[A.Stats] = None, mode: str = "auto"):
+    """Integrator::render(develop=False): RGBW film (H, W, 4) on the device.
+    mode: 'auto' (wavefront for `path`), 'mega' (per-lane megakernel) or 'wavefront'."""
     torch = _torch()
     dev = _device_index(device)
     integrator = integrator or scene.integrator()
@@ -148,6 +149,7 @@ def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int
     if film is None:
         film = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device=f"cuda:{dev}")
     flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_ACCUMULATE if accumulate else 0)
+    flags |= {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "wavefront": A.FLAG_WAVEFRONT}[mode]
     ic = integrator.c()
     A.check(A.lib().mh_render(h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(film), flags,
                               C.byref(stats) if stats is not None else None))

@@ -48,14 +48,19 @@ def main():
     big = mi.load_dict(d)
     from mitsuba_hip import _abi as A
     st = A.Stats()
-    for i in range(3):
-        torch.cuda.synchronize()
-        t0 = time.time()
-        mi.render_film(big, big.integrator(), seed=0, spp=256, stats=st)
-        torch.cuda.synchronize()
-        dt = time.time() - t0
-        print(f"512^2 x 256spp path: {dt*1e3:.1f} ms  {512*512*256/dt/1e6:.1f} Msamples/s  "
-              f"kernel {st.ms_kernel:.1f} ms rays {st.rays_closest} shadow {st.rays_shadow}", flush=True)
+    for mode in ["mega", "wavefront"]:
+        for i in range(3):
+            torch.cuda.synchronize()
+            t0 = time.time()
+            mi.render_film(big, big.integrator(), seed=0, spp=256, stats=st, mode=mode)
+            torch.cuda.synchronize()
+            dt = time.time() - t0
+            print(f"{mode}: 512^2 x 256spp path: {dt*1e3:.1f} ms  {512*512*256/dt/1e6:.1f} Msamples/s  "
+                  f"kernel {st.ms_kernel:.1f} ms trace {st.ms_trace:.1f} ms ({st.n_trace_launches} launches) "
+                  f"rays {st.rays_closest} shadow {st.rays_shadow}", flush=True)
+    f1 = mi.render_film(big, big.integrator(), seed=0, spp=64, mode="mega").cpu().numpy()
+    f2 = mi.render_film(big, big.integrator(), seed=0, spp=64, mode="wavefront").cpu().numpy()
+    print("mega vs wavefront film max rel", (np.abs(f1 - f2) / np.maximum(1, np.abs(f1))).max(), flush=True)
 
 
 if __name__ == "__main__":

@@ -74,22 +74,23 @@ def test_trace_parity():
     np.testing.assert_array_equal(v[same & hit], rv[same & hit])
 
 
-def _gpu_samples(mi, scene, integrator, seed, spp):
+def _gpu_samples(mi, scene, integrator, seed, spp, flags=0):
     from mitsuba_hip import _abi as A
     n = scene.width * scene.height * spp
     out = np.zeros(5 * n, np.float32)
     ic = integrator.c()
     A.check(A.lib().mh_render_samples(scene.handle(0), C.byref(ic), seed, spp, 0, 0,
-                                      out.ctypes.data_as(C.c_void_p), 0))
+                                      out.ctypes.data_as(C.c_void_p), flags))
     return out[:3 * n].reshape(3, n).T, out[3 * n:].reshape(2, n).T
 
 
-@pytest.mark.parametrize("itype", ["path", "prb"])
-def test_per_sample_parity(itype):
+@pytest.mark.parametrize("itype,mode", [("path", "mega"), ("prb", "mega"), ("path", "wavefront")])
+def test_per_sample_parity(itype, mode):
     mi = _mi()
+    from mitsuba_hip import _abi as A
     scene = cbox(mi, 24, 24, 8)
     integ = mi.load_dict({"type": itype, "max_depth": 8})
-    L, pos = _gpu_samples(mi, scene, integ, 3, 8)
+    L, pos = _gpu_samples(mi, scene, integ, 3, 8, A.FLAG_WAVEFRONT if mode == "wavefront" else 0)
     n = L.shape[0]
     rL, rpos, _ = O.sample_range(scene, integ, 3, 8, 0, n)
     np.testing.assert_array_equal(pos, rpos)
@@ -104,12 +105,12 @@ def _film_close(a, b, frac=0.995):
     return ok.mean() >= frac, ok.mean()
 
 
-@pytest.mark.parametrize("spp", [1, 2, 16, 64])
-def test_render_film_parity(spp):
+@pytest.mark.parametrize("spp,mode", [(1, "auto"), (2, "auto"), (16, "mega"), (16, "wavefront"), (64, "auto")])
+def test_render_film_parity(spp, mode):
     mi = _mi()
     scene = cbox(mi, 40, 32, spp)
     integ = scene.integrator()
-    film = mi.render_film(scene, integ, seed=5, spp=spp).cpu().numpy()
+    film = mi.render_film(scene, integ, seed=5, spp=spp, mode=mode).cpu().numpy()
     ref = O.render(scene, integ, seed=5, spp=spp)
     ok, frac = _film_close(film, ref)
     assert ok, f"film parity {frac}"
