@@ -172,6 +172,134 @@ MH_DEV LdsBvh stage_bvh(const DScene &S, uint4 *lds) {
     return b;
 }
 
+// ---------------------------------------------------------------------------
+// Stream traversal engine for the wavefront kernels: while-while traversal
+// (inner-node phase until every lane holds a leaf, then a grouped leaf phase)
+// with per-lane ray refill from the wave's contiguous item range.  Same hit
+// semantics as traverse<>: closest hit with t in [0, maxt], strict-< update.
+// Stack entries: inner node index, or kLeafBit | first << 3 | count.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kNoNode = 0xffffffffu;  // pop next
+constexpr uint32_t kDone = 0xfffffffeu;    // traversal complete
+
+struct TravLane {
+    V3 o, d, inv, ood;
+    float maxt, best;
+    uint32_t node, leaf, nleaf, sp;
+    Hit hit;
+};
+
+MH_DEV void trav_init(TravLane &t, const RayT &r, bool empty_scene) {
+    t.o = r.o;
+    t.d = r.d;
+    t.maxt = r.maxt;
+    t.inv = v3(rcp(r.d.x), rcp(r.d.y), rcp(r.d.z));
+    t.ood = r.o * t.inv;
+    t.best = r.maxt;
+    t.node = empty_scene ? kDone : 0u;
+    t.nleaf = 0;
+    t.leaf = 0;
+    t.sp = 0;
+    t.hit.t = __builtin_huge_valf();
+    t.hit.u = t.hit.v = 0.f;
+    t.hit.prim = MH_INVALID;
+    t.hit.shape = MH_INVALID;
+}
+
+MH_DEV void trav_take(TravLane &t, uint32_t ref) {
+    if (ref & kLeafBit) {
+        t.leaf = (ref & ~kLeafBit) >> 3;
+        t.nleaf = ref & 7u;
+        t.node = kNoNode;
+    } else {
+        t.node = ref;
+    }
+}
+
+// visit one inner node, or pop the stack (which may yield a pending leaf)
+MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint32_t stride) {
+    if (t.node == kNoNode) {
+        if (t.sp == 0) { t.node = kDone; return; }
+        --t.sp;
+        trav_take(t, stk[t.sp * stride]);
+        return;
+    }
+    const Node n = nodes[t.node];
+    bool h0, h1;
+    float t0, t1;
+    box2(n, t.inv, t.ood, t.best, h0, h1, t0, t1);
+    const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
+    const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
+    const uint32_t r0 = n0 ? (kLeafBit | (c0 << 3) | n0) : c0;
+    const uint32_t r1 = n1 ? (kLeafBit | (c1 << 3) | n1) : c1;
+    if (h0 && h1) {
+        const bool swap = t1 < t0;
+        stk[t.sp * stride] = swap ? r0 : r1;
+        ++t.sp;
+        trav_take(t, swap ? r1 : r0);
+    } else if (h0) {
+        trav_take(t, r0);
+    } else if (h1) {
+        trav_take(t, r1);
+    } else {
+        t.node = kNoNode;
+    }
+}
+
+template <bool Shadow>
+MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
+    RayT r{t.o, t.d, t.maxt};
+    for (uint32_t i = 0; i < t.nleaf; ++i) {
+        const Prim p = prims[t.leaf + i];
+        float tt, u, v;
+        if (prim_test(p, r, tt, u, v) && (Shadow || tt < t.hit.t)) {
+            t.hit.t = tt; t.hit.u = u; t.hit.v = v; t.hit.prim = p.info.y; t.hit.shape = p.info.x;
+            t.best = tt;
+            if (Shadow) { t.node = kDone; t.sp = 0; break; }
+        }
+    }
+    t.nleaf = 0;
+}
+
+// Traces items [r0, r1) of this wave.  load(item) -> RayT, store(item, hit,
+// found).  Must be called by all 64 lanes of the wave (uniform r0, r1).
+template <bool Shadow, class Load, class Store>
+MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, Store store) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool empty = B.nodes == nullptr;
+    uint32_t fetched = r0 + 64u;  // wave-uniform
+    uint32_t item = r0 + lane;
+    bool has = item < r1;
+    TravLane t;
+    if (has) trav_init(t, load(item), empty);
+    while (__any(has)) {
+        // inner phase: every active lane advances until it holds a leaf or is done
+        while (true) {
+            const bool inner = has && t.nleaf == 0 && t.node != kDone;
+            if (!__any(inner)) break;
+            if (inner) trav_inner_step(t, B.nodes, B.stack, B.stride);
+        }
+        // grouped leaf phase
+        if (has && t.nleaf) trav_leaf<Shadow>(t, B.prims);
+        // retire finished lanes and refill them from the wave's range
+        const bool fin = has && t.node == kDone && t.nleaf == 0;
+        if (fin) store(item, t.hit, t.hit.shape != MH_INVALID);
+        const bool need = fin || !has;
+        const unsigned long long m = __ballot(need);
+        const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (need) {
+            const uint32_t cand = fetched + rank;
+            has = cand < r1;
+            if (has) {
+                item = cand;
+                trav_init(t, load(item), empty);
+            }
+        }
+        fetched += (uint32_t)__popcll(m);
+    }
+}
+
 // ===========================================================================
 // SurfaceInteraction (interaction.h:464-484,731-757; rectangle.cpp:497-567;
 // mesh.cpp:1368-1536) — ad-variant branch (p = ray(t) for rectangles)

@@ -135,6 +135,13 @@ k_wf_raygen(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plan
     out[3 * plane + k] = sx; out[4 * plane + k] = sy;
 }
 
+// contiguous share of a segment for this wave (refill traversal)
+MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1) {
+    const uint32_t per = (n + it.nwaves - 1) / it.nwaves;
+    r0 = min(n, it.wave * per);
+    r1 = min(n, r0 + per);
+}
+
 template <bool InLds>
 __global__ void __launch_bounds__(256)
 k_wf_trace(DScene S, WfState w, const uint32_t *__restrict__ queue, uint32_t seg_cap, uint32_t *ctr) {
@@ -143,19 +150,18 @@ k_wf_trace(DScene S, WfState w, const uint32_t *__restrict__ queue, uint32_t seg
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t *q = queue + (size_t)it.seg * seg_cap;
-    for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
-        const uint32_t i = base + lane_id();
-        if (i < n) {
+    uint32_t r0, r1;
+    wave_range(it, n, r0, r1);
+    trace_stream<false>(
+        B, r0, r1,
+        [&](uint32_t i) {
             const uint32_t pid = q[i];
-            RayT r;
-            r.o = v3(w.ox[pid], w.oy[pid], w.oz[pid]);
-            r.d = v3(w.dx[pid], w.dy[pid], w.dz[pid]);
-            r.maxt = w.mt[pid];
-            Hit h;
-            traverse<false>(B.nodes, B.prims, B.stack, B.stride, r, h);
+            return RayT{v3(w.ox[pid], w.oy[pid], w.oz[pid]), v3(w.dx[pid], w.dy[pid], w.dz[pid]), w.mt[pid]};
+        },
+        [&](uint32_t i, const Hit &h, bool) {
+            const uint32_t pid = q[i];
             w.ht[pid] = h.t; w.hu[pid] = h.u; w.hv[pid] = h.v; w.hp[pid] = h.prim; w.hs[pid] = h.shape;
-        }
-    }
+        });
 }
 
 // one iteration of PathIntegrator::sample for every queued path
@@ -290,23 +296,22 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
     LdsBvh B = stage_bvh<InLds>(S, lds);
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
-        const uint32_t jj = base + lane_id();
-        const uint32_t j = it.seg * seg_cap + jj;
-        if (jj < n) {
-            RayT r;
-            r.o = v3(w.sox[j], w.soy[j], w.soz[j]);
-            r.d = v3(w.sdx[j], w.sdy[j], w.sdz[j]);
-            r.maxt = w.smt[j];
-            Hit h;
-            if (!traverse<true>(B.nodes, B.prims, B.stack, B.stride, r, h)) {
-                const uint32_t pid = w.sid[j];
-                V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
-                L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
-                out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
-            }
-        }
-    }
+    const uint32_t base = it.seg * seg_cap;
+    uint32_t r0, r1;
+    wave_range(it, n, r0, r1);
+    trace_stream<true>(
+        B, r0, r1,
+        [&](uint32_t i) {
+            const uint32_t j = base + i;
+            return RayT{v3(w.sox[j], w.soy[j], w.soz[j]), v3(w.sdx[j], w.sdy[j], w.sdz[j]), w.smt[j]};
+        },
+        [&](uint32_t i, const Hit &, bool occluded) {
+            if (occluded) return;
+            const uint32_t j = base + i, pid = w.sid[j];
+            V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
+            L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
+            out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
+        });
 }
 
 // ---------------------------------------------------------------------------
