@@ -463,7 +463,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     uint64_t max_samples = 1ull << 25;
     if (wavefront) {
         const char *ec = getenv("MH_WF_CHUNK");
-        max_samples = ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 23);
+        max_samples = std::min<uint64_t>(wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 23));
     }
     uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
     const uint64_t plane = (uint64_t)chunk_px * per_pixel;

@@ -56,6 +56,7 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, b
                         hipStream_t st);
 size_t wf_workspace_bytes(uint64_t cap);
 uint32_t wf_counter_words(uint32_t n_bounces);
+uint64_t wf_max_chunk();
 hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                             uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,

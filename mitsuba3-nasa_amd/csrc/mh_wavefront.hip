@@ -24,15 +24,20 @@
 
 namespace mh {
 
+// Path state is stored per queue SLOT, not per path id, in two ping-pong
+// buffers: the shade kernel reads slot i of the current queue and writes the
+// survivor's state to its compacted slot of the next queue, so every state
+// access is a coalesced SoA stream.  The path id (for the output sample
+// planes and the PCG32 stream) travels in the low 24 bits of `pd`, the depth
+// in the high 8.
 struct WfState {
-    float *ox, *oy, *oz, *dx, *dy, *dz, *mt;                   // next ray
-    float *ht, *hu, *hv;                                       // hit record
+    uint32_t *pd[2];
+    float *ox[2], *oy[2], *oz[2], *dx[2], *dy[2], *dz[2], *mt[2];
+    float *bx[2], *by[2], *bz[2], *ppx[2], *ppy[2], *ppz[2], *ppdf[2];
+    uint64_t *rng[2];
+    float *ht, *hu, *hv;                                       // hit record of the current bounce
     uint32_t *hp, *hs;
-    float *bx, *by, *bz, *eta, *ppx, *ppy, *ppz, *ppdf;        // throughput, eta, prev vertex
-    uint32_t *dep;                                             // depth
-    uint64_t *rng;                                             // PCG32 state (inc recomputed)
-    uint32_t *q0, *q1;                                         // path-id queues
-    uint32_t *sid;                                             // shadow queue
+    uint32_t *sid;                                             // shadow records
     float *sox, *soy, *soz, *sdx, *sdy, *sdz, *smt, *sax, *say, *saz, *sbx, *sby, *sbz;
 };
 
@@ -44,16 +49,18 @@ struct WfState {
 // Per bounce: kSeg x 32 uint32: [s*32 + 0] queue length, [s*32 + 1] shadow length.
 constexpr uint32_t kSeg = 64;
 constexpr uint32_t kCtrStride = kSeg * 32;
+constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
 
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 uint32_t wf_counter_words(uint32_t n_bounces) { return kCtrStride * (n_bounces + 1); }
+uint64_t wf_max_chunk() { return 1ull << kPidBits; }
 
 size_t wf_workspace_bytes(uint64_t cap) {
-    // 37 4-byte planes + 1 8-byte plane, each 256-B aligned; capacity padded
+    // 49 4-byte planes + 2 8-byte planes, each 256-B aligned; capacity padded
     // to a whole number of segments
     cap = (cap + kSeg - 1) / kSeg * kSeg;
-    return 37 * align_up(cap * 4) + align_up(cap * 8);
+    return 49 * align_up(cap * 4) + 2 * align_up(cap * 8);
 }
 
 static WfState carve(void *ws, uint64_t cap) {
@@ -62,13 +69,19 @@ static WfState carve(void *ws, uint64_t cap) {
     auto f = [&]() { float *r = reinterpret_cast<float *>(p); p += align_up(cap * 4); return r; };
     auto u = [&]() { uint32_t *r = reinterpret_cast<uint32_t *>(p); p += align_up(cap * 4); return r; };
     WfState w;
-    w.ox = f(); w.oy = f(); w.oz = f(); w.dx = f(); w.dy = f(); w.dz = f(); w.mt = f();
+    for (int k = 0; k < 2; ++k) {
+        w.pd[k] = u();
+        w.ox[k] = f(); w.oy[k] = f(); w.oz[k] = f(); w.dx[k] = f(); w.dy[k] = f(); w.dz[k] = f(); w.mt[k] = f();
+        w.bx[k] = f(); w.by[k] = f(); w.bz[k] = f(); w.ppx[k] = f(); w.ppy[k] = f(); w.ppz[k] = f(); w.ppdf[k] = f();
+    }
     w.ht = f(); w.hu = f(); w.hv = f(); w.hp = u(); w.hs = u();
-    w.bx = f(); w.by = f(); w.bz = f(); w.eta = f(); w.ppx = f(); w.ppy = f(); w.ppz = f(); w.ppdf = f();
-    w.dep = u(); w.q0 = u(); w.q1 = u(); w.sid = u();
+    w.sid = u();
     w.sox = f(); w.soy = f(); w.soz = f(); w.sdx = f(); w.sdy = f(); w.sdz = f(); w.smt = f();
     w.sax = f(); w.say = f(); w.saz = f(); w.sbx = f(); w.sby = f(); w.sbz = f();
-    w.rng = reinterpret_cast<uint64_t *>(p);
+    for (int k = 0; k < 2; ++k) {
+        w.rng[k] = reinterpret_cast<uint64_t *>(p);
+        p += align_up(cap * 8);
+    }
     return w;
 }
 
@@ -124,13 +137,13 @@ k_wf_raygen(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plan
     float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
     RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
                         __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
-    w.ox[k] = r.o.x; w.oy[k] = r.o.y; w.oz[k] = r.o.z;
-    w.dx[k] = r.d.x; w.dy[k] = r.d.y; w.dz[k] = r.d.z; w.mt[k] = r.maxt;
-    w.bx[k] = 1.f; w.by[k] = 1.f; w.bz[k] = 1.f; w.eta[k] = 1.f;
-    w.ppx[k] = 0.f; w.ppy[k] = 0.f; w.ppz[k] = 0.f; w.ppdf[k] = 1.f;
-    w.dep[k] = 0u;  // depth 0, prev_bsdf_delta = true on the first bounce
-    w.rng[k] = rng.state;
-    w.q0[k] = (uint32_t)k;  // segment s = ids [s*L, (s+1)*L) stored at [s*L, ...)
+    // slot k of buffer 0 == path k (segment s holds ids [s*L, (s+1)*L))
+    w.pd[0][k] = (uint32_t)k;  // depth 0: prev_bsdf_delta = true on the first bounce
+    w.ox[0][k] = r.o.x; w.oy[0][k] = r.o.y; w.oz[0][k] = r.o.z;
+    w.dx[0][k] = r.d.x; w.dy[0][k] = r.d.y; w.dz[0][k] = r.d.z; w.mt[0][k] = r.maxt;
+    w.bx[0][k] = 1.f; w.by[0][k] = 1.f; w.bz[0][k] = 1.f;
+    w.ppx[0][k] = 0.f; w.ppy[0][k] = 0.f; w.ppz[0][k] = 0.f; w.ppdf[0][k] = 1.f;
+    w.rng[0][k] = rng.state;
     out[k] = 0.f; out[plane + k] = 0.f; out[2 * plane + k] = 0.f;
     out[3 * plane + k] = sx; out[4 * plane + k] = sy;
 }
@@ -144,36 +157,36 @@ MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1
 
 template <bool InLds>
 __global__ void __launch_bounds__(256)
-k_wf_trace(DScene S, WfState w, const uint32_t *__restrict__ queue, uint32_t seg_cap, uint32_t *ctr) {
+k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t *q = queue + (size_t)it.seg * seg_cap;
+    const uint32_t base = it.seg * seg_cap;
+    const float *ox = w.ox[cur], *oy = w.oy[cur], *oz = w.oz[cur], *dx = w.dx[cur], *dy = w.dy[cur],
+                *dz = w.dz[cur], *mt = w.mt[cur];
     uint32_t r0, r1;
     wave_range(it, n, r0, r1);
     trace_stream<false>(
         B, r0, r1,
         [&](uint32_t i) {
-            const uint32_t pid = q[i];
-            return RayT{v3(w.ox[pid], w.oy[pid], w.oz[pid]), v3(w.dx[pid], w.dy[pid], w.dz[pid]), w.mt[pid]};
+            const uint32_t j = base + i;
+            return RayT{v3(ox[j], oy[j], oz[j]), v3(dx[j], dy[j], dz[j]), mt[j]};
         },
         [&](uint32_t i, const Hit &h, bool) {
-            const uint32_t pid = q[i];
-            w.ht[pid] = h.t; w.hu[pid] = h.u; w.hv[pid] = h.v; w.hp[pid] = h.prim; w.hs[pid] = h.shape;
+            const uint32_t j = base + i;
+            w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
         });
 }
 
 // one iteration of PathIntegrator::sample for every queued path
 __global__ void __launch_bounds__(256)
 k_wf_shade(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
-           float *out, WfState w, const uint32_t *__restrict__ queue, uint32_t *__restrict__ next_q,
-           uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+           float *out, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t *qin = queue + (size_t)it.seg * seg_cap;
-    uint32_t *qout = next_q + (size_t)it.seg * seg_cap;
-    const size_t soff = (size_t)it.seg * seg_cap;  // shadow records of this segment
+    const uint32_t sbase = it.seg * seg_cap;  // slots (state, hits, shadow records) of this segment
+    const int nxt = cur ^ 1;
     for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
         const uint32_t i = base + lane_id();
         bool alive = false, shadow = false;
@@ -184,21 +197,25 @@ k_wf_shade(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint6
         uint32_t depth = 0;
         Pcg rng;
         if (i < n) {
-            pid = qin[i];
-            ray.o = v3(w.ox[pid], w.oy[pid], w.oz[pid]);
-            ray.d = v3(w.dx[pid], w.dy[pid], w.dz[pid]);
-            ray.maxt = w.mt[pid];
+            const uint32_t j = sbase + i;
+            const uint32_t pd = w.pd[cur][j];
+            pid = pd & kPidMask;
+            depth = pd >> kPidBits;
+            ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+            ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+            ray.maxt = w.mt[cur][j];
             Hit h;
-            h.t = w.ht[pid]; h.u = w.hu[pid]; h.v = w.hv[pid]; h.prim = w.hp[pid]; h.shape = w.hs[pid];
-            tp = v3(w.bx[pid], w.by[pid], w.bz[pid]);
-            eta = w.eta[pid];
-            depth = w.dep[pid];
-            const bool prev_delta = depth == 0;  // only the camera vertex is a delta "bsdf" here
-            prev_p = v3(w.ppx[pid], w.ppy[pid], w.ppz[pid]);
-            prev_pdf = w.ppdf[pid];
+            h.t = w.ht[j]; h.u = w.hu[j]; h.v = w.hv[j]; h.prim = w.hp[j]; h.shape = w.hs[j];
+            tp = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+            // diffuse / null BSDFs only: eta stays 1 and only the camera vertex
+            // (depth 0) has a delta "previous bsdf"
+            eta = 1.f;
+            const bool prev_delta = depth == 0;
+            prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+            prev_pdf = w.ppdf[cur][j];
             uint32_t lane, px, py;
             lane_of(lm, pid, lane, px, py);
-            rng.state = w.rng[pid];
+            rng.state = w.rng[cur][j];
             rng.inc = pcg_inc(seed_value, lane);
             SI si;
             compute_si(S, ray, h, si);
@@ -268,16 +285,17 @@ k_wf_shade(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint6
             alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
         }
         // compaction: survivors -> next queue, NEE candidates -> shadow queue
-        const uint32_t slot = wave_append(ctr_next + it.seg * 32, alive);
-        const uint32_t sslot = (uint32_t)soff + wave_append(ctr + it.seg * 32 + 1, shadow);
+        const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        const uint32_t sslot = sbase + wave_append(ctr + it.seg * 32 + 1, shadow);
         if (alive) {
-            qout[slot] = pid;
-            w.ox[pid] = ray.o.x; w.oy[pid] = ray.o.y; w.oz[pid] = ray.o.z;
-            w.dx[pid] = ray.d.x; w.dy[pid] = ray.d.y; w.dz[pid] = ray.d.z; w.mt[pid] = ray.maxt;
-            w.bx[pid] = tp.x; w.by[pid] = tp.y; w.bz[pid] = tp.z; w.eta[pid] = eta;
-            w.ppx[pid] = prev_p.x; w.ppy[pid] = prev_p.y; w.ppz[pid] = prev_p.z; w.ppdf[pid] = prev_pdf;
-            w.dep[pid] = depth;
-            w.rng[pid] = rng.state;
+            w.pd[nxt][slot] = pid | (depth << kPidBits);
+            w.ox[nxt][slot] = ray.o.x; w.oy[nxt][slot] = ray.o.y; w.oz[nxt][slot] = ray.o.z;
+            w.dx[nxt][slot] = ray.d.x; w.dy[nxt][slot] = ray.d.y; w.dz[nxt][slot] = ray.d.z;
+            w.mt[nxt][slot] = ray.maxt;
+            w.bx[nxt][slot] = tp.x; w.by[nxt][slot] = tp.y; w.bz[nxt][slot] = tp.z;
+            w.ppx[nxt][slot] = prev_p.x; w.ppy[nxt][slot] = prev_p.y; w.ppz[nxt][slot] = prev_p.z;
+            w.ppdf[nxt][slot] = prev_pdf;
+            w.rng[nxt][slot] = rng.state;
         }
         if (shadow) {
             w.sid[sslot] = pid;
@@ -324,6 +342,7 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
                             hipEvent_t *trace_ev, hipStream_t st) {
     if (n == 0) return hipSuccess;
+    if (n > (1ull << kPidBits) || n_bounces > 255) return hipErrorInvalidValue;
     WfState w = carve(ws, cap);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
@@ -335,13 +354,13 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
-        uint32_t *q = (b & 1) ? w.q1 : w.q0, *qn = (b & 1) ? w.q0 : w.q1;
+        const int cur = (int)(b & 1);
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
-        if (lds) hipLaunchKernelGGL(k_wf_trace<true>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
-        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
+        if (lds) hipLaunchKernelGGL(k_wf_trace<true>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
+        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
         hipLaunchKernelGGL(k_wf_shade, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, plane, out,
-                           w, q, qn, seg_cap, c, cn);
+                           w, cur, seg_cap, c, cn);
         if (lds) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(grid), dim3(256), sh, st, S, w, plane, out, seg_cap, c);
         else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(grid), dim3(256), sh, st, S, w, plane, out, seg_cap, c);
     }
