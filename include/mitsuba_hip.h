@@ -78,7 +78,8 @@ enum {
     MH_FLAG_ACCUMULATE      = 1u << 1,  /* mh_render: add into `film_rgbw` instead of overwriting */
     MH_FLAG_NO_SYNC         = 1u << 2,  /* do not synchronise the stream before returning */
     MH_FLAG_MEGAKERNEL      = 1u << 3,  /* mh_render: force the per-lane megakernel */
-    MH_FLAG_WAVEFRONT       = 1u << 4   /* mh_render: force the wavefront (trace/shade/shadow) kernels */
+    MH_FLAG_WAVEFRONT       = 1u << 4,  /* mh_render: force the wavefront (trace/shade/shadow) kernels */
+    MH_FLAG_PRB_REPLAY      = 1u << 5   /* mh_render_backward: primal + adjoint replay even for rgb params */
 };
 
 /* ----------------------------------------------------------------------- */

@@ -749,8 +749,12 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     LaneMap lm = lane_map(L, 0);
     const uint64_t n = n_px * (L.s_end - L.s_begin);
     MH_HIP(hipEventRecord(s->ev0, st));
+    // fused single traversal when every requested parameter is an rgb constant,
+    // unless the replay is forced (MH_FLAG_MEGAKERNEL / MH_PRB_REPLAY=1)
+    const char *env_replay = getenv("MH_PRB_REPLAY");
+    const bool fused = n_bmp == 0 && !(flags & MH_FLAG_PRB_REPLAY) && !(env_replay && !strcmp(env_replay, "1"));
     MH_HIP(launch_prb_backward(s->S, *in, lm, s->S.sampler_seed + seed, n, L.spp_pp >= 4, g_in, w, ga,
-                               s->counters.as<unsigned long long>(), st));
+                               fused, s->counters.as<unsigned long long>(), st));
     MH_HIP(hipEventRecord(s->ev1, st));
     // accumulate into the caller's gradient buffers
     std::vector<float> host_tmp;

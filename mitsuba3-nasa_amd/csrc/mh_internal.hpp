@@ -65,6 +65,6 @@ hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStrea
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
                                const float *grad_in, const float *weights, const GradArgs &ga,
-                               unsigned long long *counters, hipStream_t st);
+                               bool fused, unsigned long long *counters, hipStream_t st);
 
 }  // namespace mh

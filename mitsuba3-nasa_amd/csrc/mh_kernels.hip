@@ -366,7 +366,7 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const f
     return v3(o0, o1, o2);
 }
 
-template <bool InLds>
+template <bool InLds, bool Fused>
 __global__ void __launch_bounds__(256)
 k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n,
                int coalesce, const float *__restrict__ grad_in, const float *__restrict__ weights,
@@ -390,10 +390,14 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
         RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
                             __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
         V3 dL = gather_dL(S, coalesce, grad_in, weights, sx, sy);
-        Pcg rng_primal = rng;  // sampler.clone()
-        V3 Lp = prb_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr,
-                                  n_closest, n_shadow);
-        prb_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
+        if (Fused) {
+            prb_fused(S, B, in, rng, r, dL, g, n_closest, n_shadow);
+        } else {
+            Pcg rng_primal = rng;  // sampler.clone()
+            V3 Lp = prb_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr,
+                                      n_closest, n_shadow);
+            prb_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
+        }
     }
     // block-reduce the rgb accumulators: wave butterfly, then one atomic per wave
     for (uint32_t p = 0; p < ga.n_rgb; ++p) {
@@ -493,16 +497,19 @@ hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStrea
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
                                const float *grad_in, const float *weights, const GradArgs &ga,
-                               unsigned long long *counters, hipStream_t st) {
+                               bool fused, unsigned long long *counters, hipStream_t st) {
     const uint32_t bs = 256;
     if (n == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
-    if (S.lds_bytes_bvh)
-        hipLaunchKernelGGL(k_prb_backward<true>, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
-                           seed_value, n, coalesce, grad_in, weights, ga, counters);
+    const dim3 g(blocks_for(n, bs)), b(bs);
+    if (S.lds_bytes_bvh && fused)
+        hipLaunchKernelGGL((k_prb_backward<true, true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);
+    else if (S.lds_bytes_bvh)
+        hipLaunchKernelGGL((k_prb_backward<true, false>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);
+    else if (fused)
+        hipLaunchKernelGGL((k_prb_backward<false, true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);
     else
-        hipLaunchKernelGGL(k_prb_backward<false>, dim3(blocks_for(n, bs)), dim3(bs), sh, st, S, in, lm,
-                           seed_value, n, coalesce, grad_in, weights, ga, counters);
+        hipLaunchKernelGGL((k_prb_backward<false, false>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);
     return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ FLAG_ACCUMULATE = 1 << 1
 FLAG_NO_SYNC = 1 << 2
 FLAG_MEGAKERNEL = 1 << 3
 FLAG_WAVEFRONT = 1 << 4
+FLAG_PRB_REPLAY = 1 << 5
 
 u32, u64, f32, f64 = C.c_uint32, C.c_uint64, C.c_float, C.c_double
 PF = C.POINTER(C.c_float)

@@ -177,7 +177,7 @@ def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, devic
 def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],
                     integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                     spp_begin: int = 0, spp_end: int = 0, weights=None,
-                    stats: Optional[A.Stats] = None):
+                    stats: Optional[A.Stats] = None, replay: bool = False):
     """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
     Returns a list of gradient tensors (one per key, same shape as the param)."""
     torch = _torch()
@@ -195,7 +195,8 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     A.check(A.lib().mh_render_backward(
         h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(grad_in),
         _ptr(weights) if weights is not None else None, len(keys), tex, ptrs,
-        A.FLAG_DEVICE_POINTERS, C.byref(stats) if stats is not None else None))
+        A.FLAG_DEVICE_POINTERS | (A.FLAG_PRB_REPLAY if replay else 0),
+        C.byref(stats) if stats is not None else None))
     return outs
 
 
