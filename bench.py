@@ -159,32 +159,35 @@ def main():
     value = samples_step / (ms_step / 1e3) / 1e6
 
     if rank == 0:
-        # ---- roofline of the dominant kernel (HIP events inside the C-ABI) ----
+        # ---- roofline of the dominant kernel: k_wf_trace (closest-hit stream
+        # traversal, ~35% of the step in both passes).  Timed live with HIP
+        # events recorded by mh_render around every k_wf_trace launch on the
+        # scene's stream.  Algorithmic bytes per ray: ray in (o, d, maxt: 28 B)
+        # + hit record out (t, u, v, prim, shape: 20 B) = 48 B;
+        # the BVH is LDS-resident (no HBM bytes).
         avg_f = sum(fwd_ms) / len(fwd_ms)
         avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
         n_local = H * W * args.spp
-        if avg_b > avg_f:
-            kname = "k_prb_backward"
-            # algorithmic HBM bytes per sample: dL gather of grad_in + W image
-            # (25 taps x 16 B, L2/MALL resident: counted once per pixel) -> DESIGN.md
-            bytes_launch = H * W * (12 + 4)
-            dur = avg_b
-        else:
-            kname = "k_render<path>"
-            # per sample: L (12 B) + sample position (8 B) written
-            bytes_launch = n_local * 20
-            dur = avg_f
-        achieved = bytes_launch / (dur / 1e3) / 1e9
+        launches = max(1, st_f.n_trace_launches)
+        rays_per_launch = st_f.rays_closest / launches
+        us_per_launch = st_f.ms_trace / launches * 1e3
+        bytes_launch = rays_per_launch * 48.0
+        achieved = bytes_launch / (us_per_launch / 1e6) / 1e9
+        kname = "k_wf_trace<true>" if st_f.mode == 1 else "k_render"
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):
             try:
-                traffic = json.load(open(tpath)).get(kname)
+                ent = json.load(open(tpath)).get("kernels", {}).get(kname)
+                traffic = round(ent["hbm_bytes_per_call"]) if ent else None
             except Exception:
                 traffic = None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "kernel": kname, "kernel_ms": round(dur, 3)}
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": kname, "kernel_avg_us": round(us_per_launch, 1),
+                    "algorithmic_bytes_per_launch": round(bytes_launch),
+                    "note": "traversal is VALU-issue bound, not HBM bound (DESIGN.md §4); "
+                            "traffic = PMC FETCH_SIZE*2+WRITE_SIZE per launch from profiles/pmc_traffic.json"}
         cpu = None
         if not args.no_cpu:
             cpu = cpu_baseline(scene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)

@@ -86,6 +86,7 @@ struct mh_scene {
         texcoords, faces, texels;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
+    DevBuf wf_ws_prb, wf_partial;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0;
@@ -321,7 +322,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -746,15 +747,51 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     }
 
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
-    LaneMap lm = lane_map(L, 0);
-    const uint64_t n = n_px * (L.s_end - L.s_begin);
-    MH_HIP(hipEventRecord(s->ev0, st));
+    const uint32_t S_ = L.s_end - L.s_begin;
+    const uint64_t n = n_px * S_;
     // fused single traversal when every requested parameter is an rgb constant,
-    // unless the replay is forced (MH_FLAG_MEGAKERNEL / MH_PRB_REPLAY=1)
+    // unless the replay is forced (MH_FLAG_PRB_REPLAY / MH_PRB_REPLAY=1); the
+    // fused form runs as wavefront kernels unless MH_FLAG_MEGAKERNEL / MH_MODE=mega
     const char *env_replay = getenv("MH_PRB_REPLAY");
+    const char *env_mode = getenv("MH_MODE");
     const bool fused = n_bmp == 0 && !(flags & MH_FLAG_PRB_REPLAY) && !(env_replay && !strcmp(env_replay, "1"));
-    MH_HIP(launch_prb_backward(s->S, *in, lm, s->S.sampler_seed + seed, n, L.spp_pp >= 4, g_in, w, ga,
-                               fused, s->counters.as<unsigned long long>(), st));
+    const bool wavefront = fused && in->max_depth <= 64 && !(flags & MH_FLAG_MEGAKERNEL) &&
+                           !(env_mode && !strcmp(env_mode, "mega"));
+    size_t wf_ctr_words = 0, wf_chunks = 0;
+    MH_HIP(hipEventRecord(s->ev0, st));
+    if (wavefront) {
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+        const uint32_t grid = wf_grid((uint32_t)cus * 8);
+        const char *ec = getenv("MH_WF_CHUNK");
+        const uint64_t max_samples = std::min<uint64_t>(
+            wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 23));
+        const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
+        const uint64_t cap = (uint64_t)chunk_px * S_;
+        const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
+        const uint32_t n_bounces = in->max_depth;
+        const size_t ctr_per_chunk = wf_counter_words(n_bounces);
+        MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(cap)));
+        MH_HIP(s->wf_ws_prb.alloc(wf_prb_workspace_bytes(cap)));
+        MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
+        MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));
+        MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, (size_t)grid * kMaxRgbParams * 3 * 4, st));
+        size_t chunk = 0;
+        for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
+            const uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
+            MH_HIP(launch_wavefront_prb(s->S, *in, lane_map(L, (uint32_t)p0), s->S.sampler_seed + seed,
+                                        (uint64_t)npx * S_, L.spp_pp >= 4, g_in, w, ga.slot_of_tex, n_rgb,
+                                        s->wf_ws.ptr, s->wf_ws_prb.ptr, cap,
+                                        s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
+                                        s->wf_partial.as<float>(), st));
+        }
+        MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
+        wf_ctr_words = ctr_per_chunk;
+        wf_chunks = n_chunks;
+    } else {
+        MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
+                                   g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
+    }
     MH_HIP(hipEventRecord(s->ev1, st));
     // accumulate into the caller's gradient buffers
     std::vector<float> host_tmp;
@@ -771,11 +808,25 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         }
     }
     unsigned long long ctr[2] = {0, 0};
-    MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> wctr(wf_ctr_words * wf_chunks);
+    if (wavefront)
+        MH_HIP(hipMemcpyAsync(wctr.data(), s->wf_ctr.ptr, wctr.size() * 4, hipMemcpyDeviceToHost, st));
+    else
+        MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
+    if (wavefront) {
+        const size_t per_bounce = wf_ctr_words / (in->max_depth + 1), nseg = per_bounce / 32;
+        for (size_t c = 0; c < wf_chunks; ++c)
+            for (uint32_t b = 0; b < in->max_depth; ++b)
+                for (size_t sg = 0; sg < nseg; ++sg) {
+                    ctr[0] += wctr[wf_ctr_words * c + per_bounce * b + 32 * sg + 0];
+                    ctr[1] += wctr[wf_ctr_words * c + per_bounce * b + 32 * sg + 1];
+                }
+    }
     if (stats) {
         float ms = 0.f;
         MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->mode = wavefront ? 1u : 0u;
         stats->samples = n;
         stats->rays_closest = ctr[0];
         stats->rays_shadow = ctr[1];

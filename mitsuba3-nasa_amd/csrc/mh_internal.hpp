@@ -61,6 +61,15 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
                             hipEvent_t *trace_ev, hipStream_t st);
+size_t wf_prb_workspace_bytes(uint64_t cap);
+uint32_t wf_grid(uint32_t grid);  // grid rounded to whole queue segments
+hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
+                                const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
+                                void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
+                                uint32_t grid, float *partial, hipStream_t st);
+hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
+                                 hipStream_t st);
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,

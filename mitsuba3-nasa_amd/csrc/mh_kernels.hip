@@ -306,66 +306,6 @@ __global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *
 // ---------------------------------------------------------------------------
 // PRB backward: dL gather + primal + adjoint per lane (common.py:900-983)
 // ---------------------------------------------------------------------------
-MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const float *weights,
-                    float px, float py) {
-    const uint32_t W = S.width, H = S.height;
-    float o0 = 0.f, o1 = 0.f, o2 = 0.f;
-    if (S.rfilter == MH_RFILTER_BOX) {
-        uint32_t ux = (uint32_t)(int32_t)floorf(px), uy = (uint32_t)(int32_t)floorf(py);
-        if (ux < W && uy < H) {
-            uint64_t p = (uint64_t)uy * W + ux;
-            float Wp = weights[p] == 0.f ? 1.f : weights[p];
-            o0 = grad_in[3 * p] / Wp; o1 = grad_in[3 * p + 1] / Wp; o2 = grad_in[3 * p + 2] / Wp;
-        }
-        return v3(o0, o1, o2);
-    }
-    const float radius = S.rfilter_radius;
-    if (coalesce) {
-        int32_t nn = (int32_t)ceilf(radius - 0.5f), count = 2 * nn + 1;
-        int32_t pix = (int32_t)floorf(px) - nn, piy = (int32_t)floorf(py) - nn;
-        float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
-        for (int32_t ys = 0; ys < count; ++ys) {
-            float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
-            for (int32_t xs = 0; xs < count; ++xs) {
-                float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
-                uint32_t xx = (uint32_t)(pix + xs), yy = (uint32_t)(piy + ys);
-                if (xx < W && yy < H) {
-                    uint64_t p = (uint64_t)yy * W + xx;
-                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
-                    float w = wy * wx;
-                    o0 += (grad_in[3 * p] / Wp) * w;
-                    o1 += (grad_in[3 * p + 1] / Wp) * w;
-                    o2 += (grad_in[3 * p + 2] / Wp) * w;
-                }
-            }
-        }
-    } else {
-        float pfx = px - 0.5f, pfy = py - 0.5f;
-        int32_t a0x = max((int32_t)ceilf(pfx - radius), 0), a0y = max((int32_t)ceilf(pfy - radius), 0);
-        int32_t a1x = min((int32_t)floorf(pfx + radius), (int32_t)W - 1);
-        int32_t a1y = min((int32_t)floorf(pfy + radius), (int32_t)H - 1);
-        if (!(a0x <= a1x && a0y <= a1y)) return v3(0, 0, 0);
-        uint32_t count = (uint32_t)ceilf(2.f * radius);
-        float relx = (float)a0x - pfx, rely = (float)a0y - pfy;
-        for (uint32_t ys = 0; ys < count; ++ys) {
-            float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
-            for (uint32_t xs = 0; xs < count; ++xs) {
-                float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
-                int32_t xx = a0x + (int32_t)xs, yy = a0y + (int32_t)ys;
-                if (xx <= a1x && yy <= a1y) {
-                    uint64_t p = (uint64_t)yy * W + xx;
-                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
-                    float w = wy * wx;
-                    o0 += (grad_in[3 * p] / Wp) * w;
-                    o1 += (grad_in[3 * p + 1] / Wp) * w;
-                    o2 += (grad_in[3 * p + 2] / Wp) * w;
-                }
-            }
-        }
-    }
-    return v3(o0, o1, o2);
-}
-
 template <bool InLds, bool Fused>
 __global__ void __launch_bounds__(256)
 k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n,
@@ -391,7 +331,7 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
                             __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
         V3 dL = gather_dL(S, coalesce, grad_in, weights, sx, sy);
         if (Fused) {
-            prb_fused(S, B, in, rng, r, dL, g, n_closest, n_shadow);
+            prb_fused(S, B, in, rng, r, dL, ga.n_rgb, g, n_closest, n_shadow);
         } else {
             Pcg rng_primal = rng;  // sampler.clone()
             V3 Lp = prb_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr,

@@ -207,8 +207,20 @@ MH_DEV void trav_init(TravLane &t, const RayT &r, bool empty_scene) {
     t.hit.shape = MH_INVALID;
 }
 
+// Does the lane take part in the next inner step?  It does while it has an
+// inner node to visit or a stack to pop.  A lane already holding a postponed
+// leaf keeps traversing inner nodes (speculative traversal, Aila & Laine
+// 2009) until it meets a second leaf, which it keeps in `node`.
+MH_DEV bool trav_wants(const TravLane &t) {
+    if (t.node == kDone) return false;
+    if (t.node == kNoNode) return t.sp != 0 || t.nleaf == 0;
+    return !(t.node & kLeafBit);
+}
+
+// a leaf reference is taken into the empty leaf slot; otherwise it stays in
+// `node` (processed after the held leaf)
 MH_DEV void trav_take(TravLane &t, uint32_t ref) {
-    if (ref & kLeafBit) {
+    if ((ref & kLeafBit) && t.nleaf == 0) {
         t.leaf = (ref & ~kLeafBit) >> 3;
         t.nleaf = ref & 7u;
         t.node = kNoNode;
@@ -217,13 +229,14 @@ MH_DEV void trav_take(TravLane &t, uint32_t ref) {
     }
 }
 
-// visit one inner node, or pop the stack (which may yield a pending leaf)
+// one inner step: pop if needed, then visit one inner node
 MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint32_t stride) {
     if (t.node == kNoNode) {
-        if (t.sp == 0) { t.node = kDone; return; }
+        if (t.sp == 0) { t.node = kDone; return; }  // (only reached without a held leaf)
         --t.sp;
-        trav_take(t, stk[t.sp * stride]);
-        return;
+        const uint32_t ref = stk[t.sp * stride];
+        trav_take(t, ref);
+        if (t.node == kNoNode || (t.node & kLeafBit)) return;
     }
     const Node n = nodes[t.node];
     bool h0, h1;
@@ -260,6 +273,7 @@ MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
         }
     }
     t.nleaf = 0;
+    if (t.node != kDone && t.node != kNoNode && (t.node & kLeafBit)) trav_take(t, t.node);
 }
 
 // Traces items [r0, r1) of this wave.  load(item) -> RayT, store(item, hit,
@@ -276,12 +290,14 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
     while (__any(has)) {
         // inner phase: every active lane advances until it holds a leaf or is done
         while (true) {
-            const bool inner = has && t.nleaf == 0 && t.node != kDone;
-            if (!__any(inner)) break;
+            const bool inner = has && trav_wants(t);
+            const bool ready = !has || t.nleaf != 0 || t.node == kDone;
+            if (!__any(inner) || __all(ready)) break;
             if (inner) trav_inner_step(t, B.nodes, B.stack, B.stride);
         }
         // grouped leaf phase
         if (has && t.nleaf) trav_leaf<Shadow>(t, B.prims);
+        if (has && t.node == kNoNode && t.sp == 0 && t.nleaf == 0) t.node = kDone;
         // retire finished lanes and refill them from the wave's range
         const bool fin = has && t.node == kDone && t.nleaf == 0;
         if (fin) store(item, t.hit, t.hit.shape != MH_INVALID);
@@ -865,33 +881,133 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
 }
 
 // ---------------------------------------------------------------------------
+// dL of one sample: the adjoint of ImageBlock::put + develop, i.e. the
+// filter-weighted gather of grad_in / W over the sample's footprint
+// (common.py:953-965; the W image from common.py:936-947)
+// ---------------------------------------------------------------------------
+MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const float *weights,
+                    float px, float py) {
+    const uint32_t W = S.width, H = S.height;
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+    if (S.rfilter == MH_RFILTER_BOX) {
+        uint32_t ux = (uint32_t)(int32_t)floorf(px), uy = (uint32_t)(int32_t)floorf(py);
+        if (ux < W && uy < H) {
+            uint64_t p = (uint64_t)uy * W + ux;
+            float Wp = weights[p] == 0.f ? 1.f : weights[p];
+            o0 = grad_in[3 * p] / Wp; o1 = grad_in[3 * p + 1] / Wp; o2 = grad_in[3 * p + 2] / Wp;
+        }
+        return v3(o0, o1, o2);
+    }
+    const float radius = S.rfilter_radius;
+    if (coalesce) {
+        int32_t nn = (int32_t)ceilf(radius - 0.5f), count = 2 * nn + 1;
+        int32_t pix = (int32_t)floorf(px) - nn, piy = (int32_t)floorf(py) - nn;
+        float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
+        for (int32_t ys = 0; ys < count; ++ys) {
+            float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
+            for (int32_t xs = 0; xs < count; ++xs) {
+                float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
+                uint32_t xx = (uint32_t)(pix + xs), yy = (uint32_t)(piy + ys);
+                if (xx < W && yy < H) {
+                    uint64_t p = (uint64_t)yy * W + xx;
+                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
+                    float w = wy * wx;
+                    o0 += (grad_in[3 * p] / Wp) * w;
+                    o1 += (grad_in[3 * p + 1] / Wp) * w;
+                    o2 += (grad_in[3 * p + 2] / Wp) * w;
+                }
+            }
+        }
+    } else {
+        float pfx = px - 0.5f, pfy = py - 0.5f;
+        int32_t a0x = max((int32_t)ceilf(pfx - radius), 0), a0y = max((int32_t)ceilf(pfy - radius), 0);
+        int32_t a1x = min((int32_t)floorf(pfx + radius), (int32_t)W - 1);
+        int32_t a1y = min((int32_t)floorf(pfy + radius), (int32_t)H - 1);
+        if (!(a0x <= a1x && a0y <= a1y)) return v3(0, 0, 0);
+        uint32_t count = (uint32_t)ceilf(2.f * radius);
+        float relx = (float)a0x - pfx, rely = (float)a0y - pfy;
+        for (uint32_t ys = 0; ys < count; ++ys) {
+            float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
+            for (uint32_t xs = 0; xs < count; ++xs) {
+                float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
+                int32_t xx = a0x + (int32_t)xs, yy = a0y + (int32_t)ys;
+                if (xx <= a1x && yy <= a1y) {
+                    uint64_t p = (uint64_t)yy * W + xx;
+                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
+                    float w = wy * wx;
+                    o0 += (grad_in[3 * p] / Wp) * w;
+                    o1 += (grad_in[3 * p + 1] / Wp) * w;
+                    o2 += (grad_in[3 * p + 2] / Wp) * w;
+                }
+            }
+        }
+    }
+    return v3(o0, o1, o2);
+}
+
+// ---------------------------------------------------------------------------
 // Fused PRB gradient for constant (rgb) reflectance parameters: ONE traversal
 // of the path instead of the primal + adjoint replay of
-// RBIntegrator.render_backward (common.py:953-974).  The adjoint replay
-// revisits the same vertices (same RNG stream) with L_{k+1} = L_total - P_k,
-// P_k = sum_{j<=k} (Le_j + Lr_dir_j) the primal prefix; the Lr_ind term of
-// prb.py:229-240 is therefore, per parameter slot s,
-//     sum_k dL * (L_total - P_k) * c_k / pi = dL * (L_total * A_s - B_s) / pi
-// with A_s = sum_k c_k, B_s = sum_k P_k * c_k, c_k = cos_ind / (rho * pdf).
-// The Lr_dir term needs only dL (known before the path) and is accumulated
-// immediately.  Mathematically identical to the replay; differs from it by
-// fp rounding only (the subtraction order of L), tested at 1e-3 relative.
+// RBIntegrator.render_backward (common.py:953-974).  The replay revisits the
+// same vertices (same RNG stream) with L_{k+1} = L_total - P_k, where
+// P_k = sum_{j<=k} e_j is the primal prefix of the radiance contributions
+// e_j = Le_j + Lr_dir_j; the indirect term of prb.py:229-240 summed over the
+// vertices k of slot s is therefore
+//     sum_k dL (L_total - P_k) c_k / pi = sum_j dL e_j A_s(<j) / pi,
+// c_k = cos_ind / (rho pdf) and A_s(<j) = sum_{k<j, slot k = s} c_k: every
+// radiance contribution is charged, when it is produced, to the c's of the
+// earlier vertices.  No suffix is needed, so the same form serves the
+// wavefront kernels (contributions produced in k_wf_shade / k_wf_shadow).
+// The direct term (prb.py:208-221) needs only dL.  Mathematically identical
+// to the replay; differs by fp association only (tests: 1e-3 relative).
 // ---------------------------------------------------------------------------
+MH_DEV void charge(float (&acc)[kMaxRgbParams][3], const float (&A)[kMaxRgbParams][3], uint32_t n_rgb,
+                   V3 dLe) {
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk)
+        if ((uint32_t)kk < n_rgb) {
+            acc[kk][0] = __builtin_fmaf(dLe.x, A[kk][0] * kInvPi, acc[kk][0]);
+            acc[kk][1] = __builtin_fmaf(dLe.y, A[kk][1] * kInvPi, acc[kk][1]);
+            acc[kk][2] = __builtin_fmaf(dLe.z, A[kk][2] * kInvPi, acc[kk][2]);
+        }
+}
+
+// adjoint factor c_k of a diffuse vertex (prb.py:229-240 with the
+// `inv_bsdf_weight * cos` of the local BSDF eval), zero where the replay's
+// active mask / cosines vanish
+MH_DEV V3 prb_indirect_factor(bool active_next, const SI &si, V3 wo2, V3 bsdf_weight, float bs_pdf) {
+    V3 c = v3(0, 0, 0);
+    if (active_next && si.wi.z > 0.f && wo2.z > 0.f) {
+        V3 det = bsdf_weight * bs_pdf;
+        c = v3(det.x != 0.f ? rcp(det.x) : 0.f, det.y != 0.f ? rcp(det.y) : 0.f,
+               det.z != 0.f ? rcp(det.z) : 0.f) * wo2.z;
+    }
+    return c;
+}
+
+MH_DEV void add_slot(float (&arr)[kMaxRgbParams][3], int32_t slot, V3 v) {
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk)
+    {
+        const bool m = kk == slot;  // branch-free: keeps arr in registers
+        arr[kk][0] += m ? v.x : 0.f;
+        arr[kk][1] += m ? v.y : 0.f;
+        arr[kk][2] += m ? v.z : 0.f;
+    }
+}
+
 MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                      RayT ray, V3 dL, GradCtx &g, uint32_t &n_closest, uint32_t &n_shadow) {
+                      RayT ray, V3 dL, uint32_t n_rgb, GradCtx &g, uint32_t &n_closest, uint32_t &n_shadow) {
     uint32_t depth = 0;
-    V3 L = v3(0, 0, 0);
     V3 beta = v3(1, 1, 1);
     float eta = 1.f;
     bool active = true;
     V3 prev_p = v3(0, 0, 0);
     float prev_bsdf_pdf = 1.f;
     bool prev_bsdf_delta = true;
-    float A[kMaxRgbParams][3], Bs[kMaxRgbParams][3];
+    float A[kMaxRgbParams][3];
 #pragma unroll
-    for (int k = 0; k < kMaxRgbParams; ++k)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) A[k][c] = Bs[k][c] = 0.f;
+    for (int k = 0; k < kMaxRgbParams; ++k) A[k][0] = A[k][1] = A[k][2] = 0.f;
     while (active) {
         bool active_next = active;
         Hit h;
@@ -903,14 +1019,13 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
         if (in.hide_emitters && depth == 0 && !si.valid) active_next = false;
         uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
-        V3 Le = v3(0, 0, 0);
         if (em != MH_INVALID) {
             float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
             float mis = mis_weight(prev_bsdf_pdf, em_pdf);
             V3 le = v3(0, 0, 0);
             if (active_next && si.valid && si.wi.z > 0.f)
                 le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
-            Le = (beta * mis) * le;
+            charge(g.acc, A, n_rgb, dL * ((beta * mis) * le));
         }
         active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
         bool active_em = active_next && smooth;
@@ -931,7 +1046,7 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         diffuse_eval_pdf(rho, si.wi, wo_em, active_em, bsdf_value_em, bsdf_pdf_em);
         float mis_em = mis_weight(ds.pdf, bsdf_pdf_em);
         V3 beta_mis_em = beta * mis_em;
-        V3 Lr_dir = active_em ? (beta_mis_em * bsdf_value_em) * em_weight : v3(0, 0, 0);
+        if (active_em) charge(g.acc, A, n_rgb, dL * ((beta_mis_em * bsdf_value_em) * em_weight));
         (void)rng.next_float();
         float s2x = rng.next_float(), s2y = rng.next_float();
         V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
@@ -942,7 +1057,6 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
             bs_eta = 1.f;
             bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
         }
-        L = (L + Le) + Lr_dir;  // = P_k
         ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
         eta *= bs_eta;
         beta = beta * bsdf_weight;
@@ -959,35 +1073,13 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         if (smooth) {
             const int32_t slot = g.slot_of_tex[S.bsdf_tex[b]];
             if (slot >= 0) {
-                V3 adj = v3(0, 0, 0);
                 if (active_em && si.wi.z > 0.f && wo_em.z > 0.f)
-                    adj = (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi;
-                V3 c = v3(0, 0, 0);
-                V3 wo2 = to_local(si, ray.d);
-                if (active_next && si.wi.z > 0.f && wo2.z > 0.f) {
-                    V3 det = bsdf_weight * bs_pdf;
-                    c = v3(det.x != 0.f ? rcp(det.x) : 0.f, det.y != 0.f ? rcp(det.y) : 0.f,
-                           det.z != 0.f ? rcp(det.z) : 0.f) * wo2.z;
-                }
-                V3 pc = L * c;
-#pragma unroll
-                for (int kk = 0; kk < kMaxRgbParams; ++kk)
-                    if (kk == slot) {
-                        g.acc[kk][0] += adj.x; g.acc[kk][1] += adj.y; g.acc[kk][2] += adj.z;
-                        A[kk][0] += c.x; A[kk][1] += c.y; A[kk][2] += c.z;
-                        Bs[kk][0] += pc.x; Bs[kk][1] += pc.y; Bs[kk][2] += pc.z;
-                    }
+                    add_slot(g.acc, slot, (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi);
+                add_slot(A, slot, prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf));
             }
         }
         if (si.valid) depth += 1;
         active = active_next;
-    }
-    // dL * (L_total * A - B) / pi
-#pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk) {
-        g.acc[kk][0] += ((dL.x * (L.x * A[kk][0] - Bs[kk][0]))) * kInvPi;
-        g.acc[kk][1] += ((dL.y * (L.y * A[kk][1] - Bs[kk][1]))) * kInvPi;
-        g.acc[kk][2] += ((dL.z * (L.z * A[kk][2] - Bs[kk][2]))) * kInvPi;
     }
 }
 

@@ -367,4 +367,348 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     return hipGetLastError();
 }
 
+// ===========================================================================
+// Wavefront PRB gradient (rgb parameters): RBIntegrator.render_backward
+// (common.py:828-983) in the single-traversal form of prb_fused
+// (mh_shading.hpp).  Extra per-path state: dL (gathered at raygen) and the
+// running adjoint factors A_s; a shadow record carries the gradient it
+// contributes if unoccluded (dL e_j A_s / pi plus the direct-term adjoint of
+// its own slot).  Gradients accumulate in per-thread registers across a
+// kernel's items and are folded once per kernel into a per-block partial
+// (plain read-modify-write: one block per index per launch, launches are
+// stream-ordered), so no same-address atomics; k_wf_grad_reduce sums the
+// partials in a fixed order (deterministic).
+// ===========================================================================
+constexpr int kG = kMaxRgbParams * 3;
+
+// planes addressed arithmetically (base + plane * stride): a runtime-indexed
+// pointer table in the kernel arguments would be copied to scratch
+struct WfPrb {
+    float *base;
+    uint64_t stride;  // floats between planes
+    float *partial;   // [grid][kG]
+    const int32_t *slot_of_tex;
+    uint32_t n_rgb;
+    // ping-pong k: planes [k * (3 + kG), (k + 1) * (3 + kG)): dL xyz, then A
+    MH_DEV float *dl(int k, int c) const { return base + (uint64_t)(k * (3 + kG) + c) * stride; }
+    MH_DEV float *A(int k, int c) const { return base + (uint64_t)(k * (3 + kG) + 3 + c) * stride; }
+    MH_DEV float *G(int c) const { return base + (uint64_t)(2 * (3 + kG) + c) * stride; }
+};
+
+size_t wf_prb_workspace_bytes(uint64_t cap) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    return (size_t)(6 + 2 * kG + kG) * align_up(cap * 4);
+}
+
+static WfPrb carve_prb(void *ws, uint64_t cap, float *partial, const int32_t *slot_of_tex, uint32_t n_rgb) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    WfPrb q;
+    q.base = reinterpret_cast<float *>(ws);
+    q.stride = align_up(cap * 4) / 4;
+    q.partial = partial;
+    q.slot_of_tex = slot_of_tex;
+    q.n_rgb = n_rgb;
+    return q;
+}
+
+// block-reduce the per-thread accumulators into partial[blockIdx]
+MH_DEV void flush_partial(float (&acc)[kMaxRgbParams][3], const WfPrb &q) {
+    __shared__ float red[4][kG];
+    const uint32_t wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk) {
+        if ((uint32_t)kk >= q.n_rgb) break;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v = acc[kk][c];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane_id() == 0) red[wave][kk * 3 + c] = v;
+        }
+    }
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    if (t < q.n_rgb * 3) {
+        float s = 0.f;
+        for (uint32_t w = 0; w < blockDim.x / 64u; ++w) s += red[w][t];
+        q.partial[(size_t)blockIdx.x * kG + t] += s;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_wf_raygen_prb(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, int coalesce,
+                const float *__restrict__ grad_in, const float *__restrict__ weights, WfState w,
+                WfPrb q, uint32_t *ctr) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < kSeg) {
+        const uint64_t L = seg_len(n), b = k * L;
+        ctr[k * 32] = b >= n ? 0u : (uint32_t)std::min<uint64_t>(L, n - b);
+    }
+    if (k >= n) return;
+    uint32_t lane, px, py;
+    lane_of(lm, k, lane, px, py);
+    Pcg rng;
+    rng.seed(seed_value, lane);
+    float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+    RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
+                        __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+    V3 dL = gather_dL(S, coalesce, grad_in, weights, sx, sy);
+    w.pd[0][k] = (uint32_t)k;
+    w.ox[0][k] = r.o.x; w.oy[0][k] = r.o.y; w.oz[0][k] = r.o.z;
+    w.dx[0][k] = r.d.x; w.dy[0][k] = r.d.y; w.dz[0][k] = r.d.z; w.mt[0][k] = r.maxt;
+    w.bx[0][k] = 1.f; w.by[0][k] = 1.f; w.bz[0][k] = 1.f;
+    w.ppx[0][k] = 0.f; w.ppy[0][k] = 0.f; w.ppz[0][k] = 0.f; w.ppdf[0][k] = 1.f;
+    w.rng[0][k] = rng.state;
+    q.dl(0, 0)[k] = dL.x; q.dl(0, 1)[k] = dL.y; q.dl(0, 2)[k] = dL.z;
+#pragma unroll
+    for (int c = 0; c < kG; ++c)
+        if ((uint32_t)c < q.n_rgb * 3) q.A(0, c)[k] = 0.f;
+}
+
+// one iteration of the prb_fused loop (prb.py:114-278) for every queued path
+__global__ void __launch_bounds__(256)
+k_wf_shade_prb(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
+               int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t sbase = it.seg * seg_cap;
+    const int nxt = cur ^ 1;
+    const uint32_t n_rgb = q.n_rgb;
+    float acc[kMaxRgbParams][3];
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
+    const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
+    for (uint32_t itr = 0; itr < n_iter; ++itr) {
+        const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
+        bool alive = false, shadow = false;
+        uint32_t pid = 0, depth = 0;
+        RayT ray, sray;
+        V3 beta, prev_p, dL;
+        float prev_pdf = 1.f;
+        float A[kMaxRgbParams][3], G[kMaxRgbParams][3];
+        Pcg rng;
+        if (i < n) {
+            const uint32_t j = sbase + i;
+            const uint32_t pd = w.pd[cur][j];
+            pid = pd & kPidMask;
+            depth = pd >> kPidBits;
+            ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+            ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+            ray.maxt = w.mt[cur][j];
+            Hit h;
+            h.t = w.ht[j]; h.u = w.hu[j]; h.v = w.hv[j]; h.prim = w.hp[j]; h.shape = w.hs[j];
+            beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+            prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+            prev_pdf = w.ppdf[cur][j];
+            dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
+#pragma unroll
+            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
+            const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
+            const float eta = 1.f;
+            uint32_t lane, px, py;
+            lane_of(lm, pid, lane, px, py);
+            rng.state = w.rng[cur][j];
+            rng.inc = pcg_inc(seed_value, lane);
+            SI si;
+            compute_si(S, ray, h, si);
+            const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
+            const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+            bool active_next = !(in.hide_emitters && depth == 0 && !si.valid);
+
+            // ---- emission (prb.py:143-152): charged to the earlier vertices
+            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+            if (em != MH_INVALID) {
+                float em_pdf = prev_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+                float mis = mis_weight(prev_pdf, em_pdf);
+                V3 le = v3(0, 0, 0);
+                if (active_next && si.valid && si.wi.z > 0.f)
+                    le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+                charge(acc, A, n_rgb, dL * ((beta * mis) * le));
+            }
+            active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
+            const bool active_em0 = active_next && smooth;
+
+            // ---- emitter sampling (prb.py:157-176); visibility deferred
+            float e0 = rng.next_float(), e1 = rng.next_float();
+            DirS ds;
+            ds.pdf = 0.f;
+            ds.d = v3(0, 0, 0);
+            V3 em_weight = v3(0, 0, 0);
+            if (active_em0) {
+                em_weight = area_sample_direction(S, 0, si.p, e0, e1, ds);
+                if (ds.pdf != 0.f && nonzero(em_weight)) {
+                    shadow = true;
+                    sray = spawn_ray_to(si.p, si.n, ds.p);
+                }
+            }
+            V3 rho = v3(0, 0, 0);
+            if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+            const int32_t slot = smooth ? q.slot_of_tex[S.bsdf_tex[b]] : -1;
+            if (shadow) {  // as if unoccluded; applied by k_wf_shadow_prb
+                V3 wo_em = to_local(si, ds.d);
+                V3 bsdf_value_em;
+                float bsdf_pdf_em;
+                diffuse_eval_pdf(rho, si.wi, wo_em, true, bsdf_value_em, bsdf_pdf_em);
+                float mis_em = mis_weight(ds.pdf, bsdf_pdf_em);
+                V3 beta_mis_em = beta * mis_em;
+                V3 dLe = dL * ((beta_mis_em * bsdf_value_em) * em_weight);
+#pragma unroll
+                for (int kk = 0; kk < kMaxRgbParams; ++kk) {
+                    G[kk][0] = (dLe.x * (A[kk][0] * kInvPi));
+                    G[kk][1] = (dLe.y * (A[kk][1] * kInvPi));
+                    G[kk][2] = (dLe.z * (A[kk][2] * kInvPi));
+                }
+                if (slot >= 0 && si.wi.z > 0.f && wo_em.z > 0.f)
+                    add_slot(G, slot, (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi);
+            }
+
+            // ---- BSDF sampling, RR (prb.py:181-278)
+            (void)rng.next_float();
+            float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
+            float bs_pdf = 0.f;
+            if (smooth && active_next) {
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+            }
+            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+            beta = beta * bsdf_weight;
+            prev_p = si.p;
+            prev_pdf = bs_pdf;
+            float beta_max = hmax(beta);
+            active_next = active_next && beta_max != 0.f;
+            float rr_prob = fminf(beta_max * (eta * eta), 0.95f);
+            bool rr_active = depth >= in.rr_depth;
+            if (rr_active) beta = beta * rcp(rr_prob);
+            bool rr_continue = rng.next_float() < rr_prob;
+            active_next = active_next && (!rr_active || rr_continue);
+            if (slot >= 0)
+                add_slot(A, slot, prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf));
+            if (si.valid) depth += 1;
+            alive = active_next;
+        }
+        const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        const uint32_t sslot = sbase + wave_append(ctr + it.seg * 32 + 1, shadow);
+        if (alive) {
+            w.pd[nxt][slot_n] = pid | (depth << kPidBits);
+            w.ox[nxt][slot_n] = ray.o.x; w.oy[nxt][slot_n] = ray.o.y; w.oz[nxt][slot_n] = ray.o.z;
+            w.dx[nxt][slot_n] = ray.d.x; w.dy[nxt][slot_n] = ray.d.y; w.dz[nxt][slot_n] = ray.d.z;
+            w.mt[nxt][slot_n] = ray.maxt;
+            w.bx[nxt][slot_n] = beta.x; w.by[nxt][slot_n] = beta.y; w.bz[nxt][slot_n] = beta.z;
+            w.ppx[nxt][slot_n] = prev_p.x; w.ppy[nxt][slot_n] = prev_p.y; w.ppz[nxt][slot_n] = prev_p.z;
+            w.ppdf[nxt][slot_n] = prev_pdf;
+            w.rng[nxt][slot_n] = rng.state;
+            q.dl(nxt, 0)[slot_n] = dL.x; q.dl(nxt, 1)[slot_n] = dL.y; q.dl(nxt, 2)[slot_n] = dL.z;
+#pragma unroll
+            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+                if ((uint32_t)kk < n_rgb) {
+                    q.A(nxt, kk * 3 + 0)[slot_n] = A[kk][0];
+                    q.A(nxt, kk * 3 + 1)[slot_n] = A[kk][1];
+                    q.A(nxt, kk * 3 + 2)[slot_n] = A[kk][2];
+                }
+        }
+        if (shadow) {
+            w.sox[sslot] = sray.o.x; w.soy[sslot] = sray.o.y; w.soz[sslot] = sray.o.z;
+            w.sdx[sslot] = sray.d.x; w.sdy[sslot] = sray.d.y; w.sdz[sslot] = sray.d.z; w.smt[sslot] = sray.maxt;
+#pragma unroll
+            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+                if ((uint32_t)kk < n_rgb) {
+                    q.G(kk * 3 + 0)[sslot] = G[kk][0];
+                    q.G(kk * 3 + 1)[sslot] = G[kk][1];
+                    q.G(kk * 3 + 2)[sslot] = G[kk][2];
+                }
+        }
+    }
+    flush_partial(acc, q);
+}
+
+template <bool InLds>
+__global__ void __launch_bounds__(256)
+k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t base = it.seg * seg_cap;
+    const uint32_t n_rgb = q.n_rgb;
+    float acc[kMaxRgbParams][3];
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
+    uint32_t r0, r1;
+    wave_range(it, n, r0, r1);
+    trace_stream<true>(
+        B, r0, r1,
+        [&](uint32_t i) {
+            const uint32_t j = base + i;
+            return RayT{v3(w.sox[j], w.soy[j], w.soz[j]), v3(w.sdx[j], w.sdy[j], w.sdz[j]), w.smt[j]};
+        },
+        [&](uint32_t i, const Hit &, bool occluded) {
+            if (occluded) return;
+            const uint32_t j = base + i;
+#pragma unroll
+            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+                if ((uint32_t)kk < n_rgb) {
+                    acc[kk][0] += q.G(kk * 3 + 0)[j];
+                    acc[kk][1] += q.G(kk * 3 + 1)[j];
+                    acc[kk][2] += q.G(kk * 3 + 2)[j];
+                }
+        });
+    flush_partial(acc, q);
+}
+
+// partials -> gradient buffers; block t sums entry t over all blocks
+__global__ void __launch_bounds__(256)
+k_wf_grad_reduce(const float *__restrict__ partial, uint32_t grid, float *const *bufs) {
+    __shared__ float red[4];
+    const uint32_t t = blockIdx.x;
+    float s = 0.f;
+    for (uint32_t b = threadIdx.x; b < grid; b += blockDim.x) s += partial[(size_t)b * kG + t];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) bufs[t / 3][t % 3] += (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
+                                const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
+                                void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
+                                uint32_t grid, float *partial, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (n > (1ull << kPidBits) || n_bounces > 255 || n_rgb > (uint32_t)kMaxRgbParams) return hipErrorInvalidValue;
+    WfState w = carve(ws, cap);
+    WfPrb q = carve_prb(ws_prb, cap, partial, slot_of_tex, n_rgb);
+    hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
+                       seed_value, n, coalesce, grad_in, weights, w, q, ctr);
+    const size_t sh = lds_bytes(S, 256);
+    const bool lds = S.lds_bytes_bvh != 0;
+    const uint32_t seg_cap = seg_len(n);
+    for (uint32_t b = 0; b < n_bounces; ++b) {
+        uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
+        const int cur = (int)(b & 1);
+        if (lds) hipLaunchKernelGGL(k_wf_trace<true>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
+        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
+        hipLaunchKernelGGL(k_wf_shade_prb, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, w, q, cur,
+                           seg_cap, c, cn);
+        if (lds) hipLaunchKernelGGL(k_wf_shadow_prb<true>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
+        else hipLaunchKernelGGL(k_wf_shadow_prb<false>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
+    }
+    return hipGetLastError();
+}
+
+uint32_t wf_grid(uint32_t grid) { return std::max<uint32_t>(kSeg, grid / kSeg * kSeg); }
+
+hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
+                                 hipStream_t st) {
+    if (n_rgb == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_wf_grad_reduce, dim3(n_rgb * 3), dim3(256), 0, st, partial, grid, bufs);
+    return hipGetLastError();
+}
+
 }  // namespace mh

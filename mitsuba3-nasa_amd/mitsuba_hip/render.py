@@ -177,9 +177,13 @@ def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, devic
 def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],
                     integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                     spp_begin: int = 0, spp_end: int = 0, weights=None,
-                    stats: Optional[A.Stats] = None, replay: bool = False):
+                    stats: Optional[A.Stats] = None, mode: str = "auto"):
     """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
-    Returns a list of gradient tensors (one per key, same shape as the param)."""
+    Returns a list of gradient tensors (one per key, same shape as the param).
+    mode: 'auto' (wavefront single-traversal kernels when every key is an rgb
+    constant, else the per-lane primal + adjoint replay), 'mega' (per-lane
+    single traversal) or 'replay' (per-lane primal + adjoint replay, the
+    reference's own two-pass structure)."""
     torch = _torch()
     integrator = integrator or scene.integrator()
     if integrator.type != "prb":
@@ -195,7 +199,7 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     A.check(A.lib().mh_render_backward(
         h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(grad_in),
         _ptr(weights) if weights is not None else None, len(keys), tex, ptrs,
-        A.FLAG_DEVICE_POINTERS | (A.FLAG_PRB_REPLAY if replay else 0),
+        A.FLAG_DEVICE_POINTERS | {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "replay": A.FLAG_PRB_REPLAY}[mode],
         C.byref(stats) if stats is not None else None))
     return outs
 

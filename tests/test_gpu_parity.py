@@ -140,8 +140,8 @@ def test_prb_weights_parity():
     np.testing.assert_allclose(w, rw, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("spp,replay", [(4, True), (16, True), (4, False), (16, False)])
-def test_prb_backward_rgb_parity(spp, replay):
+@pytest.mark.parametrize("spp,mode", [(4, "replay"), (16, "replay"), (4, "mega"), (16, "auto"), (4, "auto")])
+def test_prb_backward_rgb_parity(spp, mode):
     mi = _mi()
     import torch
     scene = cbox(mi, 32, 32, spp)
@@ -151,7 +151,7 @@ def test_prb_backward_rgb_parity(spp, replay):
     H, W = scene.height, scene.width
     grad_in = np.full((H, W, 3), 1.0 / (H * W * 3), np.float32)
     g = mi.render_backward(scene, params, torch.from_numpy(grad_in).cuda(), keys, integ, seed=11, spp=spp,
-                           replay=replay)
+                           mode=mode)
     g = [x.cpu().numpy() for x in g]
     ref = O.render_backward(scene, integ, 11, spp, grad_in, [params.texture_of(k) for k in keys], [(3,), (3,)])
     for a, b in zip(g, ref):
@@ -170,7 +170,29 @@ def test_prb_backward_fused_vs_replay_random_grad():
     keys = ["white.reflectance.value", "red.reflectance.value", "green.reflectance.value"]
     rng = np.random.default_rng(5)
     gi = torch.from_numpy(rng.standard_normal((40, 48, 3)).astype(np.float32)).cuda()
-    a = mi.render_backward(scene, params, gi, keys, integ, seed=4, spp=8, replay=True)
-    b = mi.render_backward(scene, params, gi, keys, integ, seed=4, spp=8, replay=False)
-    for x, y in zip(a, b):
-        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=2e-3, atol=1e-5)
+    a = mi.render_backward(scene, params, gi, keys, integ, seed=4, spp=8, mode="replay")
+    for mode in ("mega", "auto"):
+        b = mi.render_backward(scene, params, gi, keys, integ, seed=4, spp=8, mode=mode)
+        for x, y in zip(a, b):
+            np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=2e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_prb_backward_wavefront_chunked(monkeypatch):
+    """Multi-chunk wavefront backward (lane maps offset per chunk, partials
+    accumulated across chunks) equals the single-chunk run."""
+    mi = _mi()
+    import torch
+    scene = cbox(mi, 40, 24, 16)
+    integ = mi.load_dict({"type": "prb", "max_depth": 5, "hide_emitters": True})
+    params = mi.traverse(scene)
+    keys = ["white.reflectance.value", "green.reflectance.value"]
+    gi = torch.full((24, 40, 3), 1.0 / (24 * 40 * 3), dtype=torch.float32, device="cuda")
+    a = mi.render_backward(scene, params, gi, keys, integ, seed=9, spp=16)
+    monkeypatch.setenv("MH_WF_CHUNK", "2048")
+    b = mi.render_backward(scene, params, gi, keys, integ, seed=9, spp=16)
+    ref = O.render_backward(scene, integ, 9, 16, gi.cpu().numpy(), [params.texture_of(k) for k in keys],
+                            [(3,), (3,)])
+    for x, y, r in zip(a, b, ref):
+        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-4, atol=1e-8)
+        np.testing.assert_allclose(x.cpu().numpy(), r, rtol=1e-3, atol=1e-7)

@@ -27,7 +27,11 @@ def main():
     d = sys.argv[1]
     prefixes = sys.argv[2:] or None
     dur = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(d, "*kernel_trace.csv")):
+    files = glob.glob(os.path.join(d, "*kernel_trace.csv"))
+    # durations from the plain --kernel-trace pass when present (PMC passes
+    # serialise dispatches and inflate them)
+    plain = [f for f in files if os.path.basename(f).startswith("trace")]
+    for f in plain or files:
         if prefixes and not any(os.path.basename(f).startswith(p) for p in prefixes):
             continue
         for r in csv.DictReader(open(f)):
