@@ -111,27 +111,24 @@ def main():
     key = "white.reflectance.value"
     H = W = args.res
     spp_total = args.spp * world
-    s0, s1 = args.spp * rank, args.spp * (rank + 1)
     grad_in = torch.full((H, W, 3), 1.0 / (H * W * 3), dtype=torch.float32, device=dev)
     st_f, st_b = A.Stats(), A.Stats()
     film = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
 
+    from mitsuba_hip import distributed as D
+    slab = D.sample_slab(rank, world, args.spp)
+    ops = D.StepOps(
+        render_film=lambda seed, spp, b, e: mi.render_film(scene, fwd, seed=seed, spp=spp, spp_begin=b,
+                                                           spp_end=e, film=film, stats=st_f),
+        develop=lambda f: mi.develop(scene, f),
+        prb_weights=lambda seed, spp, b, e: mi.prb_weights(scene, seed, spp, b, e),
+        render_backward=lambda seed, spp, b, e, w: mi.render_backward(
+            scene, params, grad_in, [key], prb, seed=seed, spp=spp, spp_begin=b, spp_end=e, weights=w,
+            stats=st_b),
+        seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0])
+
     def step(i):
-        mi.render_film(scene, fwd, seed=i, spp=spp_total, spp_begin=s0, spp_end=s1, film=film, stats=st_f)
-        if dist_on:
-            dist.all_reduce(film)
-        img = mi.develop(scene, film)
-        if args.fwd_only:
-            return img, None
-        seed_grad = mi.sample_tea_32(i, 1)[0]
-        w = mi.prb_weights(scene, seed_grad, spp_total, s0, s1)
-        if dist_on:
-            dist.all_reduce(w)
-        g = mi.render_backward(scene, params, grad_in, [key], prb, seed=seed_grad, spp=spp_total,
-                               spp_begin=s0, spp_end=s1, weights=w, stats=st_b)[0]
-        if dist_on:
-            dist.all_reduce(g)
-        return img, g
+        return D.fwd_grad_step(ops, slab, i, with_grad=not args.fwd_only)
 
     for i in range(args.warmup):
         step(1000 + i)
@@ -150,10 +147,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, dev)
     ms_step = elapsed / args.steps * 1e3
     samples_step = world * H * W * args.spp
     value = samples_step / (ms_step / 1e3) / 1e6

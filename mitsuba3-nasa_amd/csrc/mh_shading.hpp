@@ -54,6 +54,16 @@ MH_DEV bool prim_test(const Prim &p, const RayT &r, float &t, float &u, float &v
     return p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, t, u, v) : tri_test(p, r, t, u, v);
 }
 
+// Reciprocal direction for the slab test.  A zero component (axis-aligned
+// rays) would give inf * 0 = NaN in `o * inv`; it is replaced by a tiny
+// same-signed value, which keeps the (padded, conservative) box test exact
+// in outcome.  The primitive tests still use the true direction.
+MH_DEV float safe_rcp_dir(float d) {
+    const float e = 0x1p-80f;
+    return 1.f / (__builtin_fabsf(d) > e ? d : __builtin_copysignf(e, d));
+}
+MH_DEV V3 safe_inv_dir(V3 d) { return v3(safe_rcp_dir(d.x), safe_rcp_dir(d.y), safe_rcp_dir(d.z)); }
+
 // Slab test for both children; conservative (host pads every box).
 MH_DEV void box2(const Node &n, V3 inv, V3 ood, float tmax, bool &h0, bool &h1, float &t0,
                  float &t1) {
@@ -78,7 +88,7 @@ MH_DEV void box2(const Node &n, V3 inv, V3 ood, float tmax, bool &h0, bool &h1, 
 template <bool Shadow>
 MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32_t stride,
                      const RayT &r, Hit &hit) {
-    V3 inv = v3(rcp(r.d.x), rcp(r.d.y), rcp(r.d.z));
+    V3 inv = safe_inv_dir(r.d);
     V3 ood = r.o * inv;
     float best = r.maxt;
     hit.t = __builtin_huge_valf();
@@ -194,7 +204,7 @@ MH_DEV void trav_init(TravLane &t, const RayT &r, bool empty_scene) {
     t.o = r.o;
     t.d = r.d;
     t.maxt = r.maxt;
-    t.inv = v3(rcp(r.d.x), rcp(r.d.y), rcp(r.d.z));
+    t.inv = safe_inv_dir(r.d);
     t.ood = r.o * t.inv;
     t.best = r.maxt;
     t.node = empty_scene ? kDone : 0u;

@@ -1,0 +1,86 @@
+"""Multi-GPU orchestration of the hot path.
+
+Sample-slab sharding: with N ranks and `spp` samples per pixel per rank, rank
+r renders samples [spp*r, spp*(r+1)) of EVERY pixel of a render at spp*N
+samples per pixel.  The global lane index idx = pixel * spp_total + s (and so
+the TEA seed of every lane, integrator.cpp:323-340) is the one the single-GPU
+render uses, hence the union of the slabs is sample-identical to it.  The
+only coupling is additive:
+
+  forward   film (H, W, 4) RGBW                 -> all-reduce(sum), develop
+  PRB       W image (H, W) of render_backward   -> all-reduce(sum) before the
+            dL gather (common.py:936-947), then each rank's gradient slab
+            -> all-reduce(sum)
+
+One process per GPU; torch.distributed with backend "nccl" (= RCCL over xGMI
+on ROCm), or "gloo" for the CPU tests.  No collective sits inside a kernel
+loop: three all-reduces per step, sized 4 MiB / 1 MiB / 12 B at 512².
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+
+@dataclass
+class Slab:
+    spp_total: int
+    begin: int
+    end: int
+
+
+def sample_slab(rank: int, world: int, spp_per_rank: int) -> Slab:
+    if not (0 <= rank < world) or spp_per_rank <= 0:
+        raise ValueError("sample_slab: bad rank / world / spp")
+    return Slab(spp_per_rank * world, spp_per_rank * rank, spp_per_rank * (rank + 1))
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 else None
+
+
+def all_reduce_(t):
+    """In-place sum over ranks (no-op on one rank)."""
+    d = _dist()
+    if d is not None:
+        d.all_reduce(t)
+    return t
+
+
+@dataclass
+class StepOps:
+    """The hot-path entry points one step calls (the C-ABI wrappers of
+    mitsuba_hip.render on a GPU; the tests substitute the CPU oracle)."""
+    render_film: Callable      # (seed, spp_total, begin, end) -> film tensor (H, W, 4)
+    develop: Callable          # (film) -> image (H, W, 3)
+    prb_weights: Callable      # (seed, spp_total, begin, end) -> W (H, W)
+    render_backward: Callable  # (seed, spp_total, begin, end, weights) -> [grad tensors]
+    seed_grad: Callable        # (seed) -> seed of the differential pass (TEA(seed, 1).v0)
+
+
+def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True):
+    """One benchmark step: forward render of the rank's slab + film
+    all-reduce + develop; then (with_grad) PRB render_backward of the slab
+    with the globally all-reduced W image and an all-reduced gradient."""
+    film = all_reduce_(ops.render_film(seed, slab.spp_total, slab.begin, slab.end))
+    img = ops.develop(film)
+    if not with_grad:
+        return img, None
+    sg = ops.seed_grad(seed)
+    w = all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end))
+    grads: List = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
+    for g in grads:
+        all_reduce_(g)
+    return img, grads
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    """Max of a host float over ranks (the bench's step time)."""
+    d = _dist()
+    if d is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    d.all_reduce(t, op=d.ReduceOp.MAX)
+    return float(t.item())
