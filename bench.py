@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--res", type=int, default=512)
     p.add_argument("--spp", type=int, default=256, help="samples per pixel per GPU")
     p.add_argument("--max-depth", type=int, default=8)
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     p.add_argument("--fwd-only", action="store_true")
     return p.parse_args()
@@ -180,7 +180,7 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": kname, "kernel_avg_us": round(us_per_launch, 1),
                     "algorithmic_bytes_per_launch": round(bytes_launch),
-                    "note": "traversal is VALU-issue bound, not HBM bound (DESIGN.md §4); "
+                    "note": "divergent traversal of an LDS-resident BVH: VALU issue + LDS latency bound, not HBM bound (DESIGN.md §3); "
                             "traffic = PMC FETCH_SIZE*2+WRITE_SIZE per launch from profiles/pmc_traffic.json"}
         cpu = None
         if not args.no_cpu:
