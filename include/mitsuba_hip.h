@@ -70,6 +70,8 @@ enum { MH_EMITTER_AREA = 0, MH_EMITTER_CONSTANT = 1, MH_EMITTER_DIRECTIONAL = 2 
 enum { MH_RFILTER_BOX = 0, MH_RFILTER_GAUSSIAN = 1 };         /* box.cpp, gaussian.cpp */
 enum { MH_MEDIUM_HETEROGENEOUS = 0, MH_MEDIUM_HOMOGENEOUS = 1 };
 enum { MH_PHASE_ISOTROPIC = 0, MH_PHASE_HG = 1 };
+enum { MH_MEDIUM_NO_EMITTER_SAMPLING = 1u,        /* medium.cpp:29 sample_emitters = false */
+       MH_MEDIUM_NO_SPECTRAL_EXTINCTION = 2u };   /* heterogeneous.cpp:161 has_spectral_extinction = false */
 enum { MH_INTEGRATOR_PATH = 0, MH_INTEGRATOR_VOLPATH = 1, MH_INTEGRATOR_PRB = 2 };
 
 /* Flags for mh_render / mh_render_backward / mh_trace_*                   */
@@ -141,7 +143,7 @@ typedef struct mh_medium {
     float albedo[3];            /* constant single-scattering albedo */
     float sigma_t_const;        /* homogeneous: sigma_t (before scale) */
     uint32_t grid_res[3];       /* heterogeneous: sigma_t grid resolution (x, y, z) */
-    uint32_t pad0;
+    uint32_t flags;             /* MH_MEDIUM_NO_EMITTER_SAMPLING | MH_MEDIUM_NO_SPECTRAL_EXTINCTION */
     uint64_t grid_offset;       /* heterogeneous: first float in grid_data[] (z-major: x fastest) */
     float grid_to_local[12];    /* world -> grid-local [0,1]^3 (3x4) */
     float bbox_min[3];          /* world-space AABB of the grid */

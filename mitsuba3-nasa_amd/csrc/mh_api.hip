@@ -83,7 +83,7 @@ struct mh_scene {
     DScene S{};
     // device buffers
     DevBuf nodes, prims, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
-        texcoords, faces, texels;
+        texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     DevBuf wf_ws_prb, wf_partial;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
@@ -230,7 +230,37 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         memcpy(b.frame_t, a.frame_t, 12);
         memcpy(b.frame_n, a.frame_n, 12);
         b.inv_area = a.inv_area;
+        b.interior = a.interior_medium;
+        b.exterior = a.exterior_medium;
+        if ((b.interior != MH_INVALID && b.interior >= desc->n_media) ||
+            (b.exterior != MH_INVALID && b.exterior >= desc->n_media))
+            return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: medium index out of bounds");
     }
+    // ---- media (heterogeneous.cpp / homogeneous.cpp / grid.cpp) ----
+    std::vector<DMedium> meds(desc->n_media);
+    for (uint32_t i = 0; i < desc->n_media; ++i) {
+        const mh_medium &a = desc->media[i];
+        DMedium &b = meds[i];
+        memset(&b, 0, sizeof(b));
+        b.type = a.type; b.phase = a.phase; b.flags = a.flags;
+        b.g = a.g; b.scale = a.scale; b.sigma_t_const = a.sigma_t_const;
+        // m_max_density = m_scale * m_sigmat->max() (heterogeneous.cpp:163), in float
+        b.maj = a.type == MH_MEDIUM_HOMOGENEOUS ? a.sigma_t_const * a.scale : a.scale * a.max_density;
+        memcpy(b.albedo, a.albedo, 12);
+        memcpy(b.res, a.grid_res, 12);
+        b.grid_offset = a.grid_offset;
+        memcpy(b.to_local, a.grid_to_local, sizeof(b.to_local));
+        memcpy(b.bbox_min, a.bbox_min, 12);
+        memcpy(b.bbox_max, a.bbox_max, 12);
+        if (a.type == MH_MEDIUM_HETEROGENEOUS &&
+            (a.grid_res[0] == 0 || a.grid_res[1] == 0 || a.grid_res[2] == 0 ||
+             a.grid_offset + (uint64_t)a.grid_res[0] * a.grid_res[1] * a.grid_res[2] > desc->n_grid))
+            return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: volume grid out of bounds");
+        if (a.phase == MH_PHASE_HG && !(a.g > -1.f && a.g < 1.f))
+            return fail(MH_ERR_INVALID_ARGUMENT, "The asymmetry parameter must lie in the interval (-1, 1)!");
+    }
+    if (desc->sensor.medium != MH_INVALID && desc->sensor.medium >= desc->n_media)
+        return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: sensor medium index out of bounds");
     std::vector<uint32_t> btype(desc->n_bsdfs), btex(desc->n_bsdfs);
     for (uint32_t i = 0; i < desc->n_bsdfs; ++i) {
         btype[i] = desc->bsdfs[i].type;
@@ -258,6 +288,8 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         ems[i].shape = desc->emitters[i].shape;
         memcpy(ems[i].radiance, desc->emitters[i].radiance, 12);
         memcpy(ems[i].direction, desc->emitters[i].direction, 12);
+        memcpy(ems[i].center, desc->emitters[i].scene_center, 12);
+        ems[i].radius = desc->emitters[i].scene_radius;
     }
     s->n_textures = desc->n_textures;
     s->n_bsdfs = desc->n_bsdfs;
@@ -273,6 +305,8 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
               upload(s->texcoords, desc->texcoords, desc->texcoords ? 2ull * desc->n_vertices : 0, st) == hipSuccess &&
               upload(s->faces, desc->faces, 3ull * desc->n_faces, st) == hipSuccess &&
               upload(s->texels, desc->texels, desc->n_texels, st) == hipSuccess &&
+              upload(s->media, meds.data(), meds.size(), st) == hipSuccess &&
+              upload(s->grid, desc->grid_data, desc->n_grid, st) == hipSuccess &&
               s->counters.alloc(64) == hipSuccess;
     if (!ok) return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: device upload failed");
 
@@ -289,6 +323,10 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.texcoords = s->texcoords.as<float>();
     S.faces = s->faces.as<uint32_t>();
     S.texels = s->texels.as<float>();
+    S.media = s->media.as<DMedium>();
+    S.grid = s->grid.as<float>();
+    S.n_media = desc->n_media;
+    S.camera_medium = desc->sensor.medium;
     S.n_nodes = bvh.n_nodes;
     S.n_prims = bvh.n_prims;
     S.n_emitters = desc->n_emitters;
@@ -321,7 +359,7 @@ int mh_scene_destroy(mh_scene *s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (DevBuf *b : {&s->nodes, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
-                      &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
+                      &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -427,9 +465,7 @@ static double now_ms() {
 int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
               uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
     if (!s || !in || !film_rgbw) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: NULL argument");
-    if (in->type == MH_INTEGRATOR_VOLPATH)
-        return set_error(MH_ERR_UNSUPPORTED, "mh_render: 'volpath' is not available in this build");
-    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB)
+    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_VOLPATH)
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: unknown integrator");
     if (in->rr_depth == 0)
         return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
@@ -555,7 +591,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
 int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                       uint32_t spp_begin, uint32_t spp_end, float *out, uint32_t flags) {
     if (!s || !in || !out) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: NULL argument");
-    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB)
+    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_VOLPATH)
         return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: unsupported integrator");
     if (spp == 0 || in->rr_depth == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: bad arguments");
     Layout L;

@@ -40,7 +40,8 @@ struct DShape {                 // shading-time shape record
     uint32_t vertex_offset, has_normals, has_texcoords, pad;
     float to_world[12];
     float frame_s[4], frame_t[4], frame_n[4];
-    float inv_area, pad1, pad2, pad3;
+    float inv_area;
+    uint32_t interior, exterior, pad3;  // media (MH_INVALID = none)
 };
 
 struct DTexture {
@@ -55,6 +56,17 @@ struct DEmitter {
     uint32_t type, shape, pad0, pad1;
     float radiance[4];
     float direction[4];
+    float center[3], radius;   // constant / directional: scene bounding sphere
+};
+
+struct DMedium {
+    uint32_t type, phase, flags, pad0;
+    float g, scale, maj, sigma_t_const;   // maj = scale * max(grid) (heterogeneous.cpp:163)
+    float albedo[4];
+    uint32_t res[4];
+    uint64_t grid_offset, pad1;
+    float to_local[12];
+    float bbox_min[4], bbox_max[4];
 };
 
 struct DScene {                 // kernel argument (by value)
@@ -70,7 +82,10 @@ struct DScene {                 // kernel argument (by value)
     const float *texcoords;
     const uint32_t *faces;
     const float *texels;
+    const DMedium *media;
+    const float *grid;             // volume grid data
     uint32_t n_nodes, n_prims, n_emitters, environment;
+    uint32_t n_media, camera_medium;
     uint32_t stack_size;           // BVH traversal stack entries per lane
     uint32_t lds_bytes_bvh;        // bytes of nodes + prims staged into LDS
     // sensor
@@ -218,6 +233,67 @@ MH_DEV float estrin10(float x, const float *k) {
     float x8 = x4 * x4;
     return __builtin_fmaf(x8, c4, e0);
 }
+MH_DEV float estrin6(float x, float c0, float c1, float c2, float c3, float c4, float c5) {
+    float a0 = __builtin_fmaf(x, c1, c0), a1 = __builtin_fmaf(x, c3, c2), a2 = __builtin_fmaf(x, c5, c4);
+    float x2 = x * x;
+    float b0 = __builtin_fmaf(x2, a1, a0);
+    float x4 = x2 * x2;
+    return __builtin_fmaf(x4, a2, b0);
+}
+
+// Dr.Jit 0.4.4 math.h `exp`, single precision, non-CUDA branch (Cephes range
+// reduction + Estrin polynomial + ldexp by exponent construction)
+MH_DEV float exp_dr(float x) {
+    const bool overflow = x > 88.3762626647949f, underflow = x < -88.3762626647949f;
+    float n = floorf(__builtin_fmaf(1.44269504088896340736f, x, 0.5f));
+    x = __builtin_fmaf(-n, 0.693359375f, x);
+    x = __builtin_fmaf(-n, -2.12194440e-4f, x);
+    float z = estrin6(x, 5.0000001201e-1f, 1.6666665459e-1f, 4.1665795894e-2f, 8.3334519073e-3f,
+                      1.3981999507e-3f, 1.9875691500e-4f);
+    z = __builtin_fmaf(z, x * x, x + 1.0f);
+    z = z * __uint_as_float((uint32_t)((int32_t)n + 127) << 23);
+    if (overflow) z = __builtin_huge_valf();
+    if (underflow) z = 0.f;
+    return z;
+}
+
+// Dr.Jit 0.4.4 math.h `log` (Cephes logf: frexp + polynomial)
+MH_DEV float log_dr(float x) {
+    if (!(x > 0.f)) return x == 0.f ? -__builtin_huge_valf() : __uint_as_float(0xffffffffu);
+    if (x == __builtin_huge_valf()) return x;
+    uint32_t bits = __float_as_uint(x);
+    int e;
+    float xm;
+    if ((bits & 0x7f800000u) == 0) {
+        xm = frexpf(x, &e);
+    } else {
+        e = (int)((bits >> 23) & 0xff) - 126;
+        xm = __uint_as_float((bits & 0x807fffffu) | 0x3f000000u);
+    }
+    if (xm < 0.70710678118654752440f) {
+        e -= 1;
+        xm = xm + xm - 1.0f;
+    } else {
+        xm = xm - 1.0f;
+    }
+    float z = xm * xm;
+    float y = 7.0376836292e-2f;
+    y = __builtin_fmaf(y, xm, -1.1514610310e-1f);
+    y = __builtin_fmaf(y, xm, 1.1676998740e-1f);
+    y = __builtin_fmaf(y, xm, -1.2420140846e-1f);
+    y = __builtin_fmaf(y, xm, 1.4249322787e-1f);
+    y = __builtin_fmaf(y, xm, -1.6668057665e-1f);
+    y = __builtin_fmaf(y, xm, 2.0000714765e-1f);
+    y = __builtin_fmaf(y, xm, -2.4999993993e-1f);
+    y = __builtin_fmaf(y, xm, 3.3333331174e-1f);
+    y = y * xm * z;
+    float fe = (float)e;
+    y = __builtin_fmaf(fe, -2.12194440e-4f, y);
+    y = __builtin_fmaf(z, -0.5f, y);
+    float r = xm + y;
+    return __builtin_fmaf(fe, 0.693359375f, r);
+}
+
 MH_DEV float gaussian_eval(const float *coeff, float x) {
     return fmaxf(estrin10(x * x, coeff), 0.f);
 }

@@ -64,7 +64,8 @@ k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *_
 // Forward render of one chunk: lane k in [0, n) -> samples of every pass.
 // out planes (each `plane` floats apart): Lr, Lg, Lb, posx, posy; sample
 // (k, pass) stored at pass * n + k.
-template <bool Prb, bool InLds>
+// Kind: MH_INTEGRATOR_PATH / MH_INTEGRATOR_PRB (primal) / MH_INTEGRATOR_VOLPATH
+template <int Kind, bool InLds>
 __global__ void __launch_bounds__(256)
 k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_t n_passes,
          uint64_t n, uint64_t plane, float *__restrict__ out, unsigned long long *__restrict__ counters) {
@@ -83,8 +84,12 @@ k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_
             float sx = (float)px + jx, sy = (float)py + jy;
             RayT r = camera_ray(S, __builtin_fmaf(sx, sw, -0.f), __builtin_fmaf(sy, sh, -0.f));
             V3 L;
-            if (Prb) L = prb_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow);
-            else L = path_sample(S, B, in, rng, r, n_closest, n_shadow);
+            if (Kind == MH_INTEGRATOR_PRB)
+                L = prb_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow);
+            else if (Kind == MH_INTEGRATOR_VOLPATH)
+                L = volpath_sample(S, B, in, rng, r, n_closest, n_shadow);
+            else
+                L = path_sample(S, B, in, rng, r, n_closest, n_shadow);
             uint64_t o = (uint64_t)pass * n + k;
             out[o] = L.x;
             out[plane + o] = L.y;
@@ -392,12 +397,17 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
     const uint32_t bs = 256;
     size_t sh = lds_bytes(S, bs);
     if (n == 0) return hipSuccess;
-    const bool prb = in.type == MH_INTEGRATOR_PRB, lds = S.lds_bytes_bvh != 0;
+    const bool lds = S.lds_bytes_bvh != 0;
     const dim3 g(blocks_for(n, bs)), b(bs);
-    if (prb && lds) hipLaunchKernelGGL((k_render<true, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
-    else if (prb) hipLaunchKernelGGL((k_render<true, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
-    else if (lds) hipLaunchKernelGGL((k_render<false, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
-    else hipLaunchKernelGGL((k_render<false, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);
+#define MH_LAUNCH_RENDER(K)                                                                                   \
+    do {                                                                                                      \
+        if (lds) hipLaunchKernelGGL((k_render<K, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters); \
+        else hipLaunchKernelGGL((k_render<K, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);    \
+    } while (0)
+    if (in.type == MH_INTEGRATOR_PRB) MH_LAUNCH_RENDER(MH_INTEGRATOR_PRB);
+    else if (in.type == MH_INTEGRATOR_VOLPATH) MH_LAUNCH_RENDER(MH_INTEGRATOR_VOLPATH);
+    else MH_LAUNCH_RENDER(MH_INTEGRATOR_PATH);
+#undef MH_LAUNCH_RENDER
     return hipGetLastError();
 }
 

@@ -543,6 +543,7 @@ MH_DEV float mis_weight(float a, float b) {
 struct DirS {
     V3 p, n, d;
     float dist, pdf;
+    bool delta;
 };
 
 // AreaLight::pdf_direction (emitters/area.cpp:170-200), Shape::pdf_direction (shape.cpp:377-388)
@@ -575,6 +576,7 @@ MH_DEV V3 area_sample_direction(const DScene &S, uint32_t em, V3 ref_p, float sx
     ds.p = xf_point(sh.to_world, v3(sx * 2.f - 1.f, sy * 2.f - 1.f, 0.f));
     ds.n = ld3(sh.frame_n);
     ds.pdf = sh.inv_area;
+    ds.delta = false;
     ds.d = ds.p - ref_p;
     float dist2 = dot(ds.d, ds.d);
     ds.dist = __builtin_sqrtf(dist2);
@@ -1091,6 +1093,419 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         if (si.valid) depth += 1;
         active = active_next;
     }
+}
+
+// ===========================================================================
+// volpath (integrators/volpath.cpp:95-450) and its plugins: constant /
+// directional emitters, heterogeneous / homogeneous media, grid volume,
+// HG / isotropic phase.  Same operation order as the oracle restatement
+// (oracle/mh_oracle.c, "volpath" section).
+// ===========================================================================
+constexpr float kInv4Pi = 0.07957747154594766788f;
+
+// warp::square_to_uniform_sphere (core/warp.h:250-255)
+MH_DEV V3 square_to_uniform_sphere(float sx, float sy) {
+    float z = __builtin_fmaf(-2.f, sy, 1.f);
+    float r = __builtin_sqrtf(fmaxf(__builtin_fmaf(-z, z, 1.f), 0.f));
+    float s, c;
+    sincos_cephes((2.f * kPi) * sx, s, c);
+    return v3(r * c, r * s, z);
+}
+
+// Emitter::sample_direction: area (area.cpp:118-168), constant
+// (constant.cpp:112-140), directional (directional.cpp:150-175)
+MH_DEV V3 emitter_sample_direction(const DScene &S, uint32_t em, V3 ref_p, float sx, float sy, DirS &ds) {
+    const DEmitter &e = S.emitters[em];
+    if (e.type == MH_EMITTER_AREA) return area_sample_direction(S, em, ref_p, sx, sy, ds);
+    if (e.type == MH_EMITTER_CONSTANT) {
+        V3 d = square_to_uniform_sphere(sx, sy);
+        V3 c = v3(e.center[0], e.center[1], e.center[2]);
+        float radius = fmaxf(e.radius, norm(ref_p - c)), dist = 2.f * radius;
+        ds.p = fma3s(d, dist, ref_p);
+        ds.n = -d;
+        ds.pdf = kInv4Pi;
+        ds.delta = false;
+        ds.d = d;
+        ds.dist = dist;
+        return vdiv(v3(e.radiance[0], e.radiance[1], e.radiance[2]), ds.pdf);
+    }
+    // directional: ds.p = p - d * inf (NaN where d has a zero component, as in the reference)
+    V3 d = v3(e.direction[0], e.direction[1], e.direction[2]);
+    const float dist = __builtin_huge_valf();
+    ds.p = ref_p - d * dist;
+    ds.n = d;
+    ds.pdf = 1.f;
+    ds.delta = true;
+    ds.d = -d;
+    ds.dist = dist;
+    return v3(e.radiance[0], e.radiance[1], e.radiance[2]);
+}
+
+// Scene::sample_emitter_direction without the visibility test (scene.cpp:299-353)
+MH_DEV V3 scene_sample_emitter_direction(const DScene &S, V3 ref_p, float sx, float sy, DirS &ds) {
+    ds.p = ds.n = ds.d = v3(0, 0, 0);
+    ds.dist = ds.pdf = 0.f;
+    ds.delta = false;
+    const uint32_t n = S.n_emitters;
+    if (n == 0) return v3(0, 0, 0);
+    if (n == 1) return emitter_sample_direction(S, 0, ref_p, sx, sy, ds);
+    const float nf = (float)n, scaled = sx * nf;
+    uint32_t idx = (uint32_t)scaled;
+    if (idx > n - 1) idx = n - 1;
+    V3 spec = emitter_sample_direction(S, idx, ref_p, scaled - (float)idx, sy, ds);
+    ds.pdf *= 1.f / nf;
+    return spec * nf;
+}
+
+MH_DEV V3 emitter_eval(const DScene &S, uint32_t em, const SI &si) {
+    const DEmitter &e = S.emitters[em];
+    V3 L = v3(e.radiance[0], e.radiance[1], e.radiance[2]);
+    if (e.type == MH_EMITTER_AREA) return si.wi.z > 0.f ? L : v3(0, 0, 0);
+    if (e.type == MH_EMITTER_CONSTANT) return L;
+    return v3(0, 0, 0);
+}
+
+// Scene::pdf_emitter_direction of DirectionSample3f(scene, si, ref) (scene.cpp:355-366)
+MH_DEV float emitter_pdf_direction(const DScene &S, uint32_t em, const SI &si, V3 ref_p) {
+    const DEmitter &e = S.emitters[em];
+    if (e.type == MH_EMITTER_AREA) return emitter_hit_pdf(S, em, si, ref_p);
+    if (e.type == MH_EMITTER_CONSTANT) return kInv4Pi * (1.f / (float)S.n_emitters);
+    return 0.f;
+}
+
+// ---- media -----------------------------------------------------------------
+struct MEI {
+    bool valid;
+    float t, mint;
+    V3 p, sigma_s;
+    float sigma_n, sigma_t, maj;
+    V3 fs, ft, fn;   // Frame3f(ray.d); wi = (0, 0, -1) local
+};
+
+// [drjit] Texture3f::eval_nonaccel, linear, clamp, 1 channel (grid.cpp:545-558)
+MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
+    V3 q = xf_point(m.to_local, p);
+    const int32_t rx = (int32_t)m.res[0], ry = (int32_t)m.res[1], rz = (int32_t)m.res[2];
+    float px = __builtin_fmaf(q.x, (float)rx, -0.5f), py = __builtin_fmaf(q.y, (float)ry, -0.5f),
+          pz = __builtin_fmaf(q.z, (float)rz, -0.5f);
+    int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py), iz = (int32_t)floorf(pz);
+    float w1x = px - (float)ix, w1y = py - (float)iy, w1z = pz - (float)iz;
+    float w0x = 1.f - w1x, w0y = 1.f - w1y, w0z = 1.f - w1z;
+    const int32_t x0 = min(max(ix, 0), rx - 1), x1 = min(max(ix + 1, 0), rx - 1);
+    const int32_t y0 = min(max(iy, 0), ry - 1), y1 = min(max(iy + 1, 0), ry - 1);
+    const int32_t z0 = min(max(iz, 0), rz - 1), z1 = min(max(iz + 1, 0), rz - 1);
+    const float *g = S.grid + m.grid_offset;
+    const uint64_t sy = (uint64_t)rx, sz = (uint64_t)rx * (uint64_t)ry;
+    const uint64_t b00 = (uint64_t)z0 * sz + (uint64_t)y0 * sy, b10 = (uint64_t)z0 * sz + (uint64_t)y1 * sy;
+    const uint64_t b01 = (uint64_t)z1 * sz + (uint64_t)y0 * sy, b11 = (uint64_t)z1 * sz + (uint64_t)y1 * sy;
+    float v000 = g[b00 + x0], v100 = g[b00 + x1], v010 = g[b10 + x0], v110 = g[b10 + x1];
+    float v001 = g[b01 + x0], v101 = g[b01 + x1], v011 = g[b11 + x0], v111 = g[b11 + x1];
+    float f00 = __builtin_fmaf(w0x, v000, w1x * v100), f01 = __builtin_fmaf(w0x, v001, w1x * v101),
+          f10 = __builtin_fmaf(w0x, v010, w1x * v110), f11 = __builtin_fmaf(w0x, v011, w1x * v111);
+    float f0 = __builtin_fmaf(w0y, f00, w1y * f10), f1 = __builtin_fmaf(w0y, f01, w1y * f11);
+    return __builtin_fmaf(w0z, f0, w1z * f1);
+}
+
+// BoundingBox3f::ray_intersect (core/bbox.h:303-327)
+MH_DEV bool bbox_ray_intersect(const float *mn, const float *mx, const RayT &r, float &mint, float &maxt) {
+    const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    bool active = true;
+    float t1p[3], t2p[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        active = active && (d[i] != 0.f || (o[i] > mn[i] || o[i] < mx[i]));
+        const float rc = 1.f / d[i];
+        const float t1 = (mn[i] - o[i]) * rc, t2 = (mx[i] - o[i]) * rc;
+        t1p[i] = fminf(t1, t2);
+        t2p[i] = fmaxf(t1, t2);
+    }
+    mint = fmaxf(fmaxf(t1p[0], t1p[1]), t1p[2]);
+    maxt = fminf(fminf(t2p[0], t2p[1]), t2p[2]);
+    return active && maxt >= mint;
+}
+
+// Medium::sample_interaction (medium.cpp:40-86)
+MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, float u, MEI &mei) {
+    const DMedium &m = S.media[med];
+    mei.fn = ray.d;
+    coordinate_system(ray.d, mei.fs, mei.ft);
+    float mint, maxt;
+    bool active;
+    if (m.type == MH_MEDIUM_HOMOGENEOUS) {
+        active = true; mint = 0.f; maxt = __builtin_huge_valf();   // homogeneous.cpp:184-187
+    } else {
+        active = bbox_ray_intersect(m.bbox_min, m.bbox_max, ray, mint, maxt);
+    }
+    active = active && (isfinite_(mint) || isfinite_(maxt));
+    if (!active) { mint = 0.f; maxt = __builtin_huge_valf(); }
+    mint = fmaxf(0.f, mint);
+    maxt = fminf(ray.maxt, maxt);
+    const float maj = m.maj;
+    const float sampled_t = mint + (-log_dr(1.f - u) / maj);
+    const bool valid = active && sampled_t <= maxt;
+    mei.valid = valid;
+    mei.t = valid ? sampled_t : __builtin_huge_valf();
+    mei.p = fma3s(ray.d, sampled_t, ray.o);
+    mei.mint = mint;
+    mei.maj = maj;
+    float st = 0.f;
+    if (valid) st = m.type == MH_MEDIUM_HOMOGENEOUS ? m.sigma_t_const * m.scale : m.scale * grid_eval(S, m, mei.p);
+    mei.sigma_t = st;
+    mei.sigma_s = valid ? v3(m.albedo[0], m.albedo[1], m.albedo[2]) * st : v3(0, 0, 0);
+    mei.sigma_n = m.type == MH_MEDIUM_HOMOGENEOUS ? 0.f : maj - st;
+}
+
+MH_DEV V3 mei_to_local(const MEI &m, V3 v) { return v3(dot(v, m.fs), dot(v, m.ft), dot(v, m.fn)); }
+MH_DEV V3 mei_to_world(const MEI &m, V3 v) { return fma3s(m.fn, v.z, fma3s(m.ft, v.y, m.fs * v.x)); }
+
+// HGPhaseFunction (phase/hg.cpp:66-104), IsotropicPhaseFunction
+MH_DEV float eval_hg(float g, float cos_theta) {
+    float temp = (1.f + g * g) + (2.f * g) * cos_theta;
+    return (kInv4Pi * (1.f - g * g)) / (temp * __builtin_sqrtf(temp));
+}
+MH_DEV float phase_eval(const DMedium &m, V3 wo) {
+    if (m.phase == MH_PHASE_HG) return eval_hg(m.g, dot(wo, v3(0.f, 0.f, -1.f)));
+    return kInv4Pi;
+}
+MH_DEV V3 phase_sample(const DMedium &m, float s2x, float s2y, float &pdf) {
+    if (m.phase == MH_PHASE_HG) {
+        const float g = m.g;
+        float sqr_term = (1.f - g * g) / ((1.f - g) + (2.f * g) * s2x);
+        float cos_theta = ((1.f + g * g) - sqr_term * sqr_term) / (2.f * g);
+        if (__builtin_fabsf(g) < 5.9604644775390625e-08f) cos_theta = 1.f - 2.f * s2x;
+        float sin_theta = __builtin_sqrtf(fmaxf(1.f - cos_theta * cos_theta, 0.f));
+        float sp, cp;
+        sincos_cephes((2.f * kPi) * s2y, sp, cp);
+        pdf = eval_hg(g, -cos_theta);
+        return v3(sin_theta * cp, sin_theta * sp, cos_theta);
+    }
+    pdf = kInv4Pi;
+    return square_to_uniform_sphere(s2x, s2y);
+}
+
+MH_DEV bool is_medium_transition(const DScene &S, const SI &si) {
+    if (!si.valid) return false;
+    const DShape &sh = S.shapes[si.shape];
+    return sh.interior != sh.exterior;
+}
+MH_DEV uint32_t target_medium(const DScene &S, const SI &si, V3 d) {
+    const DShape &sh = S.shapes[si.shape];
+    return dot(d, si.n) > 0.f ? sh.exterior : sh.interior;
+}
+
+MH_DEV void trace_si(const DScene &S, const LdsBvh &B, const RayT &ray, SI &si, float &si_t) {
+    Hit h;
+    traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
+    compute_si(S, ray, h, si);
+    si_t = si.valid ? h.t : __builtin_huge_valf();
+}
+
+// volpath.cpp:333-450: emitter sample + ratio-tracked transmittance.
+// ref_n = 0 for medium interactions; si_ref for surfaces (medium transitions).
+MH_DEV V3 vol_sample_emitter(const DScene &S, const LdsBvh &B, V3 ref_p, V3 ref_n, const SI *si_ref,
+                             Pcg &rng, uint32_t medium, DirS &ds, uint32_t &n_shadow) {
+    V3 transmittance = v3(1, 1, 1);
+    const float sx = rng.next_float(), sy = rng.next_float();
+    V3 emitter_val = scene_sample_emitter_direction(S, ref_p, sx, sy, ds);
+    if (ds.pdf == 0.f) return v3(0, 0, 0);
+    RayT ray = spawn_ray_to(ref_p, ref_n, ds.p);
+    const float max_dist = ray.maxt;
+    if (si_ref && is_medium_transition(S, *si_ref)) medium = target_medium(S, *si_ref, ray.d);
+    float total_dist = 0.f;
+    SI si;
+    si.valid = false;
+    float si_t = 0.f;
+    bool needs_intersection = true, active = true;
+    while (active) {
+        const float remaining_dist = max_dist - total_dist;
+        ray.maxt = remaining_dist;
+        if (!(remaining_dist > 0.f)) break;
+        bool escaped_medium = false;
+        bool active_medium = medium != MH_INVALID;
+        bool active_surface = !active_medium;
+        if (active_medium) {
+            const DMedium &m = S.media[medium];
+            MEI mei;
+            sample_interaction(S, medium, ray, rng.next_float(), mei);
+            if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = fminf(mei.t, remaining_dist);
+            if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+            if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+            needs_intersection = needs_intersection && !si.valid;
+            const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+            if (spectral) {
+                const float t = fminf(remaining_dist, fminf(mei.t, si_t)) - mei.mint;
+                const float tr = exp_dr((-t) * mei.maj);
+                const float pdf = (si_t < mei.t || mei.t > remaining_dist) ? tr : tr * mei.maj;
+                transmittance = transmittance * (pdf > 0.f ? tr / pdf : 0.f);
+            }
+            if (mei.t > remaining_dist && mei.valid) total_dist = ds.dist;
+            if (mei.t > remaining_dist) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+            escaped_medium = !mei.valid;
+            active_medium = mei.valid;
+            if (active_medium) {
+                total_dist += mei.t;
+                ray.o = mei.p;
+                si_t = si_t - mei.t;
+                transmittance = transmittance * (spectral ? mei.sigma_n : mei.sigma_n / mei.maj);
+            }
+        }
+        const bool intersect = active_surface && needs_intersection;
+        if (intersect) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+        needs_intersection = needs_intersection && !intersect;
+        active_surface = active_surface || escaped_medium;
+        if (active_surface) total_dist += si_t;
+        active_surface = active_surface && si.valid && !active_medium;
+        if (active_surface) {
+            const uint32_t b = S.shapes[si.shape].bsdf;
+            const float tn = (b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f;
+            transmittance = transmittance * tn;
+            ray = spawn_ray(si.p, si.n, ray.d);
+        }
+        ray.maxt = remaining_dist;
+        needs_intersection = needs_intersection || active_surface;
+        active = (active_medium || active_surface) && nonzero(transmittance);
+        if (active_surface && is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
+    }
+    return transmittance * emitter_val;
+}
+
+MH_DEV V3 volpath_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
+                         RayT ray, uint32_t &n_closest, uint32_t &n_shadow) {
+    float eta = 1.f;
+    V3 throughput = v3(1, 1, 1), result = v3(0, 0, 0);
+    uint32_t medium = S.camera_medium;
+    bool specular_chain = !in.hide_emitters;
+    uint32_t depth = 0;
+    (void)fminf(rng.next_float() * 3.f, 2.f);  // RGB channel (scalar majorants: all channels alike)
+    SI si;
+    si.valid = false;
+    float si_t = 0.f;
+    bool needs_intersection = true;
+    V3 last_p = v3(0, 0, 0);
+    float last_pdf = 1.f;
+    bool active = true;
+    for (;;) {
+        // ---- Russian roulette (volpath.cpp:143-151)
+        active = active && nonzero(throughput);
+        const float q = fminf(hmax(throughput) * (eta * eta), 0.95f);
+        const bool perform_rr = depth > in.rr_depth;
+        if (active) active = rng.next_float() < q || !perform_rr;
+        if (perform_rr) throughput = throughput * rcp(q);
+        active = active && depth < in.max_depth;
+        if (!active) break;
+
+        bool active_medium = medium != MH_INVALID, active_surface = !active_medium;
+        bool act_null = false, act_scatter = false, escaped = false, spectral = false;
+        MEI mei;
+        mei.valid = false;
+        mei.t = __builtin_huge_valf();
+        if (active_medium) {
+            const DMedium &m = S.media[medium];
+            sample_interaction(S, medium, ray, rng.next_float(), mei);
+            if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
+            if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+            needs_intersection = needs_intersection && !si.valid;
+            if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+            spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+            if (spectral) {
+                const float t = fminf(mei.t, si_t) - mei.mint;
+                const float tr = exp_dr((-t) * mei.maj);
+                const float pdf = si_t < mei.t ? tr : tr * mei.maj;
+                throughput = throughput * (pdf > 0.f ? tr / pdf : 0.f);
+            }
+            escaped = !mei.valid;
+            active_medium = mei.valid;
+            bool null_scatter = false;
+            if (active_medium) null_scatter = rng.next_float() >= mei.sigma_t / mei.maj;
+            act_null = null_scatter && active_medium;
+            act_scatter = !act_null && active_medium;
+            if (spectral && act_null) throughput = throughput * ((mei.sigma_n * mei.maj) / mei.sigma_n);
+            if (act_scatter) { depth += 1; last_p = mei.p; }
+        }
+        active = active && depth < in.max_depth;
+        act_scatter = act_scatter && active;
+        if (act_null) { ray.o = mei.p; si_t = si_t - mei.t; }
+        if (act_scatter) {
+            const DMedium &m = S.media[medium];
+            if (spectral) throughput = throughput * vdiv(mei.sigma_s * mei.maj, mei.sigma_t);
+            else throughput = throughput * vdiv(mei.sigma_s, mei.sigma_t);
+            const bool sample_emitters = !(m.flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+            specular_chain = !sample_emitters;
+            if (sample_emitters) {
+                DirS ds;
+                V3 emitted = vol_sample_emitter(S, B, mei.p, v3(0, 0, 0), nullptr, rng, medium, ds, n_shadow);
+                V3 wo = mei_to_local(mei, ds.d);
+                const float ph = phase_eval(m, wo);
+                const float w = mis_weight(ds.pdf, ds.delta ? 0.f : ph);
+                result = result + ((throughput * ph) * emitted) * w;
+            }
+            (void)rng.next_float();
+            const float s2x = rng.next_float(), s2y = rng.next_float();
+            float ph_pdf;
+            V3 wo = phase_sample(m, s2x, s2y, ph_pdf);
+            act_scatter = act_scatter && ph_pdf > 0.f;
+            if (act_scatter) {
+                ray = spawn_ray(mei.p, v3(0, 0, 0), mei_to_world(mei, wo));
+                needs_intersection = true;
+                last_pdf = ph_pdf;
+            }
+        }
+
+        // ---- surface interactions (volpath.cpp:254-326)
+        active_surface = active_surface || escaped;
+        if (active_surface && needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+        if (active_surface) {
+            const bool count_direct = depth == 0 || specular_chain;
+            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+            if (em != MH_INVALID && !(depth == 0 && in.hide_emitters)) {
+                float emitter_pdf = 1.f;
+                if (!count_direct) emitter_pdf = emitter_pdf_direction(S, em, si, last_p);
+                const V3 emitted = emitter_eval(S, em, si);
+                result = result + (count_direct ? throughput * emitted
+                                                : (throughput * mis_weight(last_pdf, emitter_pdf)) * emitted);
+            }
+        }
+        active_surface = active_surface && si.valid;
+        if (active_surface) {
+            const uint32_t b = S.shapes[si.shape].bsdf;
+            const bool is_null = b == MH_INVALID || S.bsdf_type[b] == MH_BSDF_NULL;
+            V3 rho = v3(0, 0, 0);
+            if (!is_null) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+            if (!is_null && depth + 1 < in.max_depth) {
+                DirS ds;
+                V3 emitted = vol_sample_emitter(S, B, si.p, si.n, &si, rng, medium, ds, n_shadow);
+                V3 wo = to_local(si, ds.d);
+                V3 bv;
+                float bp;
+                diffuse_eval_pdf(rho, si.wi, wo, true, bv, bp);
+                const float w = mis_weight(ds.pdf, ds.delta ? 0.f : bp);
+                result = result + ((throughput * bv) * w) * emitted;
+            }
+            (void)rng.next_float();
+            const float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bs_wo, weight;
+            float bs_pdf;
+            if (is_null) {
+                bs_wo = -si.wi; bs_pdf = 1.f; weight = v3(1, 1, 1);
+            } else {
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+            }
+            throughput = throughput * weight;
+            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+            needs_intersection = true;
+            if (!is_null) {
+                depth += 1;
+                last_p = si.p;
+                last_pdf = bs_pdf;
+                specular_chain = false;
+            }
+            if (is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
+        }
+        active = active && (active_surface || active_medium);
+    }
+    return result;
 }
 
 }  // namespace mh

@@ -23,6 +23,7 @@ EMITTER_AREA, EMITTER_CONSTANT, EMITTER_DIRECTIONAL = 0, 1, 2
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
 MEDIUM_HETEROGENEOUS, MEDIUM_HOMOGENEOUS = 0, 1
 PHASE_ISOTROPIC, PHASE_HG = 0, 1
+MEDIUM_NO_EMITTER_SAMPLING, MEDIUM_NO_SPECTRAL_EXTINCTION = 1, 2
 INTEGRATOR_PATH, INTEGRATOR_VOLPATH, INTEGRATOR_PRB = 0, 1, 2
 
 FLAG_DEVICE_POINTERS = 1 << 0
@@ -64,7 +65,7 @@ class Emitter(C.Structure):
 
 class Medium(C.Structure):
     _fields_ = [("type", u32), ("phase", u32), ("g", f32), ("scale", f32), ("albedo", f32 * 3),
-                ("sigma_t_const", f32), ("grid_res", u32 * 3), ("pad0", u32),
+                ("sigma_t_const", f32), ("grid_res", u32 * 3), ("flags", u32),
                 ("grid_offset", u64), ("grid_to_local", f32 * 12), ("bbox_min", f32 * 3),
                 ("bbox_max", f32 * 3), ("max_density", f32), ("pad1", f32)]
 

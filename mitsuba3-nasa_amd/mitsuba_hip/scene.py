@@ -28,6 +28,14 @@ def _f32(x):
     return np.asarray(x, dtype=np.float32)
 
 
+def _normalize32(v):
+    """dr::normalize in float32: v * rsqrt(dot(v, v)), dot as an fmadd chain."""
+    v = _f32(v)
+    d = np.float32(np.float64(v[2]) * np.float64(v[2]) +
+                   np.float64(np.float32(np.float64(v[1]) * np.float64(v[1]) + np.float64(np.float32(v[0] * v[0])))))
+    return (v * np.float32(np.float32(1.0) / np.sqrt(d, dtype=np.float32))).astype(np.float32)
+
+
 # ---------------------------------------------------------------------------
 # Integrators (integrator.cpp:22-28,1281-1298; ad/integrators/common.py:29-41)
 # ---------------------------------------------------------------------------
@@ -177,6 +185,13 @@ class _Builder:
         self.params: Dict[str, Any] = {}   # key -> ("rgb"|"bitmap", texture index)
         self.any_normals = False
         self.any_texcoords = False
+        self.media: List[A.Medium] = []
+        self.medium_ids: Dict[str, int] = {}
+        self.grids: List[np.ndarray] = []
+        self.n_grid = 0
+        self.environment = A.INVALID
+        self.bbox_min = np.full(3, np.inf, np.float32)   # Scene::bbox() over the shapes
+        self.bbox_max = np.full(3, -np.inf, np.float32)
 
     # -- textures ---------------------------------------------------------------
     def texture(self, spec, key_prefix: str, bounded=True) -> int:
@@ -254,6 +269,137 @@ class _Builder:
             return self.bsdf({"type": "diffuse"}, "__default__")
         return self.bsdf_ids["__default__"]
 
+    # -- media (heterogeneous.cpp, homogeneous.cpp, grid.cpp, hg.cpp, isotropic.cpp) ----
+    def medium(self, spec, name: str) -> int:
+        if isinstance(spec, str):
+            spec = {"type": "ref", "id": spec}
+        if spec.get("type") == "ref":
+            ref = spec["id"]
+            if ref not in self.medium_ids:
+                raise RuntimeError(f'Reference "{ref}" not found')
+            return self.medium_ids[ref]
+        if name in self.medium_ids:
+            return self.medium_ids[name]
+        ty = spec.get("type")
+        m = A.Medium()
+        m.grid_offset = 0
+        m.scale = float(np.float32(spec.get("scale", 1.0)))
+        alb = spec.get("albedo", 0.75)
+        if isinstance(alb, dict):
+            if alb.get("type") not in ("rgb", "constvolume"):
+                raise RuntimeError("hip_ad_rgb: only constant albedo volumes are supported")
+            alb = alb.get("value", alb.get("color"))
+        m.albedo[:] = [float(x) for x in _f32(np.broadcast_to(np.asarray(alb, np.float64).reshape(-1), (3,)))]
+        ph = spec.get("phase", {"type": "isotropic"})
+        if ph.get("type") == "hg":
+            g = float(ph.get("g", 0.8))
+            if g >= 1.0 or g <= -1.0:
+                raise RuntimeError("The asymmetry parameter must lie in the interval (-1, 1)!")
+            m.phase, m.g = A.PHASE_HG, float(np.float32(g))
+        elif ph.get("type") == "isotropic":
+            m.phase, m.g = A.PHASE_ISOTROPIC, 0.0
+        else:
+            raise RuntimeError(f'Phase function plugin "{ph.get("type")}" is not available in the hip_ad_rgb variant')
+        m.flags = ((0 if spec.get("sample_emitters", True) else A.MEDIUM_NO_EMITTER_SAMPLING) |
+                   (0 if spec.get("has_spectral_extinction", True) else A.MEDIUM_NO_SPECTRAL_EXTINCTION))
+        st = spec.get("sigma_t", 1.0)
+        if ty == "homogeneous":
+            if isinstance(st, dict):
+                st = st.get("value", st.get("color"))
+            v = np.asarray(st, np.float64).reshape(-1)
+            if v.size != 1 and not np.all(v == v[0]):
+                raise RuntimeError("hip_ad_rgb: spectrally varying sigma_t is not supported")
+            m.type = A.MEDIUM_HOMOGENEOUS
+            m.sigma_t_const = float(np.float32(v[0]))
+        elif ty == "heterogeneous":
+            if not isinstance(st, dict) or st.get("type") != "gridvolume":
+                raise RuntimeError("hip_ad_rgb: heterogeneous media need a 'gridvolume' sigma_t")
+            from .volume import VolumeGrid
+            if "filename" in st:
+                grid = VolumeGrid.read(st["filename"])
+            elif "data" in st:
+                grid = VolumeGrid(st["data"])
+            elif "grid" in st:
+                grid = st["grid"]
+            else:
+                raise RuntimeError("gridvolume: specify 'filename', 'data' or 'grid'")
+            if grid.channel_count() != 1:
+                raise RuntimeError("hip_ad_rgb: sigma_t grids must have one channel")
+            if st.get("filter_type", "trilinear") != "trilinear" or st.get("wrap_mode", "clamp") != "clamp":
+                raise RuntimeError("hip_ad_rgb: gridvolume supports filter_type='trilinear', wrap_mode='clamp'")
+            T = _to_transform(st.get("to_world"))
+            if st.get("use_grid_bbox", False):
+                lo, hi = grid.bbox_min.astype(np.float64), grid.bbox_max.astype(np.float64)
+                T = T @ Transform4f.translate(lo) @ Transform4f.scale(hi - lo)
+            x, y, z = grid.size()
+            m.type = A.MEDIUM_HETEROGENEOUS
+            m.grid_res[:] = [x, y, z]
+            m.grid_offset = self.n_grid
+            inv = np.linalg.inv(T.matrix)
+            m.grid_to_local[:] = [float(v) for v in _f32(inv[:3, :].reshape(-1))]
+            corners = np.array([[i, j, k] for i in (0, 1) for j in (0, 1) for k in (0, 1)], np.float64)
+            wc = np.array([T.transform_point(c) for c in corners], np.float64).astype(np.float32)
+            m.bbox_min[:] = [float(v) for v in wc.min(0)]
+            m.bbox_max[:] = [float(v) for v in wc.max(0)]
+            m.max_density = float(np.float32(st["max_value"])) if "max_value" in st else grid.max()
+            flat = np.ascontiguousarray(grid.data.reshape(-1))
+            self.grids.append(flat)
+            self.n_grid += flat.size
+            self.params[name + ".sigma_t.data"] = ("grid", len(self.media))
+        else:
+            raise RuntimeError(f'Medium plugin "{ty}" is not available in the hip_ad_rgb variant')
+        self.media.append(m)
+        idx = len(self.media) - 1
+        self.medium_ids[name] = idx
+        return idx
+
+    # -- infinite emitters (constant.cpp, directional.cpp) ---------------------------
+    def infinite_emitter(self, spec, name: str):
+        ty = spec.get("type")
+        e = A.Emitter()
+        e.shape = A.INVALID
+        key = "radiance" if ty == "constant" else "irradiance"
+        v = spec.get(key, 1.0)
+        if isinstance(v, dict):
+            v = v.get("value", v.get("color"))
+        e.radiance[:] = [float(x) for x in _f32(np.broadcast_to(np.asarray(v, np.float64).reshape(-1), (3,)))]
+        if ty == "constant":
+            if self.environment != A.INVALID:
+                raise RuntimeError("Only one environment emitter can be specified per scene.")
+            e.type = A.EMITTER_CONSTANT
+            self.environment = len(self.emitters)
+        elif ty == "directional":
+            if "to_world" in spec:
+                raise RuntimeError("hip_ad_rgb: directional emitters take 'direction' (not 'to_world')")
+            d = _normalize32(_normalize32(_f32(spec.get("direction", [0.0, 0.0, 1.0]))))
+            e.type = A.EMITTER_DIRECTIONAL
+            e.direction[:] = [float(x) for x in d]
+        else:
+            raise RuntimeError(f'Emitter plugin "{ty}" is not available in the hip_ad_rgb variant')
+        self.params[f"{name}.{key}.value"] = ("emitter_radiance", len(self.emitters))
+        self.emitters.append(e)
+
+    def _expand_bbox(self, pts):
+        pts = _f32(pts).reshape(-1, 3)
+        self.bbox_min = np.minimum(self.bbox_min, pts.min(0))
+        self.bbox_max = np.maximum(self.bbox_max, pts.max(0))
+
+    def finalize(self):
+        """Emitter::set_scene (constant.cpp:76-85, directional.cpp:100-110):
+        bounding sphere of Scene::bbox(), radius = max(RayEps, r (1 + RayEps))."""
+        ray_eps = np.float32(1500.0) * np.float32(2.0 ** -24)
+        if np.all(self.bbox_min <= self.bbox_max):
+            c = (self.bbox_max + self.bbox_min) * np.float32(0.5)
+            dd = (c - self.bbox_max).astype(np.float32)
+            r = np.sqrt(np.float32(dd[2] * dd[2]) + np.float32(dd[1] * dd[1]) + np.float32(dd[0] * dd[0]), dtype=np.float32)
+            r = max(ray_eps, np.float32(r * np.float32(1 + ray_eps)))
+        else:
+            c, r = np.zeros(3, np.float32), np.float32(1.0)
+        for e in self.emitters:
+            if e.type in (A.EMITTER_CONSTANT, A.EMITTER_DIRECTIONAL):
+                e.scene_center[:] = [float(x) for x in c]
+                e.scene_radius = float(r)
+
     # -- shapes ---------------------------------------------------------------------
     def shape(self, spec, name: str):
         ty = spec.get("type")
@@ -263,6 +409,10 @@ class _Builder:
         s = A.Shape()
         s.emitter = A.INVALID
         s.interior_medium = s.exterior_medium = A.INVALID
+        if spec.get("interior") is not None:
+            s.interior_medium = self.medium(spec["interior"], name + ".interior_medium")
+        if spec.get("exterior") is not None:
+            s.exterior_medium = self.medium(spec["exterior"], name + ".exterior_medium")
         bspec = spec.get("bsdf")
         s.bsdf = self.bsdf(bspec, name + ".bsdf") if bspec is not None else self.default_bsdf()
         if ty == "rectangle":
@@ -281,6 +431,7 @@ class _Builder:
             s.frame_n[:] = [float(x) for x in _f32(n)]
             area = np.linalg.norm(np.cross(_f32(dp_du).astype(np.float64), _f32(dp_dv).astype(np.float64)))
             s.inv_area = float(np.float32(1.0 / area))
+            self._expand_bbox([T.transform_point([x, y, 0.0]) for x in (-1.0, 1.0) for y in (-1.0, 1.0)])
         elif ty in ("cube", "mesh"):
             if ty == "cube":
                 V = np.array([T.transform_point(p) for p in _CUBE_V])
@@ -305,6 +456,7 @@ class _Builder:
             s.has_normals = int(N is not None)
             s.has_texcoords = int(UV is not None)
             self.positions.append(_f32(V))
+            self._expand_bbox(V)
             self.normals.append(_f32(N) if N is not None else np.zeros((len(V), 3), np.float32))
             self.texcoords.append(_f32(UV) if UV is not None else np.zeros((len(V), 2), np.float32))
             self.faces.append(F)
@@ -351,11 +503,12 @@ class Scene:
         self.params = builder.params
         self.shape_names = builder.shape_names
         b = builder
+        b.finalize()
         self._shapes = (A.Shape * max(len(b.shapes), 1))(*b.shapes)
         self._bsdfs = (A.Bsdf * max(len(b.bsdfs), 1))(*b.bsdfs)
         self._textures = (A.Texture * max(len(b.textures), 1))(*b.textures)
         self._emitters = (A.Emitter * max(len(b.emitters), 1))(*b.emitters)
-        self._media = (A.Medium * 1)()
+        self._media = (A.Medium * max(len(b.media), 1))(*b.media)
         cat = lambda xs, w, dt: (np.ascontiguousarray(np.concatenate(xs).reshape(-1)).astype(dt)
                                  if xs else np.zeros(w, dt))
         self.positions = cat(b.positions, 3, np.float32)
@@ -363,12 +516,12 @@ class Scene:
         self.texcoords = cat(b.texcoords, 2, np.float32)
         self.faces = cat(b.faces, 3, np.uint32)
         self.texels = cat(b.texels, 1, np.float32)
-        self.grid = np.zeros(1, np.float32)
+        self.grid = cat(b.grids, 1, np.float32)
         d = A.SceneDesc()
         d.abi_version = A.ABI_VERSION
         d.sensor = sensor
         d.n_shapes, d.n_bsdfs, d.n_textures = len(b.shapes), len(b.bsdfs), len(b.textures)
-        d.n_emitters, d.n_media = len(b.emitters), 0
+        d.n_emitters, d.n_media = len(b.emitters), len(b.media)
         d.n_vertices, d.n_faces = b.n_vertices, b.n_faces
         d.shapes = C.cast(self._shapes, C.POINTER(A.Shape))
         d.bsdfs = C.cast(self._bsdfs, C.POINTER(A.Bsdf))
@@ -382,8 +535,8 @@ class Scene:
         d.texels = self.texels.ctypes.data_as(A.PF)
         d.n_texels = b.n_texels
         d.grid_data = self.grid.ctypes.data_as(A.PF)
-        d.n_grid = 0
-        d.environment = A.INVALID
+        d.n_grid = b.n_grid
+        d.environment = b.environment
         self.desc = d
         self._handles: Dict[int, C.c_void_p] = {}
         self._streams: Dict[int, Any] = {}
@@ -512,6 +665,8 @@ def load_dict(d: Dict[str, Any]):
             continue
         if v.get("type") in ("diffuse", "null"):
             b.bsdf(v, k)
+        elif v.get("type") in ("heterogeneous", "homogeneous"):
+            b.medium(v, k)
     for k, v in d.items():
         if k == "type" or not isinstance(v, dict):
             continue
@@ -522,9 +677,13 @@ def load_dict(d: Dict[str, Any]):
             if sensor is not None:
                 raise RuntimeError("hip_ad_rgb: multiple sensors are not supported")
             sensor = _sensor(v)
+            if v.get("medium") is not None:
+                sensor.medium = b.medium(v["medium"], k + ".medium")
         elif vt in ("rectangle", "cube", "mesh"):
             b.shape(v, k)
-        elif vt in ("diffuse", "null"):
+        elif vt in ("constant", "directional"):
+            b.infinite_emitter(v, k)
+        elif vt in ("diffuse", "null", "heterogeneous", "homogeneous"):
             pass
         else:
             raise RuntimeError(f'Plugin "{vt}" is not available in the hip_ad_rgb variant')

@@ -1187,6 +1187,498 @@ static inline void lane_pixel(const wf_layout *L, uint32_t lane, uint32_t *px, u
     *px = pixel - L->W * *py;
 }
 
+/* ======================================================================== */
+/* volpath (src/integrators/volpath.cpp:95-450) and its plugins             */
+/* ======================================================================== */
+
+/* Dr.Jit 0.4.4 math.h `exp` (single precision, non-CUDA branch): Cephes
+   range reduction e^x = e^g 2^n, Estrin polynomial, ldexp, over/underflow
+   masks.  Restated from the published algorithm (parity unpinned).       */
+static inline float estrin6(float x, float c0, float c1, float c2, float c3, float c4, float c5) {
+    float a0 = fmaf(x, c1, c0), a1 = fmaf(x, c3, c2), a2 = fmaf(x, c5, c4);
+    float x2 = x * x;
+    float b0 = fmaf(x2, a1, a0), b1 = a2;
+    float x4 = x2 * x2;
+    return fmaf(x4, b1, b0);
+}
+float oracle_exp(float x) {
+    const int overflow = x > 88.3762626647949f, underflow = x < -88.3762626647949f;
+    float n = floorf(fmaf(1.44269504088896340736f, x, 0.5f));
+    x = fmaf(-n, 0.693359375f, x);
+    x = fmaf(-n, -2.12194440e-4f, x);
+    float z = estrin6(x, 5.0000001201e-1f, 1.6666665459e-1f, 4.1665795894e-2f, 8.3334519073e-3f,
+                      1.3981999507e-3f, 1.9875691500e-4f);
+    z = fmaf(z, x * x, x + 1.0f);
+    /* ldexp_finite: multiply by 2^n built from the exponent field */
+    int32_t ni = (int32_t)n;
+    z = z * u2f((uint32_t)(ni + 127) << 23);
+    if (overflow) z = INFINITY;
+    if (underflow) z = 0.f;
+    return z;
+}
+
+/* warp::square_to_uniform_sphere (core/warp.h:250-255) */
+static inline v3 square_to_uniform_sphere(float sx, float sy) {
+    float z = fmaf(-2.f, sy, 1.f);
+    float r = safe_sqrtf(fmaf(-z, z, 1.f));
+    float s, c;
+    oracle_sincos((2.f * PI_F) * sx, &s, &c);
+    return V3(r * c, r * s, z);
+}
+
+/* Emitter::sample_direction for the three emitter plugins of the path:
+   area (area.cpp:118-168), constant (constant.cpp:112-140),
+   directional (directional.cpp:150-175).                                   */
+static v3 emitter_sample_direction(const mh_scene_desc *d, uint32_t em, v3 ref_p, float sx,
+                                   float sy, dir_sample *ds) {
+    const mh_emitter *e = &d->emitters[em];
+    if (e->type == MH_EMITTER_AREA) return area_sample_direction(d, em, ref_p, sx, sy, ds);
+    if (e->type == MH_EMITTER_CONSTANT) {
+        v3 dd = square_to_uniform_sphere(sx, sy);
+        v3 c = vload(e->scene_center);
+        float radius = fmaxf(e->scene_radius, vnorm(vsub(ref_p, c))), dist = 2.f * radius;
+        ds->p = vfma_s(dd, dist, ref_p);
+        ds->n = vneg(dd);
+        ds->pdf = INV_4PI_F;
+        ds->delta = 0;
+        ds->d = dd;
+        ds->dist = dist;
+        return vdivs(vload(e->radiance), ds->pdf);
+    }
+    /* directional: ds.p = p - d * inf (NaN where d has a zero component) */
+    v3 dd = vload(e->direction);
+    float dist = INFINITY;
+    ds->p = vsub(ref_p, vscale(dd, dist));
+    ds->n = dd;
+    ds->pdf = 1.f;
+    ds->delta = 1;
+    ds->d = vneg(dd);
+    ds->dist = dist;
+    return vload(e->radiance);
+}
+
+/* Scene::sample_emitter_direction without the visibility test
+   (scene.cpp:299-353): uniform emitter selection when there are several. */
+static v3 scene_sample_emitter_direction(const mh_scene_desc *d, v3 ref_p, float sx, float sy,
+                                         dir_sample *ds) {
+    memset(ds, 0, sizeof(*ds));
+    uint32_t n = d->n_emitters;
+    if (n == 0) return V3(0, 0, 0);
+    if (n == 1) return emitter_sample_direction(d, 0, ref_p, sx, sy, ds);
+    float nf = (float)n, scaled = sx * nf;
+    uint32_t idx = (uint32_t)scaled;
+    if (idx > n - 1) idx = n - 1;
+    float sx_re = scaled - (float)idx;
+    v3 spec = emitter_sample_direction(d, idx, ref_p, sx_re, sy, ds);
+    ds->pdf *= 1.f / nf;
+    return vscale(spec, nf);
+}
+
+/* Emitter::eval at a surface hit / escaped ray */
+static v3 emitter_eval(const mh_scene_desc *d, uint32_t em, const surf_int *si) {
+    const mh_emitter *e = &d->emitters[em];
+    if (e->type == MH_EMITTER_AREA) return si->wi.z > 0.f ? vload(e->radiance) : V3(0, 0, 0);
+    if (e->type == MH_EMITTER_CONSTANT) return vload(e->radiance);
+    return V3(0, 0, 0);
+}
+
+/* Scene::pdf_emitter_direction (scene.cpp:355-366) of DirectionSample3f(scene, si, ref) */
+static float emitter_pdf_direction(const mh_scene_desc *d, uint32_t em, const surf_int *si,
+                                   v3 ref_p) {
+    const mh_emitter *e = &d->emitters[em];
+    float pmf = 1.f / (float)d->n_emitters;
+    if (e->type == MH_EMITTER_AREA) return emitter_hit_pdf(d, em, si, ref_p);
+    if (e->type == MH_EMITTER_CONSTANT) return INV_4PI_F * pmf;
+    return 0.f;
+}
+
+/* ---- media: Medium::sample_interaction (medium.cpp:40-86) ---------------- */
+typedef struct {
+    int valid;
+    float t, mint;
+    v3 p;
+    v3 sigma_s;
+    float sigma_n, sigma_t, maj;
+    v3 fs, ft, fn; /* sh_frame = Frame3f(ray.d); wi = (0, 0, -1) local */
+} med_int;
+
+/* [drjit] Texture3f::eval_nonaccel, linear filter, clamp wrap, 1 channel
+   (grid.cpp:545-558; weight form as grid.cpp:502-516)                      */
+static float grid_eval(const mh_scene_desc *d, const mh_medium *m, v3 p) {
+    v3 q = xf_point(m->grid_to_local, p);
+    const int32_t rx = (int32_t)m->grid_res[0], ry = (int32_t)m->grid_res[1], rz = (int32_t)m->grid_res[2];
+    float px = fmaf(q.x, (float)rx, -0.5f), py = fmaf(q.y, (float)ry, -0.5f), pz = fmaf(q.z, (float)rz, -0.5f);
+    int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py), iz = (int32_t)floorf(pz);
+    float w1x = px - (float)ix, w1y = py - (float)iy, w1z = pz - (float)iz;
+    float w0x = 1.f - w1x, w0y = 1.f - w1y, w0z = 1.f - w1z;
+#define CL(i, r) ((i) < 0 ? 0 : ((i) > (r) - 1 ? (r) - 1 : (i)))
+    int32_t x0 = CL(ix, rx), x1 = CL(ix + 1, rx), y0 = CL(iy, ry), y1 = CL(iy + 1, ry),
+            z0 = CL(iz, rz), z1 = CL(iz + 1, rz);
+#undef CL
+    const float *g = d->grid_data + m->grid_offset;
+#define V(x, y, z) g[((size_t)(z) * (size_t)ry + (size_t)(y)) * (size_t)rx + (size_t)(x)]
+    float v000 = V(x0, y0, z0), v100 = V(x1, y0, z0), v010 = V(x0, y1, z0), v110 = V(x1, y1, z0);
+    float v001 = V(x0, y0, z1), v101 = V(x1, y0, z1), v011 = V(x0, y1, z1), v111 = V(x1, y1, z1);
+#undef V
+    float f00 = fmaf(w0x, v000, w1x * v100), f01 = fmaf(w0x, v001, w1x * v101),
+          f10 = fmaf(w0x, v010, w1x * v110), f11 = fmaf(w0x, v011, w1x * v111);
+    float f0 = fmaf(w0y, f00, w1y * f10), f1 = fmaf(w0y, f01, w1y * f11);
+    return fmaf(w0z, f0, w1z * f1);
+}
+
+/* BoundingBox3f::ray_intersect (core/bbox.h:303-327) */
+static int bbox_ray_intersect(const float *mn, const float *mx, const ray3 *r, float *mint, float *maxt) {
+    float o[3] = {r->o.x, r->o.y, r->o.z}, dd[3] = {r->d.x, r->d.y, r->d.z};
+    int active = 1;
+    float t1p[3], t2p[3];
+    for (int i = 0; i < 3; ++i) {
+        active = active && (dd[i] != 0.f || (o[i] > mn[i] || o[i] < mx[i]));
+        float rc = 1.f / dd[i];
+        float t1 = (mn[i] - o[i]) * rc, t2 = (mx[i] - o[i]) * rc;
+        t1p[i] = fminf(t1, t2);
+        t2p[i] = fmaxf(t1, t2);
+    }
+    *mint = fmaxf(fmaxf(t1p[0], t1p[1]), t1p[2]);
+    *maxt = fminf(fminf(t2p[0], t2p[1]), t2p[2]);
+    return active && *maxt >= *mint;
+}
+
+static inline float medium_majorant(const mh_medium *m) {
+    if (m->type == MH_MEDIUM_HOMOGENEOUS) return m->sigma_t_const * m->scale;
+    return m->scale * m->max_density;
+}
+
+static void sample_interaction(const mh_scene_desc *d, uint32_t med, const ray3 *ray, float u,
+                               uint32_t channel, med_int *mei) {
+    const mh_medium *m = &d->media[med];
+    (void)channel; /* scalar majorant: index_spectrum picks the same value */
+    mei->fn = ray->d;
+    coordinate_system(ray->d, &mei->fs, &mei->ft);
+    float mint, maxt;
+    int active;
+    if (m->type == MH_MEDIUM_HOMOGENEOUS) {
+        active = 1; mint = 0.f; maxt = INFINITY;            /* homogeneous.cpp:184-187 */
+    } else {
+        active = bbox_ray_intersect(m->bbox_min, m->bbox_max, ray, &mint, &maxt);
+    }
+    active = active && (isfinitef_(mint) || isfinitef_(maxt));
+    if (!active) { mint = 0.f; maxt = INFINITY; }
+    mint = fmaxf(0.f, mint);
+    maxt = fminf(ray->maxt, maxt);
+    float maj = medium_majorant(m);
+    float sampled_t = mint + (-oracle_log(1.f - u) / maj);
+    int valid = active && sampled_t <= maxt;
+    mei->valid = valid;
+    mei->t = valid ? sampled_t : INFINITY;
+    mei->p = vfma_s(ray->d, sampled_t, ray->o);
+    mei->mint = mint;
+    mei->maj = maj;
+    /* get_scattering_coefficients (heterogeneous.cpp:188-200 / homogeneous.cpp:166-182) */
+    float st = 0.f;
+    if (valid) st = m->type == MH_MEDIUM_HOMOGENEOUS ? m->sigma_t_const * m->scale
+                                                      : m->scale * grid_eval(d, m, mei->p);
+    mei->sigma_t = st;
+    mei->sigma_s = vscale(vload(m->albedo), st);
+    if (!valid) mei->sigma_s = V3(0, 0, 0);
+    mei->sigma_n = m->type == MH_MEDIUM_HOMOGENEOUS ? 0.f : maj - st;
+}
+
+static inline v3 mei_to_local(const med_int *m, v3 v) {
+    return V3(vdot(v, m->fs), vdot(v, m->ft), vdot(v, m->fn));
+}
+static inline v3 mei_to_world(const med_int *m, v3 v) {
+    return vfma_s(m->fn, v.z, vfma_s(m->ft, v.y, vscale(m->fs, v.x)));
+}
+
+/* HGPhaseFunction (phase/hg.cpp:66-104), IsotropicPhaseFunction (isotropic.cpp) */
+static inline float eval_hg(float g, float cos_theta) {
+    float temp = (1.f + g * g) + (2.f * g) * cos_theta;
+    return (INV_4PI_F * (1.f - g * g)) / (temp * sqrtf(temp));
+}
+static float phase_eval(const mh_medium *m, v3 wo) {
+    if (m->phase == MH_PHASE_HG) return eval_hg(m->g, vdot(wo, V3(0.f, 0.f, -1.f)));
+    return INV_4PI_F;
+}
+static v3 phase_sample(const mh_medium *m, float s2x, float s2y, float *pdf) {
+    if (m->phase == MH_PHASE_HG) {
+        float g = m->g;
+        float sqr_term = (1.f - g * g) / ((1.f - g) + (2.f * g) * s2x);
+        float cos_theta = ((1.f + g * g) - sqr_term * sqr_term) / (2.f * g);
+        if (fabsf(g) < 5.9604644775390625e-08f) cos_theta = 1.f - 2.f * s2x;
+        float sin_theta = safe_sqrtf(1.f - cos_theta * cos_theta);
+        float sp, cp;
+        oracle_sincos((2.f * PI_F) * s2y, &sp, &cp);
+        *pdf = eval_hg(g, -cos_theta);
+        return V3(sin_theta * cp, sin_theta * sp, cos_theta);
+    }
+    *pdf = INV_4PI_F;
+    return square_to_uniform_sphere(s2x, s2y);
+}
+
+static inline int is_medium_transition(const mh_scene_desc *d, const surf_int *si) {
+    if (!si->valid) return 0;
+    const mh_shape *sh = &d->shapes[si->shape];
+    return sh->interior_medium != sh->exterior_medium;
+}
+/* SurfaceInteraction::target_medium: dot(d, n) > 0 ? exterior : interior */
+static inline uint32_t target_medium(const mh_scene_desc *d, const surf_int *si, v3 dir) {
+    const mh_shape *sh = &d->shapes[si->shape];
+    return vdot(dir, si->n) > 0.f ? sh->exterior_medium : sh->interior_medium;
+}
+
+static inline float index_spectrum(v3 s, uint32_t ch) { return ch == 1 ? s.y : (ch == 2 ? s.z : s.x); }
+
+/* volpath.cpp:333-450: emitter sample + ratio-tracked transmittance.
+   ref_n = 0 for medium interactions.  si_ref != NULL for surfaces.        */
+static v3 vol_sample_emitter(const scene_view *sv, v3 ref_p, v3 ref_n, const surf_int *si_ref,
+                             pcg32 *rng, uint32_t medium, uint32_t channel, dir_sample *ds,
+                             uint64_t *counters) {
+    const mh_scene_desc *d = sv->d;
+    v3 transmittance = V3(1, 1, 1);
+    float sx = pcg_float(rng), sy = pcg_float(rng);
+    v3 emitter_val = scene_sample_emitter_direction(d, ref_p, sx, sy, ds);
+    if (ds->pdf == 0.f) return V3(0, 0, 0);
+    ray3 ray = spawn_ray_to(ref_p, ref_n, ds->p);
+    float max_dist = ray.maxt;
+    if (si_ref && is_medium_transition(d, si_ref)) medium = target_medium(d, si_ref, ray.d);
+    float total_dist = 0.f;
+    surf_int si;
+    memset(&si, 0, sizeof(si));
+    si.t = 0.f;
+    int needs_intersection = 1, active = 1;
+    while (active) {
+        float remaining_dist = max_dist - total_dist;
+        ray.maxt = remaining_dist;
+        active = active && remaining_dist > 0.f;
+        if (!active) break;
+        int escaped_medium = 0;
+        int active_medium = medium != MH_INVALID;
+        int active_surface = !active_medium;
+        med_int mei;
+        memset(&mei, 0, sizeof(mei));
+        mei.t = INFINITY;
+        if (active_medium) {
+            const mh_medium *m = &d->media[medium];
+            sample_interaction(d, medium, &ray, pcg_float(rng), channel, &mei);
+            if (m->type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = fminf(mei.t, remaining_dist);
+            if (needs_intersection) {
+                pi_rec pi;
+                trace_closest(sv, &ray, &pi);
+                if (counters) counters[1]++;
+                compute_si(d, &ray, &pi, &si);
+            }
+            if (si.t < mei.t) { mei.t = INFINITY; mei.valid = 0; }
+            needs_intersection = needs_intersection && !si.valid;
+            /* has_spectral_extinction (heterogeneous.cpp:161, homogeneous.cpp:143) */
+            const int spectral = !(m->flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+            if (spectral) {
+                float t = fminf(remaining_dist, fminf(mei.t, si.t)) - mei.mint;
+                float tr = oracle_exp((-t) * mei.maj);
+                float pdf = (si.t < mei.t || mei.t > remaining_dist) ? tr : tr * mei.maj;
+                float f = pdf > 0.f ? tr / pdf : 0.f;
+                transmittance = vscale(transmittance, f);
+            }
+            if (mei.t > remaining_dist && mei.valid) total_dist = ds->dist;
+            if (mei.t > remaining_dist) { mei.t = INFINITY; mei.valid = 0; }
+            escaped_medium = !mei.valid;
+            active_medium = mei.valid;
+            if (active_medium) {
+                total_dist += mei.t;
+                ray.o = mei.p;
+                si.t = si.t - mei.t;
+                if (spectral) transmittance = vscale(transmittance, mei.sigma_n);
+                else transmittance = vscale(transmittance, mei.sigma_n / mei.maj);
+            }
+        }
+        int intersect = active_surface && needs_intersection;
+        if (intersect) {
+            pi_rec pi;
+            trace_closest(sv, &ray, &pi);
+            if (counters) counters[1]++;
+            compute_si(d, &ray, &pi, &si);
+        }
+        needs_intersection = needs_intersection && !intersect;
+        active_surface = active_surface || escaped_medium;
+        if (active_surface) total_dist += si.t;
+        active_surface = active_surface && si.valid && !active_medium;
+        if (active_surface) {
+            uint32_t b = si_bsdf(d, &si);
+            /* eval_null_transmission: null -> 1, diffuse -> 0 */
+            float tn = (b != MH_INVALID && d->bsdfs[b].type == MH_BSDF_NULL) ? 1.f : 0.f;
+            transmittance = vscale(transmittance, tn);
+            ray = spawn_ray(si.p, si.n, ray.d);
+        }
+        ray.maxt = remaining_dist;
+        needs_intersection = needs_intersection || active_surface;
+        active = (active_medium || active_surface) &&
+                 (transmittance.x != 0.f || transmittance.y != 0.f || transmittance.z != 0.f);
+        if (active_surface && is_medium_transition(d, &si)) medium = target_medium(d, &si, ray.d);
+    }
+    return vmul(transmittance, emitter_val);
+}
+
+static inline float mis_weight_vol(float a, float b) { return mis_weight(a, b); } /* volpath.cpp:463-468 */
+
+static v3 volpath_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
+                         int *valid_out, uint64_t *counters) {
+    const mh_scene_desc *d = sv->d;
+    int valid_ray = !in->hide_emitters && d->environment != MH_INVALID;
+    float eta = 1.f;
+    v3 throughput = V3(1, 1, 1), result = V3(0, 0, 0);
+    uint32_t medium = d->sensor.medium;
+    int specular_chain = !in->hide_emitters;
+    uint32_t depth = 0;
+    uint32_t channel = (uint32_t)fminf(pcg_float(rng) * 3.f, 2.f);
+    surf_int si;
+    memset(&si, 0, sizeof(si));
+    int needs_intersection = 1;
+    v3 last_p = V3(0, 0, 0);
+    float last_pdf = 1.f;
+    int active = 1;
+    for (;;) {
+        /* ---- Russian roulette (volpath.cpp:143-151) ---- */
+        active = active && (throughput.x != 0.f || throughput.y != 0.f || throughput.z != 0.f);
+        float q = fminf(vmax(throughput) * (eta * eta), 0.95f);
+        int perform_rr = depth > in->rr_depth;
+        if (active) active = pcg_float(rng) < q || !perform_rr;
+        if (perform_rr) throughput = vscale(throughput, rcpf_(q));
+        active = active && depth < in->max_depth;
+        if (!active) break;
+
+        int active_medium = medium != MH_INVALID, active_surface = !active_medium;
+        int act_null = 0, act_scatter = 0, escaped = 0, spectral = 0;
+        med_int mei;
+        memset(&mei, 0, sizeof(mei));
+        mei.t = INFINITY;
+        if (active_medium) {
+            const mh_medium *m = &d->media[medium];
+            sample_interaction(d, medium, &ray, pcg_float(rng), channel, &mei);
+            if (m->type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
+            if (needs_intersection) {
+                pi_rec pi;
+                trace_closest(sv, &ray, &pi);
+                if (counters) counters[0]++;
+                compute_si(d, &ray, &pi, &si);
+            }
+            needs_intersection = needs_intersection && !si.valid;
+            if (si.t < mei.t) { mei.t = INFINITY; mei.valid = 0; }
+            spectral = !(m->flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+            if (spectral) {
+                float t = fminf(mei.t, si.t) - mei.mint;
+                float tr = oracle_exp((-t) * mei.maj);
+                float pdf = si.t < mei.t ? tr : tr * mei.maj;
+                float f = pdf > 0.f ? tr / pdf : 0.f;
+                throughput = vscale(throughput, f);
+            }
+            escaped = !mei.valid;
+            active_medium = mei.valid;
+            int null_scatter = 0;
+            if (active_medium) null_scatter = pcg_float(rng) >= mei.sigma_t / mei.maj;
+            act_null = null_scatter && active_medium;
+            act_scatter = !act_null && active_medium;
+            if (spectral && act_null) throughput = vscale(throughput, (mei.sigma_n * mei.maj) / mei.sigma_n);
+            if (act_scatter) { depth += 1; last_p = mei.p; }
+        }
+        active = active && depth < in->max_depth;
+        act_scatter = act_scatter && active;
+        if (act_null) { ray.o = mei.p; si.t = si.t - mei.t; }
+        if (act_scatter) {
+            const mh_medium *m = &d->media[medium];
+            v3 ss = mei.sigma_s;
+            if (spectral) throughput = vmul(throughput, vdivs(vscale(ss, mei.maj), mei.sigma_t));
+            else throughput = vmul(throughput, vdivs(ss, mei.sigma_t));
+            int sample_emitters = !(m->flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+            valid_ray = 1;
+            specular_chain = !sample_emitters;
+            if (sample_emitters) {
+                dir_sample ds;
+                v3 emitted = vol_sample_emitter(sv, mei.p, V3(0, 0, 0), NULL, rng, medium, channel, &ds, counters);
+                v3 wo = mei_to_local(&mei, ds.d);
+                float ph = phase_eval(m, wo);
+                float w = mis_weight_vol(ds.pdf, ds.delta ? 0.f : ph);
+                result = vadd(result, vscale(vmul(vscale(throughput, ph), emitted), w));
+            }
+            (void)pcg_float(rng);
+            float s2x = pcg_float(rng), s2y = pcg_float(rng);
+            float ph_pdf;
+            v3 wo = phase_sample(m, s2x, s2y, &ph_pdf);
+            throughput = vscale(throughput, 1.f);
+            act_scatter = act_scatter && ph_pdf > 0.f;
+            if (act_scatter) {
+                ray = spawn_ray(mei.p, V3(0, 0, 0), mei_to_world(&mei, wo));
+                needs_intersection = 1;
+                last_pdf = ph_pdf;
+                throughput = vscale(throughput, 1.f);
+            }
+        }
+
+        /* ---- surface interactions (volpath.cpp:254-326) ---- */
+        active_surface = active_surface || escaped;
+        if (active_surface && needs_intersection) {
+            pi_rec pi;
+            trace_closest(sv, &ray, &pi);
+            if (counters) counters[0]++;
+            compute_si(d, &ray, &pi, &si);
+        }
+        if (active_surface) {
+            int count_direct = depth == 0 || specular_chain;
+            uint32_t em = si_emitter(d, &si);
+            if (em != MH_INVALID && !(depth == 0 && in->hide_emitters)) {
+                float emitter_pdf = 1.f;
+                if (!count_direct) emitter_pdf = emitter_pdf_direction(d, em, &si, last_p);
+                v3 emitted = emitter_eval(d, em, &si);
+                v3 contrib = count_direct ? vmul(throughput, emitted)
+                                          : vmul(vscale(throughput, mis_weight_vol(last_pdf, emitter_pdf)), emitted);
+                result = vadd(result, contrib);
+            }
+        }
+        active_surface = active_surface && si.valid;
+        if (active_surface) {
+            uint32_t b = si_bsdf(d, &si);
+            int is_null = b == MH_INVALID || d->bsdfs[b].type == MH_BSDF_NULL;
+            int smooth = !is_null;
+            v3 rho = V3(0, 0, 0);
+            if (smooth) rho = tex_eval(d, d->bsdfs[b].reflectance, si.uvx, si.uvy);
+            if (smooth && depth + 1 < in->max_depth) {
+                dir_sample ds;
+                v3 emitted = vol_sample_emitter(sv, si.p, si.n, &si, rng, medium, channel, &ds, counters);
+                v3 wo = to_local(&si, ds.d);
+                v3 bv;
+                float bp;
+                diffuse_eval_pdf(rho, si.wi, wo, 1, &bv, &bp);
+                float w = mis_weight_vol(ds.pdf, ds.delta ? 0.f : bp);
+                result = vadd(result, vmul(vscale(vmul(throughput, bv), w), emitted));
+            }
+            (void)pcg_float(rng);
+            float s2x = pcg_float(rng), s2y = pcg_float(rng);
+            bsdf_sample bs;
+            v3 weight;
+            if (is_null) {
+                bs.wo = vneg(si.wi); bs.pdf = 1.f; bs.eta = 1.f; bs.sampled_delta = 0; bs.sampled_null = 1;
+                weight = V3(1, 1, 1);
+            } else {
+                diffuse_sample(rho, si.wi, s2x, s2y, 1, &bs, &weight);
+            }
+            throughput = vmul(throughput, weight);
+            eta *= bs.eta;
+            ray = spawn_ray(si.p, si.n, to_world(&si, bs.wo));
+            needs_intersection = 1;
+            if (!bs.sampled_null) {
+                depth += 1;
+                last_p = si.p;
+                last_pdf = bs.pdf;
+                valid_ray = 1;
+                /* specular_chain |= delta (never for diffuse); &= !smooth */
+                specular_chain = 0;
+            }
+            if (is_medium_transition(d, &si)) medium = target_medium(d, &si, ray.d);
+        }
+        active = active && (active_surface || active_medium);
+    }
+    *valid_out = valid_ray;
+    return result;
+}
+
 static inline float inv_size(uint32_t n) { return 1.f / (float)n; }
 
 /* one sample of one lane: jitter, camera ray, integrator (render_sample,
@@ -1205,6 +1697,8 @@ static v3 lane_sample(const scene_view *sv, const mh_integrator *in, const wf_la
     pos_out[1] = sy;
     if (in->type == MH_INTEGRATOR_PRB)
         return prb_sample(sv, in, rng, r, V3(0, 0, 0), V3(0, 0, 0), NULL, valid_out);
+    if (in->type == MH_INTEGRATOR_VOLPATH)
+        return volpath_sample(sv, in, rng, r, valid_out, counters);
     return path_sample(sv, in, rng, r, valid_out, counters);
 }
 
@@ -1213,7 +1707,6 @@ int oracle_sample_range(const mh_scene_desc *desc, const mh_integrator *integ, u
                         float *out_pos, uint32_t *out_valid) {
     scene_view sv;
     if (scene_view_init(&sv, desc)) return 1;
-    if (integ->type == MH_INTEGRATOR_VOLPATH) { scene_view_free(&sv); return fail("volpath: not in oracle yet"); }
     if (spp == 0) spp = desc->sensor.sample_count;
     wf_layout L;
     wf_init(&desc->sensor, spp, &L);
@@ -1367,7 +1860,6 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
                      uint32_t n_params, const uint32_t *param_tex, float *const *grads) {
     scene_view sv;
     if (scene_view_init(&sv, desc)) return 1;
-    if (in && in->type == MH_INTEGRATOR_VOLPATH) { scene_view_free(&sv); return fail("volpath: not in oracle yet"); }
     const mh_sensor *s = &desc->sensor;
     if (spp == 0) spp = s->sample_count;
     wf_layout L;

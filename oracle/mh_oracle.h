@@ -37,6 +37,7 @@ void  oracle_sampler_floats(uint32_t seed_value, uint32_t lane, uint32_t n, floa
 float oracle_gaussian_eval(const float coeff[10], float x);
 void  oracle_sincos(float x, float *s, float *c);
 float oracle_log(float x);
+float oracle_exp(float x);
 void  oracle_diffuse_eval_pdf(const float wi[3], const float wo[3], const float rho[3],
                               float value[3], float *pdf);
 void  oracle_square_to_cosine_hemisphere(const float s[2], float out[3]);
