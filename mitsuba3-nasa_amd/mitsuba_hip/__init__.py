@@ -24,7 +24,7 @@ from .render import (SceneParameters, develop, prb_weights, render, render_backw
                      render_film, sample_tea_32, traverse)
 from .scene import Integrator, Scene, cornell_box, gaussian_coefficients, load_dict
 from .transform import ScalarTransform4f, Transform4f
-from .scenes import volume_cube
+from .scenes import cornell_box_bitmap, volume_cube
 from .volume import VolumeGrid, fbm_grid
 
 __version__ = "0.1.0"
@@ -67,4 +67,4 @@ def is_available() -> bool:
 __all__ = ["set_variant", "variant", "variants", "load_dict", "cornell_box", "render", "traverse",
            "render_backward", "render_film", "develop", "prb_weights", "SceneParameters", "Scene",
            "Integrator", "Transform4f", "ScalarTransform4f", "sample_tea_32", "MitsubaHipError",
-           "gaussian_coefficients", "is_available", "volume_cube", "VolumeGrid", "fbm_grid"]
+           "gaussian_coefficients", "is_available", "volume_cube", "cornell_box_bitmap", "VolumeGrid", "fbm_grid"]

@@ -11,8 +11,22 @@ from typing import Optional
 
 import numpy as np
 
+from .scene import cornell_box
 from .transform import Transform4f
 from .volume import fbm_grid
+
+
+def cornell_box_bitmap(tex_res: int = 64, width: int = 512, height: int = 512, spp: int = 64):
+    """Configuration 3(b): cornell_box with white's
+    reflectance replaced by a tex_res^2 x 3 `bitmap` initialised to the
+    constant (0.885809, 0.698859, 0.666422); key 'white.reflectance.data'."""
+    d = cornell_box()
+    white = np.asarray(d["white"]["reflectance"]["value"], np.float32)
+    d["white"]["reflectance"] = {"type": "bitmap", "data": np.tile(white, (tex_res, tex_res, 1)),
+                                 "filter_type": "bilinear", "wrap_mode": "repeat", "raw": True}
+    d["sensor"]["film"]["width"], d["sensor"]["film"]["height"] = width, height
+    d["sensor"]["sampler"]["sample_count"] = spp
+    return d
 
 
 def volume_cube(width: int = 256, height: int = 256, spp: int = 64, grid: Optional[np.ndarray] = None,

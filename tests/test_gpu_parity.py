@@ -236,3 +236,26 @@ def test_volpath_white_furnace_gpu():
     scene = _vol_scene(mi, 32, 32, 256, albedo=1.0, sky=1.0, sun=None, scale=5.0, max_depth=-1)
     img = mi.develop(scene, mi.render_film(scene, seed=0, spp=256)).cpu().numpy()
     assert abs(img.mean() - 1.0) < 0.01
+
+
+# ---------------------------------------------------------------------------
+# PRB wrt a bitmap texture (config 3(b)): texel gradients, replay path
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("spp", [4, 16])
+def test_prb_backward_bitmap_parity(spp):
+    mi = _mi()
+    import torch
+    scene = mi.load_dict(mi.cornell_box_bitmap(tex_res=8, width=32, height=24, spp=spp))
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    keys = ["white.reflectance.data", "red.reflectance.value"]
+    H, W = scene.height, scene.width
+    rng = np.random.default_rng(2)
+    gi = rng.random((H, W, 3)).astype(np.float32) / (H * W * 3)
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=13, spp=spp)
+    ref = O.render_backward(scene, integ, 13, spp, gi, [params.texture_of(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    for a, b in zip(g, ref):
+        a = a.cpu().numpy()
+        assert a.shape == b.shape
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max())

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Config 4 measurement: volpath, heterogeneous 256^3 fBm
+medium + HG, 256x256 @ 64 spp, one MI355X.  Prints one JSON line (not the
+driver's bench line: bench.py measures BASELINE.json's headline metric)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mitsuba3-nasa_amd"), os.path.join(ROOT, "tests")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--cpu-spp", type=int, default=4)
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+    import torch
+    import mitsuba_hip as mi
+    from mitsuba_hip import _abi as A
+    mi.set_variant("hip_ad_rgb")
+    t0 = time.time()
+    grid = mi.fbm_grid(a.grid)
+    scene = mi.load_dict(mi.volume_cube(a.res, a.res, a.spp, grid=grid))
+    t_load = time.time() - t0
+    film = torch.empty((a.res, a.res, 4), dtype=torch.float32, device="cuda")
+    st = A.Stats()
+    mi.render_film(scene, seed=100, spp=a.spp, film=film, stats=st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ks = []
+    for i in range(a.steps):
+        mi.render_film(scene, seed=i, spp=a.spp, film=film, stats=st)
+        ks.append(st.ms_kernel)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    n = a.res * a.res * a.spp
+    out = {"metric": "Msamples/s volpath config 4", "value": round(n / dt / 1e6, 2), "unit": "Msamples/s",
+           "ms_per_render": round(dt * 1e3, 3), "kernel_ms": round(sum(ks) / len(ks), 3),
+           "rays_closest_per_sample": round(st.rays_closest / n, 3),
+           "rays_shadow_per_sample": round(st.rays_shadow / n, 3),
+           "config": {"film": f"{a.res}x{a.res}", "spp": a.spp, "grid": f"{a.grid}^3 fBm",
+                      "scene_load_s": round(t_load, 2)}}
+    if not a.no_cpu:
+        import oracle_py as O
+        thr = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+        t0 = time.perf_counter()
+        O.render(scene, seed=0, spp=a.cpu_spp, threads=thr)
+        tc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(a.res * a.res * a.cpu_spp / tc / 1e6, 3), "unit": "Msamples/s",
+                               "cores": thr, "kind": "port", "sample": f"{a.res}^2 @ {a.cpu_spp} spp, {tc:.1f} s"}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
