@@ -18,6 +18,7 @@
 
 #include "mh_device.hpp"
 #include "mh_internal.hpp"
+#include "mh_shading.hpp"
 
 using namespace mh;
 
@@ -319,14 +320,25 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.textures = s->textures.as<DTexture>();
     S.emitters = s->emitters.as<DEmitter>();
     S.positions = s->positions.as<float>();
-    S.normals = s->normals.as<float>();
-    S.texcoords = s->texcoords.as<float>();
+    S.normals = desc->normals ? s->normals.as<float>() : nullptr;
+    S.texcoords = desc->texcoords ? s->texcoords.as<float>() : nullptr;
     S.faces = s->faces.as<uint32_t>();
     S.texels = s->texels.as<float>();
     S.media = s->media.as<DMedium>();
     S.grid = s->grid.as<float>();
     S.n_media = desc->n_media;
     S.camera_medium = desc->sensor.medium;
+    S.n_shapes = desc->n_shapes;
+    S.n_bsdfs = desc->n_bsdfs;
+    S.n_textures = desc->n_textures;
+    S.n_vertices = desc->n_vertices;
+    S.n_faces = desc->n_faces;
+    {
+        const TabLayout TL = tab_layout(S.n_shapes, S.n_bsdfs, S.n_textures, desc->n_emitters, S.n_vertices,
+                                        S.n_faces, S.normals != nullptr && S.n_vertices,
+                                        S.texcoords != nullptr && S.n_vertices);
+        S.tab_bytes = TL.total <= 16384 ? TL.total : 0u;  // staged into LDS by the shade kernels
+    }
     S.n_nodes = bvh.n_nodes;
     S.n_prims = bvh.n_prims;
     S.n_emitters = desc->n_emitters;

@@ -86,6 +86,9 @@ struct DScene {                 // kernel argument (by value)
     const float *grid;             // volume grid data
     uint32_t n_nodes, n_prims, n_emitters, environment;
     uint32_t n_media, camera_medium;
+    // small shading tables (shapes .. faces) staged into LDS by the shade
+    // kernels when tab_bytes != 0 (mh_shading.hpp stage_tables)
+    uint32_t n_shapes, n_bsdfs, n_textures, n_vertices, n_faces, tab_bytes;
     uint32_t stack_size;           // BVH traversal stack entries per lane
     uint32_t lds_bytes_bvh;        // bytes of nodes + prims staged into LDS
     // sensor

@@ -183,6 +183,71 @@ MH_DEV LdsBvh stage_bvh(const DScene &S, uint4 *lds) {
 }
 
 // ---------------------------------------------------------------------------
+// LDS staging of the small shading tables (shapes, BSDFs, textures,
+// emitters, mesh vertices / normals / uvs / faces).  A shading lane walks a
+// chain of dependent lookups (shape -> bsdf -> texture, shape -> face ->
+// vertices, emitter -> shape); from LDS each link costs ~100 cycles instead
+// of an L2 round trip.  The returned scene view points into LDS; callers
+// instantiate this unconditionally (template) so hipcc emits ds_read.
+// Layout and size: tab_layout (host and device agree).
+// ---------------------------------------------------------------------------
+struct TabLayout {
+    uint32_t shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals, texcoords, faces, total;
+};
+__host__ __device__ inline TabLayout tab_layout(uint32_t n_shapes, uint32_t n_bsdfs, uint32_t n_textures,
+                                                uint32_t n_emitters, uint32_t n_vertices, uint32_t n_faces,
+                                                bool normals, bool texcoords) {
+    auto al = [](uint32_t x) { return (x + 15u) & ~15u; };
+    TabLayout L;
+    uint32_t o = 0;
+    L.shapes = o; o += al(n_shapes * (uint32_t)sizeof(DShape));
+    L.bsdf_type = o; o += al(n_bsdfs * 4u);
+    L.bsdf_tex = o; o += al(n_bsdfs * 4u);
+    L.textures = o; o += al(n_textures * (uint32_t)sizeof(DTexture));
+    L.emitters = o; o += al(n_emitters * (uint32_t)sizeof(DEmitter));
+    L.positions = o; o += al(n_vertices * 12u);
+    L.normals = o; o += normals ? al(n_vertices * 12u) : 0u;
+    L.texcoords = o; o += texcoords ? al(n_vertices * 8u) : 0u;
+    L.faces = o; o += al(n_faces * 12u);
+    L.total = o;
+    return L;
+}
+
+MH_DEV void lds_copy(uint8_t *dst, const void *src, uint32_t bytes) {
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    for (uint32_t i = threadIdx.x; i < bytes / 4u; i += blockDim.x) d[i] = s[i];
+}
+
+MH_DEV DScene stage_tables(const DScene &S, uint4 *lds) {
+    DScene T = S;
+    uint8_t *b = reinterpret_cast<uint8_t *>(lds);
+    const bool has_n = S.normals != nullptr && S.n_vertices, has_t = S.texcoords != nullptr && S.n_vertices;
+    const TabLayout L = tab_layout(S.n_shapes, S.n_bsdfs, S.n_textures, S.n_emitters, S.n_vertices, S.n_faces,
+                                   has_n, has_t);
+    lds_copy(b + L.shapes, S.shapes, S.n_shapes * (uint32_t)sizeof(DShape));
+    lds_copy(b + L.bsdf_type, S.bsdf_type, S.n_bsdfs * 4u);
+    lds_copy(b + L.bsdf_tex, S.bsdf_tex, S.n_bsdfs * 4u);
+    lds_copy(b + L.textures, S.textures, S.n_textures * (uint32_t)sizeof(DTexture));
+    lds_copy(b + L.emitters, S.emitters, S.n_emitters * (uint32_t)sizeof(DEmitter));
+    lds_copy(b + L.positions, S.positions, S.n_vertices * 12u);
+    if (has_n) lds_copy(b + L.normals, S.normals, S.n_vertices * 12u);
+    if (has_t) lds_copy(b + L.texcoords, S.texcoords, S.n_vertices * 8u);
+    lds_copy(b + L.faces, S.faces, S.n_faces * 12u);
+    __syncthreads();
+    T.shapes = reinterpret_cast<const DShape *>(b + L.shapes);
+    T.bsdf_type = reinterpret_cast<const uint32_t *>(b + L.bsdf_type);
+    T.bsdf_tex = reinterpret_cast<const uint32_t *>(b + L.bsdf_tex);
+    T.textures = reinterpret_cast<const DTexture *>(b + L.textures);
+    T.emitters = reinterpret_cast<const DEmitter *>(b + L.emitters);
+    T.positions = reinterpret_cast<const float *>(b + L.positions);
+    if (has_n) T.normals = reinterpret_cast<const float *>(b + L.normals);
+    if (has_t) T.texcoords = reinterpret_cast<const float *>(b + L.texcoords);
+    T.faces = reinterpret_cast<const uint32_t *>(b + L.faces);
+    return T;
+}
+
+// ---------------------------------------------------------------------------
 // Stream traversal engine for the wavefront kernels: while-while traversal
 // (inner-node phase until every lane holds a leaf, then a grouped leaf phase)
 // with per-lane ray refill from the wave's contiguous item range.  Same hit
@@ -323,6 +388,105 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
             }
         }
         fetched += (uint32_t)__popcll(m);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-coherent ("packet") traversal engine for small BVHs: the 64 lanes of
+// a wave walk the BVH together (Wald et al. 2001 ray packets, on the 64-wide
+// SIMD).  A child is entered when ANY lane's ray overlaps it; node and
+// primitive records are read at wave-uniform addresses (LDS broadcast, no
+// bank conflicts), the child indices and the primitive type are
+// readfirstlane'd so every branch and the stack are scalar; a primitive is
+// tested by the lanes whose ray overlapped its leaf.  No lane diverges, no
+// per-lane stack exists.  Same hit semantics as traverse<>: closest hit with
+// t in [0, maxt] and strict-< update (only the visiting order differs, which
+// matters for exact-t ties alone).  Items [r0, r1) of the wave in batches of 64.
+// ---------------------------------------------------------------------------
+// Node / primitive records are read through the constant address space at
+// wave-uniform indices, so hipcc emits s_load (scalar cache) and the box /
+// primitive tests take them as SGPR operands; the visiting decisions are
+// ballots (SGPR masks) — the whole control path is scalar.
+typedef const __attribute__((address_space(4))) float CFloat;
+template <class T>
+MH_DEV T load_uniform(const T *base, uint32_t i) {
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    CFloat *p = (CFloat *)(base + i);
+    T r;
+    float *d = reinterpret_cast<float *>(&r);
+#pragma unroll
+    for (uint32_t k = 0; k < sizeof(T) / 4; ++k) d[k] = p[k];
+    return r;
+}
+
+template <bool Shadow>
+MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool lane_hit, const RayT &r,
+                        Hit &hit, float &best) {
+    for (uint32_t i = 0; i < count; ++i) {
+        const Prim p = load_uniform(prims, first + i);
+        if (lane_hit && (!Shadow || hit.shape == MH_INVALID)) {
+            float tt, u, v;
+            const bool ok = p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, tt, u, v) : tri_test(p, r, tt, u, v);
+            if (ok && (Shadow || tt < hit.t)) {
+                hit.t = tt; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x;
+                best = tt;
+            }
+        }
+    }
+}
+
+// gnodes / gprims: the BVH in global memory (read via the scalar cache);
+// B provides the LDS stack region (one wave-uniform stack per wave).
+template <bool Shadow, class Load, class Store>
+MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const LdsBvh &B, uint32_t r0, uint32_t r1,
+                         Load load, Store store) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t *ws = B.stack - lane;  // wave-uniform stack: entry k at ws[k * stride]
+    for (uint32_t base = r0; base < r1; base += 64u) {
+        const uint32_t item = base + lane;
+        const bool has = item < r1;
+        RayT r;
+        if (has) r = load(item);
+        else r = RayT{v3(0, 0, 0), v3(0, 0, 1), -1.f};
+        const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
+        float best = r.maxt;
+        Hit hit;
+        hit.t = __builtin_huge_valf();
+        hit.u = hit.v = 0.f;
+        hit.prim = MH_INVALID;
+        hit.shape = MH_INVALID;
+        bool act = has && gnodes != nullptr;
+        uint32_t node = 0, sp = 0;
+        while (__any(act)) {
+            const Node n = load_uniform(gnodes, node);
+            bool h0, h1;
+            float t0, t1;
+            box2(n, inv, ood, best, h0, h1, t0, t1);
+            h0 = h0 && act;
+            h1 = h1 && act;
+            const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
+            const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
+            bool any0 = __any(h0), any1 = __any(h1);
+            if (any0 && n0) { packet_leaf<Shadow>(gprims, c0, n0, h0, r, hit, best); any0 = false; }
+            if (any1 && n1) { packet_leaf<Shadow>(gprims, c1, n1, h1, r, hit, best); any1 = false; }
+            if (Shadow) act = act && hit.shape == MH_INVALID;
+            if (any0 && any1) {
+                const unsigned long long both = __ballot(h0 && h1), pref1 = __ballot(h0 && h1 && t1 < t0);
+                const bool first1 = 2u * (uint32_t)__popcll(pref1) > (uint32_t)__popcll(both);
+                ws[sp * B.stride] = first1 ? c0 : c1;
+                ++sp;
+                node = first1 ? c1 : c0;
+            } else if (any0) {
+                node = c0;
+            } else if (any1) {
+                node = c1;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                node = __builtin_amdgcn_readfirstlane(ws[sp * B.stride]);
+            }
+        }
+        if (has) store(item, hit, hit.shape != MH_INVALID);
     }
 }
 

@@ -19,6 +19,8 @@
 // CPU oracle.  Work is pulled by waves from an atomic head (no host sync
 // between bounces: queue counts stay on the device).
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "mh_shading.hpp"
 
@@ -50,6 +52,25 @@ struct WfState {
 constexpr uint32_t kSeg = 64;
 constexpr uint32_t kCtrStride = kSeg * 32;
 constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
+
+// Traversal engine of the stream kernels: wave-coherent packets for small
+// BVHs (every wave visits about the whole tree anyway; no divergence, no
+// per-lane stack, broadcast node reads), per-lane while-while otherwise.
+// MH_TRAVERSAL=packet|lane overrides (tests cover both).
+constexpr uint32_t kPacketMaxPrims = 64;
+static bool use_packet(const DScene &S) {
+    const char *e = getenv("MH_TRAVERSAL");
+    if (e && !strcmp(e, "packet")) return true;
+    if (e && !strcmp(e, "lane")) return false;
+    return S.n_prims <= kPacketMaxPrims;
+}
+#define MH_WF_DISPATCH(K, ...)                                                                        \
+    do {                                                                                              \
+        if (lds && packet) hipLaunchKernelGGL((K<true, true>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);   \
+        else if (lds) hipLaunchKernelGGL((K<true, false>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);     \
+        else if (packet) hipLaunchKernelGGL((K<false, true>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((K<false, false>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);             \
+    } while (0)
 
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -155,7 +176,8 @@ MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1
     r1 = min(n, r0 + per);
 }
 
-template <bool InLds>
+// Packet: wave-coherent engine (small BVHs) instead of the per-lane stream engine
+template <bool InLds, bool Packet>
 __global__ void __launch_bounds__(256)
 k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -167,22 +189,26 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
                 *dz = w.dz[cur], *mt = w.mt[cur];
     uint32_t r0, r1;
     wave_range(it, n, r0, r1);
-    trace_stream<false>(
-        B, r0, r1,
-        [&](uint32_t i) {
-            const uint32_t j = base + i;
-            return RayT{v3(ox[j], oy[j], oz[j]), v3(dx[j], dy[j], dz[j]), mt[j]};
-        },
-        [&](uint32_t i, const Hit &h, bool) {
-            const uint32_t j = base + i;
-            w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
-        });
+    auto load = [&](uint32_t i) {
+        const uint32_t j = base + i;
+        return RayT{v3(ox[j], oy[j], oz[j]), v3(dx[j], dy[j], dz[j]), mt[j]};
+    };
+    auto store = [&](uint32_t i, const Hit &h, bool) {
+        const uint32_t j = base + i;
+        w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
+    };
+    if (Packet) trace_packet<false>(S.nodes, S.prims, B, r0, r1, load, store);
+    else trace_stream<false>(B, r0, r1, load, store);
 }
 
 // one iteration of PathIntegrator::sample for every queued path
+// Staged: shading tables in LDS (stage_tables)
+template <bool Staged>
 __global__ void __launch_bounds__(256)
-k_wf_shade(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
+k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
            float *out, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+    extern __shared__ uint4 lds[];
+    const DScene S = Staged ? stage_tables(S0, lds) : S0;
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t sbase = it.seg * seg_cap;  // slots (state, hits, shadow records) of this segment
@@ -307,7 +333,7 @@ k_wf_shade(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint6
     }
 }
 
-template <bool InLds>
+template <bool InLds, bool Packet>
 __global__ void __launch_bounds__(256)
 k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -317,19 +343,19 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
     const uint32_t base = it.seg * seg_cap;
     uint32_t r0, r1;
     wave_range(it, n, r0, r1);
-    trace_stream<true>(
-        B, r0, r1,
-        [&](uint32_t i) {
-            const uint32_t j = base + i;
-            return RayT{v3(w.sox[j], w.soy[j], w.soz[j]), v3(w.sdx[j], w.sdy[j], w.sdz[j]), w.smt[j]};
-        },
-        [&](uint32_t i, const Hit &, bool occluded) {
-            if (occluded) return;
-            const uint32_t j = base + i, pid = w.sid[j];
-            V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
-            L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
-            out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
-        });
+    auto load = [&](uint32_t i) {
+        const uint32_t j = base + i;
+        return RayT{v3(w.sox[j], w.soy[j], w.soz[j]), v3(w.sdx[j], w.sdy[j], w.sdz[j]), w.smt[j]};
+    };
+    auto store = [&](uint32_t i, const Hit &, bool occluded) {
+        if (occluded) return;
+        const uint32_t j = base + i, pid = w.sid[j];
+        V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
+        L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
+        out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
+    };
+    if (Packet) trace_packet<true>(S.nodes, S.prims, B, r0, r1, load, store);
+    else trace_stream<true>(B, r0, r1, load, store);
 }
 
 // ---------------------------------------------------------------------------
@@ -349,20 +375,22 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     hipLaunchKernelGGL(k_wf_raygen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                        seed_value, n, plane, out, w, ctr);
     const size_t sh = lds_bytes(S, 256);
-    const bool lds = S.lds_bytes_bvh != 0;
+    const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
-        if (lds) hipLaunchKernelGGL(k_wf_trace<true>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
-        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
+        MH_WF_DISPATCH(k_wf_trace, S, w, cur, seg_cap, c);
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
-        hipLaunchKernelGGL(k_wf_shade, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, plane, out,
-                           w, cur, seg_cap, c, cn);
-        if (lds) hipLaunchKernelGGL(k_wf_shadow<true>, dim3(grid), dim3(256), sh, st, S, w, plane, out, seg_cap, c);
-        else hipLaunchKernelGGL(k_wf_shadow<false>, dim3(grid), dim3(256), sh, st, S, w, plane, out, seg_cap, c);
+        if (S.tab_bytes)
+            hipLaunchKernelGGL(k_wf_shade<true>, dim3(grid), dim3(256), S.tab_bytes, st, S, in, lm, seed_value,
+                               plane, out, w, cur, seg_cap, c, cn);
+        else
+            hipLaunchKernelGGL(k_wf_shade<false>, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, plane, out,
+                               w, cur, seg_cap, c, cn);
+        MH_WF_DISPATCH(k_wf_shadow, S, w, plane, out, seg_cap, c);
     }
     return hipGetLastError();
 }
@@ -466,9 +494,12 @@ k_wf_raygen_prb(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, int coale
 }
 
 // one iteration of the prb_fused loop (prb.py:114-278) for every queued path
+template <bool Staged>
 __global__ void __launch_bounds__(256)
-k_wf_shade_prb(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
+k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+    extern __shared__ uint4 lds[];
+    const DScene S = Staged ? stage_tables(S0, lds) : S0;
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t sbase = it.seg * seg_cap;
@@ -625,7 +656,7 @@ k_wf_shade_prb(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, W
     flush_partial(acc, q);
 }
 
-template <bool InLds>
+template <bool InLds, bool Packet>
 __global__ void __launch_bounds__(256)
 k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -639,23 +670,23 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     for (int kk = 0; kk < kMaxRgbParams; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
     uint32_t r0, r1;
     wave_range(it, n, r0, r1);
-    trace_stream<true>(
-        B, r0, r1,
-        [&](uint32_t i) {
-            const uint32_t j = base + i;
-            return RayT{v3(w.sox[j], w.soy[j], w.soz[j]), v3(w.sdx[j], w.sdy[j], w.sdz[j]), w.smt[j]};
-        },
-        [&](uint32_t i, const Hit &, bool occluded) {
-            if (occluded) return;
-            const uint32_t j = base + i;
+    auto load = [&](uint32_t i) {
+        const uint32_t j = base + i;
+        return RayT{v3(w.sox[j], w.soy[j], w.soz[j]), v3(w.sdx[j], w.sdy[j], w.sdz[j]), w.smt[j]};
+    };
+    auto store = [&](uint32_t i, const Hit &, bool occluded) {
+        if (occluded) return;
+        const uint32_t j = base + i;
 #pragma unroll
-            for (int kk = 0; kk < kMaxRgbParams; ++kk)
-                if ((uint32_t)kk < n_rgb) {
-                    acc[kk][0] += q.G(kk * 3 + 0)[j];
-                    acc[kk][1] += q.G(kk * 3 + 1)[j];
-                    acc[kk][2] += q.G(kk * 3 + 2)[j];
-                }
-        });
+        for (int kk = 0; kk < kMaxRgbParams; ++kk)
+            if ((uint32_t)kk < n_rgb) {
+                acc[kk][0] += q.G(kk * 3 + 0)[j];
+                acc[kk][1] += q.G(kk * 3 + 1)[j];
+                acc[kk][2] += q.G(kk * 3 + 2)[j];
+            }
+    };
+    if (Packet) trace_packet<true>(S.nodes, S.prims, B, r0, r1, load, store);
+    else trace_stream<true>(B, r0, r1, load, store);
     flush_partial(acc, q);
 }
 
@@ -687,17 +718,19 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                        seed_value, n, coalesce, grad_in, weights, w, q, ctr);
     const size_t sh = lds_bytes(S, 256);
-    const bool lds = S.lds_bytes_bvh != 0;
+    const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
-        if (lds) hipLaunchKernelGGL(k_wf_trace<true>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
-        else hipLaunchKernelGGL(k_wf_trace<false>, dim3(grid), dim3(256), sh, st, S, w, cur, seg_cap, c);
-        hipLaunchKernelGGL(k_wf_shade_prb, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, w, q, cur,
-                           seg_cap, c, cn);
-        if (lds) hipLaunchKernelGGL(k_wf_shadow_prb<true>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
-        else hipLaunchKernelGGL(k_wf_shadow_prb<false>, dim3(grid), dim3(256), sh, st, S, w, q, seg_cap, c);
+        MH_WF_DISPATCH(k_wf_trace, S, w, cur, seg_cap, c);
+        if (S.tab_bytes)
+            hipLaunchKernelGGL(k_wf_shade_prb<true>, dim3(grid), dim3(256), S.tab_bytes, st, S, in, lm, seed_value,
+                               w, q, cur, seg_cap, c, cn);
+        else
+            hipLaunchKernelGGL(k_wf_shade_prb<false>, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, w, q,
+                               cur, seg_cap, c, cn);
+        MH_WF_DISPATCH(k_wf_shadow_prb, S, w, q, seg_cap, c);
     }
     return hipGetLastError();
 }

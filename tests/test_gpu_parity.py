@@ -84,8 +84,13 @@ def _gpu_samples(mi, scene, integrator, seed, spp, flags=0):
     return out[:3 * n].reshape(3, n).T, out[3 * n:].reshape(2, n).T
 
 
-@pytest.mark.parametrize("itype,mode", [("path", "mega"), ("prb", "mega"), ("path", "wavefront")])
-def test_per_sample_parity(itype, mode):
+@pytest.mark.parametrize("itype,mode", [("path", "mega"), ("prb", "mega"), ("path", "wavefront"),
+                                        ("path", "wavefront-lane")])
+def test_per_sample_parity(itype, mode, monkeypatch):
+    """wavefront: packet engine (small BVH default); wavefront-lane: per-lane engine."""
+    if mode == "wavefront-lane":
+        monkeypatch.setenv("MH_TRAVERSAL", "lane")
+        mode = "wavefront"
     mi = _mi()
     from mitsuba_hip import _abi as A
     scene = cbox(mi, 24, 24, 8)
@@ -178,7 +183,8 @@ def test_prb_backward_fused_vs_replay_random_grad():
 
 
 @pytest.mark.gpu
-def test_prb_backward_wavefront_chunked(monkeypatch):
+@pytest.mark.parametrize("engine", ["packet", "lane"])
+def test_prb_backward_wavefront_chunked(monkeypatch, engine):
     """Multi-chunk wavefront backward (lane maps offset per chunk, partials
     accumulated across chunks) equals the single-chunk run."""
     mi = _mi()
@@ -188,6 +194,7 @@ def test_prb_backward_wavefront_chunked(monkeypatch):
     params = mi.traverse(scene)
     keys = ["white.reflectance.value", "green.reflectance.value"]
     gi = torch.full((24, 40, 3), 1.0 / (24 * 40 * 3), dtype=torch.float32, device="cuda")
+    monkeypatch.setenv("MH_TRAVERSAL", engine)
     a = mi.render_backward(scene, params, gi, keys, integ, seed=9, spp=16)
     monkeypatch.setenv("MH_WF_CHUNK", "2048")
     b = mi.render_backward(scene, params, gi, keys, integ, seed=9, spp=16)
