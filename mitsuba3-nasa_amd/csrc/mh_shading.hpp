@@ -241,8 +241,10 @@ MH_DEV DScene stage_tables(const DScene &S, uint4 *lds) {
     T.textures = reinterpret_cast<const DTexture *>(b + L.textures);
     T.emitters = reinterpret_cast<const DEmitter *>(b + L.emitters);
     T.positions = reinterpret_cast<const float *>(b + L.positions);
-    if (has_n) T.normals = reinterpret_cast<const float *>(b + L.normals);
-    if (has_t) T.texcoords = reinterpret_cast<const float *>(b + L.texcoords);
+    // unconditional (a select between LDS and global would force flat loads);
+    // compute_si reads them only for shapes that have normals / uvs
+    T.normals = reinterpret_cast<const float *>(b + L.normals);
+    T.texcoords = reinterpret_cast<const float *>(b + L.texcoords);
     T.faces = reinterpret_cast<const uint32_t *>(b + L.faces);
     return T;
 }
@@ -1137,10 +1139,10 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const f
 // The direct term (prb.py:208-221) needs only dL.  Mathematically identical
 // to the replay; differs by fp association only (tests: 1e-3 relative).
 // ---------------------------------------------------------------------------
-MH_DEV void charge(float (&acc)[kMaxRgbParams][3], const float (&A)[kMaxRgbParams][3], uint32_t n_rgb,
-                   V3 dLe) {
+template <int NR>
+MH_DEV void charge(float (&acc)[NR][3], const float (&A)[NR][3], uint32_t n_rgb, V3 dLe) {
 #pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk)
+    for (int kk = 0; kk < NR; ++kk)
         if ((uint32_t)kk < n_rgb) {
             acc[kk][0] = __builtin_fmaf(dLe.x, A[kk][0] * kInvPi, acc[kk][0]);
             acc[kk][1] = __builtin_fmaf(dLe.y, A[kk][1] * kInvPi, acc[kk][1]);
@@ -1161,9 +1163,10 @@ MH_DEV V3 prb_indirect_factor(bool active_next, const SI &si, V3 wo2, V3 bsdf_we
     return c;
 }
 
-MH_DEV void add_slot(float (&arr)[kMaxRgbParams][3], int32_t slot, V3 v) {
+template <int NR>
+MH_DEV void add_slot(float (&arr)[NR][3], int32_t slot, V3 v) {
 #pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk)
+    for (int kk = 0; kk < NR; ++kk)
     {
         const bool m = kk == slot;  // branch-free: keeps arr in registers
         arr[kk][0] += m ? v.x : 0.f;

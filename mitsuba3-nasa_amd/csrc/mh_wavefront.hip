@@ -71,6 +71,13 @@ static bool use_packet(const DScene &S) {
         else if (packet) hipLaunchKernelGGL((K<false, true>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);  \
         else hipLaunchKernelGGL((K<false, false>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);             \
     } while (0)
+#define MH_WF_DISPATCH_NR(K, NR, ...)                                                                 \
+    do {                                                                                              \
+        if (lds && packet) hipLaunchKernelGGL((K<true, true, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);   \
+        else if (lds) hipLaunchKernelGGL((K<true, false, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);     \
+        else if (packet) hipLaunchKernelGGL((K<false, true, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);  \
+        else hipLaunchKernelGGL((K<false, false, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);             \
+    } while (0)
 
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -204,7 +211,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
 // one iteration of PathIntegrator::sample for every queued path
 // Staged: shading tables in LDS (stage_tables)
 template <bool Staged>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 5)
 k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
            float *out, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     extern __shared__ uint4 lds[];
@@ -440,11 +447,12 @@ static WfPrb carve_prb(void *ws, uint64_t cap, float *partial, const int32_t *sl
 }
 
 // block-reduce the per-thread accumulators into partial[blockIdx]
-MH_DEV void flush_partial(float (&acc)[kMaxRgbParams][3], const WfPrb &q) {
+template <int NR>
+MH_DEV void flush_partial(float (&acc)[NR][3], const WfPrb &q) {
     __shared__ float red[4][kG];
     const uint32_t wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk) {
+    for (int kk = 0; kk < NR; ++kk) {
         if ((uint32_t)kk >= q.n_rgb) break;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -494,8 +502,9 @@ k_wf_raygen_prb(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, int coale
 }
 
 // one iteration of the prb_fused loop (prb.py:114-278) for every queued path
-template <bool Staged>
-__global__ void __launch_bounds__(256)
+// NR: rgb slot arrays (1 when a single rgb parameter is differentiated)
+template <bool Staged, int NR>
+__global__ void __launch_bounds__(256, 5)
 k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     extern __shared__ uint4 lds[];
@@ -505,9 +514,9 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
     const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
     const uint32_t n_rgb = q.n_rgb;
-    float acc[kMaxRgbParams][3];
+    float acc[NR][3];
 #pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
+    for (int kk = 0; kk < NR; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
     const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
     for (uint32_t itr = 0; itr < n_iter; ++itr) {
         const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
@@ -516,7 +525,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
         RayT ray, sray;
         V3 beta, prev_p, dL;
         float prev_pdf = 1.f;
-        float A[kMaxRgbParams][3], G[kMaxRgbParams][3];
+        float A[NR][3], G[NR][3];
         Pcg rng;
         if (i < n) {
             const uint32_t j = sbase + i;
@@ -533,7 +542,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
             prev_pdf = w.ppdf[cur][j];
             dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
 #pragma unroll
-            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+            for (int kk = 0; kk < NR; ++kk)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
             const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
@@ -586,7 +595,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
                 V3 beta_mis_em = beta * mis_em;
                 V3 dLe = dL * ((beta_mis_em * bsdf_value_em) * em_weight);
 #pragma unroll
-                for (int kk = 0; kk < kMaxRgbParams; ++kk) {
+                for (int kk = 0; kk < NR; ++kk) {
                     G[kk][0] = (dLe.x * (A[kk][0] * kInvPi));
                     G[kk][1] = (dLe.y * (A[kk][1] * kInvPi));
                     G[kk][2] = (dLe.z * (A[kk][2] * kInvPi));
@@ -634,7 +643,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
             w.rng[nxt][slot_n] = rng.state;
             q.dl(nxt, 0)[slot_n] = dL.x; q.dl(nxt, 1)[slot_n] = dL.y; q.dl(nxt, 2)[slot_n] = dL.z;
 #pragma unroll
-            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+            for (int kk = 0; kk < NR; ++kk)
                 if ((uint32_t)kk < n_rgb) {
                     q.A(nxt, kk * 3 + 0)[slot_n] = A[kk][0];
                     q.A(nxt, kk * 3 + 1)[slot_n] = A[kk][1];
@@ -645,7 +654,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
             w.sox[sslot] = sray.o.x; w.soy[sslot] = sray.o.y; w.soz[sslot] = sray.o.z;
             w.sdx[sslot] = sray.d.x; w.sdy[sslot] = sray.d.y; w.sdz[sslot] = sray.d.z; w.smt[sslot] = sray.maxt;
 #pragma unroll
-            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+            for (int kk = 0; kk < NR; ++kk)
                 if ((uint32_t)kk < n_rgb) {
                     q.G(kk * 3 + 0)[sslot] = G[kk][0];
                     q.G(kk * 3 + 1)[sslot] = G[kk][1];
@@ -656,7 +665,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
     flush_partial(acc, q);
 }
 
-template <bool InLds, bool Packet>
+template <bool InLds, bool Packet, int NR>
 __global__ void __launch_bounds__(256)
 k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -665,9 +674,9 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t base = it.seg * seg_cap;
     const uint32_t n_rgb = q.n_rgb;
-    float acc[kMaxRgbParams][3];
+    float acc[NR][3];
 #pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
+    for (int kk = 0; kk < NR; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
     uint32_t r0, r1;
     wave_range(it, n, r0, r1);
     auto load = [&](uint32_t i) {
@@ -678,7 +687,7 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
         if (occluded) return;
         const uint32_t j = base + i;
 #pragma unroll
-        for (int kk = 0; kk < kMaxRgbParams; ++kk)
+        for (int kk = 0; kk < NR; ++kk)
             if ((uint32_t)kk < n_rgb) {
                 acc[kk][0] += q.G(kk * 3 + 0)[j];
                 acc[kk][1] += q.G(kk * 3 + 1)[j];
@@ -724,13 +733,23 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         MH_WF_DISPATCH(k_wf_trace, S, w, cur, seg_cap, c);
-        if (S.tab_bytes)
-            hipLaunchKernelGGL(k_wf_shade_prb<true>, dim3(grid), dim3(256), S.tab_bytes, st, S, in, lm, seed_value,
-                               w, q, cur, seg_cap, c, cn);
-        else
-            hipLaunchKernelGGL(k_wf_shade_prb<false>, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, w, q,
-                               cur, seg_cap, c, cn);
-        MH_WF_DISPATCH(k_wf_shadow_prb, S, w, q, seg_cap, c);
+        if (n_rgb == 1) {
+            if (S.tab_bytes)
+                hipLaunchKernelGGL((k_wf_shade_prb<true, 1>), dim3(grid), dim3(256), S.tab_bytes, st, S, in, lm,
+                                   seed_value, w, q, cur, seg_cap, c, cn);
+            else
+                hipLaunchKernelGGL((k_wf_shade_prb<false, 1>), dim3(grid), dim3(256), 0, st, S, in, lm, seed_value,
+                                   w, q, cur, seg_cap, c, cn);
+        } else {
+            if (S.tab_bytes)
+                hipLaunchKernelGGL((k_wf_shade_prb<true, kMaxRgbParams>), dim3(grid), dim3(256), S.tab_bytes, st, S,
+                                   in, lm, seed_value, w, q, cur, seg_cap, c, cn);
+            else
+                hipLaunchKernelGGL((k_wf_shade_prb<false, kMaxRgbParams>), dim3(grid), dim3(256), 0, st, S, in, lm,
+                                   seed_value, w, q, cur, seg_cap, c, cn);
+        }
+        if (n_rgb == 1) MH_WF_DISPATCH_NR(k_wf_shadow_prb, 1, S, w, q, seg_cap, c);
+        else MH_WF_DISPATCH_NR(k_wf_shadow_prb, kMaxRgbParams, S, w, q, seg_cap, c);
     }
     return hipGetLastError();
 }
