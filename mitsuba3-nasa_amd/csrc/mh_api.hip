@@ -87,7 +87,7 @@ struct mh_scene {
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
-    DevBuf wf_ws_prb, wf_partial;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
+    DevBuf wf_ws_prb, wf_partial, gw;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0;
@@ -372,7 +372,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -795,6 +795,10 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     }
 
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    // grad_in / W once per pixel (the adjoint of develop)
+    MH_HIP(s->gw.alloc(n_px * 12));
+    MH_HIP(launch_grad_over_w(n_px, g_in, w, s->gw.as<float>(), st));
+    g_in = s->gw.as<float>();
     const uint32_t S_ = L.s_end - L.s_begin;
     const uint64_t n = n_px * S_;
     // fused single traversal when every requested parameter is an rgb constant,

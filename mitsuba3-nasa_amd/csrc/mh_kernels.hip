@@ -297,6 +297,18 @@ k_splat_generic(DScene S, LaneMap lm, uint32_t n_passes, uint64_t n, uint64_t pl
     (void)nch;
 }
 
+// adjoint of develop: grad_in / (W == 0 ? 1 : W), once per pixel (the
+// division Dr.Jit's AD of `rgb / W` performs); gathered per sample by gather_dL
+__global__ void k_grad_over_w(uint64_t n_px, const float *__restrict__ grad_in, const float *__restrict__ w,
+                              float *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    const float Wp = w[i] == 0.f ? 1.f : w[i];
+    out[3 * i] = grad_in[3 * i] / Wp;
+    out[3 * i + 1] = grad_in[3 * i + 1] / Wp;
+    out[3 * i + 2] = grad_in[3 * i + 2] / Wp;
+}
+
 // HDRFilm::develop (films/hdrfilm.cpp:349-405)
 __global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *__restrict__ rgb) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -334,7 +346,7 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
         float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
         RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
                             __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
-        V3 dL = gather_dL(S, coalesce, grad_in, weights, sx, sy);
+        V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
         if (Fused) {
             prb_fused(S, B, in, rng, r, dL, ga.n_rgb, g, n_closest, n_shadow);
         } else {
@@ -435,6 +447,12 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, b
             hipLaunchKernelGGL(k_splat_generic<0>, dim3(blocks_for(n, bs)), dim3(bs), 0, st, S,
                                lm, n_passes, n, plane, in, film, seed_value, coalesce);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st) {
+    if (n_px == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_grad_over_w, dim3(blocks_for(n_px, 256)), dim3(256), 0, st, n_px, grad_in, w, out);
     return hipGetLastError();
 }
 

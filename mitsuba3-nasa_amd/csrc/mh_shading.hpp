@@ -1063,36 +1063,40 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
 // filter-weighted gather of grad_in / W over the sample's footprint
 // (common.py:953-965; the W image from common.py:936-947)
 // ---------------------------------------------------------------------------
-MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const float *weights,
-                    float px, float py) {
+// gw: grad_in / (W == 0 ? 1 : W) per pixel (k_grad_over_w), i.e. the adjoint
+// of develop, which Dr.Jit also evaluates once per pixel.
+MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *__restrict__ gw, float px, float py) {
     const uint32_t W = S.width, H = S.height;
     float o0 = 0.f, o1 = 0.f, o2 = 0.f;
     if (S.rfilter == MH_RFILTER_BOX) {
         uint32_t ux = (uint32_t)(int32_t)floorf(px), uy = (uint32_t)(int32_t)floorf(py);
         if (ux < W && uy < H) {
             uint64_t p = (uint64_t)uy * W + ux;
-            float Wp = weights[p] == 0.f ? 1.f : weights[p];
-            o0 = grad_in[3 * p] / Wp; o1 = grad_in[3 * p + 1] / Wp; o2 = grad_in[3 * p + 2] / Wp;
+            o0 = gw[3 * p]; o1 = gw[3 * p + 1]; o2 = gw[3 * p + 2];
         }
         return v3(o0, o1, o2);
     }
     const float radius = S.rfilter_radius;
     if (coalesce) {
         int32_t nn = (int32_t)ceilf(radius - 0.5f), count = 2 * nn + 1;
+        if (count > 5) count = 5;  // radius <= 2.5 (host-checked for this path)
         int32_t pix = (int32_t)floorf(px) - nn, piy = (int32_t)floorf(py) - nn;
         float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
+        float wxs[5];
+#pragma unroll
+        for (int32_t xs = 0; xs < 5; ++xs) wxs[xs] = xs < count ? gaussian_eval(S.filter_coeff, relx + (float)xs) : 0.f;
         for (int32_t ys = 0; ys < count; ++ys) {
             float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
-            for (int32_t xs = 0; xs < count; ++xs) {
-                float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
-                uint32_t xx = (uint32_t)(pix + xs), yy = (uint32_t)(piy + ys);
-                if (xx < W && yy < H) {
+            uint32_t yy = (uint32_t)(piy + ys);
+#pragma unroll
+            for (int32_t xs = 0; xs < 5; ++xs) {
+                uint32_t xx = (uint32_t)(pix + xs);
+                if (xs < count && xx < W && yy < H) {
                     uint64_t p = (uint64_t)yy * W + xx;
-                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
-                    float w = wy * wx;
-                    o0 += (grad_in[3 * p] / Wp) * w;
-                    o1 += (grad_in[3 * p + 1] / Wp) * w;
-                    o2 += (grad_in[3 * p + 2] / Wp) * w;
+                    float w = wy * wxs[xs];
+                    o0 += gw[3 * p] * w;
+                    o1 += gw[3 * p + 1] * w;
+                    o2 += gw[3 * p + 2] * w;
                 }
             }
         }
@@ -1111,11 +1115,10 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *grad_in, const f
                 int32_t xx = a0x + (int32_t)xs, yy = a0y + (int32_t)ys;
                 if (xx <= a1x && yy <= a1y) {
                     uint64_t p = (uint64_t)yy * W + xx;
-                    float Wp = weights[p] == 0.f ? 1.f : weights[p];
                     float w = wy * wx;
-                    o0 += (grad_in[3 * p] / Wp) * w;
-                    o1 += (grad_in[3 * p + 1] / Wp) * w;
-                    o2 += (grad_in[3 * p + 2] / Wp) * w;
+                    o0 += gw[3 * p] * w;
+                    o1 += gw[3 * p + 1] * w;
+                    o2 += gw[3 * p + 2] * w;
                 }
             }
         }

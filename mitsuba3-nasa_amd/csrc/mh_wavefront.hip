@@ -488,7 +488,7 @@ k_wf_raygen_prb(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, int coale
     float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
     RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
                         __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
-    V3 dL = gather_dL(S, coalesce, grad_in, weights, sx, sy);
+    V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W
     w.pd[0][k] = (uint32_t)k;
     w.ox[0][k] = r.o.x; w.oy[0][k] = r.o.y; w.oz[0][k] = r.o.z;
     w.dx[0][k] = r.d.x; w.dy[0][k] = r.d.y; w.dz[0][k] = r.d.z; w.mt[0][k] = r.maxt;
