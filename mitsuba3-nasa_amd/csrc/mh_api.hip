@@ -209,7 +209,18 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         }
     }
     BvhOut bvh;
-    build_bvh(bp, bvh);
+    {
+        // Leaf size / SAH traversal cost per engine (measured, tools/exp_bvh_leaf.sh):
+        // small scenes take the packet engine, where a wave tests every leaf some
+        // lane reaches and node visits are the serial part -> few, large leaves
+        // (12, C_t = 4); otherwise the per-lane engine (8, C_t = 2).  Leaf counts
+        // <= 31 (5-bit field of the stream engine's stack entries); env overrides.
+        const bool small = bp.size() <= 64;
+        const char *el = getenv("MH_BVH_LEAF"), *ec = getenv("MH_BVH_CT");
+        uint32_t max_leaf = el ? (uint32_t)std::max(2, std::min(31, atoi(el))) : (small ? 12u : 8u);
+        float ct = ec ? (float)atof(ec) : (small ? 4.0f : 2.0f);
+        build_bvh(bp, bvh, max_leaf, ct);
+    }
     s->bvh_nodes = bvh.n_nodes;
     s->bvh_prims = bvh.n_prims;
     s->bvh_depth = bvh.depth;

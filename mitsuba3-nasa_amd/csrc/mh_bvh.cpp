@@ -37,7 +37,7 @@ struct Box {
 };
 
 constexpr int kBins = 16;
-constexpr uint32_t kMaxLeaf = 4;
+// leaf limits: the per-lane stream engine packs the count in 3 bits (<= 7)
 constexpr uint32_t kMaxDepth = 48;
 
 struct Builder {
@@ -46,6 +46,8 @@ struct Builder {
     std::vector<Node> nodes;
     std::vector<uint32_t> order;  // final prim order
     uint32_t max_depth = 0;
+    uint32_t kMaxLeaf = 4;
+    float trav_cost = 1.0f;  // SAH traversal cost relative to one primitive test
 
     explicit Builder(const std::vector<BuildPrim> &prims) : p(prims) {
         idx.resize(p.size());
@@ -117,7 +119,7 @@ struct Builder {
             return b + n / 2;
         }
         const float area = node_box.area();
-        if (!force && area > 0.f && 1.0f + best_cost / area >= (float)n) return e;
+        if (!force && area > 0.f && trav_cost + best_cost / area >= (float)n) return e;
         const int a = best_axis;
         const float ext = cb.hi[a] - cb.lo[a];
         auto mid_it = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t q) {
@@ -175,10 +177,12 @@ struct Builder {
 
 }  // namespace
 
-void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out) {
+void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf, float trav_cost) {
     out = BvhOut();
     if (in.empty()) return;
     Builder bld(in);
+    bld.kMaxLeaf = std::max<uint32_t>(2, max_leaf);
+    bld.trav_cost = trav_cost;
     const uint32_t n = (uint32_t)in.size();
     if (n == 1) {
         // root with two identical single-prim leaves (the traversal needs an inner root)
@@ -213,7 +217,8 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out) {
         q.a = make_float4(bp.rec[0], bp.rec[1], bp.rec[2], bp.rec[3]);
         q.b = make_float4(bp.rec[4], bp.rec[5], bp.rec[6], bp.rec[7]);
         q.c = make_float4(bp.rec[8], bp.rec[9], bp.rec[10], bp.rec[11]);
-        q.info = make_uint4(bp.shape, bp.prim, bp.type, 0u);
+        // w: position in scene order (shapes, then faces) = the tie-break key
+        q.info = make_uint4(bp.shape, bp.prim, bp.type, bld.order[i]);
         dst[i] = q;
     }
 }

@@ -32,7 +32,7 @@ struct alignas(16) Node {       // 64 B: two child boxes (Aila-Laine BVH2 layout
 
 struct alignas(16) Prim {       // 64 B primitive record
     float4 a, b, c;             // triangle: v0, e1 = v1 - v0, e2 = v2 - v0; rectangle: to_object rows
-    uint4 info;                 // x: shape, y: prim index (face; ~0 for rectangles), z: type
+    uint4 info;                 // x: shape, y: prim index (face; ~0 for rectangles), z: type, w: scene-order key
 };
 
 struct DShape {                 // shading-time shape record

@@ -40,7 +40,8 @@ struct BvhOut {
     std::vector<uint8_t> prims;  // sizeof(Prim) * n_prims (reordered)
     uint32_t n_nodes = 0, n_prims = 0, depth = 0;
 };
-void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out);
+// max_leaf <= 31 (5-bit leaf count of the per-lane stream engine's stack entries)
+void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf = 4, float trav_cost = 1.0f);
 
 // ---- kernel launchers (mh_kernels.hip) -------------------------------------
 size_t lds_bytes(const DScene &S, uint32_t block);

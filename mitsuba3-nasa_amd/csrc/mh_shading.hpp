@@ -15,6 +15,7 @@ namespace mh {
 struct Hit {
     float t, u, v;
     uint32_t prim, shape;
+    uint32_t key;  // scene-order key of the hit primitive (exact-t tie-break)
 };
 
 struct RayT {
@@ -64,6 +65,14 @@ MH_DEV float safe_rcp_dir(float d) {
 }
 MH_DEV V3 safe_inv_dir(V3 d) { return v3(safe_rcp_dir(d.x), safe_rcp_dir(d.y), safe_rcp_dir(d.z)); }
 
+// Closest-hit update rule.  Exact-t ties (coincident surfaces, e.g. a cube
+// standing on the floor) resolve to the lowest (shape, prim) — the scene
+// order in which the oracle's brute force (and a scalar scene walk) meets
+// them — so the result does not depend on the BVH's visiting order.
+MH_DEV bool closer(float tt, const Prim &p, const Hit &hit) {
+    return tt < hit.t || (tt == hit.t && p.info.w < hit.key);
+}
+
 // Slab test for both children; conservative (host pads every box).
 MH_DEV void box2(const Node &n, V3 inv, V3 ood, float tmax, bool &h0, bool &h1, float &t0,
                  float &t1) {
@@ -95,6 +104,7 @@ MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32
     hit.u = hit.v = 0.f;
     hit.prim = MH_INVALID;
     hit.shape = MH_INVALID;
+    hit.key = MH_INVALID;
     if (nodes == nullptr) return false;  // scene without primitives
     uint32_t sp = 0;
     uint32_t node = 0;
@@ -111,9 +121,9 @@ MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32
             for (uint32_t i = 0; i < n0; ++i) {
                 const Prim p = prims[c0 + i];
                 float t, u, v;
-                if (prim_test(p, r, t, u, v) && (Shadow || t < hit.t)) {
+                if (prim_test(p, r, t, u, v) && (Shadow || closer(t, p, hit))) {
                     if (Shadow) return true;
-                    hit.t = t; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x;
+                    hit.t = t; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x; hit.key = p.info.w;
                     best = t;
                 }
             }
@@ -123,9 +133,9 @@ MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32
             for (uint32_t i = 0; i < n1; ++i) {
                 const Prim p = prims[c1 + i];
                 float t, u, v;
-                if (prim_test(p, r, t, u, v) && (Shadow || t < hit.t)) {
+                if (prim_test(p, r, t, u, v) && (Shadow || closer(t, p, hit))) {
                     if (Shadow) return true;
-                    hit.t = t; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x;
+                    hit.t = t; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x; hit.key = p.info.w;
                     best = t;
                 }
             }
@@ -254,7 +264,7 @@ MH_DEV DScene stage_tables(const DScene &S, uint4 *lds) {
 // (inner-node phase until every lane holds a leaf, then a grouped leaf phase)
 // with per-lane ray refill from the wave's contiguous item range.  Same hit
 // semantics as traverse<>: closest hit with t in [0, maxt], strict-< update.
-// Stack entries: inner node index, or kLeafBit | first << 3 | count.
+// Stack entries: inner node index, or kLeafBit | first << 5 | count (count <= 31).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kNoNode = 0xffffffffu;  // pop next
@@ -282,6 +292,7 @@ MH_DEV void trav_init(TravLane &t, const RayT &r, bool empty_scene) {
     t.hit.u = t.hit.v = 0.f;
     t.hit.prim = MH_INVALID;
     t.hit.shape = MH_INVALID;
+    t.hit.key = MH_INVALID;
 }
 
 // Does the lane take part in the next inner step?  It does while it has an
@@ -298,8 +309,8 @@ MH_DEV bool trav_wants(const TravLane &t) {
 // `node` (processed after the held leaf)
 MH_DEV void trav_take(TravLane &t, uint32_t ref) {
     if ((ref & kLeafBit) && t.nleaf == 0) {
-        t.leaf = (ref & ~kLeafBit) >> 3;
-        t.nleaf = ref & 7u;
+        t.leaf = (ref & ~kLeafBit) >> 5;
+        t.nleaf = ref & 31u;
         t.node = kNoNode;
     } else {
         t.node = ref;
@@ -321,8 +332,8 @@ MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint3
     box2(n, t.inv, t.ood, t.best, h0, h1, t0, t1);
     const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
     const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
-    const uint32_t r0 = n0 ? (kLeafBit | (c0 << 3) | n0) : c0;
-    const uint32_t r1 = n1 ? (kLeafBit | (c1 << 3) | n1) : c1;
+    const uint32_t r0 = n0 ? (kLeafBit | (c0 << 5) | n0) : c0;
+    const uint32_t r1 = n1 ? (kLeafBit | (c1 << 5) | n1) : c1;
     if (h0 && h1) {
         const bool swap = t1 < t0;
         stk[t.sp * stride] = swap ? r0 : r1;
@@ -343,8 +354,8 @@ MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
     for (uint32_t i = 0; i < t.nleaf; ++i) {
         const Prim p = prims[t.leaf + i];
         float tt, u, v;
-        if (prim_test(p, r, tt, u, v) && (Shadow || tt < t.hit.t)) {
-            t.hit.t = tt; t.hit.u = u; t.hit.v = v; t.hit.prim = p.info.y; t.hit.shape = p.info.x;
+        if (prim_test(p, r, tt, u, v) && (Shadow || closer(tt, p, t.hit))) {
+            t.hit.t = tt; t.hit.u = u; t.hit.v = v; t.hit.prim = p.info.y; t.hit.shape = p.info.x; t.hit.key = p.info.w;
             t.best = tt;
             if (Shadow) { t.node = kDone; t.sp = 0; break; }
         }
@@ -429,8 +440,8 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
         if (lane_hit && (!Shadow || hit.shape == MH_INVALID)) {
             float tt, u, v;
             const bool ok = p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, tt, u, v) : tri_test(p, r, tt, u, v);
-            if (ok && (Shadow || tt < hit.t)) {
-                hit.t = tt; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x;
+            if (ok && (Shadow || closer(tt, p, hit))) {
+                hit.t = tt; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x; hit.key = p.info.w;
                 best = tt;
             }
         }
@@ -457,6 +468,7 @@ MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const LdsBvh &B
         hit.u = hit.v = 0.f;
         hit.prim = MH_INVALID;
         hit.shape = MH_INVALID;
+        hit.key = MH_INVALID;
         bool act = has && gnodes != nullptr;
         uint32_t node = 0, sp = 0;
         while (__any(act)) {
