@@ -266,3 +266,20 @@ def test_prb_backward_bitmap_parity(spp):
         a = a.cpu().numpy()
         assert a.shape == b.shape
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max())
+
+
+# ---------------------------------------------------------------------------
+# Config 5: W*H*spp > 2^32 -> passes of spp_per_pass samples, each lane's RNG
+# continuing across passes (integrator.cpp:281-295, 353-357)
+# ---------------------------------------------------------------------------
+@pytest.mark.slow
+def test_multipass_config5_slab_parity():
+    mi = _mi()
+    scene = cbox(mi, 2048, 2048, 1024)
+    integ = mi.load_dict({"type": "path", "max_depth": 4})
+    # 2048^2 * 1024 = 2^32 > 2^32 - 1: two passes of 512; lanes [0, 2) of every pixel
+    film = mi.render_film(scene, integ, seed=2, spp=1024, spp_begin=0, spp_end=2).cpu().numpy()
+    ref = O.render(scene, integ, seed=2, spp=1024, spp_begin=0, spp_end=2)
+    assert ref[..., 3].sum() > 0
+    ok, frac = _film_close(film, ref)
+    assert ok, f"film parity {frac}"
