@@ -65,8 +65,11 @@ k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *_
 // out planes (each `plane` floats apart): Lr, Lg, Lb, posx, posy; sample
 // (k, pass) stored at pass * n + k.
 // Kind: MH_INTEGRATOR_PATH / MH_INTEGRATOR_PRB (primal) / MH_INTEGRATOR_VOLPATH
+#ifndef MH_VOL_WAVES
+#define MH_VOL_WAVES 4  // volpath: 128 VGPRs (+ some scratch) measured +10 % over 2 waves (tools/exp_volwaves.sh)
+#endif
 template <int Kind, bool InLds>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, Kind == MH_INTEGRATOR_VOLPATH ? MH_VOL_WAVES : 1)
 k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_t n_passes,
          uint64_t n, uint64_t plane, float *__restrict__ out, unsigned long long *__restrict__ counters) {
     extern __shared__ uint4 lds[];
