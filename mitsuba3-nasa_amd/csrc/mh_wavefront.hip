@@ -176,6 +176,19 @@ k_wf_raygen(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plan
     out[3 * plane + k] = sx; out[4 * plane + k] = sy;
 }
 
+// does any wave of this workgroup get items of its segment?  (uniform per
+// block: lets empty workgroups of short late-bounce queues exit before
+// staging anything into LDS)
+MH_DEV bool block_has_stride_work(const SegIter &it, uint32_t n) {
+    const uint32_t first_wave = (blockIdx.x / kSeg) * (blockDim.x / 64u);
+    return first_wave * 64u < n;
+}
+MH_DEV bool block_has_range_work(const SegIter &it, uint32_t n) {
+    const uint32_t first_wave = (blockIdx.x / kSeg) * (blockDim.x / 64u);
+    const uint32_t per = (n + it.nwaves - 1) / it.nwaves;
+    return first_wave * per < n;
+}
+
 // contiguous share of a segment for this wave (refill traversal)
 MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1) {
     const uint32_t per = (n + it.nwaves - 1) / it.nwaves;
@@ -188,9 +201,10 @@ template <bool InLds, bool Packet>
 __global__ void __launch_bounds__(256)
 k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh<InLds>(S, lds);
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_range_work(it, n)) return;
+    LdsBvh B = stage_bvh<InLds && !Packet>(S, lds);  // the packet engine reads the BVH via s_load
     const uint32_t base = it.seg * seg_cap;
     const float *ox = w.ox[cur], *oy = w.oy[cur], *oz = w.oz[cur], *dx = w.dx[cur], *dy = w.dy[cur],
                 *dz = w.dz[cur], *mt = w.mt[cur];
@@ -215,9 +229,10 @@ __global__ void __launch_bounds__(256, 5)
 k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
            float *out, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     extern __shared__ uint4 lds[];
-    const DScene S = Staged ? stage_tables(S0, lds) : S0;
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_stride_work(it, n)) return;
+    const DScene S = Staged ? stage_tables(S0, lds) : S0;
     const uint32_t sbase = it.seg * seg_cap;  // slots (state, hits, shadow records) of this segment
     const int nxt = cur ^ 1;
     for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
@@ -344,9 +359,10 @@ template <bool InLds, bool Packet>
 __global__ void __launch_bounds__(256)
 k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh<InLds>(S, lds);
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_range_work(it, n)) return;
+    LdsBvh B = stage_bvh<InLds && !Packet>(S, lds);
     const uint32_t base = it.seg * seg_cap;
     uint32_t r0, r1;
     wave_range(it, n, r0, r1);
@@ -508,9 +524,10 @@ __global__ void __launch_bounds__(256, 5)
 k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     extern __shared__ uint4 lds[];
-    const DScene S = Staged ? stage_tables(S0, lds) : S0;
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_stride_work(it, n)) return;
+    const DScene S = Staged ? stage_tables(S0, lds) : S0;
     const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
     const uint32_t n_rgb = q.n_rgb;
@@ -669,9 +686,10 @@ template <bool InLds, bool Packet, int NR>
 __global__ void __launch_bounds__(256)
 k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
-    LdsBvh B = stage_bvh<InLds>(S, lds);
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_range_work(it, n)) return;
+    LdsBvh B = stage_bvh<InLds && !Packet>(S, lds);
     const uint32_t base = it.seg * seg_cap;
     const uint32_t n_rgb = q.n_rgb;
     float acc[NR][3];
