@@ -767,11 +767,83 @@ MH_DEV V3 area_sample_direction(const DScene &S, uint32_t em, V3 ref_p, float sx
     return vdiv(v3(e.radiance[0], e.radiance[1], e.radiance[2]), ds.pdf);
 }
 
-// Scene::sample_emitter_direction, single emitter (scene.cpp:335-346), with
-// the shadow test; a sample whose weight is exactly zero traces no shadow ray.
+constexpr float kInv4Pi = 0.07957747154594766788f;
+
+// warp::square_to_uniform_sphere (core/warp.h:250-255)
+MH_DEV V3 square_to_uniform_sphere(float sx, float sy) {
+    float z = __builtin_fmaf(-2.f, sy, 1.f);
+    float r = __builtin_sqrtf(fmaxf(__builtin_fmaf(-z, z, 1.f), 0.f));
+    float s, c;
+    sincos_cephes((2.f * kPi) * sx, s, c);
+    return v3(r * c, r * s, z);
+}
+
+// Emitter::sample_direction: area (area.cpp:118-168), constant
+// (constant.cpp:112-140), directional (directional.cpp:150-175)
+MH_DEV V3 emitter_sample_direction(const DScene &S, uint32_t em, V3 ref_p, float sx, float sy, DirS &ds) {
+    const DEmitter &e = S.emitters[em];
+    if (e.type == MH_EMITTER_AREA) return area_sample_direction(S, em, ref_p, sx, sy, ds);
+    if (e.type == MH_EMITTER_CONSTANT) {
+        V3 d = square_to_uniform_sphere(sx, sy);
+        V3 c = v3(e.center[0], e.center[1], e.center[2]);
+        float radius = fmaxf(e.radius, norm(ref_p - c)), dist = 2.f * radius;
+        ds.p = fma3s(d, dist, ref_p);
+        ds.n = -d;
+        ds.pdf = kInv4Pi;
+        ds.delta = false;
+        ds.d = d;
+        ds.dist = dist;
+        return vdiv(v3(e.radiance[0], e.radiance[1], e.radiance[2]), ds.pdf);
+    }
+    // directional: ds.p = p - d * inf (NaN where d has a zero component, as in the reference)
+    V3 d = v3(e.direction[0], e.direction[1], e.direction[2]);
+    const float dist = __builtin_huge_valf();
+    ds.p = ref_p - d * dist;
+    ds.n = d;
+    ds.pdf = 1.f;
+    ds.delta = true;
+    ds.d = -d;
+    ds.dist = dist;
+    return v3(e.radiance[0], e.radiance[1], e.radiance[2]);
+}
+
+// Scene::sample_emitter_direction without the visibility test (scene.cpp:299-353)
+MH_DEV V3 scene_sample_emitter_direction(const DScene &S, V3 ref_p, float sx, float sy, DirS &ds) {
+    ds.p = ds.n = ds.d = v3(0, 0, 0);
+    ds.dist = ds.pdf = 0.f;
+    ds.delta = false;
+    const uint32_t n = S.n_emitters;
+    if (n == 0) return v3(0, 0, 0);
+    if (n == 1) return emitter_sample_direction(S, 0, ref_p, sx, sy, ds);
+    const float nf = (float)n, scaled = sx * nf;
+    uint32_t idx = (uint32_t)scaled;
+    if (idx > n - 1) idx = n - 1;
+    V3 spec = emitter_sample_direction(S, idx, ref_p, scaled - (float)idx, sy, ds);
+    ds.pdf *= 1.f / nf;
+    return spec * nf;
+}
+
+MH_DEV V3 emitter_eval(const DScene &S, uint32_t em, const SI &si) {
+    const DEmitter &e = S.emitters[em];
+    V3 L = v3(e.radiance[0], e.radiance[1], e.radiance[2]);
+    if (e.type == MH_EMITTER_AREA) return si.wi.z > 0.f ? L : v3(0, 0, 0);
+    if (e.type == MH_EMITTER_CONSTANT) return L;
+    return v3(0, 0, 0);
+}
+
+// Scene::pdf_emitter_direction of DirectionSample3f(scene, si, ref) (scene.cpp:355-366)
+MH_DEV float emitter_pdf_direction(const DScene &S, uint32_t em, const SI &si, V3 ref_p) {
+    const DEmitter &e = S.emitters[em];
+    if (e.type == MH_EMITTER_AREA) return emitter_hit_pdf(S, em, si, ref_p);
+    if (e.type == MH_EMITTER_CONSTANT) return kInv4Pi * (1.f / (float)S.n_emitters);
+    return 0.f;
+}
+
+// Scene::sample_emitter_direction (scene.cpp:299-353) with the shadow test;
+// a sample whose weight is exactly zero traces no shadow ray.
 MH_DEV V3 sample_emitter_direction(const DScene &S, const LdsBvh &B, const SI &si, float sx,
                                    float sy, DirS &ds, uint32_t &n_shadow) {
-    V3 spec = area_sample_direction(S, 0, si.p, sx, sy, ds);
+    V3 spec = scene_sample_emitter_direction(S, si.p, sx, sy, ds);
     if (ds.pdf != 0.f && nonzero(spec)) {
         RayT r = spawn_ray_to(si.p, si.n, ds.p);
         Hit h;
@@ -858,11 +930,11 @@ MH_DEV V3 path_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &
         // ---- direct emission (path.cpp:158-174)
         uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
         if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
             float mis_bsdf = mis_weight(prev_bsdf_pdf, em_pdf);
             V3 le = v3(0, 0, 0);
-            if (prev_bsdf_pdf > 0.f && si.valid && si.wi.z > 0.f)
-                le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+            if (prev_bsdf_pdf > 0.f)
+                le = emitter_eval(S, em, si);
             result = fma3(throughput, le * mis_bsdf, result);
         }
 
@@ -876,6 +948,7 @@ MH_DEV V3 path_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &
         DirS ds;
         ds.pdf = 0.f;
         ds.d = v3(0, 0, 0);
+        ds.delta = false;
         V3 em_weight = v3(0, 0, 0), wo = v3(0, 0, 0);
         if (active_em) {
             em_weight = sample_emitter_direction(S, B, si, e0, e1, ds, n_shadow);
@@ -899,7 +972,7 @@ MH_DEV V3 path_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &
 
         // ---- emitter sampling contribution (path.cpp:220-230)
         if (active_em) {
-            float mis_em = mis_weight(ds.pdf, bsdf_pdf);
+            float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf);
             result = fma3(throughput, (bsdf_val * em_weight) * mis_em, result);
         }
 
@@ -991,11 +1064,11 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
         uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
         V3 Le = v3(0, 0, 0);
         if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
             float mis = mis_weight(prev_bsdf_pdf, em_pdf);
             V3 le = v3(0, 0, 0);
-            if (active_next && si.valid && si.wi.z > 0.f)
-                le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+            if (active_next)
+                le = emitter_eval(S, em, si);
             Le = (beta * mis) * le;
         }
 
@@ -1006,6 +1079,7 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
         DirS ds;
         ds.pdf = 0.f;
         ds.d = v3(0, 0, 0);
+        ds.delta = false;
         V3 em_weight = v3(0, 0, 0);
         if (active_em) {
             em_weight = sample_emitter_direction(S, B, si, e0, e1, ds, n_shadow);
@@ -1017,7 +1091,7 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
         V3 bsdf_value_em;
         float bsdf_pdf_em;
         diffuse_eval_pdf(rho, si.wi, wo_em, active_em, bsdf_value_em, bsdf_pdf_em);
-        float mis_em = mis_weight(ds.pdf, bsdf_pdf_em);
+        float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
         V3 beta_mis_em = beta * mis_em;
         V3 Lr_dir = active_em ? (beta_mis_em * bsdf_value_em) * em_weight : v3(0, 0, 0);
 
@@ -1214,11 +1288,11 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         if (in.hide_emitters && depth == 0 && !si.valid) active_next = false;
         uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
         if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
             float mis = mis_weight(prev_bsdf_pdf, em_pdf);
             V3 le = v3(0, 0, 0);
-            if (active_next && si.valid && si.wi.z > 0.f)
-                le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+            if (active_next)
+                le = emitter_eval(S, em, si);
             charge(g.acc, A, n_rgb, dL * ((beta * mis) * le));
         }
         active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
@@ -1227,6 +1301,7 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         DirS ds;
         ds.pdf = 0.f;
         ds.d = v3(0, 0, 0);
+        ds.delta = false;
         V3 em_weight = v3(0, 0, 0);
         if (active_em) {
             em_weight = sample_emitter_direction(S, B, si, e0, e1, ds, n_shadow);
@@ -1238,7 +1313,7 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         V3 bsdf_value_em;
         float bsdf_pdf_em;
         diffuse_eval_pdf(rho, si.wi, wo_em, active_em, bsdf_value_em, bsdf_pdf_em);
-        float mis_em = mis_weight(ds.pdf, bsdf_pdf_em);
+        float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
         V3 beta_mis_em = beta * mis_em;
         if (active_em) charge(g.acc, A, n_rgb, dL * ((beta_mis_em * bsdf_value_em) * em_weight));
         (void)rng.next_float();
@@ -1283,78 +1358,6 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
 // HG / isotropic phase.  Same operation order as the oracle restatement
 // (oracle/mh_oracle.c, "volpath" section).
 // ===========================================================================
-constexpr float kInv4Pi = 0.07957747154594766788f;
-
-// warp::square_to_uniform_sphere (core/warp.h:250-255)
-MH_DEV V3 square_to_uniform_sphere(float sx, float sy) {
-    float z = __builtin_fmaf(-2.f, sy, 1.f);
-    float r = __builtin_sqrtf(fmaxf(__builtin_fmaf(-z, z, 1.f), 0.f));
-    float s, c;
-    sincos_cephes((2.f * kPi) * sx, s, c);
-    return v3(r * c, r * s, z);
-}
-
-// Emitter::sample_direction: area (area.cpp:118-168), constant
-// (constant.cpp:112-140), directional (directional.cpp:150-175)
-MH_DEV V3 emitter_sample_direction(const DScene &S, uint32_t em, V3 ref_p, float sx, float sy, DirS &ds) {
-    const DEmitter &e = S.emitters[em];
-    if (e.type == MH_EMITTER_AREA) return area_sample_direction(S, em, ref_p, sx, sy, ds);
-    if (e.type == MH_EMITTER_CONSTANT) {
-        V3 d = square_to_uniform_sphere(sx, sy);
-        V3 c = v3(e.center[0], e.center[1], e.center[2]);
-        float radius = fmaxf(e.radius, norm(ref_p - c)), dist = 2.f * radius;
-        ds.p = fma3s(d, dist, ref_p);
-        ds.n = -d;
-        ds.pdf = kInv4Pi;
-        ds.delta = false;
-        ds.d = d;
-        ds.dist = dist;
-        return vdiv(v3(e.radiance[0], e.radiance[1], e.radiance[2]), ds.pdf);
-    }
-    // directional: ds.p = p - d * inf (NaN where d has a zero component, as in the reference)
-    V3 d = v3(e.direction[0], e.direction[1], e.direction[2]);
-    const float dist = __builtin_huge_valf();
-    ds.p = ref_p - d * dist;
-    ds.n = d;
-    ds.pdf = 1.f;
-    ds.delta = true;
-    ds.d = -d;
-    ds.dist = dist;
-    return v3(e.radiance[0], e.radiance[1], e.radiance[2]);
-}
-
-// Scene::sample_emitter_direction without the visibility test (scene.cpp:299-353)
-MH_DEV V3 scene_sample_emitter_direction(const DScene &S, V3 ref_p, float sx, float sy, DirS &ds) {
-    ds.p = ds.n = ds.d = v3(0, 0, 0);
-    ds.dist = ds.pdf = 0.f;
-    ds.delta = false;
-    const uint32_t n = S.n_emitters;
-    if (n == 0) return v3(0, 0, 0);
-    if (n == 1) return emitter_sample_direction(S, 0, ref_p, sx, sy, ds);
-    const float nf = (float)n, scaled = sx * nf;
-    uint32_t idx = (uint32_t)scaled;
-    if (idx > n - 1) idx = n - 1;
-    V3 spec = emitter_sample_direction(S, idx, ref_p, scaled - (float)idx, sy, ds);
-    ds.pdf *= 1.f / nf;
-    return spec * nf;
-}
-
-MH_DEV V3 emitter_eval(const DScene &S, uint32_t em, const SI &si) {
-    const DEmitter &e = S.emitters[em];
-    V3 L = v3(e.radiance[0], e.radiance[1], e.radiance[2]);
-    if (e.type == MH_EMITTER_AREA) return si.wi.z > 0.f ? L : v3(0, 0, 0);
-    if (e.type == MH_EMITTER_CONSTANT) return L;
-    return v3(0, 0, 0);
-}
-
-// Scene::pdf_emitter_direction of DirectionSample3f(scene, si, ref) (scene.cpp:355-366)
-MH_DEV float emitter_pdf_direction(const DScene &S, uint32_t em, const SI &si, V3 ref_p) {
-    const DEmitter &e = S.emitters[em];
-    if (e.type == MH_EMITTER_AREA) return emitter_hit_pdf(S, em, si, ref_p);
-    if (e.type == MH_EMITTER_CONSTANT) return kInv4Pi * (1.f / (float)S.n_emitters);
-    return 0.f;
-}
-
 // ---- media -----------------------------------------------------------------
 struct MEI {
     bool valid;

@@ -271,11 +271,11 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
             // ---- direct emission (path.cpp:158-174)
             const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
             if (em != MH_INVALID) {
-                float em_pdf = prev_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+                float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
                 float mis_bsdf = mis_weight(prev_pdf, em_pdf);
                 V3 le = v3(0, 0, 0);
-                if (prev_pdf > 0.f && si.valid && si.wi.z > 0.f)
-                    le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+                if (prev_pdf > 0.f)
+                    le = emitter_eval(S, em, si);
                 V3 L = v3(out[pid], out[plane + pid], out[2 * plane + pid]);
                 L = fma3(tp, le * mis_bsdf, L);
                 out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
@@ -290,9 +290,10 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
             DirS ds;
             ds.pdf = 0.f;
             ds.d = v3(0, 0, 0);
+            ds.delta = false;
             V3 em_weight = v3(0, 0, 0), wo = v3(0, 0, 0);
             if (active_em) {
-                em_weight = area_sample_direction(S, 0, si.p, e0, e1, ds);
+                em_weight = scene_sample_emitter_direction(S, si.p, e0, e1, ds);
                 if (ds.pdf != 0.f && nonzero(em_weight)) {
                     shadow = true;
                     sray = spawn_ray_to(si.p, si.n, ds.p);
@@ -315,7 +316,7 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
             }
             if (shadow) {  // (path.cpp:220-230), applied by k_wf_shadow if unoccluded
                 a_nee = tp;
-                b_nee = (bsdf_val * em_weight) * mis_weight(ds.pdf, bsdf_pdf);
+                b_nee = (bsdf_val * em_weight) * (ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf));
             }
 
             // ---- BSDF sampling, state update, Russian roulette (path.cpp:234-280)
@@ -577,11 +578,11 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
             // ---- emission (prb.py:143-152): charged to the earlier vertices
             const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
             if (em != MH_INVALID) {
-                float em_pdf = prev_delta ? 0.f : emitter_hit_pdf(S, em, si, prev_p);
+                float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
                 float mis = mis_weight(prev_pdf, em_pdf);
                 V3 le = v3(0, 0, 0);
-                if (active_next && si.valid && si.wi.z > 0.f)
-                    le = v3(S.emitters[em].radiance[0], S.emitters[em].radiance[1], S.emitters[em].radiance[2]);
+                if (active_next)
+                    le = emitter_eval(S, em, si);
                 charge(acc, A, n_rgb, dL * ((beta * mis) * le));
             }
             active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
@@ -592,9 +593,10 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
             DirS ds;
             ds.pdf = 0.f;
             ds.d = v3(0, 0, 0);
+            ds.delta = false;
             V3 em_weight = v3(0, 0, 0);
             if (active_em0) {
-                em_weight = area_sample_direction(S, 0, si.p, e0, e1, ds);
+                em_weight = scene_sample_emitter_direction(S, si.p, e0, e1, ds);
                 if (ds.pdf != 0.f && nonzero(em_weight)) {
                     shadow = true;
                     sray = spawn_ray_to(si.p, si.n, ds.p);
@@ -608,7 +610,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
                 V3 bsdf_value_em;
                 float bsdf_pdf_em;
                 diffuse_eval_pdf(rho, si.wi, wo_em, true, bsdf_value_em, bsdf_pdf_em);
-                float mis_em = mis_weight(ds.pdf, bsdf_pdf_em);
+                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
                 V3 beta_mis_em = beta * mis_em;
                 V3 dLe = dL * ((beta_mis_em * bsdf_value_em) * em_weight);
 #pragma unroll

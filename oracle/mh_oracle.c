@@ -893,15 +893,19 @@ static v3 area_sample_direction(const mh_scene_desc *d, uint32_t em, v3 ref_p, f
     return vdivs(vload(e->radiance), ds->pdf);
 }
 
-/* Scene::sample_emitter_direction, single emitter branch (scene.cpp:335-346),
-   test_visibility = true.  A shadow ray whose contribution is exactly zero
-   (back-facing light sample) is skipped: it cannot change the result.     */
+/* defined with the volpath plugins below */
+static v3 scene_sample_emitter_direction(const mh_scene_desc *d, v3 ref_p, float sx, float sy,
+                                         dir_sample *ds);
+static v3 emitter_eval(const mh_scene_desc *d, uint32_t em, const surf_int *si);
+static float emitter_pdf_direction(const mh_scene_desc *d, uint32_t em, const surf_int *si, v3 ref_p);
+
+/* Scene::sample_emitter_direction (scene.cpp:299-353), test_visibility =
+   true.  A shadow ray whose contribution is exactly zero (back-facing light
+   sample) is skipped: it cannot change the result.                        */
 static v3 sample_emitter_direction(const scene_view *sv, const surf_int *si, float sx, float sy,
                                    dir_sample *ds, uint64_t *n_shadow) {
     const mh_scene_desc *d = sv->d;
-    memset(ds, 0, sizeof(*ds));
-    if (d->n_emitters == 0) return V3(0, 0, 0);
-    v3 spec = area_sample_direction(d, 0, si->p, sx, sy, ds);
+    v3 spec = scene_sample_emitter_direction(d, si->p, sx, sy, ds);
     if (ds->pdf != 0.f && (spec.x != 0.f || spec.y != 0.f || spec.z != 0.f)) {
         ray3 r = spawn_ray_to(si->p, si->n, ds->p);
         if (n_shadow) (*n_shadow)++;
@@ -979,10 +983,10 @@ static v3 path_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng,
         /* ---- direct emission (path.cpp:158-174) ---- */
         uint32_t em = si_emitter(d, &si);
         if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(d, em, &si, prev_p);
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_pdf_direction(d, em, &si, prev_p);
             float mis_bsdf = mis_weight(prev_bsdf_pdf, em_pdf);
             v3 le = V3(0, 0, 0);
-            if (prev_bsdf_pdf > 0.f && si.valid && si.wi.z > 0.f) le = vload(d->emitters[em].radiance);
+            if (prev_bsdf_pdf > 0.f) le = emitter_eval(d, em, &si);
             result = vfma(throughput, vscale(le, mis_bsdf), result);
         }
 
@@ -1076,10 +1080,10 @@ static v3 prb_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng, 
         uint32_t em = si_emitter(d, &si);
         v3 Le = V3(0, 0, 0);
         if (em != MH_INVALID) {
-            float em_pdf = prev_bsdf_delta ? 0.f : emitter_hit_pdf(d, em, &si, prev_p);
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_pdf_direction(d, em, &si, prev_p);
             float mis = mis_weight(prev_bsdf_pdf, em_pdf);
             v3 le = V3(0, 0, 0);
-            if (active_next && si.valid && si.wi.z > 0.f) le = vload(d->emitters[em].radiance);
+            if (active_next) le = emitter_eval(d, em, &si);
             Le = vmul(vscale(beta, mis), le);
         }
 
