@@ -174,9 +174,18 @@ def main():
         launches = max(1, st_f.n_trace_launches)
         rays_per_launch = st_f.rays_closest / launches
         us_per_launch = st_f.ms_trace / launches * 1e3
-        bytes_launch = rays_per_launch * 48.0
+        if st_f.mode == 2:
+            # fused bounce kernel: per path-bounce the state is read
+            # (pd 4 + ray 28 + throughput 12 + prev_p 12 + prev_pdf 4 + PCG 8 + L 12
+            # = 80 B) and written for survivors (80 B); a finished path writes L (12 B).
+            # sum of queue lengths R = rays_closest, survivors R - N, deaths N = samples
+            R, N = float(st_f.rays_closest), float(n_local)
+            bytes_launch = (80.0 * R + 80.0 * (R - N) + 12.0 * N) / launches
+            kname = "k_wf_bounce"
+        else:
+            bytes_launch = rays_per_launch * 48.0
+            kname = "k_wf_trace" if st_f.mode == 1 else "k_render"
         achieved = bytes_launch / (us_per_launch / 1e6) / 1e9
-        kname = "k_wf_trace" if st_f.mode == 1 else "k_render"
         traffic = None
         tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):

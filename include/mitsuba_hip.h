@@ -203,9 +203,9 @@ typedef struct mh_stats {
     uint64_t bounces;           /* active lane-bounces */
     double   ms_total;          /* wall time of the call (host clock, ms) */
     double   ms_kernel;         /* device time of the dominant kernel (hipEvents, ms) */
-    double   ms_trace;          /* wavefront: device time of all k_wf_trace launches (ms) */
-    uint64_t n_trace_launches;  /* wavefront: number of k_wf_trace launches */
-    uint32_t mode;              /* 0 megakernel, 1 wavefront */
+    double   ms_trace;          /* wavefront: device time of all k_wf_trace (mode 1) / k_wf_bounce (mode 2) launches (ms) */
+    uint64_t n_trace_launches;  /* wavefront: number of those launches */
+    uint32_t mode;              /* 0 megakernel, 1 wavefront (trace/shade/shadow), 2 wavefront fused bounce kernel */
     uint32_t pad0;
 } mh_stats;
 

@@ -606,7 +606,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         stats->ms_kernel = kernel_ms;
         stats->ms_trace = trace_ms;
         stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces : 0;
-        stats->mode = wavefront ? 1u : 0u;
+        stats->mode = wavefront ? (wf_fused(s->S) ? 2u : 1u) : 0u;
     }
     return MH_OK;
 }

@@ -63,7 +63,8 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
                             hipEvent_t *trace_ev, hipStream_t st);
 size_t wf_prb_workspace_bytes(uint64_t cap);
-uint32_t wf_grid(uint32_t grid);  // grid rounded to whole queue segments
+uint32_t wf_grid(uint32_t grid);
+bool wf_fused(const DScene &S);  // launch_wavefront runs the fused bounce kernel  // grid rounded to whole queue segments
 hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                 uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
                                 const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,

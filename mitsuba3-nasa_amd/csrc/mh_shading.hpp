@@ -450,6 +450,53 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
 
 // gnodes / gprims: the BVH in global memory (read via the scalar cache);
 // B provides the LDS stack region (one wave-uniform stack per wave).
+// One batch: the wave's 64 rays (act: lanes that hold a ray).  ws: the
+// wave-uniform stack (entry k at ws[k * stride]).
+template <bool Shadow>
+MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, uint32_t stride, const RayT &r,
+                        bool act) {
+    const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
+    float best = r.maxt;
+    Hit hit;
+    hit.t = __builtin_huge_valf();
+    hit.u = hit.v = 0.f;
+    hit.prim = MH_INVALID;
+    hit.shape = MH_INVALID;
+    hit.key = MH_INVALID;
+    act = act && gnodes != nullptr;
+    uint32_t node = 0, sp = 0;
+    while (__any(act)) {
+        const Node n = load_uniform(gnodes, node);
+        bool h0, h1;
+        float t0, t1;
+        box2(n, inv, ood, best, h0, h1, t0, t1);
+        h0 = h0 && act;
+        h1 = h1 && act;
+        const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
+        const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
+        bool any0 = __any(h0), any1 = __any(h1);
+        if (any0 && n0) { packet_leaf<Shadow>(gprims, c0, n0, h0, r, hit, best); any0 = false; }
+        if (any1 && n1) { packet_leaf<Shadow>(gprims, c1, n1, h1, r, hit, best); any1 = false; }
+        if (Shadow) act = act && hit.shape == MH_INVALID;
+        if (any0 && any1) {
+            const unsigned long long both = __ballot(h0 && h1), pref1 = __ballot(h0 && h1 && t1 < t0);
+            const bool first1 = 2u * (uint32_t)__popcll(pref1) > (uint32_t)__popcll(both);
+            ws[sp * stride] = first1 ? c0 : c1;
+            ++sp;
+            node = first1 ? c1 : c0;
+        } else if (any0) {
+            node = c0;
+        } else if (any1) {
+            node = c1;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = __builtin_amdgcn_readfirstlane(ws[sp * stride]);
+        }
+    }
+    return hit;
+}
+
 template <bool Shadow, class Load, class Store>
 MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const LdsBvh &B, uint32_t r0, uint32_t r1,
                          Load load, Store store) {
@@ -461,45 +508,7 @@ MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const LdsBvh &B
         RayT r;
         if (has) r = load(item);
         else r = RayT{v3(0, 0, 0), v3(0, 0, 1), -1.f};
-        const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
-        float best = r.maxt;
-        Hit hit;
-        hit.t = __builtin_huge_valf();
-        hit.u = hit.v = 0.f;
-        hit.prim = MH_INVALID;
-        hit.shape = MH_INVALID;
-        hit.key = MH_INVALID;
-        bool act = has && gnodes != nullptr;
-        uint32_t node = 0, sp = 0;
-        while (__any(act)) {
-            const Node n = load_uniform(gnodes, node);
-            bool h0, h1;
-            float t0, t1;
-            box2(n, inv, ood, best, h0, h1, t0, t1);
-            h0 = h0 && act;
-            h1 = h1 && act;
-            const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
-            const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
-            bool any0 = __any(h0), any1 = __any(h1);
-            if (any0 && n0) { packet_leaf<Shadow>(gprims, c0, n0, h0, r, hit, best); any0 = false; }
-            if (any1 && n1) { packet_leaf<Shadow>(gprims, c1, n1, h1, r, hit, best); any1 = false; }
-            if (Shadow) act = act && hit.shape == MH_INVALID;
-            if (any0 && any1) {
-                const unsigned long long both = __ballot(h0 && h1), pref1 = __ballot(h0 && h1 && t1 < t0);
-                const bool first1 = 2u * (uint32_t)__popcll(pref1) > (uint32_t)__popcll(both);
-                ws[sp * B.stride] = first1 ? c0 : c1;
-                ++sp;
-                node = first1 ? c1 : c0;
-            } else if (any0) {
-                node = c0;
-            } else if (any1) {
-                node = c1;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                node = __builtin_amdgcn_readfirstlane(ws[sp * B.stride]);
-            }
-        }
+        const Hit hit = packet_batch<Shadow>(gnodes, gprims, ws, B.stride, r, has);
         if (has) store(item, hit, hit.shape != MH_INVALID);
     }
 }

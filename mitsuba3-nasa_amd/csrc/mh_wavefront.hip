@@ -37,6 +37,7 @@ struct WfState {
     float *ox[2], *oy[2], *oz[2], *dx[2], *dy[2], *dz[2], *mt[2];
     float *bx[2], *by[2], *bz[2], *ppx[2], *ppy[2], *ppz[2], *ppdf[2];
     uint64_t *rng[2];
+    float *lx[2], *ly[2], *lz[2];                              // radiance so far (fused bounce kernel)
     float *ht, *hu, *hv;                                       // hit record of the current bounce
     uint32_t *hp, *hs;
     uint32_t *sid;                                             // shadow records
@@ -64,6 +65,11 @@ static bool use_packet(const DScene &S) {
     if (e && !strcmp(e, "lane")) return false;
     return S.n_prims <= kPacketMaxPrims;
 }
+// MH_WF_FUSED=0 keeps the three-kernel pipeline (trace / shade / shadow)
+static bool wf_unfused() {
+    const char *e = getenv("MH_WF_FUSED");
+    return e && !strcmp(e, "0");
+}
 #define MH_WF_DISPATCH(K, ...)                                                                        \
     do {                                                                                              \
         if (lds && packet) hipLaunchKernelGGL((K<true, true>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);   \
@@ -85,10 +91,10 @@ uint32_t wf_counter_words(uint32_t n_bounces) { return kCtrStride * (n_bounces +
 uint64_t wf_max_chunk() { return 1ull << kPidBits; }
 
 size_t wf_workspace_bytes(uint64_t cap) {
-    // 49 4-byte planes + 2 8-byte planes, each 256-B aligned; capacity padded
+    // 55 4-byte planes + 2 8-byte planes, each 256-B aligned; capacity padded
     // to a whole number of segments
     cap = (cap + kSeg - 1) / kSeg * kSeg;
-    return 49 * align_up(cap * 4) + 2 * align_up(cap * 8);
+    return 55 * align_up(cap * 4) + 2 * align_up(cap * 8);
 }
 
 static WfState carve(void *ws, uint64_t cap) {
@@ -101,6 +107,7 @@ static WfState carve(void *ws, uint64_t cap) {
         w.pd[k] = u();
         w.ox[k] = f(); w.oy[k] = f(); w.oz[k] = f(); w.dx[k] = f(); w.dy[k] = f(); w.dz[k] = f(); w.mt[k] = f();
         w.bx[k] = f(); w.by[k] = f(); w.bz[k] = f(); w.ppx[k] = f(); w.ppy[k] = f(); w.ppz[k] = f(); w.ppdf[k] = f();
+        w.lx[k] = f(); w.ly[k] = f(); w.lz[k] = f();
     }
     w.ht = f(); w.hu = f(); w.hv = f(); w.hp = u(); w.hs = u();
     w.sid = u();
@@ -172,6 +179,7 @@ k_wf_raygen(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plan
     w.bx[0][k] = 1.f; w.by[0][k] = 1.f; w.bz[0][k] = 1.f;
     w.ppx[0][k] = 0.f; w.ppy[0][k] = 0.f; w.ppz[0][k] = 0.f; w.ppdf[0][k] = 1.f;
     w.rng[0][k] = rng.state;
+    w.lx[0][k] = 0.f; w.ly[0][k] = 0.f; w.lz[0][k] = 0.f;
     out[k] = 0.f; out[plane + k] = 0.f; out[2 * plane + k] = 0.f;
     out[3 * plane + k] = sx; out[4 * plane + k] = sy;
 }
@@ -356,6 +364,149 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused bounce kernel (small scenes: packet engine + LDS-staged tables).  For
+// every queued path of the bounce: the closest-hit packet trace, one
+// iteration of PathIntegrator::sample (path.cpp:142-281), the NEE shadow
+// packet trace and the deferred `result = fma(throughput, bsdf_val *
+// em_weight * mis, result)`, with L carried in the path state and written to
+// the sample planes once, when the path ends.  Same per-lane operations in
+// the same order as k_wf_trace -> k_wf_shade -> k_wf_shadow (bit-identical),
+// without the hit and shadow records in HBM, and with the traversal VALU of
+// one wave overlapping the state streams of the others.
+// LDS: shading tables (tab_bytes) + one traversal stack per wave.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 4)
+k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane, float *out,
+            WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+    extern __shared__ uint4 lds[];
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_stride_work(it, n)) return;
+    const DScene S = stage_tables(S0, lds);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
+                   (threadIdx.x >> 6) * S0.stack_size;
+    const uint32_t sbase = it.seg * seg_cap;
+    const int nxt = cur ^ 1;
+    uint32_t n_shadow = 0;
+    for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
+        const uint32_t i = base + lane_id();
+        const bool has = i < n;
+        const uint32_t j = sbase + i;
+        bool alive = false, shadow = false;
+        uint32_t pid = 0, depth = 0;
+        RayT ray{v3(0, 0, 0), v3(0, 0, 1), -1.f}, sray{v3(0, 0, 0), v3(0, 0, 1), -1.f};
+        V3 tp, a_nee, b_nee, prev_p, L;
+        float eta = 1.f, prev_pdf = 1.f;
+        Pcg rng;
+        if (has) {
+            const uint32_t pd = w.pd[cur][j];
+            pid = pd & kPidMask;
+            depth = pd >> kPidBits;
+            ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+            ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+            ray.maxt = w.mt[cur][j];
+        }
+        const Hit h = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, ray, has);
+        if (has) {
+            tp = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+            L = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
+            eta = 1.f;  // diffuse / null BSDFs: eta stays 1, only the camera vertex is delta
+            const bool prev_delta = depth == 0;
+            prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+            prev_pdf = w.ppdf[cur][j];
+            uint32_t lane, px, py;
+            lane_of(lm, pid, lane, px, py);
+            rng.state = w.rng[cur][j];
+            rng.inc = pcg_inc(seed_value, lane);
+            SI si;
+            compute_si(S, ray, h, si);
+
+            // ---- direct emission (path.cpp:158-174)
+            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+            if (em != MH_INVALID) {
+                float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
+                float mis_bsdf = mis_weight(prev_pdf, em_pdf);
+                V3 le = v3(0, 0, 0);
+                if (prev_pdf > 0.f) le = emitter_eval(S, em, si);
+                L = fma3(tp, le * mis_bsdf, L);
+            }
+            const bool active_next = (depth + 1 < in.max_depth) && si.valid;
+            const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
+            const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+            const bool active_em = active_next && smooth;
+
+            // ---- emitter sampling (path.cpp:187-208); visibility below
+            float e0 = rng.next_float(), e1 = rng.next_float();
+            DirS ds;
+            ds.pdf = 0.f;
+            ds.d = v3(0, 0, 0);
+            ds.delta = false;
+            V3 em_weight = v3(0, 0, 0), wo = v3(0, 0, 0);
+            if (active_em) {
+                em_weight = scene_sample_emitter_direction(S, si.p, e0, e1, ds);
+                if (ds.pdf != 0.f && nonzero(em_weight)) {
+                    shadow = true;
+                    sray = spawn_ray_to(si.p, si.n, ds.p);
+                }
+                wo = to_local(si, ds.d);
+            }
+
+            // ---- BSDF eval + sample (path.cpp:212-216)
+            (void)rng.next_float();
+            float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bsdf_val = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0), bs_wo = v3(0, 0, 0);
+            float bsdf_pdf = 0.f, bs_pdf = 0.f, bs_eta = 0.f;
+            if (smooth) {
+                V3 rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+                diffuse_eval_pdf(rho, si.wi, wo, true, bsdf_val, bsdf_pdf);
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                bs_eta = 1.f;
+                bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+            }
+            if (shadow) {  // (path.cpp:220-230), applied below if unoccluded
+                a_nee = tp;
+                b_nee = (bsdf_val * em_weight) * (ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf));
+            }
+
+            // ---- BSDF sampling, state update, Russian roulette (path.cpp:234-280)
+            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+            tp = tp * bsdf_weight;
+            eta *= bs_eta;
+            prev_p = si.p;
+            prev_pdf = bs_pdf;
+            if (si.valid) depth += 1;
+            float tmax = hmax(tp);
+            float rr_prob = fminf(tmax * (eta * eta), 0.95f);
+            bool rr_active = depth >= in.rr_depth;
+            bool rr_continue = rng.next_float() < rr_prob;
+            if (rr_active) tp = tp * rcp(rr_prob);
+            alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
+        }
+        // ---- visibility of the NEE sample (scene.cpp:201-210)
+        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, sray, shadow);
+        if (shadow && sh.shape == MH_INVALID) L = fma3(a_nee, b_nee, L);
+        n_shadow += (uint32_t)__popcll(__ballot(shadow));
+        // ---- compaction: survivors -> next queue; finished paths -> sample planes
+        const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        if (alive) {
+            w.pd[nxt][slot] = pid | (depth << kPidBits);
+            w.ox[nxt][slot] = ray.o.x; w.oy[nxt][slot] = ray.o.y; w.oz[nxt][slot] = ray.o.z;
+            w.dx[nxt][slot] = ray.d.x; w.dy[nxt][slot] = ray.d.y; w.dz[nxt][slot] = ray.d.z;
+            w.mt[nxt][slot] = ray.maxt;
+            w.bx[nxt][slot] = tp.x; w.by[nxt][slot] = tp.y; w.bz[nxt][slot] = tp.z;
+            w.ppx[nxt][slot] = prev_p.x; w.ppy[nxt][slot] = prev_p.y; w.ppz[nxt][slot] = prev_p.z;
+            w.ppdf[nxt][slot] = prev_pdf;
+            w.rng[nxt][slot] = rng.state;
+            w.lx[nxt][slot] = L.x; w.ly[nxt][slot] = L.y; w.lz[nxt][slot] = L.z;
+        } else if (has) {
+            out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
+        }
+    }
+    if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
+}
+
 template <bool InLds, bool Packet>
 __global__ void __launch_bounds__(256)
 k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, uint32_t *ctr) {
@@ -402,9 +553,17 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
+    const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
+        if (fused) {
+            if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
+            hipLaunchKernelGGL(k_wf_bounce, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S, in, lm,
+                               seed_value, plane, out, w, cur, seg_cap, c, cn);
+            if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
+            continue;
+        }
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
         MH_WF_DISPATCH(k_wf_trace, S, w, cur, seg_cap, c);
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
@@ -773,6 +932,8 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     }
     return hipGetLastError();
 }
+
+bool wf_fused(const DScene &S) { return use_packet(S) && S.tab_bytes != 0 && !wf_unfused(); }
 
 uint32_t wf_grid(uint32_t grid) { return std::max<uint32_t>(kSeg, grid / kSeg * kSeg); }
 

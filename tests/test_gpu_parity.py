@@ -85,11 +85,16 @@ def _gpu_samples(mi, scene, integrator, seed, spp, flags=0):
 
 
 @pytest.mark.parametrize("itype,mode", [("path", "mega"), ("prb", "mega"), ("path", "wavefront"),
-                                        ("path", "wavefront-lane")])
+                                        ("path", "wavefront-lane"), ("path", "wavefront-unfused")])
 def test_per_sample_parity(itype, mode, monkeypatch):
-    """wavefront: packet engine (small BVH default); wavefront-lane: per-lane engine."""
+    """wavefront: fused bounce kernel with the packet engine (small-BVH default);
+    wavefront-unfused: trace / shade / shadow kernels with the packet engine;
+    wavefront-lane: trace / shade / shadow kernels with the per-lane engine."""
     if mode == "wavefront-lane":
         monkeypatch.setenv("MH_TRAVERSAL", "lane")
+        mode = "wavefront"
+    if mode == "wavefront-unfused":
+        monkeypatch.setenv("MH_WF_FUSED", "0")
         mode = "wavefront"
     mi = _mi()
     from mitsuba_hip import _abi as A
