@@ -843,6 +843,180 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
     flush_partial(acc, q);
 }
 
+// Fused PRB bounce kernel (small scenes): closest-hit packet trace + one
+// iteration of the prb_fused loop + the NEE packet visibility test, whose
+// gradient record is charged at once (same operations and order as
+// k_wf_trace -> k_wf_shade_prb -> k_wf_shadow_prb; only the order in which
+// the per-thread gradient registers accumulate differs).
+template <int NR>
+__global__ void __launch_bounds__(256, 4)
+k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
+                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+    extern __shared__ uint4 lds[];
+    const SegIter it = seg_iter();
+    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!block_has_stride_work(it, n)) return;
+    const DScene S = stage_tables(S0, lds);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
+                   (threadIdx.x >> 6) * S0.stack_size;
+    uint32_t n_shadow = 0;
+    const uint32_t sbase = it.seg * seg_cap;
+    const int nxt = cur ^ 1;
+    const uint32_t n_rgb = q.n_rgb;
+    float acc[NR][3];
+#pragma unroll
+    for (int kk = 0; kk < NR; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
+    const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
+    for (uint32_t itr = 0; itr < n_iter; ++itr) {
+        const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
+        bool alive = false, shadow = false;
+        uint32_t pid = 0, depth = 0;
+        RayT ray{v3(0, 0, 0), v3(0, 0, 1), -1.f}, sray{v3(0, 0, 0), v3(0, 0, 1), -1.f};
+        V3 beta, prev_p, dL;
+        float prev_pdf = 1.f;
+        float A[NR][3], G[NR][3];
+        Pcg rng;
+        const uint32_t j = sbase + i;
+        if (i < n) {
+            const uint32_t pd = w.pd[cur][j];
+            pid = pd & kPidMask;
+            depth = pd >> kPidBits;
+            ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+            ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+            ray.maxt = w.mt[cur][j];
+        }
+        const Hit h = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, ray, i < n);
+        if (i < n) {
+            beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+            prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+            prev_pdf = w.ppdf[cur][j];
+            dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
+#pragma unroll
+            for (int kk = 0; kk < NR; ++kk)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
+            const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
+            const float eta = 1.f;
+            uint32_t lane, px, py;
+            lane_of(lm, pid, lane, px, py);
+            rng.state = w.rng[cur][j];
+            rng.inc = pcg_inc(seed_value, lane);
+            SI si;
+            compute_si(S, ray, h, si);
+            const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
+            const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+            bool active_next = !(in.hide_emitters && depth == 0 && !si.valid);
+
+            // ---- emission (prb.py:143-152): charged to the earlier vertices
+            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+            if (em != MH_INVALID) {
+                float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
+                float mis = mis_weight(prev_pdf, em_pdf);
+                V3 le = v3(0, 0, 0);
+                if (active_next)
+                    le = emitter_eval(S, em, si);
+                charge(acc, A, n_rgb, dL * ((beta * mis) * le));
+            }
+            active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
+            const bool active_em0 = active_next && smooth;
+
+            // ---- emitter sampling (prb.py:157-176); visibility deferred
+            float e0 = rng.next_float(), e1 = rng.next_float();
+            DirS ds;
+            ds.pdf = 0.f;
+            ds.d = v3(0, 0, 0);
+            ds.delta = false;
+            V3 em_weight = v3(0, 0, 0);
+            if (active_em0) {
+                em_weight = scene_sample_emitter_direction(S, si.p, e0, e1, ds);
+                if (ds.pdf != 0.f && nonzero(em_weight)) {
+                    shadow = true;
+                    sray = spawn_ray_to(si.p, si.n, ds.p);
+                }
+            }
+            V3 rho = v3(0, 0, 0);
+            if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+            const int32_t slot = smooth ? q.slot_of_tex[S.bsdf_tex[b]] : -1;
+            if (shadow) {  // as if unoccluded; applied after the visibility test
+                V3 wo_em = to_local(si, ds.d);
+                V3 bsdf_value_em;
+                float bsdf_pdf_em;
+                diffuse_eval_pdf(rho, si.wi, wo_em, true, bsdf_value_em, bsdf_pdf_em);
+                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
+                V3 beta_mis_em = beta * mis_em;
+                V3 dLe = dL * ((beta_mis_em * bsdf_value_em) * em_weight);
+#pragma unroll
+                for (int kk = 0; kk < NR; ++kk) {
+                    G[kk][0] = (dLe.x * (A[kk][0] * kInvPi));
+                    G[kk][1] = (dLe.y * (A[kk][1] * kInvPi));
+                    G[kk][2] = (dLe.z * (A[kk][2] * kInvPi));
+                }
+                if (slot >= 0 && si.wi.z > 0.f && wo_em.z > 0.f)
+                    add_slot(G, slot, (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi);
+            }
+
+            // ---- BSDF sampling, RR (prb.py:181-278)
+            (void)rng.next_float();
+            float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
+            float bs_pdf = 0.f;
+            if (smooth && active_next) {
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+            }
+            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+            beta = beta * bsdf_weight;
+            prev_p = si.p;
+            prev_pdf = bs_pdf;
+            float beta_max = hmax(beta);
+            active_next = active_next && beta_max != 0.f;
+            float rr_prob = fminf(beta_max * (eta * eta), 0.95f);
+            bool rr_active = depth >= in.rr_depth;
+            if (rr_active) beta = beta * rcp(rr_prob);
+            bool rr_continue = rng.next_float() < rr_prob;
+            active_next = active_next && (!rr_active || rr_continue);
+            if (slot >= 0)
+                add_slot(A, slot, prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf));
+            if (si.valid) depth += 1;
+            alive = active_next;
+        }
+        // ---- visibility of the NEE sample; the record is charged if unoccluded
+        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, sray, shadow);
+        if (shadow && sh.shape == MH_INVALID) {
+#pragma unroll
+            for (int kk = 0; kk < NR; ++kk)
+                if ((uint32_t)kk < n_rgb) {
+                    acc[kk][0] += G[kk][0];
+                    acc[kk][1] += G[kk][1];
+                    acc[kk][2] += G[kk][2];
+                }
+        }
+        n_shadow += (uint32_t)__popcll(__ballot(shadow));
+        const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        if (alive) {
+            w.pd[nxt][slot_n] = pid | (depth << kPidBits);
+            w.ox[nxt][slot_n] = ray.o.x; w.oy[nxt][slot_n] = ray.o.y; w.oz[nxt][slot_n] = ray.o.z;
+            w.dx[nxt][slot_n] = ray.d.x; w.dy[nxt][slot_n] = ray.d.y; w.dz[nxt][slot_n] = ray.d.z;
+            w.mt[nxt][slot_n] = ray.maxt;
+            w.bx[nxt][slot_n] = beta.x; w.by[nxt][slot_n] = beta.y; w.bz[nxt][slot_n] = beta.z;
+            w.ppx[nxt][slot_n] = prev_p.x; w.ppy[nxt][slot_n] = prev_p.y; w.ppz[nxt][slot_n] = prev_p.z;
+            w.ppdf[nxt][slot_n] = prev_pdf;
+            w.rng[nxt][slot_n] = rng.state;
+            q.dl(nxt, 0)[slot_n] = dL.x; q.dl(nxt, 1)[slot_n] = dL.y; q.dl(nxt, 2)[slot_n] = dL.z;
+#pragma unroll
+            for (int kk = 0; kk < NR; ++kk)
+                if ((uint32_t)kk < n_rgb) {
+                    q.A(nxt, kk * 3 + 0)[slot_n] = A[kk][0];
+                    q.A(nxt, kk * 3 + 1)[slot_n] = A[kk][1];
+                    q.A(nxt, kk * 3 + 2)[slot_n] = A[kk][2];
+                }
+        }
+    }
+    if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
+    flush_partial(acc, q);
+}
+
 template <bool InLds, bool Packet, int NR>
 __global__ void __launch_bounds__(256)
 k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
@@ -908,9 +1082,20 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     const size_t sh = lds_bytes(S, 256);
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
+    const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
+    const size_t sh_fused = S.tab_bytes + 16u * S.stack_size;
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
+        if (fused) {
+            if (n_rgb == 1)
+                hipLaunchKernelGGL((k_wf_bounce_prb<1>), dim3(grid), dim3(256), sh_fused, st, S, in, lm, seed_value,
+                                   w, q, cur, seg_cap, c, cn);
+            else
+                hipLaunchKernelGGL((k_wf_bounce_prb<kMaxRgbParams>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,
+                                   seed_value, w, q, cur, seg_cap, c, cn);
+            continue;
+        }
         MH_WF_DISPATCH(k_wf_trace, S, w, cur, seg_cap, c);
         if (n_rgb == 1) {
             if (S.tab_bytes)

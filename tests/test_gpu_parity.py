@@ -188,7 +188,7 @@ def test_prb_backward_fused_vs_replay_random_grad():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("engine", ["packet", "lane"])
+@pytest.mark.parametrize("engine", ["packet", "lane", "packet-unfused"])
 def test_prb_backward_wavefront_chunked(monkeypatch, engine):
     """Multi-chunk wavefront backward (lane maps offset per chunk, partials
     accumulated across chunks) equals the single-chunk run."""
@@ -199,7 +199,9 @@ def test_prb_backward_wavefront_chunked(monkeypatch, engine):
     params = mi.traverse(scene)
     keys = ["white.reflectance.value", "green.reflectance.value"]
     gi = torch.full((24, 40, 3), 1.0 / (24 * 40 * 3), dtype=torch.float32, device="cuda")
-    monkeypatch.setenv("MH_TRAVERSAL", engine)
+    monkeypatch.setenv("MH_TRAVERSAL", engine.split("-")[0])
+    if engine.endswith("unfused"):
+        monkeypatch.setenv("MH_WF_FUSED", "0")
     a = mi.render_backward(scene, params, gi, keys, integ, seed=9, spp=16)
     monkeypatch.setenv("MH_WF_CHUNK", "2048")
     b = mi.render_backward(scene, params, gi, keys, integ, seed=9, spp=16)
