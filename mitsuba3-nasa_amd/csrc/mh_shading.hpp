@@ -30,12 +30,12 @@ MH_DEV bool tri_test(const Prim &p, const RayT &r, float &t, float &u, float &v)
     float inv_det = rcp(dot(e1, pvec));
     V3 tvec = r.o - v0;
     u = dot(tvec, pvec) * inv_det;
-    bool active = u >= 0.f && u <= 1.f;
     V3 qvec = cross(tvec, e1);
     v = dot(r.d, qvec) * inv_det;
-    active = active && v >= 0.f && u + v <= 1.f;
     t = dot(e2, qvec) * inv_det;
-    return active && t >= 0.f && t <= r.maxt;
+    // Non-short-circuit masks: every lane evaluates the whole test, so the
+    // compiler emits v_cmp/s_and instead of exec-mask branches.
+    return (u >= 0.f) & (u <= 1.f) & (v >= 0.f) & (u + v <= 1.f) & (t >= 0.f) & (t <= r.maxt);
 }
 
 // Rectangle::ray_intersect_preliminary_impl (shapes/rectangle.cpp:446-470)
@@ -47,8 +47,8 @@ MH_DEV bool rect_test(const Prim &p, const RayT &r, float &t, float &u, float &v
     V3 local = fma3s(d, t, o);
     u = local.x;
     v = local.y;
-    return t >= 0.f && t <= r.maxt && __builtin_fabsf(local.x) <= 1.f &&
-           __builtin_fabsf(local.y) <= 1.f;
+    return (t >= 0.f) & (t <= r.maxt) & (__builtin_fabsf(local.x) <= 1.f) &
+           (__builtin_fabsf(local.y) <= 1.f);
 }
 
 MH_DEV bool prim_test(const Prim &p, const RayT &r, float &t, float &u, float &v) {
@@ -70,7 +70,7 @@ MH_DEV V3 safe_inv_dir(V3 d) { return v3(safe_rcp_dir(d.x), safe_rcp_dir(d.y), s
 // order in which the oracle's brute force (and a scalar scene walk) meets
 // them — so the result does not depend on the BVH's visiting order.
 MH_DEV bool closer(float tt, const Prim &p, const Hit &hit) {
-    return tt < hit.t || (tt == hit.t && p.info.w < hit.key);
+    return (tt < hit.t) | ((tt == hit.t) & (p.info.w < hit.key));
 }
 
 // Slab test for both children; conservative (host pads every box).
@@ -437,14 +437,17 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
                         Hit &hit, float &best) {
     for (uint32_t i = 0; i < count; ++i) {
         const Prim p = load_uniform(prims, first + i);
-        if (lane_hit && (!Shadow || hit.shape == MH_INVALID)) {
-            float tt, u, v;
-            const bool ok = p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, tt, u, v) : tri_test(p, r, tt, u, v);
-            if (ok && (Shadow || closer(tt, p, hit))) {
-                hit.t = tt; hit.u = u; hit.v = v; hit.prim = p.info.y; hit.shape = p.info.x; hit.key = p.info.w;
-                best = tt;
-            }
-        }
+        // Branch-free: all lanes test, the hit update is a per-lane select
+        float tt, u, v;
+        const bool ok = p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, tt, u, v) : tri_test(p, r, tt, u, v);
+        const bool take = lane_hit & ok & (Shadow ? hit.shape == MH_INVALID : closer(tt, p, hit));
+        hit.t = take ? tt : hit.t;
+        hit.u = take ? u : hit.u;
+        hit.v = take ? v : hit.v;
+        hit.prim = take ? p.info.y : hit.prim;
+        hit.shape = take ? p.info.x : hit.shape;
+        hit.key = take ? p.info.w : hit.key;
+        best = take ? tt : best;
     }
 }
 
