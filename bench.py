@@ -162,12 +162,13 @@ def main():
     value = samples_step / (ms_step / 1e3) / 1e6
 
     if rank == 0:
-        # ---- roofline of the dominant kernel: k_wf_trace (closest-hit stream
-        # traversal, ~35% of the step in both passes).  Timed live with HIP
-        # events recorded by mh_render around every k_wf_trace launch on the
-        # scene's stream.  Algorithmic bytes per ray: ray in (o, d, maxt: 28 B)
-        # + hit record out (t, u, v, prim, shape: 20 B) = 48 B;
-        # the BVH is LDS-resident (no HBM bytes).
+        # ---- roofline of the dominant kernel.  With the fused wavefront
+        # (stats.mode 2) that is k_wf_bounce: one launch = one bounce of every
+        # live path (closest trace + shading + NEE visibility), ~88% of the
+        # forward pass.  mh_render times every launch with HIP events on the
+        # scene's stream (stats.ms_trace / n_trace_launches).  Algorithmic
+        # bytes per launch are stated below and in DESIGN.md §4; the BVH and
+        # shading tables are LDS / scalar-cache resident (no HBM bytes).
         avg_f = sum(fwd_ms) / len(fwd_ms)
         avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
         n_local = H * W * args.spp
