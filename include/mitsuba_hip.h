@@ -14,7 +14,7 @@
  *   mh_scene_create / mh_scene_destroy
  *       Scene::Scene + accel_init_gpu (OptiX GAS/IAS build)
  *       src/render/scene.cpp:22-96, src/render/scene_optix.inl:304-547
- *   mh_scene_update_texture / mh_scene_update_rgb
+ *   mh_scene_update_texture / mh_scene_update_rgb / mh_scene_update_medium
  *       SceneParameters.update -> Scene::parameters_changed
  *       src/python/python/util.py:292-350, src/render/scene.cpp:481-529
  *   mh_render
@@ -72,7 +72,19 @@ enum { MH_MEDIUM_HETEROGENEOUS = 0, MH_MEDIUM_HOMOGENEOUS = 1 };
 enum { MH_PHASE_ISOTROPIC = 0, MH_PHASE_HG = 1 };
 enum { MH_MEDIUM_NO_EMITTER_SAMPLING = 1u,        /* medium.cpp:29 sample_emitters = false */
        MH_MEDIUM_NO_SPECTRAL_EXTINCTION = 2u };   /* heterogeneous.cpp:161 has_spectral_extinction = false */
-enum { MH_INTEGRATOR_PATH = 0, MH_INTEGRATOR_VOLPATH = 1, MH_INTEGRATOR_PRB = 2 };
+enum { MH_INTEGRATOR_PATH = 0, MH_INTEGRATOR_VOLPATH = 1, MH_INTEGRATOR_PRB = 2,
+       MH_INTEGRATOR_PRBVOLPATH = 3 };                        /* python/ad/integrators/prbvolpath.py */
+
+/* Differentiable parameter ids of mh_render_backward (param_textures[]):
+ * a texture index (kind 0: '<bsdf>.reflectance.value' / '.data'), or a kind
+ * tag | medium index.  Medium parameters need MH_INTEGRATOR_PRBVOLPATH.
+ *   MH_PARAM_MEDIUM_SIGMA_T | m : '<medium>.sigma_t.data' (heterogeneous grid,
+ *                                 res_x*res_y*res_z floats) or '.value'
+ *                                 (homogeneous, 1 float)
+ *   MH_PARAM_MEDIUM_ALBEDO | m  : '<medium>.albedo.value' (3 floats)        */
+#define MH_PARAM_KIND_MASK      0xF0000000u
+#define MH_PARAM_MEDIUM_SIGMA_T 0x10000000u
+#define MH_PARAM_MEDIUM_ALBEDO  0x20000000u
 
 /* Flags for mh_render / mh_render_backward / mh_trace_*                   */
 enum {
@@ -227,6 +239,17 @@ int mh_scene_set_stream(mh_scene *scene, void *stream);
 
 /* Parameter updates (traverse()/update() of 'x.reflectance.value' / '.data'). */
 int mh_scene_update_rgb(mh_scene *scene, uint32_t texture, const float value[3]);
+/*
+ * Medium parameters (SceneParameters.update -> HeterogeneousMedium /
+ * HomogeneousMedium::parameters_changed, heterogeneous.cpp:176-178):
+ *   albedo  : 3 floats (host) or NULL
+ *   sigma_t : homogeneous sigma_t value (1 float, host) or NULL
+ *   grid    : heterogeneous sigma_t grid (n = res_x*res_y*res_z floats; host,
+ *             or device with MH_FLAG_DEVICE_POINTERS) or NULL.  The majorant
+ *             is recomputed as scale * max(grid).
+ */
+int mh_scene_update_medium(mh_scene *scene, uint32_t medium, const float *albedo, const float *sigma_t,
+                           const float *grid, uint64_t n, uint32_t flags);
 int mh_scene_update_texture(mh_scene *scene, uint32_t texture, const float *data, uint64_t n_floats);
 
 /*
@@ -256,8 +279,11 @@ int mh_develop(mh_scene *scene, const float *film_rgbw, float *image_rgb, uint32
 
 /*
  * Reverse-mode derivative of render(): accumulates d(loss)/d(param) for each
- * listed texture parameter into grads[k] (3 floats for MH_TEX_RGB, W*H*C for
- * MH_TEX_BITMAP).  `grad_in` is d(loss)/d(image), H*W*3.
+ * listed parameter into grads[k] (3 floats for MH_TEX_RGB, W*H*C for
+ * MH_TEX_BITMAP; medium ids: see MH_PARAM_*).  `grad_in` is d(loss)/d(image),
+ * H*W*3.  integrator: MH_INTEGRATOR_PRB (prb.py) or MH_INTEGRATOR_PRBVOLPATH
+ * (prbvolpath.py: primal + adjoint replay per lane; grid gradients are
+ * scattered with float atomics, so their summation order is not fixed).
  *   weights_rgbw (optional, device flag applies): the per-pixel filter-weight
  *   image W of the backward pass; pass NULL to compute it in-call.  Multi-GPU
  *   callers compute the W image per slab with mh_prb_weights, all-reduce it

@@ -90,7 +90,9 @@ struct mh_scene {
     DevBuf wf_ws_prb, wf_partial, gw;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
-    uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0;
+    std::vector<mh_medium> h_media;
+    std::vector<DMedium> h_dmedia;
+    uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0, n_media = 0;
     uint64_t n_texels = 0;
     uint32_t bvh_nodes = 0, bvh_prims = 0, bvh_depth = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -271,6 +273,9 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         if (a.phase == MH_PHASE_HG && !(a.g > -1.f && a.g < 1.f))
             return fail(MH_ERR_INVALID_ARGUMENT, "The asymmetry parameter must lie in the interval (-1, 1)!");
     }
+    s->h_media.assign(desc->media, desc->media + desc->n_media);
+    s->h_dmedia = meds;
+    s->n_media = desc->n_media;
     if (desc->sensor.medium != MH_INVALID && desc->sensor.medium >= desc->n_media)
         return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: sensor medium index out of bounds");
     std::vector<uint32_t> btype(desc->n_bsdfs), btex(desc->n_bsdfs);
@@ -339,6 +344,11 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.grid = s->grid.as<float>();
     S.n_media = desc->n_media;
     S.camera_medium = desc->sensor.medium;
+    S.vol_flags = 0;
+    for (uint32_t i = 0; i < desc->n_shapes; ++i)
+        for (uint32_t mm : {desc->shapes[i].interior_medium, desc->shapes[i].exterior_medium})
+            if (mm != MH_INVALID)
+                S.vol_flags |= desc->media[mm].type == MH_MEDIUM_HOMOGENEOUS ? kVolNeeHomogeneous : kVolHandleNull;
     S.n_shapes = desc->n_shapes;
     S.n_bsdfs = desc->n_bsdfs;
     S.n_textures = desc->n_textures;
@@ -439,6 +449,48 @@ int mh_scene_update_texture(mh_scene *s, uint32_t tex, const float *data, uint64
     return MH_OK;
 }
 
+// SceneParameters.update of a medium's differentiable parameters
+// (heterogeneous.cpp:169-178 / homogeneous.cpp:150-155): albedo, homogeneous
+// sigma_t, heterogeneous sigma_t grid; the majorant is recomputed as
+// parameters_changed does (m_max_density = scale * max(grid)).
+int mh_scene_update_medium(mh_scene *s, uint32_t medium, const float *albedo, const float *sigma_t,
+                           const float *grid, uint64_t n, uint32_t flags) {
+    if (!s) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: NULL scene");
+    if (medium >= s->n_media) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: medium index out of bounds");
+    MH_HIP(hipSetDevice(s->device));
+    mh_medium &a = s->h_media[medium];
+    DMedium &b = s->h_dmedia[medium];
+    if (albedo) {
+        memcpy(a.albedo, albedo, 12);
+        memcpy(b.albedo, albedo, 12);
+    }
+    if (sigma_t) {
+        if (a.type != MH_MEDIUM_HOMOGENEOUS)
+            return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: sigma_t value of a heterogeneous medium (use grid)");
+        a.sigma_t_const = b.sigma_t_const = *sigma_t;
+        b.maj = b.sigma_t_const * b.scale;
+    }
+    if (grid) {
+        if (a.type != MH_MEDIUM_HETEROGENEOUS)
+            return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: grid of a homogeneous medium");
+        if (n != (uint64_t)a.grid_res[0] * a.grid_res[1] * a.grid_res[2])
+            return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: size mismatch");
+        float *dst = s->grid.as<float>() + a.grid_offset;
+        MH_HIP(hipMemcpyAsync(dst, grid, n * 4, (flags & MH_FLAG_DEVICE_POINTERS) ? hipMemcpyDeviceToDevice
+                                                                                 : hipMemcpyHostToDevice, s->stream));
+        MH_HIP(s->tmp_b.alloc(16));
+        MH_HIP(launch_grid_max(dst, n, s->tmp_b.as<uint32_t>(), s->stream));
+        uint32_t key = 0;
+        MH_HIP(hipMemcpyAsync(&key, s->tmp_b.ptr, 4, hipMemcpyDeviceToHost, s->stream));
+        MH_HIP(hipStreamSynchronize(s->stream));
+        a.max_density = ordered_key_to_float(key);
+        b.maj = b.scale * a.max_density;
+    }
+    MH_HIP(hipMemcpyAsync(s->media.as<DMedium>() + medium, &b, sizeof(DMedium), hipMemcpyHostToDevice, s->stream));
+    MH_HIP(hipStreamSynchronize(s->stream));
+    return MH_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Render
 // ---------------------------------------------------------------------------
@@ -488,7 +540,7 @@ static double now_ms() {
 int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
               uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
     if (!s || !in || !film_rgbw) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: NULL argument");
-    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_VOLPATH)
+    if (in->type > MH_INTEGRATOR_PRBVOLPATH)
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: unknown integrator");
     if (in->rr_depth == 0)
         return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
@@ -614,7 +666,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
 int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                       uint32_t spp_begin, uint32_t spp_end, float *out, uint32_t flags) {
     if (!s || !in || !out) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: NULL argument");
-    if (in->type != MH_INTEGRATOR_PATH && in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_VOLPATH)
+    if (in->type > MH_INTEGRATOR_PRBVOLPATH)
         return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: unsupported integrator");
     if (spp == 0 || in->rr_depth == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: bad arguments");
     Layout L;
@@ -711,8 +763,9 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                        float *const *grads, uint32_t flags, mh_stats *stats) {
     if (!s || !in || !grad_in || (n_params && (!param_tex || !grads)))
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: NULL argument");
-    if (in->type != MH_INTEGRATOR_PRB)
-        return set_error(MH_ERR_UNSUPPORTED, "render_backward(): requires the 'prb' integrator");
+    if (in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_PRBVOLPATH)
+        return set_error(MH_ERR_UNSUPPORTED, "render_backward(): requires the 'prb' or 'prbvolpath' integrator");
+    const bool vol = in->type == MH_INTEGRATOR_PRBVOLPATH;
     if (in->rr_depth == 0)
         return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: spp must be > 0");
@@ -731,46 +784,74 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
 
     // ---- parameter slots ----
+    // small slots 0..n_small-1 (register accumulators): rgb textures, medium
+    // albedo, homogeneous sigma_t; large slots (global atomics): bitmaps, grids
     std::vector<int32_t> slot_of_tex(std::max<uint32_t>(s->n_textures, 1), -1);
+    std::vector<int32_t> sigma_slot(std::max<uint32_t>(s->n_media, 1), -1), albedo_slot(sigma_slot);
     std::vector<uint32_t> is_rgb(kMaxParams, 0);
     std::vector<float *> bufs(kMaxParams, nullptr);
     std::vector<size_t> counts(kMaxParams, 0);
     std::vector<uint32_t> slot_of_param(n_params);
-    uint32_t n_rgb = 0, n_bmp = 0;
+    uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0;
     for (uint32_t k = 0; k < n_params; ++k) {
-        uint32_t t = param_tex[k];
-        if (t >= s->n_textures) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: texture index out of bounds");
-        if (slot_of_tex[t] >= 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: duplicate parameter");
-        const DTexture &tx = s->h_textures[t];
+        const uint32_t kind = param_tex[k] & MH_PARAM_KIND_MASK, idx = param_tex[k] & ~MH_PARAM_KIND_MASK;
+        int32_t *owner;
+        bool small;
+        size_t cnt;
+        if (kind == 0) {
+            if (idx >= s->n_textures) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: texture index out of bounds");
+            const DTexture &tx = s->h_textures[idx];
+            owner = &slot_of_tex[idx];
+            small = tx.type == MH_TEX_RGB;
+            cnt = small ? 3 : (size_t)tx.width * tx.height * tx.channels;
+        } else if (kind == MH_PARAM_MEDIUM_SIGMA_T || kind == MH_PARAM_MEDIUM_ALBEDO) {
+            if (!vol)
+                return set_error(MH_ERR_UNSUPPORTED, "render_backward(): medium parameters require the 'prbvolpath' integrator");
+            if (idx >= s->n_media) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: medium index out of bounds");
+            const mh_medium &m = s->h_media[idx];
+            ++n_medium_params;
+            if (kind == MH_PARAM_MEDIUM_ALBEDO) {
+                owner = &albedo_slot[idx]; small = true; cnt = 3;
+            } else {
+                owner = &sigma_slot[idx];
+                small = m.type == MH_MEDIUM_HOMOGENEOUS;
+                cnt = small ? 1 : (size_t)m.grid_res[0] * m.grid_res[1] * m.grid_res[2];
+            }
+        } else {
+            return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: unknown parameter kind");
+        }
+        if (*owner >= 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: duplicate parameter");
         int slot;
-        if (tx.type == MH_TEX_RGB) {
+        if (small) {
             if (n_rgb >= (uint32_t)kMaxRgbParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many rgb parameters");
             slot = (int)n_rgb++;
             is_rgb[slot] = 1;
-            counts[slot] = 3;
         } else {
             if (n_bmp >= (uint32_t)kMaxBitmapParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many bitmap parameters");
             slot = kMaxRgbParams + (int)n_bmp++;
-            counts[slot] = (size_t)tx.width * tx.height * tx.channels;
         }
-        slot_of_tex[t] = slot;
+        counts[slot] = cnt;
+        *owner = slot;
         slot_of_param[k] = (uint32_t)slot;
     }
     // gradient buffers: device scratch, zeroed, accumulated into the caller's
     size_t total = 0;
     std::vector<size_t> off(kMaxParams, 0);
-    for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += counts[k]; }
+    for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += (counts[k] + 3) / 4 * 4; }
     MH_HIP(s->tmp_c.alloc(std::max<size_t>(total, 1) * 4));
     MH_HIP(hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st));
     for (int k = 0; k < kMaxParams; ++k) bufs[k] = counts[k] ? s->tmp_c.as<float>() + off[k] : nullptr;
-    // meta block: slot_of_tex | is_rgb | bufs
-    size_t meta_bytes = slot_of_tex.size() * 4 + kMaxParams * 4 + kMaxParams * 8 + 64;
+    // meta block: slot_of_tex | is_rgb | bufs | sigma_slot | albedo_slot
+    auto al16 = [](size_t x) { return (x + 15) / 16 * 16; };
+    const size_t o_slot = 0, o_isrgb = al16(slot_of_tex.size() * 4), o_bufs = al16(o_isrgb + kMaxParams * 4),
+                 o_sig = al16(o_bufs + kMaxParams * 8), o_alb = al16(o_sig + sigma_slot.size() * 4),
+                 meta_bytes = al16(o_alb + albedo_slot.size() * 4);
     std::vector<uint8_t> meta(meta_bytes, 0);
-    size_t o_slot = 0, o_isrgb = (slot_of_tex.size() * 4 + 15) / 16 * 16,
-           o_bufs = (o_isrgb + kMaxParams * 4 + 15) / 16 * 16;
     memcpy(meta.data() + o_slot, slot_of_tex.data(), slot_of_tex.size() * 4);
     memcpy(meta.data() + o_isrgb, is_rgb.data(), kMaxParams * 4);
     memcpy(meta.data() + o_bufs, bufs.data(), kMaxParams * 8);
+    memcpy(meta.data() + o_sig, sigma_slot.data(), sigma_slot.size() * 4);
+    memcpy(meta.data() + o_alb, albedo_slot.data(), albedo_slot.size() * 4);
     MH_HIP(s->grad_meta.alloc(meta_bytes));
     MH_HIP(hipMemcpyAsync(s->grad_meta.ptr, meta.data(), meta_bytes, hipMemcpyHostToDevice, st));
     GradArgs ga;
@@ -778,6 +859,8 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     ga.is_rgb = reinterpret_cast<const uint32_t *>(s->grad_meta.as<uint8_t>() + o_isrgb);
     ga.bufs = reinterpret_cast<float *const *>(s->grad_meta.as<uint8_t>() + o_bufs);
     ga.n_rgb = n_rgb;
+    ga.sigma_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_sig) : nullptr;
+    ga.albedo_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_alb) : nullptr;
 
     // ---- grad_in / weights on the device ----
     const float *g_in = grad_in;
@@ -817,7 +900,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     // fused form runs as wavefront kernels unless MH_FLAG_MEGAKERNEL / MH_MODE=mega
     const char *env_replay = getenv("MH_PRB_REPLAY");
     const char *env_mode = getenv("MH_MODE");
-    const bool fused = n_bmp == 0 && !(flags & MH_FLAG_PRB_REPLAY) && !(env_replay && !strcmp(env_replay, "1"));
+    const bool fused = !vol && n_bmp == 0 && !(flags & MH_FLAG_PRB_REPLAY) && !(env_replay && !strcmp(env_replay, "1"));
     const bool wavefront = fused && in->max_depth <= 64 && !(flags & MH_FLAG_MEGAKERNEL) &&
                            !(env_mode && !strcmp(env_mode, "mega"));
     size_t wf_ctr_words = 0, wf_chunks = 0;
@@ -862,7 +945,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         uint32_t slot = slot_of_param[k];
         size_t c = counts[slot];
         if (dev) {
-            MH_HIP(hipMemcpyAsync(grads[k], bufs[slot], c * 4, hipMemcpyDeviceToDevice, st));
+            MH_HIP(launch_accumulate(grads[k], bufs[slot], c, st));
         } else {
             host_tmp.resize(c);
             MH_HIP(hipMemcpyAsync(host_tmp.data(), bufs[slot], c * 4, hipMemcpyDeviceToHost, st));

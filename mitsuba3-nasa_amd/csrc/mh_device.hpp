@@ -69,6 +69,10 @@ struct DMedium {
     float bbox_min[4], bbox_max[4];
 };
 
+// PRBVolpathIntegrator.prepare_scene (prbvolpath.py:76-89), from the media of the shapes
+constexpr uint32_t kVolHandleNull = 1u;       // some medium is heterogeneous
+constexpr uint32_t kVolNeeHomogeneous = 2u;   // some medium is homogeneous
+
 struct DScene {                 // kernel argument (by value)
     const Node *nodes;
     const Prim *prims;
@@ -86,6 +90,7 @@ struct DScene {                 // kernel argument (by value)
     const float *grid;             // volume grid data
     uint32_t n_nodes, n_prims, n_emitters, environment;
     uint32_t n_media, camera_medium;
+    uint32_t vol_flags;            // prbvolpath prepare_scene flags (kVol*)
     // small shading tables (shapes .. faces) staged into LDS by the shade
     // kernels when tab_bytes != 0 (mh_shading.hpp stage_tables)
     uint32_t n_shapes, n_bsdfs, n_textures, n_vertices, n_faces, tab_bytes;

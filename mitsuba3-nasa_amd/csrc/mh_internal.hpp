@@ -26,7 +26,10 @@ struct GradArgs {
     const int32_t *slot_of_tex;  // device: texture -> slot or -1
     float *const *bufs;          // device: slot -> gradient buffer
     const uint32_t *is_rgb;      // device: slot -> 1 if rgb
-    uint32_t n_rgb;              // rgb slots are 0 .. n_rgb-1
+    uint32_t n_rgb;              // small (register-accumulated) slots are 0 .. n_rgb-1:
+                                 // rgb textures, medium albedo, homogeneous sigma_t
+    const int32_t *sigma_slot;   // device: medium -> sigma_t slot or -1 (prbvolpath)
+    const int32_t *albedo_slot;  // device: medium -> albedo slot or -1 (prbvolpath)
 };
 
 // ---- BVH builder (host, binned SAH) --------------------------------------
@@ -72,6 +75,15 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 uint32_t grid, float *partial, hipStream_t st);
 hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
                                  hipStream_t st);
+// max of a float array (gridvolume max for the majorant), as an order-preserving
+// uint key in *key (initialised by the launcher)
+hipError_t launch_grid_max(const float *data, uint64_t n, uint32_t *key, hipStream_t st);
+inline float ordered_key_to_float(uint32_t k) {
+    union { uint32_t u; float f; } c;
+    c.u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    return c.f;
+}
+hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream_t st);  // dst += src
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,

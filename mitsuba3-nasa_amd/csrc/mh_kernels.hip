@@ -64,12 +64,13 @@ k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *_
 // Forward render of one chunk: lane k in [0, n) -> samples of every pass.
 // out planes (each `plane` floats apart): Lr, Lg, Lb, posx, posy; sample
 // (k, pass) stored at pass * n + k.
-// Kind: MH_INTEGRATOR_PATH / MH_INTEGRATOR_PRB (primal) / MH_INTEGRATOR_VOLPATH
+// Kind: MH_INTEGRATOR_PATH / MH_INTEGRATOR_PRB (primal) / MH_INTEGRATOR_VOLPATH /
+// MH_INTEGRATOR_PRBVOLPATH (primal)
 #ifndef MH_VOL_WAVES
 #define MH_VOL_WAVES 4  // volpath: 128 VGPRs (+ some scratch) measured +10 % over 2 waves (tools/exp_volwaves.sh)
 #endif
 template <int Kind, bool InLds>
-__global__ void __launch_bounds__(256, Kind == MH_INTEGRATOR_VOLPATH ? MH_VOL_WAVES : 1)
+__global__ void __launch_bounds__(256, (Kind == MH_INTEGRATOR_VOLPATH || Kind == MH_INTEGRATOR_PRBVOLPATH) ? MH_VOL_WAVES : 1)
 k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_t n_passes,
          uint64_t n, uint64_t plane, float *__restrict__ out, unsigned long long *__restrict__ counters) {
     extern __shared__ uint4 lds[];
@@ -91,6 +92,8 @@ k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_
                 L = prb_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow);
             else if (Kind == MH_INTEGRATOR_VOLPATH)
                 L = volpath_sample(S, B, in, rng, r, n_closest, n_shadow);
+            else if (Kind == MH_INTEGRATOR_PRBVOLPATH)
+                L = prbvol_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow);
             else
                 L = path_sample(S, B, in, rng, r, n_closest, n_shadow);
             uint64_t o = (uint64_t)pass * n + k;
@@ -323,6 +326,36 @@ __global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *
     rgb[3 * i + 2] = v.z / d;
 }
 
+// small (register-accumulated) gradient slots: wave butterfly, then one
+// atomic per wave and component
+MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
+    for (uint32_t p = 0; p < ga.n_rgb; ++p) {
+        const int slot = (int)p;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+                if (kk == slot) v = g.acc[kk][c];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(ga.bufs[slot] + c, v);
+        }
+    }
+}
+
+MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
+    GradCtx g;
+    g.slot_of_tex = ga.slot_of_tex;
+    g.bufs = ga.bufs;
+    g.is_rgb = ga.is_rgb;
+    g.sigma_slot = ga.sigma_slot;
+    g.albedo_slot = ga.albedo_slot;
+#pragma unroll
+    for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
+    return g;
+}
+
 // ---------------------------------------------------------------------------
 // PRB backward: dL gather + primal + adjoint per lane (common.py:900-983)
 // ---------------------------------------------------------------------------
@@ -333,12 +366,7 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
                GradArgs ga, unsigned long long *__restrict__ counters) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
-    GradCtx g;
-    g.slot_of_tex = ga.slot_of_tex;
-    g.bufs = ga.bufs;
-    g.is_rgb = ga.is_rgb;
-#pragma unroll
-    for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
+    GradCtx g = make_grad_ctx(ga);
     uint32_t n_closest = 0, n_shadow = 0;
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) {
@@ -359,20 +387,39 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
             prb_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
         }
     }
-    // block-reduce the rgb accumulators: wave butterfly, then one atomic per wave
-    for (uint32_t p = 0; p < ga.n_rgb; ++p) {
-        const int slot = (int)p;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            float v = 0.f;
-#pragma unroll
-            for (int kk = 0; kk < kMaxRgbParams; ++kk)
-                if (kk == slot) v = g.acc[kk][c];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if ((threadIdx.x & 63) == 0) atomicAdd(ga.bufs[slot] + c, v);
-        }
+    flush_small_slots(g, ga);
+    if (counters) {
+        wave_count(&counters[0], n_closest);
+        wave_count(&counters[1], n_shadow);
     }
+}
+
+// prbvolpath backward: dL gather + primal + adjoint replay per lane
+// (RBIntegrator.render_backward, common.py:900-983, with prbvolpath.sample)
+template <bool InLds>
+__global__ void __launch_bounds__(256, MH_VOL_WAVES)
+k_prbvol_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, int coalesce,
+                  const float *__restrict__ grad_in, GradArgs ga, unsigned long long *__restrict__ counters) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    GradCtx g = make_grad_ctx(ga);
+    uint32_t n_closest = 0, n_shadow = 0;
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) {
+        uint32_t lane, px, py;
+        lane_of(lm, k, lane, px, py);
+        Pcg rng;
+        rng.seed(seed_value, lane);
+        float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+        RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
+                            __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+        V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
+        Pcg rng_primal = rng;  // sampler.clone()
+        V3 Lp = prbvol_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest,
+                                     n_shadow);
+        prbvol_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
+    }
+    flush_small_slots(g, ga);
     if (counters) {
         wave_count(&counters[0], n_closest);
         wave_count(&counters[1], n_shadow);
@@ -421,6 +468,7 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
     } while (0)
     if (in.type == MH_INTEGRATOR_PRB) MH_LAUNCH_RENDER(MH_INTEGRATOR_PRB);
     else if (in.type == MH_INTEGRATOR_VOLPATH) MH_LAUNCH_RENDER(MH_INTEGRATOR_VOLPATH);
+    else if (in.type == MH_INTEGRATOR_PRBVOLPATH) MH_LAUNCH_RENDER(MH_INTEGRATOR_PRBVOLPATH);
     else MH_LAUNCH_RENDER(MH_INTEGRATOR_PATH);
 #undef MH_LAUNCH_RENDER
     return hipGetLastError();
@@ -459,6 +507,38 @@ hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *
     return hipGetLastError();
 }
 
+// order-preserving float -> uint key (negative floats reversed)
+__global__ void k_grid_max(const float *__restrict__ data, uint64_t n, uint32_t *__restrict__ key) {
+    uint32_t best = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t u = __float_as_uint(data[i]);
+        const uint32_t k = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        best = max(best, k);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(key, best);
+}
+
+hipError_t launch_grid_max(const float *data, uint64_t n, uint32_t *key, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(key, 0, 4, st);
+    if (e != hipSuccess || n == 0) return e;
+    const uint32_t g = (uint32_t)std::min<uint64_t>(blocks_for(n, 256), 2048);
+    hipLaunchKernelGGL(k_grid_max, dim3(g), dim3(256), 0, st, data, n, key);
+    return hipGetLastError();
+}
+
+__global__ void k_accumulate(float *__restrict__ dst, const float *__restrict__ src, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
+hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n, 256)), dim3(256), 0, st, dst, src, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st) {
     if (n_px == 0) return hipSuccess;
     hipLaunchKernelGGL(k_develop, dim3(blocks_for(n_px, 256)), dim3(256), 0, st, n_px, film, rgb);
@@ -473,7 +553,12 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
     if (n == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
     const dim3 g(blocks_for(n, bs)), b(bs);
-    if (S.lds_bytes_bvh && fused)
+    if (in.type == MH_INTEGRATOR_PRBVOLPATH) {
+        if (S.lds_bytes_bvh)
+            hipLaunchKernelGGL((k_prbvol_backward<true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters);
+        else
+            hipLaunchKernelGGL((k_prbvol_backward<false>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters);
+    } else if (S.lds_bytes_bvh && fused)
         hipLaunchKernelGGL((k_prb_backward<true, true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);
     else if (S.lds_bytes_bvh)
         hipLaunchKernelGGL((k_prb_backward<true, false>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);

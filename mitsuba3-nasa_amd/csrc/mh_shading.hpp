@@ -1018,7 +1018,17 @@ struct GradCtx {
     float *const *bufs;           // per slot gradient buffer
     const uint32_t *is_rgb;       // per slot
     float acc[kMaxRgbParams][3];  // per-lane accumulators for rgb params
+    const int32_t *sigma_slot;    // prbvolpath: medium -> sigma_t slot or -1 (nullptr: none)
+    const int32_t *albedo_slot;   // prbvolpath: medium -> albedo slot or -1 (nullptr: none)
 };
+
+// register accumulator of a small (rgb / scalar) parameter slot; the
+// unrolled compare keeps acc[][] in VGPRs (a runtime index would spill it)
+MH_DEV void acc_add(GradCtx &g, int32_t k, V3 a) {
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk)
+        if (kk == k) { g.acc[kk][0] += a.x; g.acc[kk][1] += a.y; g.acc[kk][2] += a.z; }
+}
 
 MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3 adj, GradCtx &g) {
     int32_t k = g.slot_of_tex[tex];
@@ -1703,6 +1713,320 @@ MH_DEV V3 volpath_sample(const DScene &S, const LdsBvh &B, const IntegratorParam
         active = active && (active_surface || active_medium);
     }
     return result;
+}
+
+
+// ===========================================================================
+// PRBVolpathIntegrator (python/ad/integrators/prbvolpath.py:91-431)
+//   primal (Adj == false) or adjoint replay (Adj == true, L = primal radiance)
+//   Same operation order as the oracle restatement (oracle/mh_oracle.c,
+//   "PRBVolpathIntegrator" section).
+// ===========================================================================
+// adjoint of sigma_t(p) = scale * Texture3f(grid).eval(p) (heterogeneous.cpp:192)
+// or scale * sigma_t (homogeneous.cpp:158); adj = d loss / d sigma_t(p)
+MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, GradCtx &g) {
+    if (!g.sigma_slot) return;
+    const int32_t k = g.sigma_slot[med];
+    if (k < 0) return;
+    const DMedium &m = S.media[med];
+    const float as = adj * m.scale;
+    if (m.type == MH_MEDIUM_HOMOGENEOUS) { acc_add(g, k, v3(as, 0.f, 0.f)); return; }
+    V3 q = xf_point(m.to_local, p);
+    const int32_t rx = (int32_t)m.res[0], ry = (int32_t)m.res[1], rz = (int32_t)m.res[2];
+    float px = __builtin_fmaf(q.x, (float)rx, -0.5f), py = __builtin_fmaf(q.y, (float)ry, -0.5f),
+          pz = __builtin_fmaf(q.z, (float)rz, -0.5f);
+    int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py), iz = (int32_t)floorf(pz);
+    float w1x = px - (float)ix, w1y = py - (float)iy, w1z = pz - (float)iz;
+    float w0x = 1.f - w1x, w0y = 1.f - w1y, w0z = 1.f - w1z;
+    const int32_t xs[2] = {min(max(ix, 0), rx - 1), min(max(ix + 1, 0), rx - 1)};
+    const int32_t ys[2] = {min(max(iy, 0), ry - 1), min(max(iy + 1, 0), ry - 1)};
+    const int32_t zs[2] = {min(max(iz, 0), rz - 1), min(max(iz + 1, 0), rz - 1)};
+    float *buf = g.bufs[k];
+    const uint64_t sy = (uint64_t)rx, sz = (uint64_t)rx * (uint64_t)ry;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+        const float w = ((bz ? w1z : w0z) * (by ? w1y : w0y)) * (bx ? w1x : w0x);
+        unsafeAtomicAdd(buf + (uint64_t)zs[bz] * sz + (uint64_t)ys[by] * sy + (uint64_t)xs[bx], as * w);
+    }
+}
+
+MH_DEV void albedo_backward(uint32_t med, V3 adj, GradCtx &g) {
+    if (!g.albedo_slot) return;
+    const int32_t k = g.albedo_slot[med];
+    if (k >= 0) acc_add(g, k, adj);
+}
+
+// PRBVolpathIntegrator.sample_emitter (prbvolpath.py:336-431): emitter sample
+// + ratio-tracked transmittance; Adj: replay with the cloned sampler and
+// back-propagate dL * adj_emitted through every tr_multiplier (:412-414)
+template <bool Adj>
+MH_DEV V3 pvp_sample_emitter(const DScene &S, const LdsBvh &B, const MEI &mei_ref, const SI &si_ref,
+                             bool active_medium, Pcg &rng, uint32_t medium, DirS &ds, V3 adj_emitted, V3 dL,
+                             GradCtx *g, uint32_t &n_shadow) {
+    const V3 ref_p = active_medium ? mei_ref.p : si_ref.p;
+    const V3 ref_n = active_medium ? v3(0.f, 0.f, 0.f) : si_ref.n;
+    const float sx = rng.next_float(), sy = rng.next_float();
+    const V3 emitter_val = scene_sample_emitter_direction(S, ref_p, sx, sy, ds);
+    if (ds.pdf == 0.f) return v3(0.f, 0.f, 0.f);
+    if (!active_medium && is_medium_transition(S, si_ref)) medium = target_medium(S, si_ref, ds.d);
+    RayT ray = spawn_ray(ref_p, ref_n, ds.d);
+    const float k_dist = 1.f - kShadowEps;   // (1.0 - ShadowEpsilon), exact in float
+    const bool nee_hom = S.vol_flags & kVolNeeHomogeneous;
+    float total_dist = 0.f, si_t = 0.f;
+    SI si;
+    si.valid = false;
+    bool needs_intersection = true, active = true;
+    V3 transmittance = v3(1.f, 1.f, 1.f);
+    while (active) {
+        const float remaining_dist = ds.dist * k_dist - total_dist;
+        ray.maxt = remaining_dist;
+        if (!(remaining_dist > 0.f)) break;
+        if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+        needs_intersection = false;
+        bool act_med = medium != MH_INVALID, act_surf = !act_med, escaped = false, hom = false;
+        float hom_t = 0.f;
+        MEI mei;
+        mei.valid = false;
+        mei.t = 0.f;
+        mei.maj = 1.f;
+        mei.p = v3(0.f, 0.f, 0.f);
+        V3 trm = v3(1.f, 1.f, 1.f);
+        if (act_med) {
+            const DMedium &m = S.media[medium];
+            sample_interaction(S, medium, ray, rng.next_float(), mei);
+            if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+            if (nee_hom && m.type == MH_MEDIUM_HOMOGENEOUS) {
+                mei.t = fminf(remaining_dist, si_t);
+                hom_t = fminf(mei.t, si_t) - mei.mint;
+                const float tr = exp_dr((-hom_t) * mei.maj);
+                trm = v3(tr, tr, tr);
+                hom = true;
+                mei.t = __builtin_huge_valf();
+                mei.valid = false;
+            }
+            escaped = !mei.valid;
+            act_med = mei.valid;
+            if (act_med) {
+                ray.o = mei.p;
+                si_t = si_t - mei.t;
+                trm = trm * (mei.sigma_n / mei.maj);
+            }
+        }
+        act_surf = (act_surf || escaped) && si.valid && !act_med;
+        if (act_surf) {
+            const uint32_t b = S.shapes[si.shape].bsdf;
+            trm = trm * ((b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f);
+        }
+        if (Adj && (act_med || hom) && (act_med || act_surf)) {
+            // backward(tr_multiplier * detach(dL * adj_emitted / tr_multiplier))
+            const float tc[3] = {trm.x, trm.y, trm.z}, dc[3] = {dL.x, dL.y, dL.z},
+                        ac[3] = {adj_emitted.x, adj_emitted.y, adj_emitted.z};
+            float gs = 0.f;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float up = tc[c] > 0.f ? (dc[c] * ac[c]) / tc[c] : 0.f;
+                gs += act_med ? up * (-1.f / mei.maj) : up * (-hom_t * tc[c]);
+            }
+            sigma_t_backward(S, medium, mei.p, gs, *g);
+        }
+        transmittance = transmittance * trm;
+        if (act_surf) ray = spawn_ray(si.p, si.n, ray.d);
+        needs_intersection = act_surf;
+        active = (act_med || act_surf) && nonzero(transmittance);
+        if (active) total_dist += act_med ? mei.t : si_t;
+        if (act_surf && is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
+    }
+    return emitter_val * transmittance;
+}
+
+template <bool Adj>
+MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, RayT ray,
+                        V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow) {
+    const bool handle_null = S.vol_flags & kVolHandleNull;
+    uint32_t depth = 0;
+    if (!Adj) L = v3(0.f, 0.f, 0.f);
+    V3 throughput = v3(1.f, 1.f, 1.f);
+    float eta = 1.f;
+    bool active = true, needs_intersection = true;
+    SI si;
+    si.valid = false;
+    float si_t = 0.f;
+    uint32_t medium = MH_INVALID;   // "TODO: support sensors inside media" (prbvolpath.py:123-124)
+    (void)fminf(3.f * rng.next_float(), 2.f);   // RGB channel (scalar majorants: all channels alike)
+    while (active) {
+        // ---- Russian roulette (:142-149)
+        active = active && nonzero(throughput);
+        const float q = fminf(hmax(throughput) * (eta * eta), 0.99f);
+        const bool perform_rr = depth > in.rr_depth;
+        if (active) active = rng.next_float() < q || !perform_rr;
+        if (perform_rr) throughput = throughput * rcp(q);
+        if (!active) break;
+
+        bool active_medium = medium != MH_INVALID, active_surface = !active_medium;
+        bool escaped = false, act_null = false, act_scatter = false;
+        float fw = 1.f, P = 1.f, mt = 0.f;
+        V3 weight = v3(1.f, 1.f, 1.f);
+        MEI mei;
+        mei.valid = false;
+        mei.t = 0.f;
+        mei.maj = 1.f;
+        mei.sigma_t = 0.f;
+        mei.p = v3(0.f, 0.f, 0.f);
+        mei.sigma_s = v3(0.f, 0.f, 0.f);
+        const uint32_t med = medium;
+        // ---- medium interaction (:157-204)
+        if (active_medium) {
+            const DMedium &m = S.media[med];
+            sample_interaction(S, med, ray, rng.next_float(), mei);
+            if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
+            if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+            needs_intersection = false;
+            if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+            // transmittance_eval_pdf (medium.cpp:101-112)
+            mt = fminf(mei.t, si_t) - mei.mint;
+            const float tr = exp_dr((-mt) * mei.maj);
+            const float tr_pdf = si_t < mei.t ? tr : tr * mei.maj;
+            fw = tr_pdf > 0.f ? tr / tr_pdf : 0.f;
+            weight = v3(fw, fw, fw);
+            escaped = !mei.valid;
+            active_medium = mei.valid;
+            if (handle_null) {
+                P = mei.sigma_t / mei.maj;
+                if (active_medium) act_null = rng.next_float() >= P;
+                act_scatter = !act_null && active_medium;
+                if (act_null) weight = weight * (mei.sigma_n / (1.f - P));
+            } else {
+                act_scatter = active_medium;
+            }
+            if (act_scatter) depth += 1;
+        }
+        active = active && depth < in.max_depth;
+        act_scatter = act_scatter && active;
+        if (handle_null && act_null) { ray.o = mei.p; si_t = si_t - mei.t; }
+        if (act_scatter)
+            weight = v3(weight.x * (mei.sigma_s.x / P), weight.y * (mei.sigma_s.y / P), weight.z * (mei.sigma_s.z / P));
+        throughput = throughput * weight;
+        if (Adj && (active_medium || escaped)) {
+            // backward(dL * weight * Lo), Lo = L / max(1e-8, weight) (:202-204)
+            const DMedium &m = S.media[med];
+            const bool homog = m.type == MH_MEDIUM_HOMOGENEOUS;
+            const float wc[3] = {weight.x, weight.y, weight.z}, Lc[3] = {L.x, L.y, L.z}, dc[3] = {dL.x, dL.y, dL.z};
+            const float al[3] = {m.albedo[0], m.albedo[1], m.albedo[2]};
+            const float ss[3] = {mei.sigma_s.x, mei.sigma_s.y, mei.sigma_s.z};
+            const float dfw = homog ? -mt * fw : 0.f;   // d (tr / tr_pdf) / d sigma_t
+            float gs = 0.f, ga[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float up = dc[c] * (Lc[c] / fmaxf(1e-8f, wc[c]));
+                float dws, dwa = 0.f;
+                if (act_scatter) {
+                    dws = dfw * ss[c] / P + fw * al[c] / P;   // sigma_s = sigma_t * albedo
+                    dwa = fw * mei.sigma_t / P;
+                } else if (act_null) {
+                    dws = -fw / (1.f - P);
+                } else {
+                    dws = dfw;
+                }
+                gs += up * dws;
+                ga[c] = up * dwa;
+            }
+            sigma_t_backward(S, med, mei.p, gs, *g);
+            if (act_scatter) albedo_backward(med, v3(ga[0], ga[1], ga[2]), *g);
+        }
+
+        // ---- surface interaction (:212-238)
+        active_surface = active_surface || escaped;
+        if (active_surface && needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+        active_surface = active_surface && si.valid;
+        const uint32_t b = active_surface ? S.shapes[si.shape].bsdf : MH_INVALID;
+        const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+        V3 rho = v3(0.f, 0.f, 0.f);
+        if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+
+        // ---- emitter sampling (:242-270)
+        const bool active_e_surface = active_surface && smooth && depth + 1 < in.max_depth;
+        const bool sample_emitters = med != MH_INVALID && !(S.media[med].flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+        const bool active_e_medium = act_scatter && sample_emitters;
+        if (active_e_surface || active_e_medium) {
+            const Pcg nee_rng = rng;   // sampler.clone()
+            DirS ds;
+            const V3 emitted = pvp_sample_emitter<false>(S, B, mei, si, active_e_medium, rng, medium, ds,
+                                                         v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), nullptr, n_shadow);
+            V3 nee_w, bv = v3(0.f, 0.f, 0.f);
+            float nee_pdf, bp = 0.f;
+            const V3 wo_s = to_local(si, ds.d);
+            if (active_e_surface) {
+                diffuse_eval_pdf(rho, si.wi, wo_s, true, bv, bp);
+                nee_w = bv;
+                nee_pdf = bp;
+            } else {
+                const float ph = phase_eval(S.media[med], mei_to_local(mei, ds.d));
+                nee_w = v3(ph, ph, ph);
+                nee_pdf = ph;
+            }
+            if (ds.delta) nee_pdf = 0.f;
+            const float mis = mis_weight(ds.pdf, nee_pdf);
+            const V3 contrib = ((throughput * nee_w) * mis) * emitted;
+            L = Adj ? L + (-contrib) : L + contrib;
+            if (Adj) {
+                Pcg r2 = nee_rng;
+                DirS ds2;
+                pvp_sample_emitter<true>(S, B, mei, si, active_e_medium, r2, medium, ds2, contrib, dL, g, n_shadow);
+                if (active_e_surface && si.wi.z > 0.f && wo_s.z > 0.f) {
+                    // backward(dL * contrib) through bsdf_val = rho / pi * cos
+                    const V3 adj = ((((dL * emitted) * mis) * throughput) * kInvPi) * wo_s.z;
+                    tex_backward(S, S.bsdf_tex[b], si.uvx, si.uvy, adj, *g);
+                }
+            }
+        }
+
+        // ---- phase function sampling (:274-294)
+        if (act_scatter) {
+            (void)rng.next_float();
+            const float s2x = rng.next_float(), s2y = rng.next_float();
+            float ph_pdf;
+            const V3 wo = phase_sample(S.media[med], s2x, s2y, ph_pdf);
+            act_scatter = act_scatter && ph_pdf > 0.f;
+            if (act_scatter) {
+                ray = spawn_ray(mei.p, v3(0.f, 0.f, 0.f), mei_to_world(mei, wo));
+                needs_intersection = true;
+            }
+        }
+
+        // ---- BSDF sampling (:298-331)
+        if (active_surface) {
+            (void)rng.next_float();
+            const float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bs_wo, bw;
+            float bs_pdf;
+            if (!smooth) {
+                bs_wo = -si.wi; bs_pdf = 1.f; bw = v3(1.f, 1.f, 1.f);
+            } else {
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                bw = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0.f, 0.f, 0.f);
+            }
+            active_surface = active_surface && bs_pdf > 0.f;
+            if (active_surface) {
+                if (Adj && smooth && si.wi.z > 0.f && bs_wo.z > 0.f) {
+                    // Lo = bsdf_eval * detach(L / max(1e-8, bsdf_eval)) (:305-312)
+                    const V3 be = (rho * kInvPi) * bs_wo.z;
+                    V3 adj = v3(dL.x * (L.x / fmaxf(1e-8f, be.x)), dL.y * (L.y / fmaxf(1e-8f, be.y)),
+                                dL.z * (L.z / fmaxf(1e-8f, be.z)));
+                    adj = (adj * kInvPi) * bs_wo.z;
+                    tex_backward(S, S.bsdf_tex[b], si.uvx, si.uvy, adj, *g);
+                }
+                throughput = throughput * bw;
+                ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+                needs_intersection = true;
+                if (smooth) depth += 1;
+                if (is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
+            }
+        }
+        active = active && (active_surface || active_medium);
+    }
+    return L;
 }
 
 }  // namespace mh

@@ -24,7 +24,11 @@ RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
 MEDIUM_HETEROGENEOUS, MEDIUM_HOMOGENEOUS = 0, 1
 PHASE_ISOTROPIC, PHASE_HG = 0, 1
 MEDIUM_NO_EMITTER_SAMPLING, MEDIUM_NO_SPECTRAL_EXTINCTION = 1, 2
-INTEGRATOR_PATH, INTEGRATOR_VOLPATH, INTEGRATOR_PRB = 0, 1, 2
+INTEGRATOR_PATH, INTEGRATOR_VOLPATH, INTEGRATOR_PRB, INTEGRATOR_PRBVOLPATH = 0, 1, 2, 3
+# differentiable parameter ids of mh_render_backward (texture index, or kind | medium)
+PARAM_KIND_MASK = 0xF0000000
+PARAM_MEDIUM_SIGMA_T = 0x10000000
+PARAM_MEDIUM_ALBEDO = 0x20000000
 
 FLAG_DEVICE_POINTERS = 1 << 0
 FLAG_ACCUMULATE = 1 << 1
@@ -106,7 +110,7 @@ EXPORTS = [
     "mh_last_error", "mh_abi_version", "mh_device_count", "mh_scene_create", "mh_scene_destroy",
     "mh_scene_set_stream", "mh_scene_update_rgb", "mh_scene_update_texture", "mh_render",
     "mh_develop", "mh_prb_weights", "mh_render_backward", "mh_trace_closest", "mh_trace_shadow",
-    "mh_scene_bvh_info", "mh_render_samples",
+    "mh_scene_bvh_info", "mh_render_samples", "mh_scene_update_medium",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -144,6 +148,7 @@ def lib():
     L.mh_scene_set_stream.argtypes = [vp, vp]
     L.mh_scene_update_rgb.argtypes = [vp, u32, PF]
     L.mh_scene_update_texture.argtypes = [vp, u32, PF, u64]
+    L.mh_scene_update_medium.argtypes = [vp, u32, vp, vp, vp, u64, u32]
     L.mh_render.argtypes = [vp, C.POINTER(Integrator), u32, u32, u32, u32, vp, u32, C.POINTER(Stats)]
     L.mh_develop.argtypes = [vp, vp, vp, u32]
     L.mh_render_samples.argtypes = [vp, C.POINTER(Integrator), u32, u32, u32, u32, vp, u32]

@@ -51,8 +51,10 @@ def _ptr(t) -> C.c_void_p:
 
 class SceneParameters:
     """util.py:13-290 (SceneParameters) restricted to the differentiable
-    texture parameters on the hot path ('<bsdf>.reflectance.value' and
-    '<bsdf>.reflectance.data')."""
+    parameters on the hot path: '<bsdf>.reflectance.value' / '.data' and the
+    medium parameters '<medium>.sigma_t.data' (grid, shape (z, y, x, 1) as the
+    reference's TensorXf), '<medium>.sigma_t.value' (homogeneous) and
+    '<medium>.albedo.value'."""
 
     def __init__(self, scene: Scene, device=None):
         torch = _torch()
@@ -66,6 +68,13 @@ class SceneParameters:
             elif kind == "bitmap":
                 t = scene.texture(idx)
                 v = torch.from_numpy(scene.texture_data(idx).reshape(t.height, t.width, t.channels).copy())
+            elif kind == "grid":
+                m = scene.medium(idx)
+                v = torch.from_numpy(scene.grid_data(idx).reshape(m.grid_res[2], m.grid_res[1], m.grid_res[0], 1).copy())
+            elif kind == "medium_sigma_t":
+                v = torch.tensor([scene.medium(idx).sigma_t_const], dtype=torch.float32)
+            elif kind == "medium_albedo":
+                v = torch.tensor(list(scene.medium(idx).albedo), dtype=torch.float32)
             else:
                 continue
             if device is not None:
@@ -103,6 +112,15 @@ class SceneParameters:
     def texture_of(self, k) -> int:
         return self._kind[k][1]
 
+    def param_id(self, k) -> int:
+        """mh_render_backward parameter id (include/mitsuba_hip.h MH_PARAM_*)."""
+        kind, idx = self._kind[k]
+        if kind in ("grid", "medium_sigma_t"):
+            return A.PARAM_MEDIUM_SIGMA_T | idx
+        if kind == "medium_albedo":
+            return A.PARAM_MEDIUM_ALBEDO | idx
+        return idx
+
     def update(self, values: Optional[Dict] = None):
         """Push modified values into every device copy of the scene."""
         if values:
@@ -117,6 +135,20 @@ class SceneParameters:
                 self.scene.texture(idx).value[:] = [float(x) for x in arr]
                 for h in self.scene._handles.values():
                     A.check(L.mh_scene_update_rgb(h, idx, arr.ctypes.data_as(A.PF)))
+            elif kind in ("grid", "medium_sigma_t", "medium_albedo"):
+                m = self.scene.medium(idx)
+                if kind == "grid":
+                    self.scene.grid_data(idx)[:] = arr
+                    m.max_density = float(arr.max()) if arr.size else 0.0   # parameters_changed
+                elif kind == "medium_sigma_t":
+                    m.sigma_t_const = float(arr[0])
+                else:
+                    m.albedo[:] = [float(x) for x in arr]
+                p = arr.ctypes.data_as(C.c_void_p)
+                for h in self.scene._handles.values():
+                    A.check(L.mh_scene_update_medium(h, idx, p if kind == "medium_albedo" else None,
+                                                     p if kind == "medium_sigma_t" else None,
+                                                     p if kind == "grid" else None, arr.size, 0))
             else:
                 dst = self.scene.texture_data(idx)
                 dst[:] = arr
@@ -186,13 +218,13 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     reference's own two-pass structure)."""
     torch = _torch()
     integrator = integrator or scene.integrator()
-    if integrator.type != "prb":
-        raise A.MitsubaHipError("render_backward(): requires the 'prb' integrator")
+    if integrator.type not in ("prb", "prbvolpath"):
+        raise A.MitsubaHipError("render_backward(): requires the 'prb' or 'prbvolpath' integrator")
     spp = spp or scene.sample_count()
     dev = grad_in.device.index or 0
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
     grad_in = grad_in.to(torch.float32).contiguous()
-    tex = (C.c_uint32 * max(len(keys), 1))(*[params.texture_of(k) for k in keys])
+    tex = (C.c_uint32 * max(len(keys), 1))(*[params.param_id(k) for k in keys])
     outs = [torch.zeros(params[k].shape, dtype=torch.float32, device=grad_in.device) for k in keys]
     ptrs = (C.c_void_p * max(len(keys), 1))(*[o.data_ptr() for o in outs])
     ic = integrator.c()

@@ -40,13 +40,14 @@ def _normalize32(v):
 # Integrators (integrator.cpp:22-28,1281-1298; ad/integrators/common.py:29-41)
 # ---------------------------------------------------------------------------
 class Integrator:
-    TYPES = {"path": A.INTEGRATOR_PATH, "volpath": A.INTEGRATOR_VOLPATH, "prb": A.INTEGRATOR_PRB}
+    TYPES = {"path": A.INTEGRATOR_PATH, "volpath": A.INTEGRATOR_VOLPATH, "prb": A.INTEGRATOR_PRB,
+             "prbvolpath": A.INTEGRATOR_PRBVOLPATH}
 
     def __init__(self, type_: str, props: Dict[str, Any]):
         if type_ not in self.TYPES:
             raise RuntimeError(f'Plugin "{type_}" is not available in the hip_ad_rgb variant')
         self.type = type_
-        default_depth = 6 if type_ == "prb" else -1
+        default_depth = 6 if type_ in ("prb", "prbvolpath") else -1
         max_depth = int(props.get("max_depth", default_depth))
         if max_depth < 0 and max_depth != -1:
             raise RuntimeError('"max_depth" must be set to -1 (infinite) or a value >= 0')
@@ -311,6 +312,7 @@ class _Builder:
                 raise RuntimeError("hip_ad_rgb: spectrally varying sigma_t is not supported")
             m.type = A.MEDIUM_HOMOGENEOUS
             m.sigma_t_const = float(np.float32(v[0]))
+            self.params[name + ".sigma_t.value"] = ("medium_sigma_t", len(self.media))
         elif ty == "heterogeneous":
             if not isinstance(st, dict) or st.get("type") != "gridvolume":
                 raise RuntimeError("hip_ad_rgb: heterogeneous media need a 'gridvolume' sigma_t")
@@ -348,6 +350,7 @@ class _Builder:
             self.params[name + ".sigma_t.data"] = ("grid", len(self.media))
         else:
             raise RuntimeError(f'Medium plugin "{ty}" is not available in the hip_ad_rgb variant')
+        self.params[name + ".albedo.value"] = ("medium_albedo", len(self.media))
         self.media.append(m)
         idx = len(self.media) - 1
         self.medium_ids[name] = idx
@@ -558,6 +561,14 @@ class Scene:
 
     def texture(self, idx: int) -> A.Texture:
         return self._textures[idx]
+
+    def medium(self, idx: int) -> A.Medium:
+        return self._media[idx]
+
+    def grid_data(self, idx: int) -> np.ndarray:
+        m = self._media[idx]
+        n = m.grid_res[0] * m.grid_res[1] * m.grid_res[2]
+        return self.grid[m.grid_offset:m.grid_offset + n]
 
     def texture_data(self, idx: int) -> np.ndarray:
         t = self._textures[idx]

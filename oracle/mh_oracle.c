@@ -1683,6 +1683,350 @@ static v3 volpath_sample(const scene_view *sv, const mh_integrator *in, pcg32 *r
     return result;
 }
 
+/* ------------------------------------------------------------------------ */
+/* PRBVolpathIntegrator (src/python/python/ad/integrators/prbvolpath.py)     */
+/* primal: grad == NULL; adjoint: grad != NULL with L_in = primal radiance   */
+/* ------------------------------------------------------------------------ */
+typedef struct { int handle_null, nee_hom; } pvp_flags;
+
+/* prepare_scene (prbvolpath.py:76-89): flags from the media of the shapes;
+   use_nee is always True. */
+static void pvp_prepare(const mh_scene_desc *d, pvp_flags *f) {
+    f->handle_null = 0;
+    f->nee_hom = 0;
+    for (uint32_t i = 0; i < d->n_shapes; ++i) {
+        uint32_t ms[2] = {d->shapes[i].interior_medium, d->shapes[i].exterior_medium};
+        for (int k = 0; k < 2; ++k) {
+            if (ms[k] == MH_INVALID) continue;
+            if (d->media[ms[k]].type == MH_MEDIUM_HOMOGENEOUS) f->nee_hom = 1;
+            else f->handle_null = 1;
+        }
+    }
+}
+
+/* adjoint of sigma_t(p) = scale * Texture3f(grid).eval(p) (heterogeneous.cpp:192)
+   or scale * sigma_t (homogeneous.cpp:158): adj = d loss / d sigma_t(p) */
+static void sigma_t_backward(const mh_scene_desc *d, uint32_t med, v3 p, double adj, grad_sink *g) {
+    for (uint32_t k = 0; k < g->n_params; ++k) {
+        if (g->tex[k] != (MH_PARAM_MEDIUM_SIGMA_T | med)) continue;
+        const mh_medium *m = &d->media[med];
+        double *a = g->acc[k];
+        const double as = adj * (double)m->scale;
+        if (m->type == MH_MEDIUM_HOMOGENEOUS) { a[0] += as; continue; }
+        /* grid_eval's taps and weights (Texture3f linear, clamp) */
+        v3 q = xf_point(m->grid_to_local, p);
+        const int32_t rx = (int32_t)m->grid_res[0], ry = (int32_t)m->grid_res[1], rz = (int32_t)m->grid_res[2];
+        float px = fmaf(q.x, (float)rx, -0.5f), py = fmaf(q.y, (float)ry, -0.5f), pz = fmaf(q.z, (float)rz, -0.5f);
+        int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py), iz = (int32_t)floorf(pz);
+        double w1[3] = {px - (float)ix, py - (float)iy, pz - (float)iz};
+        double w0[3] = {1.0 - (float)w1[0], 1.0 - (float)w1[1], 1.0 - (float)w1[2]};
+#define CL(i, r) ((i) < 0 ? 0 : ((i) > (r) - 1 ? (r) - 1 : (i)))
+        int32_t xs[2] = {CL(ix, rx), CL(ix + 1, rx)}, ys[2] = {CL(iy, ry), CL(iy + 1, ry)},
+                zs[2] = {CL(iz, rz), CL(iz + 1, rz)};
+#undef CL
+        for (int c = 0; c < 8; ++c) {
+            const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+            const double w = (bz ? w1[2] : w0[2]) * (by ? w1[1] : w0[1]) * (bx ? w1[0] : w0[0]);
+            a[((size_t)zs[bz] * (size_t)ry + (size_t)ys[by]) * (size_t)rx + (size_t)xs[bx]] += as * w;
+        }
+    }
+}
+
+/* adjoint of the constant albedo (constvolume 'albedo.value') */
+static void albedo_backward(uint32_t med, v3 adj, grad_sink *g) {
+    for (uint32_t k = 0; k < g->n_params; ++k) {
+        if (g->tex[k] != (MH_PARAM_MEDIUM_ALBEDO | med)) continue;
+        g->acc[k][0] += adj.x; g->acc[k][1] += adj.y; g->acc[k][2] += adj.z;
+    }
+}
+
+/* PRBVolpathIntegrator.sample_emitter (prbvolpath.py:336-431).  primal
+   (grad == NULL): transmittance detached.  adjoint: replays the walk with a
+   cloned sampler and back-propagates dL * adj_emitted through every
+   tr_multiplier (prbvolpath.py:412-414). */
+static v3 pvp_sample_emitter(const scene_view *sv, const pvp_flags *f, const med_int *mei_ref,
+                             const surf_int *si_ref, int active_medium, pcg32 *rng, uint32_t medium,
+                             uint32_t channel, dir_sample *ds, v3 adj_emitted, v3 dL, grad_sink *grad,
+                             uint64_t *counters) {
+    const mh_scene_desc *d = sv->d;
+    /* ref_interaction[active_medium] = mei; [active_surface] = si */
+    const v3 ref_p = active_medium ? mei_ref->p : si_ref->p;
+    const v3 ref_n = active_medium ? V3(0, 0, 0) : si_ref->n;
+    float sx = pcg_float(rng), sy = pcg_float(rng);
+    v3 emitter_val = scene_sample_emitter_direction(d, ref_p, sx, sy, ds);
+    if (ds->pdf == 0.f) return V3(0, 0, 0);   /* emitter_val[invalid] = 0; loop inactive */
+    if (!active_medium && is_medium_transition(d, si_ref)) medium = target_medium(d, si_ref, ds->d);
+    ray3 ray = spawn_ray(ref_p, ref_n, ds->d);
+    const float k_dist = 1.f - SHADOW_EPS;   /* (1.0 - ShadowEpsilon): exact in float */
+    float total_dist = 0.f;
+    surf_int si;
+    memset(&si, 0, sizeof(si));
+    int needs_intersection = 1, active = 1;
+    v3 transmittance = V3(1, 1, 1);
+    while (active) {
+        const float remaining_dist = ds->dist * k_dist - total_dist;
+        ray.maxt = remaining_dist;
+        active = active && remaining_dist > 0.f;
+        if (!active) break;
+        if (needs_intersection) {
+            pi_rec pi;
+            trace_closest(sv, &ray, &pi);
+            if (counters) counters[1]++;
+            compute_si(d, &ray, &pi, &si);
+        }
+        needs_intersection = 0;
+        int act_med = medium != MH_INVALID, act_surf = !act_med, escaped = 0, hom = 0;
+        float hom_t = 0.f;
+        med_int mei;
+        memset(&mei, 0, sizeof(mei));
+        v3 trm = V3(1, 1, 1);
+        if (act_med) {
+            const mh_medium *m = &d->media[medium];
+            sample_interaction(d, medium, &ray, pcg_float(rng), channel, &mei);
+            if (si.t < mei.t) { mei.t = INFINITY; mei.valid = 0; }
+            if (f->nee_hom && m->type == MH_MEDIUM_HOMOGENEOUS) {
+                /* direct transmittance to the next surface / segment end (:390-394) */
+                mei.t = fminf(remaining_dist, si.t);
+                hom_t = fminf(mei.t, si.t) - mei.mint;
+                float tr = oracle_exp((-hom_t) * mei.maj);
+                trm = V3(tr, tr, tr);
+                hom = 1;
+                mei.t = INFINITY;
+                mei.valid = 0;
+            }
+            escaped = !mei.valid;
+            act_med = mei.valid;
+            if (act_med) {
+                ray.o = mei.p;
+                si.t = si.t - mei.t;
+                trm = vscale(trm, mei.sigma_n / mei.maj);
+            }
+        }
+        act_surf = (act_surf || escaped) && si.valid && !act_med;
+        if (act_surf) {
+            uint32_t b = si_bsdf(d, &si);
+            float bv = (b != MH_INVALID && d->bsdfs[b].type == MH_BSDF_NULL) ? 1.f : 0.f;
+            trm = vscale(trm, bv);
+        }
+        if (grad && (act_med || act_surf)) {
+            /* backward(tr_multiplier * detach(dL * adj_emitted / tr_multiplier)) */
+            const float tc[3] = {trm.x, trm.y, trm.z};
+            const float dc[3] = {dL.x, dL.y, dL.z}, ac[3] = {adj_emitted.x, adj_emitted.y, adj_emitted.z};
+            double gs = 0.0;
+            for (int c = 0; c < 3; ++c) {
+                if (!(tc[c] > 0.f)) continue;
+                const double up = (double)((dc[c] * ac[c]) / tc[c]);
+                if (act_med) gs += up * (-1.0 / (double)mei.maj);              /* d(sigma_n/maj)/d sigma_t */
+                else if (hom) gs += up * (-(double)hom_t * (double)tc[c]);     /* d exp(-t sigma_t) */
+            }
+            if (act_med || hom) sigma_t_backward(d, medium, mei.p, gs, grad);
+        }
+        transmittance = vmul(transmittance, trm);
+        if (act_surf) ray = spawn_ray(si.p, si.n, ray.d);
+        needs_intersection = act_surf;
+        active = (act_med || act_surf) &&
+                 (transmittance.x != 0.f || transmittance.y != 0.f || transmittance.z != 0.f);
+        if (active) total_dist += act_med ? mei.t : si.t;
+        if (act_surf && is_medium_transition(d, &si)) medium = target_medium(d, &si, ray.d);
+    }
+    return vmul(emitter_val, transmittance);
+}
+
+static v3 prbvol_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
+                        v3 dL, v3 L_in, grad_sink *grad, int *valid_out, uint64_t *counters) {
+    const mh_scene_desc *d = sv->d;
+    const int primal = grad == NULL;
+    pvp_flags f;
+    pvp_prepare(d, &f);
+    uint32_t depth = 0;
+    v3 L = primal ? V3(0, 0, 0) : L_in;
+    v3 throughput = V3(1, 1, 1);
+    float eta = 1.f;
+    int active = 1, valid_ray = 0, needs_intersection = 1;
+    surf_int si;
+    memset(&si, 0, sizeof(si));
+    uint32_t medium = MH_INVALID;   /* "TODO: support sensors inside media" (:123-124) */
+    uint32_t channel = (uint32_t)fminf(3.f * pcg_float(rng), 2.f);
+    while (active) {
+        /* ---- Russian roulette (:142-149) ---- */
+        active = active && (throughput.x != 0.f || throughput.y != 0.f || throughput.z != 0.f);
+        const float q = fminf(vmax(throughput) * (eta * eta), 0.99f);
+        const int perform_rr = depth > in->rr_depth;
+        if (active) active = pcg_float(rng) < q || !perform_rr;
+        if (perform_rr) throughput = vscale(throughput, rcpf_(q));
+        if (!active) break;
+
+        int active_medium = medium != MH_INVALID, active_surface = !active_medium;
+        int escaped = 0, act_null = 0, act_scatter = 0;
+        float fw = 1.f, P = 1.f, mt = 0.f;
+        v3 weight = V3(1, 1, 1);
+        med_int mei;
+        memset(&mei, 0, sizeof(mei));
+        const mh_medium *m = active_medium ? &d->media[medium] : NULL;
+        /* ---- medium interaction (:157-204) ---- */
+        if (active_medium) {
+            sample_interaction(d, medium, &ray, pcg_float(rng), channel, &mei);
+            if (m->type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
+            if (needs_intersection) {
+                pi_rec pi;
+                trace_closest(sv, &ray, &pi);
+                if (counters) counters[0]++;
+                compute_si(d, &ray, &pi, &si);
+            }
+            needs_intersection = 0;
+            if (si.t < mei.t) { mei.t = INFINITY; mei.valid = 0; }
+            /* transmittance_eval_pdf (medium.cpp:101-112) */
+            mt = fminf(mei.t, si.t) - mei.mint;
+            const float tr = oracle_exp((-mt) * mei.maj);
+            const float tr_pdf = si.t < mei.t ? tr : tr * mei.maj;
+            fw = tr_pdf > 0.f ? tr / tr_pdf : 0.f;
+            weight = V3(fw, fw, fw);
+            escaped = !mei.valid;
+            active_medium = mei.valid;
+            if (f.handle_null) {
+                P = mei.sigma_t / mei.maj;
+                if (active_medium) act_null = pcg_float(rng) >= P;
+                act_scatter = !act_null && active_medium;
+                if (act_null) weight = vscale(weight, mei.sigma_n / (1.f - P));
+            } else {
+                act_scatter = active_medium;
+            }
+            if (act_scatter) depth += 1;
+        }
+        active = active && depth < in->max_depth;
+        act_scatter = act_scatter && active;
+        if (f.handle_null && act_null) { ray.o = mei.p; si.t = si.t - mei.t; }
+        if (act_scatter)
+            weight = V3(weight.x * (mei.sigma_s.x / P), weight.y * (mei.sigma_s.y / P),
+                        weight.z * (mei.sigma_s.z / P));
+        throughput = vmul(throughput, weight);
+        if (!primal && (active_medium || escaped)) {
+            /* backward(dL * weight * Lo), Lo = L / max(1e-8, weight) (:202-204) */
+            const int homog = m->type == MH_MEDIUM_HOMOGENEOUS;
+            const float wc[3] = {weight.x, weight.y, weight.z}, Lc[3] = {L.x, L.y, L.z},
+                        dc[3] = {dL.x, dL.y, dL.z}, al[3] = {m->albedo[0], m->albedo[1], m->albedo[2]},
+                        ss[3] = {mei.sigma_s.x, mei.sigma_s.y, mei.sigma_s.z};
+            double gs = 0.0, ga[3] = {0, 0, 0};
+            for (int c = 0; c < 3; ++c) {
+                const double up = (double)dc[c] * (double)(Lc[c] / fmaxf(1e-8f, wc[c]));
+                double dws = 0.0, dwa = 0.0;   /* d weight_c / d sigma_t(p), d weight_c / d albedo_c */
+                const double dfw = homog ? -(double)mt * (double)fw : 0.0;   /* d (tr/tr_pdf) */
+                if (act_scatter) {
+                    dws = dfw * (double)ss[c] / P + (double)fw * al[c] / P;   /* sigma_s = sigma_t * albedo */
+                    dwa = (double)fw * (double)mei.sigma_t / P;
+                } else if (act_null) {
+                    dws = (double)fw * (-1.0) / (double)(1.f - P);
+                } else {
+                    dws = dfw;
+                }
+                gs += up * dws;
+                ga[c] = up * dwa;
+            }
+            sigma_t_backward(d, medium, mei.p, gs, grad);
+            if (act_scatter) albedo_backward(medium, V3((float)ga[0], (float)ga[1], (float)ga[2]), grad);
+        }
+
+        /* ---- surface interaction (:212-238) ---- */
+        active_surface = active_surface || escaped;
+        if (active_surface && needs_intersection) {
+            pi_rec pi;
+            trace_closest(sv, &ray, &pi);
+            if (counters) counters[0]++;
+            compute_si(d, &ray, &pi, &si);
+        }
+        active_surface = active_surface && si.valid;
+        uint32_t b = active_surface ? si_bsdf(d, &si) : MH_INVALID;
+        const int smooth = b != MH_INVALID && d->bsdfs[b].type == MH_BSDF_DIFFUSE;
+        v3 rho = V3(0, 0, 0);
+        if (smooth) rho = tex_eval(d, d->bsdfs[b].reflectance, si.uvx, si.uvy);
+
+        /* ---- emitter sampling (:242-270) ---- */
+        const int active_e_surface = active_surface && smooth && depth + 1 < in->max_depth;
+        const int sample_emitters = m && !(m->flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+        const int active_e_medium = act_scatter && sample_emitters;
+        if (active_e_surface || active_e_medium) {
+            pcg32 nee_rng = *rng;   /* sampler.clone() */
+            dir_sample ds;
+            v3 emitted = pvp_sample_emitter(sv, &f, &mei, &si, active_e_medium, rng, medium, channel, &ds,
+                                            V3(0, 0, 0), V3(0, 0, 0), NULL, counters);
+            v3 nee_w, bv = V3(0, 0, 0);
+            float nee_pdf, bp = 0.f;
+            v3 wo_s = to_local(&si, ds.d);
+            if (active_e_surface) {
+                diffuse_eval_pdf(rho, si.wi, wo_s, 1, &bv, &bp);
+                nee_w = bv;
+                nee_pdf = bp;
+            } else {
+                float ph = phase_eval(m, mei_to_local(&mei, ds.d));
+                nee_w = V3(ph, ph, ph);
+                nee_pdf = ph;
+            }
+            if (ds.delta) nee_pdf = 0.f;
+            const float mis = mis_weight(ds.pdf, nee_pdf);
+            v3 contrib = vmul(vscale(vmul(throughput, nee_w), mis), emitted);
+            L = primal ? vadd(L, contrib) : vadd(L, vneg(contrib));
+            if (!primal) {
+                dir_sample ds2;
+                pvp_sample_emitter(sv, &f, &mei, &si, active_e_medium, &nee_rng, medium, channel, &ds2,
+                                   contrib, dL, grad, NULL);
+                if (active_e_surface && si.wi.z > 0.f && wo_s.z > 0.f) {
+                    /* backward(dL * contrib) through bsdf_val = rho / pi * cos */
+                    v3 adj = vscale(vscale(vmul(vscale(vmul(dL, emitted), mis), throughput), INV_PI_F), wo_s.z);
+                    tex_backward(d, d->bsdfs[b].reflectance, si.uvx, si.uvy, adj, grad);
+                }
+            }
+        }
+
+        /* ---- phase function sampling (:274-294) ---- */
+        valid_ray = valid_ray || act_scatter;
+        if (act_scatter) {
+            (void)pcg_float(rng);
+            const float s2x = pcg_float(rng), s2y = pcg_float(rng);
+            float ph_pdf;
+            v3 wo = phase_sample(m, s2x, s2y, &ph_pdf);
+            act_scatter = act_scatter && ph_pdf > 0.f;
+            if (act_scatter) {
+                ray = spawn_ray(mei.p, V3(0, 0, 0), mei_to_world(&mei, wo));
+                needs_intersection = 1;
+            }
+        }
+
+        /* ---- BSDF sampling (:298-331) ---- */
+        if (active_surface) {
+            (void)pcg_float(rng);
+            const float s2x = pcg_float(rng), s2y = pcg_float(rng);
+            bsdf_sample bs;
+            v3 bw;
+            if (!smooth) {
+                bs.wo = vneg(si.wi); bs.pdf = 1.f; bs.eta = 1.f; bs.sampled_delta = 0; bs.sampled_null = 1;
+                bw = V3(1, 1, 1);
+            } else {
+                diffuse_sample(rho, si.wi, s2x, s2y, 1, &bs, &bw);
+            }
+            active_surface = active_surface && bs.pdf > 0.f;
+            if (active_surface) {
+                if (!primal && smooth && si.wi.z > 0.f && bs.wo.z > 0.f) {
+                    /* Lo = bsdf_eval * detach(L / max(1e-8, bsdf_eval)) (:305-312) */
+                    v3 be = vscale(vscale(rho, INV_PI_F), bs.wo.z);
+                    v3 adj = V3(dL.x * (L.x / fmaxf(1e-8f, be.x)), dL.y * (L.y / fmaxf(1e-8f, be.y)),
+                                dL.z * (L.z / fmaxf(1e-8f, be.z)));
+                    adj = vscale(vscale(adj, INV_PI_F), bs.wo.z);
+                    tex_backward(d, d->bsdfs[b].reflectance, si.uvx, si.uvy, adj, grad);
+                }
+                throughput = vmul(throughput, bw);
+                eta *= bs.eta;
+                ray = spawn_ray(si.p, si.n, to_world(&si, bs.wo));
+                needs_intersection = 1;
+                if (!bs.sampled_null) { depth += 1; valid_ray = 1; }
+                if (is_medium_transition(d, &si)) medium = target_medium(d, &si, ray.d);
+            }
+        }
+        active = active && (active_surface || active_medium);
+    }
+    *valid_out = valid_ray;
+    return primal ? L : dL;
+}
+
 static inline float inv_size(uint32_t n) { return 1.f / (float)n; }
 
 /* one sample of one lane: jitter, camera ray, integrator (render_sample,
@@ -1703,6 +2047,8 @@ static v3 lane_sample(const scene_view *sv, const mh_integrator *in, const wf_la
         return prb_sample(sv, in, rng, r, V3(0, 0, 0), V3(0, 0, 0), NULL, valid_out);
     if (in->type == MH_INTEGRATOR_VOLPATH)
         return volpath_sample(sv, in, rng, r, valid_out, counters);
+    if (in->type == MH_INTEGRATOR_PRBVOLPATH)
+        return prbvol_sample(sv, in, rng, r, V3(0, 0, 0), V3(0, 0, 0), NULL, valid_out, counters);
     return path_sample(sv, in, rng, r, valid_out, counters);
 }
 
@@ -1847,15 +2193,34 @@ static void *band_worker(void *arg) {
                                             fmaf(sy, inv_size(L->H), -0.f));
                         v3 dL = gather_dL(s, coalesce, j->grad_in, j->weights, sx, sy);
                         pcg32 rng_primal = rng; /* sampler.clone() */
-                        v3 Lp = prb_sample(j->sv, j->in, &rng_primal, r, V3(0, 0, 0),
-                                           V3(0, 0, 0), NULL, &valid);
-                        prb_sample(j->sv, j->in, &rng, r, dL, Lp, &j->sink, &valid);
+                        if (j->in->type == MH_INTEGRATOR_PRBVOLPATH) {
+                            v3 Lp = prbvol_sample(j->sv, j->in, &rng_primal, r, V3(0, 0, 0),
+                                                  V3(0, 0, 0), NULL, &valid, NULL);
+                            prbvol_sample(j->sv, j->in, &rng, r, dL, Lp, &j->sink, &valid, NULL);
+                        } else {
+                            v3 Lp = prb_sample(j->sv, j->in, &rng_primal, r, V3(0, 0, 0),
+                                               V3(0, 0, 0), NULL, &valid);
+                            prb_sample(j->sv, j->in, &rng, r, dL, Lp, &j->sink, &valid);
+                        }
                     }
                 }
             }
         }
     }
     return NULL;
+}
+
+/* number of gradient entries of a parameter id (texture index or MH_PARAM_*) */
+static size_t param_count(const mh_scene_desc *desc, uint32_t id) {
+    const uint32_t kind = id & MH_PARAM_KIND_MASK, idx = id & ~MH_PARAM_KIND_MASK;
+    if (kind == MH_PARAM_MEDIUM_ALBEDO) return 3;
+    if (kind == MH_PARAM_MEDIUM_SIGMA_T) {
+        const mh_medium *m = &desc->media[idx];
+        return m->type == MH_MEDIUM_HOMOGENEOUS
+                   ? 1 : (size_t)m->grid_res[0] * m->grid_res[1] * m->grid_res[2];
+    }
+    const mh_texture *tx = &desc->textures[idx];
+    return tx->type == MH_TEX_RGB ? 3 : (size_t)tx->width * tx->height * tx->channels;
 }
 
 static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kind kind,
@@ -1897,19 +2262,15 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
             j->sink.n_params = n_params;
             j->sink.tex = param_tex;
             j->sink.acc = (double **)calloc(n_params ? n_params : 1, sizeof(double *));
-            for (uint32_t k = 0; k < n_params; ++k) {
-                const mh_texture *tx = &desc->textures[param_tex[k]];
-                size_t cnt = tx->type == MH_TEX_RGB ? 3 : (size_t)tx->width * tx->height * tx->channels;
-                j->sink.acc[k] = (double *)calloc(cnt, sizeof(double));
-            }
+            for (uint32_t k = 0; k < n_params; ++k)
+                j->sink.acc[k] = (double *)calloc(param_count(desc, param_tex[k]), sizeof(double));
         }
         pthread_create(&th[t], NULL, band_worker, j);
     }
     for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
     if (kind == JOB_BACKWARD) {
         for (uint32_t k = 0; k < n_params; ++k) {
-            const mh_texture *tx = &desc->textures[param_tex[k]];
-            size_t cnt = tx->type == MH_TEX_RGB ? 3 : (size_t)tx->width * tx->height * tx->channels;
+            size_t cnt = param_count(desc, param_tex[k]);
             for (size_t c = 0; c < cnt; ++c) {
                 double sum = 0.0;
                 for (int t = 0; t < n_threads; ++t) sum += jobs[t].sink.acc[k][c];
@@ -1965,7 +2326,16 @@ int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ
                            uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
                            const float *grad_in, const float *weights, uint32_t n_params,
                            const uint32_t *param_textures, float *const *grads, int n_threads) {
-    if (integ->type != MH_INTEGRATOR_PRB) return fail("render_backward: requires the 'prb' integrator");
+    if (integ->type != MH_INTEGRATOR_PRB && integ->type != MH_INTEGRATOR_PRBVOLPATH)
+        return fail("render_backward: requires the 'prb' or 'prbvolpath' integrator");
+    for (uint32_t k = 0; k < n_params; ++k) {
+        const uint32_t kind = param_textures[k] & MH_PARAM_KIND_MASK, idx = param_textures[k] & ~MH_PARAM_KIND_MASK;
+        if (kind == 0 ? idx >= desc->n_textures
+                      : (kind != MH_PARAM_MEDIUM_SIGMA_T && kind != MH_PARAM_MEDIUM_ALBEDO) || idx >= desc->n_media)
+            return fail("render_backward: parameter index out of bounds");
+        if (kind != 0 && integ->type != MH_INTEGRATOR_PRBVOLPATH)
+            return fail("render_backward: medium parameters require the 'prbvolpath' integrator");
+    }
     const mh_sensor *s = &desc->sensor;
     float *w_local = NULL;
     if (!weights) {
