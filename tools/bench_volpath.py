@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Config 4 measurement: volpath, heterogeneous 256^3 fBm
-medium + HG, 256x256 @ 64 spp, one MI355X.  Prints one JSON line (not the
-driver's bench line: bench.py measures BASELINE.json's headline metric)."""
+medium + HG, 256x256 @ 64 spp, one MI355X.  --integrator prbvolpath times the
+§8(f) extension instead: one step = prbvolpath forward + render_backward wrt
+the sigma_t grid and the albedo.  Prints one JSON line (not the driver's
+bench line: bench.py measures BASELINE.json's headline metric)."""
 import argparse
 import json
 import os
@@ -20,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--cpu-spp", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--integrator", default="volpath", choices=["volpath", "prbvolpath"])
     a = ap.parse_args()
     import torch
     import mitsuba_hip as mi
@@ -27,8 +30,12 @@ def main():
     mi.set_variant("hip_ad_rgb")
     t0 = time.time()
     grid = mi.fbm_grid(a.grid)
-    scene = mi.load_dict(mi.volume_cube(a.res, a.res, a.spp, grid=grid))
+    d = mi.volume_cube(a.res, a.res, a.spp, grid=grid)
+    d["integrator"]["type"] = a.integrator
+    scene = mi.load_dict(d)
     t_load = time.time() - t0
+    if a.integrator == "prbvolpath":
+        return bench_prbvolpath(a, mi, A, scene, t_load)
     film = torch.empty((a.res, a.res, 4), dtype=torch.float32, device="cuda")
     st = A.Stats()
     mi.render_film(scene, seed=100, spp=a.spp, film=film, stats=st)
@@ -55,6 +62,50 @@ def main():
         tc = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": round(a.res * a.res * a.cpu_spp / tc / 1e6, 3), "unit": "Msamples/s",
                                "cores": thr, "kind": "port", "sample": f"{a.res}^2 @ {a.cpu_spp} spp, {tc:.1f} s"}
+    print(json.dumps(out), flush=True)
+
+
+def bench_prbvolpath(a, mi, A, scene, t_load):
+    import torch
+    params = mi.traverse(scene)
+    keys = ["medium1.sigma_t.data", "medium1.albedo.value"]
+    gi = torch.full((a.res, a.res, 3), 1.0 / (a.res * a.res * 3), device="cuda")
+    sf, sb = A.Stats(), A.Stats()
+
+    def step(seed):
+        film = mi.render_film(scene, seed=seed, spp=a.spp, stats=sf)
+        g = mi.render_backward(scene, params, gi, keys, seed=seed + 1, spp=a.spp, stats=sb)
+        return film, g
+
+    step(100)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kf, kb = [], []
+    for i in range(a.steps):
+        _, g = step(2 * i)
+        kf.append(sf.ms_kernel)
+        kb.append(sb.ms_kernel)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    n = a.res * a.res * a.spp
+    out = {"metric": "Msamples/s prbvolpath fwd + grad (sigma_t grid, albedo)", "value": round(n / dt / 1e6, 2),
+           "unit": "Msamples/s", "ms_per_step": round(dt * 1e3, 3),
+           "fwd_kernel_ms": round(sum(kf) / len(kf), 3), "bwd_kernel_ms": round(sum(kb) / len(kb), 3),
+           "grad_sigma_t_abs_sum": float(g[0].abs().sum()), "grad_albedo": [float(x) for x in g[1]],
+           "config": {"film": f"{a.res}x{a.res}", "spp": a.spp, "grid": f"{a.grid}^3 fBm",
+                      "scene_load_s": round(t_load, 2)}}
+    if not a.no_cpu:
+        import numpy as np
+        import oracle_py as O
+        thr = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+        integ = scene.integrator()
+        t0 = time.perf_counter()
+        O.render(scene, integ, seed=0, spp=a.cpu_spp, threads=thr)
+        O.render_backward(scene, integ, 1, a.cpu_spp, gi.cpu().numpy(), [params.param_id(k) for k in keys],
+                          [tuple(params[k].shape) for k in keys], threads=thr)
+        tc = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(a.res * a.res * a.cpu_spp / tc / 1e6, 3), "unit": "Msamples/s",
+                               "cores": thr, "kind": "port", "sample": f"{a.res}^2 @ {a.cpu_spp} spp fwd+bwd, {tc:.1f} s"}
     print(json.dumps(out), flush=True)
 
 
