@@ -407,7 +407,7 @@ class _Builder:
     def shape(self, spec, name: str):
         ty = spec.get("type")
         T = _to_transform(spec.get("to_world"))
-        if spec.get("flip_normals", False):
+        if spec.get("flip_normals", False) and ty in ("rectangle", "cube"):
             T = T @ Transform4f.scale([1.0, 1.0, -1.0])
         s = A.Shape()
         s.emitter = A.INVALID
@@ -435,22 +435,51 @@ class _Builder:
             area = np.linalg.norm(np.cross(_f32(dp_du).astype(np.float64), _f32(dp_dv).astype(np.float64)))
             s.inv_area = float(np.float32(1.0 / area))
             self._expand_bbox([T.transform_point([x, y, 0.0]) for x in (-1.0, 1.0) for y in (-1.0, 1.0)])
-        elif ty in ("cube", "mesh"):
+        elif ty in ("cube", "mesh", "obj", "ply"):
+            M = T.matrix
+            xp = lambda P: (np.asarray(P, np.float64).reshape(-1, 3) @ M[:3, :3].T + M[:3, 3])
+            IT = T.inverse_transpose[:3, :3]
+
+            def xn(Nn):
+                n = np.asarray(Nn, np.float64).reshape(-1, 3) @ IT.T
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    return n / np.linalg.norm(n, axis=1, keepdims=True)
             if ty == "cube":
                 V = np.array([T.transform_point(p) for p in _CUBE_V])
                 N = np.array([T.transform_normal(n) / np.linalg.norm(T.transform_normal(n)) for n in _CUBE_N])
                 UV = np.array(_CUBE_UV, dtype=np.float64)
                 F = np.array(_CUBE_F, dtype=np.uint32)
-            else:  # in-memory mesh: {'type': 'mesh', 'vertex_positions', 'faces', ...}
-                V = np.array([T.transform_point(p) for p in np.asarray(spec["vertex_positions"]).reshape(-1, 3)])
+            elif ty == "mesh":  # in-memory mesh: {'type': 'mesh', 'vertex_positions', 'faces', ...}
+                V = xp(spec["vertex_positions"])
                 F = np.asarray(spec["faces"], dtype=np.uint32).reshape(-1, 3)
                 N = spec.get("vertex_normals")
-                if N is not None:
-                    N = np.array([T.transform_normal(n) / np.linalg.norm(T.transform_normal(n))
-                                  for n in np.asarray(N).reshape(-1, 3)])
+                if N is not None:   # stored as given unless a to_world is applied
+                    N = xn(N) if "to_world" in spec else np.asarray(N, np.float32).reshape(-1, 3)
                 UV = spec.get("vertex_texcoords")
                 if UV is not None:
                     UV = np.asarray(UV, dtype=np.float64).reshape(-1, 2)
+            else:  # obj.cpp / ply.cpp (mitsuba_hip/meshio.py)
+                from . import meshio
+                fn = spec.get("filename")
+                if fn is None:
+                    raise RuntimeError(f'"{ty}" shape: property "filename" is required')
+                face_normals = bool(spec.get("face_normals", False))
+                rd = meshio.read_obj if ty == "obj" else meshio.read_ply
+                m = rd(fn, flip_tex_coords=bool(spec.get("flip_tex_coords", ty == "obj")), face_normals=face_normals)
+                V = _f32(xp(m["positions"])).astype(np.float64)
+                F = m["faces"]
+                if F.size and F.max() >= len(V):
+                    raise RuntimeError(f'Error while loading {ty.upper()} file: face index out of range')
+                N = xn(m["normals"]) if m["normals"] is not None else None
+                if m["recompute_normals"] and len(F):
+                    N = meshio.recompute_vertex_normals(V, F).astype(np.float64)
+                UV = m["texcoords"]
+                if spec.get("flip_normals", False):
+                    # Mesh::m_flip_normals: reversed winding flips the geometric
+                    # normal; shading normals are negated
+                    F = F[:, [0, 2, 1]].copy()
+                    if N is not None:
+                        N = -N
             s.type = A.SHAPE_MESH
             s.face_offset = self.n_faces
             s.face_count = len(F)
@@ -690,7 +719,7 @@ def load_dict(d: Dict[str, Any]):
             sensor = _sensor(v)
             if v.get("medium") is not None:
                 sensor.medium = b.medium(v["medium"], k + ".medium")
-        elif vt in ("rectangle", "cube", "mesh"):
+        elif vt in ("rectangle", "cube", "mesh", "obj", "ply"):
             b.shape(v, k)
         elif vt in ("constant", "directional"):
             b.infinite_emitter(v, k)
