@@ -26,6 +26,8 @@ from .scene import Integrator, Scene, cornell_box, gaussian_coefficients, load_d
 from .transform import ScalarTransform4f, Transform4f
 from .scenes import cornell_box_bitmap, volume_cube
 from .volume import VolumeGrid, fbm_grid
+from .xml import load_file, load_string
+from . import meshio
 
 __version__ = "0.1.0"
 MI_VERSION = "3.5.0"  # reference version this backend mirrors (include/mitsuba/mitsuba.h:11-13)
@@ -67,4 +69,5 @@ def is_available() -> bool:
 __all__ = ["set_variant", "variant", "variants", "load_dict", "cornell_box", "render", "traverse",
            "render_backward", "render_film", "develop", "prb_weights", "SceneParameters", "Scene",
            "Integrator", "Transform4f", "ScalarTransform4f", "sample_tea_32", "MitsubaHipError",
-           "gaussian_coefficients", "is_available", "volume_cube", "cornell_box_bitmap", "VolumeGrid", "fbm_grid"]
+           "gaussian_coefficients", "is_available", "volume_cube", "cornell_box_bitmap", "VolumeGrid", "fbm_grid",
+           "load_file", "load_string", "meshio"]
