@@ -68,6 +68,7 @@ enum { MH_BSDF_DIFFUSE = 0, MH_BSDF_NULL = 1 };               /* diffuse.cpp, nu
 enum { MH_TEX_RGB = 0, MH_TEX_BITMAP = 1 };                   /* srgb.cpp, bitmap.cpp */
 enum { MH_EMITTER_AREA = 0, MH_EMITTER_CONSTANT = 1, MH_EMITTER_DIRECTIONAL = 2 };
 enum { MH_RFILTER_BOX = 0, MH_RFILTER_GAUSSIAN = 1 };         /* box.cpp, gaussian.cpp */
+enum { MH_PIXEL_RGB = 0, MH_PIXEL_Y = 1, MH_PIXEL_XYZ = 2 };   /* Bitmap::PixelFormat rgb / luminance / xyz */
 enum { MH_MEDIUM_HETEROGENEOUS = 0, MH_MEDIUM_HOMOGENEOUS = 1 };
 enum { MH_PHASE_ISOTROPIC = 0, MH_PHASE_HG = 1 };
 enum { MH_MEDIUM_NO_EMITTER_SAMPLING = 1u,        /* medium.cpp:29 sample_emitters = false */
@@ -175,7 +176,7 @@ typedef struct mh_sensor {
     uint32_t sample_count;      /* sampler.sample_count */
     uint32_t sampler_seed;      /* sampler base seed ('seed' property, default 0) */
     uint32_t medium;            /* camera medium index or MH_INVALID */
-    uint32_t pad0;
+    uint32_t pixel_format;      /* MH_PIXEL_*: hdrfilm 'pixel_format' of mh_develop's output */
 } mh_sensor;
 
 typedef struct mh_scene_desc {
@@ -274,7 +275,9 @@ int mh_render_samples(mh_scene *scene, const mh_integrator *integrator, uint32_t
                       uint32_t spp, uint32_t spp_begin, uint32_t spp_end, float *out,
                       uint32_t flags);
 
-/* RGBW film -> RGB image (H*W*3): rgb / (w == 0 ? 1 : w). */
+/* RGBW film -> developed image (HDRFilm::develop, hdrfilm.cpp:304-405):
+ * H*W*3 for MH_PIXEL_RGB (rgb / w) and MH_PIXEL_XYZ (srgb_to_xyz(rgb) / w),
+ * H*W*1 for MH_PIXEL_Y (luminance(rgb) / w); w == 0 divides by 1. */
 int mh_develop(mh_scene *scene, const float *film_rgbw, float *image_rgb, uint32_t flags);
 
 /*

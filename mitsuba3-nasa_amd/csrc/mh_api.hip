@@ -92,7 +92,7 @@ struct mh_scene {
     std::vector<DTexture> h_textures;
     std::vector<mh_medium> h_media;
     std::vector<DMedium> h_dmedia;
-    uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0, n_media = 0;
+    uint32_t n_textures = 0, n_bsdfs = 0, n_shapes = 0, n_media = 0, pixel_format = MH_PIXEL_RGB;
     uint64_t n_texels = 0;
     uint32_t bvh_nodes = 0, bvh_prims = 0, bvh_depth = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -273,6 +273,9 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         if (a.phase == MH_PHASE_HG && !(a.g > -1.f && a.g < 1.f))
             return fail(MH_ERR_INVALID_ARGUMENT, "The asymmetry parameter must lie in the interval (-1, 1)!");
     }
+    if (desc->sensor.pixel_format > MH_PIXEL_XYZ)
+        return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: unknown pixel format");
+    s->pixel_format = desc->sensor.pixel_format;
     s->h_media.assign(desc->media, desc->media + desc->n_media);
     s->h_dmedia = meds;
     s->n_media = desc->n_media;
@@ -707,16 +710,17 @@ int mh_develop(mh_scene *s, const float *film_rgbw, float *image_rgb, uint32_t f
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)s->S.width * s->S.height;
+    const uint32_t fmt = s->pixel_format, ch = fmt == MH_PIXEL_Y ? 1 : 3;
     if (flags & MH_FLAG_DEVICE_POINTERS) {
-        MH_HIP(launch_develop(n_px, film_rgbw, image_rgb, st));
+        MH_HIP(launch_develop(n_px, film_rgbw, image_rgb, fmt, st));
         if (!(flags & MH_FLAG_NO_SYNC)) MH_HIP(hipStreamSynchronize(st));
         return MH_OK;
     }
     MH_HIP(s->tmp_a.alloc(n_px * 16));
-    MH_HIP(s->tmp_b.alloc(n_px * 12));
+    MH_HIP(s->tmp_b.alloc(n_px * 4 * ch));
     MH_HIP(hipMemcpyAsync(s->tmp_a.ptr, film_rgbw, n_px * 16, hipMemcpyHostToDevice, st));
-    MH_HIP(launch_develop(n_px, s->tmp_a.as<float>(), s->tmp_b.as<float>(), st));
-    MH_HIP(hipMemcpyAsync(image_rgb, s->tmp_b.ptr, n_px * 12, hipMemcpyDeviceToHost, st));
+    MH_HIP(launch_develop(n_px, s->tmp_a.as<float>(), s->tmp_b.as<float>(), fmt, st));
+    MH_HIP(hipMemcpyAsync(image_rgb, s->tmp_b.ptr, n_px * 4 * ch, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
     return MH_OK;
 }

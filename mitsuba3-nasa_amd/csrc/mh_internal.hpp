@@ -85,7 +85,7 @@ inline float ordered_key_to_float(uint32_t k) {
 }
 hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream_t st);  // dst += src
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
-hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st);
+hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
                                const float *grad_in, const float *weights, const GradArgs &ga,

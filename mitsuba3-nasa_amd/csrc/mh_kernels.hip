@@ -315,15 +315,28 @@ __global__ void k_grad_over_w(uint64_t n_px, const float *__restrict__ grad_in, 
     out[3 * i + 2] = grad_in[3 * i + 2] / Wp;
 }
 
-// HDRFilm::develop (films/hdrfilm.cpp:349-405)
-__global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *__restrict__ rgb) {
+// HDRFilm::develop (films/hdrfilm.cpp:349-405): rgb / w, or luminance(rgb) / w
+// (spectrum.h:431-434), or srgb_to_xyz(rgb) / w (spectrum.h:396-402, matrix
+// product as column fmadds)
+template <int Fmt>
+__global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_px) return;
     float4 v = reinterpret_cast<const float4 *>(film)[i];
     float d = v.w == 0.f ? 1.f : v.w;
-    rgb[3 * i] = v.x / d;
-    rgb[3 * i + 1] = v.y / d;
-    rgb[3 * i + 2] = v.z / d;
+    if (Fmt == MH_PIXEL_Y) {
+        out[i] = ((v.x * 0.212671f + v.y * 0.715160f) + v.z * 0.072169f) / d;
+        return;
+    }
+    float a = v.x, b = v.y, c = v.z;
+    if (Fmt == MH_PIXEL_XYZ) {
+        a = __builtin_fmaf(0.180423f, v.z, __builtin_fmaf(0.357580f, v.y, 0.412453f * v.x));
+        b = __builtin_fmaf(0.072169f, v.z, __builtin_fmaf(0.715160f, v.y, 0.212671f * v.x));
+        c = __builtin_fmaf(0.950227f, v.z, __builtin_fmaf(0.119193f, v.y, 0.019334f * v.x));
+    }
+    out[3 * i] = a / d;
+    out[3 * i + 1] = b / d;
+    out[3 * i + 2] = c / d;
 }
 
 // small (register-accumulated) gradient slots: wave butterfly, then one
@@ -539,9 +552,12 @@ hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, hipStream_t st) {
+hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st) {
     if (n_px == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_develop, dim3(blocks_for(n_px, 256)), dim3(256), 0, st, n_px, film, rgb);
+    const dim3 g(blocks_for(n_px, 256)), b(256);
+    if (fmt == MH_PIXEL_Y) hipLaunchKernelGGL(k_develop<MH_PIXEL_Y>, g, b, 0, st, n_px, film, rgb);
+    else if (fmt == MH_PIXEL_XYZ) hipLaunchKernelGGL(k_develop<MH_PIXEL_XYZ>, g, b, 0, st, n_px, film, rgb);
+    else hipLaunchKernelGGL(k_develop<MH_PIXEL_RGB>, g, b, 0, st, n_px, film, rgb);
     return hipGetLastError();
 }
 

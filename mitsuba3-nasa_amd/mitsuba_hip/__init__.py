@@ -27,7 +27,8 @@ from .transform import ScalarTransform4f, Transform4f
 from .scenes import cornell_box_bitmap, volume_cube
 from .volume import VolumeGrid, fbm_grid
 from .xml import load_file, load_string
-from . import meshio
+from . import meshio, imageio, util
+from .imageio import write_bitmap, read_bitmap
 
 __version__ = "0.1.0"
 MI_VERSION = "3.5.0"  # reference version this backend mirrors (include/mitsuba/mitsuba.h:11-13)
@@ -70,4 +71,5 @@ __all__ = ["set_variant", "variant", "variants", "load_dict", "cornell_box", "re
            "render_backward", "render_film", "develop", "prb_weights", "SceneParameters", "Scene",
            "Integrator", "Transform4f", "ScalarTransform4f", "sample_tea_32", "MitsubaHipError",
            "gaussian_coefficients", "is_available", "volume_cube", "cornell_box_bitmap", "VolumeGrid", "fbm_grid",
-           "load_file", "load_string", "meshio"]
+           "load_file", "load_string", "meshio", "imageio",
+           "write_bitmap", "read_bitmap"]

@@ -21,6 +21,7 @@ BSDF_DIFFUSE, BSDF_NULL = 0, 1
 TEX_RGB, TEX_BITMAP = 0, 1
 EMITTER_AREA, EMITTER_CONSTANT, EMITTER_DIRECTIONAL = 0, 1, 2
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
+PIXEL_RGB, PIXEL_Y, PIXEL_XYZ = 0, 1, 2
 MEDIUM_HETEROGENEOUS, MEDIUM_HOMOGENEOUS = 0, 1
 PHASE_ISOTROPIC, PHASE_HG = 0, 1
 MEDIUM_NO_EMITTER_SAMPLING, MEDIUM_NO_SPECTRAL_EXTINCTION = 1, 2
@@ -78,7 +79,7 @@ class Sensor(C.Structure):
     _fields_ = [("to_world", f32 * 16), ("sample_to_camera", f32 * 16), ("near_clip", f32),
                 ("far_clip", f32), ("width", u32), ("height", u32), ("rfilter", u32),
                 ("rfilter_radius", f32), ("filter_coeff", f32 * 10), ("sample_count", u32),
-                ("sampler_seed", u32), ("medium", u32), ("pad0", u32)]
+                ("sampler_seed", u32), ("medium", u32), ("pixel_format", u32)]
 
 
 class SceneDesc(C.Structure):

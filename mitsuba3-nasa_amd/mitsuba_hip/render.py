@@ -192,7 +192,8 @@ def develop(scene: Scene, film, device=None):
     torch = _torch()
     dev = film.device.index or 0
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
-    out = torch.empty((scene.height, scene.width, 3), dtype=torch.float32, device=film.device)
+    ch = 1 if scene.desc.sensor.pixel_format == A.PIXEL_Y else 3
+    out = torch.empty((scene.height, scene.width, ch), dtype=torch.float32, device=film.device)
     A.check(A.lib().mh_develop(h, _ptr(film.contiguous()), _ptr(out), A.FLAG_DEVICE_POINTERS))
     return out
 
@@ -204,6 +205,24 @@ def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, devic
     w = torch.empty((scene.height, scene.width), dtype=torch.float32, device=f"cuda:{dev}")
     A.check(A.lib().mh_prb_weights(h, seed, spp, spp_begin, spp_end, _ptr(w), A.FLAG_DEVICE_POINTERS))
     return w
+
+
+# srgb_to_xyz (spectrum.h:396-402); row 1 is luminance (spectrum.h:431-434)
+_SRGB_TO_XYZ = [[0.412453, 0.357580, 0.180423], [0.212671, 0.715160, 0.072169], [0.019334, 0.119193, 0.950227]]
+
+
+def _grad_to_rgb(scene: Scene, grad_in):
+    """Adjoint of the develop colour conversion: d loss / d (weighted rgb)
+    from d loss / d image for luminance / xyz films (the 1/W factor is
+    applied by mh_render_backward)."""
+    torch = _torch()
+    fmt = scene.desc.sensor.pixel_format
+    if fmt == A.PIXEL_RGB:
+        return grad_in
+    M = torch.tensor(_SRGB_TO_XYZ, dtype=torch.float32, device=grad_in.device)
+    if fmt == A.PIXEL_Y:
+        return grad_in.reshape(scene.height, scene.width, 1) * M[1]
+    return grad_in.reshape(scene.height, scene.width, 3) @ M
 
 
 def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],
@@ -223,7 +242,7 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     spp = spp or scene.sample_count()
     dev = grad_in.device.index or 0
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
-    grad_in = grad_in.to(torch.float32).contiguous()
+    grad_in = _grad_to_rgb(scene, grad_in.to(torch.float32)).contiguous()
     tex = (C.c_uint32 * max(len(keys), 1))(*[params.param_id(k) for k in keys])
     outs = [torch.zeros(params[k].shape, dtype=torch.float32, device=grad_in.device) for k in keys]
     ptrs = (C.c_void_p * max(len(keys), 1))(*[o.data_ptr() for o in outs])

@@ -214,8 +214,15 @@ class _Builder:
             self.params[key_prefix + ".value"] = ("rgb", idx)
         elif ty == "bitmap":
             data = spec.get("data")
+            if data is None and "filename" in spec:   # bitmap.cpp: file images (mitsuba_hip/imageio.py)
+                from .imageio import read_bitmap
+                data = read_bitmap(spec["filename"], raw=bool(spec.get("raw", False)))
+                if data.shape[2] == 4:
+                    data = data[..., :3]
+                elif data.shape[2] == 2:
+                    data = data[..., :1]
             if data is None:
-                raise RuntimeError("bitmap: only in-memory 'data' tensors are supported by this loader")
+                raise RuntimeError("bitmap: specify 'data' or 'filename'")
             arr = np.asarray(data, dtype=np.float32)
             if arr.ndim == 2:
                 arr = arr[:, :, None]
@@ -647,13 +654,16 @@ def _sensor(spec: Dict[str, Any]) -> A.Sensor:
     if film.get("type", "hdrfilm") != "hdrfilm":
         raise RuntimeError(f'Film plugin "{film.get("type")}" is not available in the hip_ad_rgb variant')
     W, H = int(film.get("width", 768)), int(film.get("height", 576))
-    pf = film.get("pixel_format", "rgb")
-    if pf != "rgb":
-        raise RuntimeError(f'hdrfilm: pixel_format "{pf}" is not available in the hip_ad_rgb variant (rgb only)')
+    pf = film.get("pixel_format", "rgb").lower()
+    pix = {"rgb": A.PIXEL_RGB, "luminance": A.PIXEL_Y, "xyz": A.PIXEL_XYZ}.get(pf)
+    if pix is None:
+        raise RuntimeError(f'hdrfilm: pixel_format "{pf}" is not available in the hip_ad_rgb variant '
+                           '(rgb, luminance, xyz; alpha films are not)')
     if "crop_offset_x" in film or "crop_width" in film:
         raise RuntimeError("hdrfilm: crop windows are not available in the hip_ad_rgb variant")
     rf = film.get("rfilter", {"type": "gaussian"})
     s = A.Sensor()
+    s.pixel_format = pix
     if rf.get("type", "gaussian") == "gaussian":
         coeff, radius = gaussian_coefficients(float(rf.get("stddev", 0.5)))
         s.rfilter = A.RFILTER_GAUSSIAN

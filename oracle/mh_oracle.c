@@ -347,11 +347,28 @@ static void splat(const mh_sensor *s, film_band *f, float px, float py, const fl
 
 /* HDRFilm::develop (src/films/hdrfilm.cpp:349-405) */
 void oracle_develop(uint32_t w, uint32_t h, const float *film, float *rgb) {
+    oracle_develop_format(w, h, MH_PIXEL_RGB, film, rgb);
+}
+
+/* HDRFilm::develop (hdrfilm.cpp:313-401): luminance / srgb_to_xyz of the
+   weighted sums (spectrum.h:396-402, 431-434), then the weight division */
+void oracle_develop_format(uint32_t w, uint32_t h, uint32_t fmt, const float *film, float *out) {
     size_t n = (size_t)w * h;
     for (size_t i = 0; i < n; ++i) {
-        float W = film[4 * i + 3];
+        const float *v = film + 4 * i;
+        float W = v[3];
         float d = (W == 0.f) ? 1.f : W;
-        for (int c = 0; c < 3; ++c) rgb[3 * i + c] = film[4 * i + c] / d;
+        if (fmt == MH_PIXEL_Y) {
+            out[i] = ((v[0] * 0.212671f + v[1] * 0.715160f) + v[2] * 0.072169f) / d;
+            continue;
+        }
+        float c[3] = {v[0], v[1], v[2]};
+        if (fmt == MH_PIXEL_XYZ) {
+            c[0] = fmaf(0.180423f, v[2], fmaf(0.357580f, v[1], 0.412453f * v[0]));
+            c[1] = fmaf(0.072169f, v[2], fmaf(0.715160f, v[1], 0.212671f * v[0]));
+            c[2] = fmaf(0.950227f, v[2], fmaf(0.119193f, v[1], 0.019334f * v[0]));
+        }
+        for (int k = 0; k < 3; ++k) out[3 * i + k] = c[k] / d;
     }
 }
 

@@ -66,6 +66,7 @@ int oracle_render(const mh_scene_desc *desc, const mh_integrator *integ, uint32_
                   uint32_t spp, uint32_t spp_begin, uint32_t spp_end, int n_threads,
                   float *film_rgbw);
 void oracle_develop(uint32_t w, uint32_t h, const float *film_rgbw, float *rgb);
+void oracle_develop_format(uint32_t w, uint32_t h, uint32_t pixel_format, const float *film_rgbw, float *out);
 
 /* PRB: per-pixel filter-weight image W (H*W) of the backward pass. */
 int oracle_prb_weights(const mh_scene_desc *desc, uint32_t seed, uint32_t spp,

@@ -46,6 +46,7 @@ def lib():
     L.oracle_render.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32, C.c_uint32,
                                 C.c_uint32, C.c_uint32, C.c_int, vp]
     L.oracle_develop.argtypes = [C.c_uint32, C.c_uint32, vp, vp]
+    L.oracle_develop_format.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]
     L.oracle_prb_weights.argtypes = [C.POINTER(A.SceneDesc), C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.c_int, vp]
     L.oracle_render_backward.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32,
@@ -78,10 +79,10 @@ def render(scene, integrator=None, seed=0, spp=0, spp_begin=0, spp_end=0, thread
     return film
 
 
-def develop(film):
+def develop(film, pixel_format=0):
     h, w = film.shape[:2]
-    out = np.zeros((h, w, 3), np.float32)
-    lib().oracle_develop(w, h, _p(np.ascontiguousarray(film)), _p(out))
+    out = np.zeros((h, w, 1 if pixel_format == 1 else 3), np.float32)
+    lib().oracle_develop_format(w, h, pixel_format, _p(np.ascontiguousarray(film)), _p(out))
     return out
 
 

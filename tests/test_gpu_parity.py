@@ -406,3 +406,37 @@ def test_multi_emitter_prb_backward_parity():
         g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=21, spp=8, mode=mode)
         for a, b in zip(g, ref):
             np.testing.assert_allclose(a.cpu().numpy(), b, rtol=1e-3, atol=1e-7)
+
+
+# ---------------------------------------------------------------------------
+# hdrfilm pixel formats: luminance / xyz develop,
+# and the PRB adjoint through the colour conversion
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("pf", ["rgb", "luminance", "xyz"])
+def test_develop_pixel_format_parity(pf):
+    mi = _mi()
+    d = mi.cornell_box()
+    d["sensor"]["film"].update(width=24, height=20, pixel_format=pf)
+    scene = mi.load_dict(d)
+    film = mi.render_film(scene, seed=1, spp=8)
+    img = mi.develop(scene, film).cpu().numpy()
+    ref = O.develop(film.cpu().numpy(), scene.desc.sensor.pixel_format)
+    assert img.shape == ref.shape
+    np.testing.assert_array_equal(img, ref)
+
+
+def test_prb_backward_luminance_film():
+    """d(sum Y)/d rho through a luminance film == the rgb adjoint with
+    grad_rgb = [0.212671, 0.715160, 0.072169] per pixel."""
+    mi = _mi()
+    import torch
+    d = mi.cornell_box()
+    d["sensor"]["film"].update(width=24, height=20, pixel_format="luminance")
+    scene = mi.load_dict(d)
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    gy = torch.ones((20, 24, 1), device="cuda")
+    g = mi.render_backward(scene, params, gy, ["white.reflectance.value"], integ, seed=3, spp=8)[0].cpu().numpy()
+    grgb = np.broadcast_to(np.array([0.212671, 0.715160, 0.072169], np.float32), (20, 24, 3)).copy()
+    ref = O.render_backward(scene, integ, 3, 8, grgb, [params.texture_of("white.reflectance.value")], [(3,)])[0]
+    np.testing.assert_allclose(g, ref, rtol=1e-3)
