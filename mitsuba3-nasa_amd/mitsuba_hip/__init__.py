@@ -20,14 +20,14 @@ from __future__ import annotations
 
 from . import _abi
 from ._abi import MitsubaHipError
-from .render import (SceneParameters, develop, prb_weights, render, render_backward,
+from .render import (SceneParameters, develop, prb_weights, render, render_1, render_backward,
                      render_film, sample_tea_32, traverse)
 from .scene import Integrator, Scene, cornell_box, gaussian_coefficients, load_dict
 from .transform import ScalarTransform4f, Transform4f
 from .scenes import cornell_box_bitmap, volume_cube
 from .volume import VolumeGrid, fbm_grid
 from .xml import load_file, load_string
-from . import meshio, imageio, util
+from . import meshio, imageio, util, ad
 from .imageio import write_bitmap, read_bitmap
 
 __version__ = "0.1.0"
@@ -72,4 +72,4 @@ __all__ = ["set_variant", "variant", "variants", "load_dict", "cornell_box", "re
            "Integrator", "Transform4f", "ScalarTransform4f", "sample_tea_32", "MitsubaHipError",
            "gaussian_coefficients", "is_available", "volume_cube", "cornell_box_bitmap", "VolumeGrid", "fbm_grid",
            "load_file", "load_string", "meshio", "imageio",
-           "write_bitmap", "read_bitmap"]
+           "write_bitmap", "read_bitmap", "ad", "render_1"]

@@ -306,3 +306,11 @@ def render(scene: Scene, params: Optional[SceneParameters] = None, sensor: int =
         return develop(scene, film)
     values = [params[k] for k in keys]
     return _render_op().apply(scene, params, keys, integrator, (seed, seed_grad), (spp, spp_grad), *values)
+
+
+def render_1(scene: Scene, sensor: int = 0, seed: int = 0, spp: int = 0, integrator: Optional[Integrator] = None):
+    """SamplingIntegrator::render_1 (integrator.cpp:398-743), the fork's
+    radiance-meter loop.  The reference only implements it for monochromatic
+    and spectral variants; in an RGB variant (hip_ad_rgb mirrors llvm_ad_rgb)
+    it raises the same error."""
+    raise A.MitsubaHipError("This render loop only supports monochromatic and spectral modes!")

@@ -440,3 +440,38 @@ def test_prb_backward_luminance_film():
     grgb = np.broadcast_to(np.array([0.212671, 0.715160, 0.072169], np.float32), (20, 24, 3)).copy()
     ref = O.render_backward(scene, integ, 3, 8, grgb, [params.texture_of("white.reflectance.value")], [(3,)])[0]
     np.testing.assert_allclose(g, ref, rtol=1e-3)
+
+
+# ---------------------------------------------------------------------------
+# The optimisation loop around the path:
+# mi.render -> loss.backward (PRB render_backward) -> mi.ad.Adam -> update
+# ---------------------------------------------------------------------------
+def test_inverse_rendering_loop_recovers_albedo():
+    mi = _mi()
+    import torch
+    d = mi.cornell_box()
+    d["sensor"]["film"].update(width=32, height=32)
+    d["integrator"] = {"type": "prb", "max_depth": 4}
+    scene = mi.load_dict(d)
+    key = "red.reflectance.value"
+    params = mi.traverse(scene, device="cuda")
+    target = params[key].clone()
+    ref = mi.render(scene, seed=100, spp=128)
+    params[key] = torch.tensor([0.2, 0.2, 0.2], device="cuda")
+    params.update()
+    opt = mi.ad.Adam(lr=0.05)
+    opt[key] = params[key]
+    params.update(opt)
+    err0 = float((params[key] - target).abs().max())
+    losses = []
+    for it in range(40):
+        img = mi.render(scene, params, seed=it, spp=16)
+        loss = ((img - ref) ** 2).mean()
+        loss.backward()
+        opt.step()
+        opt[key] = opt[key].detach().clamp(0.0, 1.0)
+        params.update(opt)
+        losses.append(float(loss))
+    err = float((params[key].detach() - target).abs().max())
+    assert np.mean(losses[-5:]) < 0.25 * np.mean(losses[:3]), losses
+    assert err < 0.35 * err0, (err, err0, params[key])
