@@ -51,6 +51,9 @@ struct WfState {
 // spot (MI355X_MICROARCH.md "dequeue": one word saturates at ~88 ops/us).
 // Per bounce: kSeg x 32 uint32: [s*32 + 0] queue length, [s*32 + 1] shadow length.
 constexpr uint32_t kSeg = 64;
+#ifndef MH_BOUNCE_WAVES
+#define MH_BOUNCE_WAVES 4  // fused bounce kernels: waves per SIMD the register budget targets
+#endif
 constexpr uint32_t kCtrStride = kSeg * 32;
 constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
 
@@ -376,7 +379,7 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
 // one wave overlapping the state streams of the others.
 // LDS: shading tables (tab_bytes) + one traversal stack per wave.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 4)
+__global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane, float *out,
             WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     extern __shared__ uint4 lds[];
@@ -849,7 +852,7 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
 // k_wf_trace -> k_wf_shade_prb -> k_wf_shadow_prb; only the order in which
 // the per-thread gradient registers accumulate differs).
 template <int NR>
-__global__ void __launch_bounds__(256, 4)
+__global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
                 int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
     extern __shared__ uint4 lds[];

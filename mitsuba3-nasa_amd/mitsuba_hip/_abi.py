@@ -115,7 +115,8 @@ EXPORTS = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmitsuba_hip.so")
+# MH_LIB selects an alternative build of the same library (A/B experiments, tools/)
+LIB_PATH = os.environ.get("MH_LIB") or os.path.join(_HERE, "libmitsuba_hip.so")
 _lib = None
 
 
