@@ -262,7 +262,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         b.maj = a.type == MH_MEDIUM_HOMOGENEOUS ? a.sigma_t_const * a.scale : a.scale * a.max_density;
         memcpy(b.albedo, a.albedo, 12);
         memcpy(b.res, a.grid_res, 12);
-        b.grid_offset = a.grid_offset;
+        b.grid_offset = 0;   // bricked offset: assigned below
         memcpy(b.to_local, a.grid_to_local, sizeof(b.to_local));
         memcpy(b.bbox_min, a.bbox_min, 12);
         memcpy(b.bbox_max, a.bbox_max, 12);
@@ -276,6 +276,15 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     if (desc->sensor.pixel_format > MH_PIXEL_XYZ)
         return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: unknown pixel format");
     s->pixel_format = desc->sensor.pixel_format;
+    // density grids in the 4^3-brick device layout (grid_index)
+    std::vector<float> bricked;
+    for (uint32_t i = 0; i < desc->n_media; ++i) {
+        if (desc->media[i].type != MH_MEDIUM_HETEROGENEOUS) continue;
+        meds[i].grid_offset = bricked.size();
+        bricked.resize(bricked.size() + grid_bricked_size(desc->media[i].grid_res));
+        grid_to_bricks(desc->grid_data + desc->media[i].grid_offset, desc->media[i].grid_res,
+                       bricked.data() + meds[i].grid_offset);
+    }
     s->h_media.assign(desc->media, desc->media + desc->n_media);
     s->h_dmedia = meds;
     s->n_media = desc->n_media;
@@ -326,7 +335,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
               upload(s->faces, desc->faces, 3ull * desc->n_faces, st) == hipSuccess &&
               upload(s->texels, desc->texels, desc->n_texels, st) == hipSuccess &&
               upload(s->media, meds.data(), meds.size(), st) == hipSuccess &&
-              upload(s->grid, desc->grid_data, desc->n_grid, st) == hipSuccess &&
+              upload(s->grid, bricked.data(), bricked.size(), st) == hipSuccess &&
               s->counters.alloc(64) == hipSuccess;
     if (!ok) return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: device upload failed");
 
@@ -478,11 +487,14 @@ int mh_scene_update_medium(mh_scene *s, uint32_t medium, const float *albedo, co
             return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: grid of a homogeneous medium");
         if (n != (uint64_t)a.grid_res[0] * a.grid_res[1] * a.grid_res[2])
             return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_update_medium: size mismatch");
-        float *dst = s->grid.as<float>() + a.grid_offset;
-        MH_HIP(hipMemcpyAsync(dst, grid, n * 4, (flags & MH_FLAG_DEVICE_POINTERS) ? hipMemcpyDeviceToDevice
+        // linear copy on the device (staging), then the max and the brick scatter
+        MH_HIP(s->tmp_e.alloc(n * 4));
+        float *lin = s->tmp_e.as<float>();
+        MH_HIP(hipMemcpyAsync(lin, grid, n * 4, (flags & MH_FLAG_DEVICE_POINTERS) ? hipMemcpyDeviceToDevice
                                                                                  : hipMemcpyHostToDevice, s->stream));
+        MH_HIP(launch_grid_to_bricks(lin, a.grid_res, s->grid.as<float>() + b.grid_offset, s->stream));
         MH_HIP(s->tmp_b.alloc(16));
-        MH_HIP(launch_grid_max(dst, n, s->tmp_b.as<uint32_t>(), s->stream));
+        MH_HIP(launch_grid_max(lin, n, s->tmp_b.as<uint32_t>(), s->stream));
         uint32_t key = 0;
         MH_HIP(hipMemcpyAsync(&key, s->tmp_b.ptr, 4, hipMemcpyDeviceToHost, s->stream));
         MH_HIP(hipStreamSynchronize(s->stream));

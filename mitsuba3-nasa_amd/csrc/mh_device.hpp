@@ -64,7 +64,7 @@ struct DMedium {
     float g, scale, maj, sigma_t_const;   // maj = scale * max(grid) (heterogeneous.cpp:163)
     float albedo[4];
     uint32_t res[4];
-    uint64_t grid_offset, pad1;
+    uint64_t grid_offset, pad1;   // grid_offset: first float of the medium's bricked grid (grid_index)
     float to_local[12];
     float bbox_min[4], bbox_max[4];
 };

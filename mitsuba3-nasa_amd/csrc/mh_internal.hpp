@@ -83,6 +83,10 @@ inline float ordered_key_to_float(uint32_t k) {
     c.u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
     return c.f;
 }
+// linear (z, y, x) grid -> 4^3-brick device layout (grid_index, mh_shading.hpp)
+uint64_t grid_bricked_size(const uint32_t res[3]);
+void grid_to_bricks(const float *src, const uint32_t res[3], float *dst);
+hipError_t launch_grid_to_bricks(const float *src, const uint32_t res[3], float *dst, hipStream_t st);
 hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream_t st);  // dst += src
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st);

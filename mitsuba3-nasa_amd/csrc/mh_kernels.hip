@@ -546,6 +546,37 @@ __global__ void k_accumulate(float *__restrict__ dst, const float *__restrict__ 
     if (i < n) dst[i] += src[i];
 }
 
+uint64_t grid_bricked_size(const uint32_t res[3]) {
+    return (uint64_t)((res[0] + 3) / 4) * ((res[1] + 3) / 4) * ((res[2] + 3) / 4) * 64u;
+}
+
+void grid_to_bricks(const float *src, const uint32_t res[3], float *dst) {
+    const int32_t rx = (int32_t)res[0], ry = (int32_t)res[1], rz = (int32_t)res[2];
+    std::fill(dst, dst + grid_bricked_size(res), 0.f);
+    for (int32_t z = 0; z < rz; ++z)
+        for (int32_t y = 0; y < ry; ++y)
+            for (int32_t x = 0; x < rx; ++x)
+                dst[grid_index(x, y, z, rx, ry)] = src[((uint64_t)z * ry + y) * rx + x];
+}
+
+__global__ void k_grid_to_bricks(const float *__restrict__ src, int32_t rx, int32_t ry, int32_t rz,
+                                 float *__restrict__ dst) {
+    const uint64_t n = (uint64_t)rx * ry * rz;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t x = (int32_t)(i % rx), y = (int32_t)((i / rx) % ry), z = (int32_t)(i / ((uint64_t)rx * ry));
+        dst[grid_index(x, y, z, rx, ry)] = src[i];
+    }
+}
+
+hipError_t launch_grid_to_bricks(const float *src, const uint32_t res[3], float *dst, hipStream_t st) {
+    const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (uint32_t)std::min<uint64_t>(blocks_for(n, 256), 4096);
+    hipLaunchKernelGGL(k_grid_to_bricks, dim3(g), dim3(256), 0, st, src, (int32_t)res[0], (int32_t)res[1],
+                       (int32_t)res[2], dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_accumulate, dim3(blocks_for(n, 256)), dim3(256), 0, st, dst, src, n);

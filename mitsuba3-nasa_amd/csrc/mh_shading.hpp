@@ -1389,6 +1389,18 @@ struct MEI {
     V3 fs, ft, fn;   // Frame3f(ray.d); wi = (0, 0, -1) local
 };
 
+// Device layout of a density grid: 4x4x4 bricks of 64 floats (256 B), bricks
+// x-fastest, texels x-fastest inside a brick.  The 8 taps of a trilinear
+// lookup then fall in one brick 27/64 of the time (never in more than 8)
+// instead of always spanning 4 rows 1 KiB / 256 KiB apart, and the lookups
+// along a ray walk neighbouring bricks.  Values are unchanged (bit-exact);
+// the host API and gradients keep the reference's linear (z, y, x) layout.
+__host__ __device__ __forceinline__ uint64_t grid_index(int32_t x, int32_t y, int32_t z, int32_t rx, int32_t ry) {
+    const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2;
+    const uint64_t brick = ((uint64_t)((uint32_t)z >> 2) * nby + ((uint32_t)y >> 2)) * nbx + ((uint32_t)x >> 2);
+    return brick * 64u + ((((uint32_t)z & 3u) << 4) | (((uint32_t)y & 3u) << 2) | ((uint32_t)x & 3u));
+}
+
 // [drjit] Texture3f::eval_nonaccel, linear, clamp, 1 channel (grid.cpp:545-558)
 MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     V3 q = xf_point(m.to_local, p);
@@ -1402,11 +1414,10 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     const int32_t y0 = min(max(iy, 0), ry - 1), y1 = min(max(iy + 1, 0), ry - 1);
     const int32_t z0 = min(max(iz, 0), rz - 1), z1 = min(max(iz + 1, 0), rz - 1);
     const float *g = S.grid + m.grid_offset;
-    const uint64_t sy = (uint64_t)rx, sz = (uint64_t)rx * (uint64_t)ry;
-    const uint64_t b00 = (uint64_t)z0 * sz + (uint64_t)y0 * sy, b10 = (uint64_t)z0 * sz + (uint64_t)y1 * sy;
-    const uint64_t b01 = (uint64_t)z1 * sz + (uint64_t)y0 * sy, b11 = (uint64_t)z1 * sz + (uint64_t)y1 * sy;
-    float v000 = g[b00 + x0], v100 = g[b00 + x1], v010 = g[b10 + x0], v110 = g[b10 + x1];
-    float v001 = g[b01 + x0], v101 = g[b01 + x1], v011 = g[b11 + x0], v111 = g[b11 + x1];
+    float v000 = g[grid_index(x0, y0, z0, rx, ry)], v100 = g[grid_index(x1, y0, z0, rx, ry)];
+    float v010 = g[grid_index(x0, y1, z0, rx, ry)], v110 = g[grid_index(x1, y1, z0, rx, ry)];
+    float v001 = g[grid_index(x0, y0, z1, rx, ry)], v101 = g[grid_index(x1, y0, z1, rx, ry)];
+    float v011 = g[grid_index(x0, y1, z1, rx, ry)], v111 = g[grid_index(x1, y1, z1, rx, ry)];
     float f00 = __builtin_fmaf(w0x, v000, w1x * v100), f01 = __builtin_fmaf(w0x, v001, w1x * v101),
           f10 = __builtin_fmaf(w0x, v010, w1x * v110), f11 = __builtin_fmaf(w0x, v011, w1x * v111);
     float f0 = __builtin_fmaf(w0y, f00, w1y * f10), f1 = __builtin_fmaf(w0y, f01, w1y * f11);

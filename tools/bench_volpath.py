@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=4)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--integrator", default="volpath", choices=["volpath", "prbvolpath"])
+    ap.add_argument("--no-nee", action="store_true", help="medium sample_emitters = false (diagnostic)")
     a = ap.parse_args()
     import torch
     import mitsuba_hip as mi
@@ -32,6 +33,8 @@ def main():
     grid = mi.fbm_grid(a.grid)
     d = mi.volume_cube(a.res, a.res, a.spp, grid=grid)
     d["integrator"]["type"] = a.integrator
+    if a.no_nee:
+        d["medium1"]["sample_emitters"] = False
     scene = mi.load_dict(d)
     t_load = time.time() - t0
     if a.integrator == "prbvolpath":
