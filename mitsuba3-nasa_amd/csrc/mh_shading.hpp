@@ -1518,80 +1518,113 @@ MH_DEV void trace_si(const DScene &S, const LdsBvh &B, const RayT &ray, SI &si, 
     si_t = si.valid ? h.t : __builtin_huge_valf();
 }
 
-// volpath.cpp:333-450: emitter sample + ratio-tracked transmittance.
-// ref_n = 0 for medium interactions; si_ref for surfaces (medium transitions).
-MH_DEV V3 vol_sample_emitter(const DScene &S, const LdsBvh &B, V3 ref_p, V3 ref_n, const SI *si_ref,
-                             Pcg &rng, uint32_t medium, DirS &ds, uint32_t &n_shadow) {
-    V3 transmittance = v3(1, 1, 1);
-    const float sx = rng.next_float(), sy = rng.next_float();
-    V3 emitter_val = scene_sample_emitter_direction(S, ref_p, sx, sy, ds);
-    if (ds.pdf == 0.f) return v3(0, 0, 0);
-    RayT ray = spawn_ray_to(ref_p, ref_n, ds.p);
-    const float max_dist = ray.maxt;
-    if (si_ref && is_medium_transition(S, *si_ref)) medium = target_medium(S, *si_ref, ray.d);
-    float total_dist = 0.f;
+// volpath.cpp:333-450: emitter sample + ratio-tracked transmittance, split
+// into nee_begin (the emitter sample and the shadow ray) and nee_step (one
+// trip of the transmittance loop) so the walk can interleave with the other
+// lanes' path steps (volpath_advance).  Same operations in the same order as
+// a single call (oracle: vol_sample_emitter).
+struct NeeState {
+    RayT ray;
     SI si;
-    si.valid = false;
-    float si_t = 0.f;
-    bool needs_intersection = true, active = true;
-    while (active) {
-        const float remaining_dist = max_dist - total_dist;
-        ray.maxt = remaining_dist;
-        if (!(remaining_dist > 0.f)) break;
-        bool escaped_medium = false;
-        bool active_medium = medium != MH_INVALID;
-        bool active_surface = !active_medium;
-        if (active_medium) {
-            const DMedium &m = S.media[medium];
-            MEI mei;
-            sample_interaction(S, medium, ray, rng.next_float(), mei);
-            if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = fminf(mei.t, remaining_dist);
-            if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
-            if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
-            needs_intersection = needs_intersection && !si.valid;
-            const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
-            if (spectral) {
-                const float t = fminf(remaining_dist, fminf(mei.t, si_t)) - mei.mint;
-                const float tr = exp_dr((-t) * mei.maj);
-                const float pdf = (si_t < mei.t || mei.t > remaining_dist) ? tr : tr * mei.maj;
-                transmittance = transmittance * (pdf > 0.f ? tr / pdf : 0.f);
-            }
-            if (mei.t > remaining_dist && mei.valid) total_dist = ds.dist;
-            if (mei.t > remaining_dist) { mei.t = __builtin_huge_valf(); mei.valid = false; }
-            escaped_medium = !mei.valid;
-            active_medium = mei.valid;
-            if (active_medium) {
-                total_dist += mei.t;
-                ray.o = mei.p;
-                si_t = si_t - mei.t;
-                transmittance = transmittance * (spectral ? mei.sigma_n : mei.sigma_n / mei.maj);
-            }
-        }
-        const bool intersect = active_surface && needs_intersection;
-        if (intersect) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
-        needs_intersection = needs_intersection && !intersect;
-        active_surface = active_surface || escaped_medium;
-        if (active_surface) total_dist += si_t;
-        active_surface = active_surface && si.valid && !active_medium;
-        if (active_surface) {
-            const uint32_t b = S.shapes[si.shape].bsdf;
-            const float tn = (b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f;
-            transmittance = transmittance * tn;
-            ray = spawn_ray(si.p, si.n, ray.d);
-        }
-        ray.maxt = remaining_dist;
-        needs_intersection = needs_intersection || active_surface;
-        active = (active_medium || active_surface) && nonzero(transmittance);
-        if (active_surface && is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
-    }
-    return transmittance * emitter_val;
+    V3 transmittance, emitter_val;
+    float max_dist, total_dist, si_t;
+    uint32_t medium;
+    bool needs_intersection;
+};
+
+// returns false when there is nothing to walk (ds.pdf == 0: emitted = 0)
+MH_DEV bool nee_begin(const DScene &S, V3 ref_p, V3 ref_n, const SI *si_ref, Pcg &rng, uint32_t medium, DirS &ds,
+                      NeeState &ns) {
+    ns.transmittance = v3(1, 1, 1);
+    const float sx = rng.next_float(), sy = rng.next_float();
+    ns.emitter_val = scene_sample_emitter_direction(S, ref_p, sx, sy, ds);
+    if (ds.pdf == 0.f) return false;
+    ns.ray = spawn_ray_to(ref_p, ref_n, ds.p);
+    ns.max_dist = ns.ray.maxt;
+    if (si_ref && is_medium_transition(S, *si_ref)) medium = target_medium(S, *si_ref, ns.ray.d);
+    ns.medium = medium;
+    ns.total_dist = 0.f;
+    ns.si.valid = false;
+    ns.si_t = 0.f;
+    ns.needs_intersection = true;
+    return true;
 }
 
-// The volpath loop as a resumable state machine: volpath_init + one
-// volpath_step per iteration of volpath.cpp's `while (loop(active))`;
-// volpath_sample runs it to completion.  (Restarting a lane on its next
-// sample as soon as its path ends -- path regeneration -- was measured
-// slower: 70 vs 86 Msamples/s on config 4)
+MH_DEV V3 nee_result(const NeeState &ns) { return ns.transmittance * ns.emitter_val; }
+
+// one trip of the transmittance loop; false when the loop has ended
+MH_DEV bool nee_step(const DScene &S, const LdsBvh &B, Pcg &rng, const DirS &ds, NeeState &ns, uint32_t &n_shadow) {
+    RayT &ray = ns.ray;
+    SI &si = ns.si;
+    float &si_t = ns.si_t, &total_dist = ns.total_dist;
+    V3 &transmittance = ns.transmittance;
+    uint32_t &medium = ns.medium;
+    bool &needs_intersection = ns.needs_intersection;
+    const float remaining_dist = ns.max_dist - total_dist;
+    ray.maxt = remaining_dist;
+    if (!(remaining_dist > 0.f)) return false;
+    bool escaped_medium = false;
+    bool active_medium = medium != MH_INVALID;
+    bool active_surface = !active_medium;
+    if (active_medium) {
+        const DMedium &m = S.media[medium];
+        MEI mei;
+        sample_interaction(S, medium, ray, rng.next_float(), mei);
+        if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = fminf(mei.t, remaining_dist);
+        if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+        if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+        needs_intersection = needs_intersection && !si.valid;
+        const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+        if (spectral) {
+            const float t = fminf(remaining_dist, fminf(mei.t, si_t)) - mei.mint;
+            const float tr = exp_dr((-t) * mei.maj);
+            const float pdf = (si_t < mei.t || mei.t > remaining_dist) ? tr : tr * mei.maj;
+            transmittance = transmittance * (pdf > 0.f ? tr / pdf : 0.f);
+        }
+        if (mei.t > remaining_dist && mei.valid) total_dist = ds.dist;
+        if (mei.t > remaining_dist) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+        escaped_medium = !mei.valid;
+        active_medium = mei.valid;
+        if (active_medium) {
+            total_dist += mei.t;
+            ray.o = mei.p;
+            si_t = si_t - mei.t;
+            transmittance = transmittance * (spectral ? mei.sigma_n : mei.sigma_n / mei.maj);
+        }
+    }
+    const bool intersect = active_surface && needs_intersection;
+    if (intersect) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+    needs_intersection = needs_intersection && !intersect;
+    active_surface = active_surface || escaped_medium;
+    if (active_surface) total_dist += si_t;
+    active_surface = active_surface && si.valid && !active_medium;
+    if (active_surface) {
+        const uint32_t b = S.shapes[si.shape].bsdf;
+        const float tn = (b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f;
+        transmittance = transmittance * tn;
+        ray = spawn_ray(si.p, si.n, ray.d);
+    }
+    ray.maxt = remaining_dist;
+    needs_intersection = needs_intersection || active_surface;
+    const bool active = (active_medium || active_surface) && nonzero(transmittance);
+    if (active_surface && is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
+    return active;
+}
+
+// The volpath loop (volpath.cpp:95-450) as a resumable state machine.  One
+// trip of `while (loop(active))` is pre -> [NEE walk] -> post:
+//   pre   Russian roulette, the medium interaction and, for surface paths,
+//         the hit and its emission, up to the emitter sample;
+//   NEE   the ratio-tracked shadow walk, one trip per advance;
+//   post  the contribution of the emitter sample, phase / BSDF sampling.
+// volpath_advance moves a lane by one unit, so in a wave the lanes that walk a
+// long shadow ray and the lanes that continue their paths advance together
+// instead of the latter idling through the former's loop.
+// Per lane the operations and random draws are exactly those of the nested
+// loops (oracle: volpath_sample).
+enum : uint32_t { kVolPre = 0, kVolNee = 1, kVolPost = 2 };
+enum : uint32_t { kNeeNone = 0, kNeeMedium = 1, kNeeSurface = 2 };
+
 struct VolState {
     RayT ray;
     V3 throughput, result, last_p;
@@ -1599,6 +1632,14 @@ struct VolState {
     float si_t, last_pdf, eta;
     uint32_t medium, depth;
     bool specular_chain, needs_intersection;
+    // between pre and post
+    uint32_t mode, nee_kind;
+    bool active, active_medium, active_surface, act_scatter;
+    MEI mei;
+    V3 rho, pend;       // surface albedo; pending contribution factor
+    float pend_w;       // medium: MIS weight applied after the emitted radiance
+    DirS ds;
+    NeeState ns;
 };
 
 MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT ray, VolState &v) {
@@ -1615,151 +1656,200 @@ MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, 
     v.needs_intersection = true;
     v.last_p = v3(0, 0, 0);
     v.last_pdf = 1.f;
+    v.mode = kVolPre;
 }
 
-// one loop iteration; false when the path has ended (v.result is final)
-MH_DEV bool volpath_step(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, VolState &v,
-                         uint32_t &n_closest, uint32_t &n_shadow) {
+// pre: false when the path ends at the loop head
+MH_DEV bool volpath_pre(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, VolState &v,
+                        uint32_t &n_closest) {
     RayT &ray = v.ray;
     V3 &throughput = v.throughput, &result = v.result, &last_p = v.last_p;
     SI &si = v.si;
     float &si_t = v.si_t, &last_pdf = v.last_pdf, &eta = v.eta;
     uint32_t &medium = v.medium, &depth = v.depth;
     bool &specular_chain = v.specular_chain, &needs_intersection = v.needs_intersection;
-    bool active = true;
-    {
-        // ---- Russian roulette (volpath.cpp:143-151)
-        active = active && nonzero(throughput);
-        const float q = fminf(hmax(throughput) * (eta * eta), 0.95f);
-        const bool perform_rr = depth > in.rr_depth;
-        if (active) active = rng.next_float() < q || !perform_rr;
-        if (perform_rr) throughput = throughput * rcp(q);
-        active = active && depth < in.max_depth;
-        if (!active) return false;
+    MEI &mei = v.mei;
+    // ---- Russian roulette (volpath.cpp:143-151)
+    bool active = nonzero(throughput);
+    const float q = fminf(hmax(throughput) * (eta * eta), 0.95f);
+    const bool perform_rr = depth > in.rr_depth;
+    if (active) active = rng.next_float() < q || !perform_rr;
+    if (perform_rr) throughput = throughput * rcp(q);
+    active = active && depth < in.max_depth;
+    if (!active) return false;
 
-        bool active_medium = medium != MH_INVALID, active_surface = !active_medium;
-        bool act_null = false, act_scatter = false, escaped = false, spectral = false;
-        MEI mei;
-        mei.valid = false;
-        mei.t = __builtin_huge_valf();
-        if (active_medium) {
-            const DMedium &m = S.media[medium];
-            sample_interaction(S, medium, ray, rng.next_float(), mei);
-            if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
-            if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
-            needs_intersection = needs_intersection && !si.valid;
-            if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
-            spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
-            if (spectral) {
-                const float t = fminf(mei.t, si_t) - mei.mint;
-                const float tr = exp_dr((-t) * mei.maj);
-                const float pdf = si_t < mei.t ? tr : tr * mei.maj;
-                throughput = throughput * (pdf > 0.f ? tr / pdf : 0.f);
-            }
-            escaped = !mei.valid;
-            active_medium = mei.valid;
-            bool null_scatter = false;
-            if (active_medium) null_scatter = rng.next_float() >= mei.sigma_t / mei.maj;
-            act_null = null_scatter && active_medium;
-            act_scatter = !act_null && active_medium;
-            if (spectral && act_null) throughput = throughput * ((mei.sigma_n * mei.maj) / mei.sigma_n);
-            if (act_scatter) { depth += 1; last_p = mei.p; }
+    bool active_medium = medium != MH_INVALID, active_surface = !active_medium;
+    bool act_null = false, act_scatter = false, escaped = false, spectral = false;
+    mei.valid = false;
+    mei.t = __builtin_huge_valf();
+    if (active_medium) {
+        const DMedium &m = S.media[medium];
+        sample_interaction(S, medium, ray, rng.next_float(), mei);
+        if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
+        if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+        needs_intersection = needs_intersection && !si.valid;
+        if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+        spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+        if (spectral) {
+            const float t = fminf(mei.t, si_t) - mei.mint;
+            const float tr = exp_dr((-t) * mei.maj);
+            const float pdf = si_t < mei.t ? tr : tr * mei.maj;
+            throughput = throughput * (pdf > 0.f ? tr / pdf : 0.f);
         }
-        active = active && depth < in.max_depth;
-        act_scatter = act_scatter && active;
-        if (act_null) { ray.o = mei.p; si_t = si_t - mei.t; }
-        if (act_scatter) {
-            const DMedium &m = S.media[medium];
-            if (spectral) throughput = throughput * vdiv(mei.sigma_s * mei.maj, mei.sigma_t);
-            else throughput = throughput * vdiv(mei.sigma_s, mei.sigma_t);
-            const bool sample_emitters = !(m.flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
-            specular_chain = !sample_emitters;
-            if (sample_emitters) {
-                DirS ds;
-                V3 emitted = vol_sample_emitter(S, B, mei.p, v3(0, 0, 0), nullptr, rng, medium, ds, n_shadow);
-                V3 wo = mei_to_local(mei, ds.d);
-                const float ph = phase_eval(m, wo);
-                const float w = mis_weight(ds.pdf, ds.delta ? 0.f : ph);
-                result = result + ((throughput * ph) * emitted) * w;
-            }
-            (void)rng.next_float();
-            const float s2x = rng.next_float(), s2y = rng.next_float();
-            float ph_pdf;
-            V3 wo = phase_sample(m, s2x, s2y, ph_pdf);
-            act_scatter = act_scatter && ph_pdf > 0.f;
-            if (act_scatter) {
-                ray = spawn_ray(mei.p, v3(0, 0, 0), mei_to_world(mei, wo));
-                needs_intersection = true;
-                last_pdf = ph_pdf;
-            }
-        }
-
-        // ---- surface interactions (volpath.cpp:254-326)
-        active_surface = active_surface || escaped;
-        if (active_surface && needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
-        if (active_surface) {
-            const bool count_direct = depth == 0 || specular_chain;
-            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
-            if (em != MH_INVALID && !(depth == 0 && in.hide_emitters)) {
-                float emitter_pdf = 1.f;
-                if (!count_direct) emitter_pdf = emitter_pdf_direction(S, em, si, last_p);
-                const V3 emitted = emitter_eval(S, em, si);
-                result = result + (count_direct ? throughput * emitted
-                                                : (throughput * mis_weight(last_pdf, emitter_pdf)) * emitted);
-            }
-        }
-        active_surface = active_surface && si.valid;
-        if (active_surface) {
-            const uint32_t b = S.shapes[si.shape].bsdf;
-            const bool is_null = b == MH_INVALID || S.bsdf_type[b] == MH_BSDF_NULL;
-            V3 rho = v3(0, 0, 0);
-            if (!is_null) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
-            if (!is_null && depth + 1 < in.max_depth) {
-                DirS ds;
-                V3 emitted = vol_sample_emitter(S, B, si.p, si.n, &si, rng, medium, ds, n_shadow);
-                V3 wo = to_local(si, ds.d);
-                V3 bv;
-                float bp;
-                diffuse_eval_pdf(rho, si.wi, wo, true, bv, bp);
-                const float w = mis_weight(ds.pdf, ds.delta ? 0.f : bp);
-                result = result + ((throughput * bv) * w) * emitted;
-            }
-            (void)rng.next_float();
-            const float s2x = rng.next_float(), s2y = rng.next_float();
-            V3 bs_wo, weight;
-            float bs_pdf;
-            if (is_null) {
-                bs_wo = -si.wi; bs_pdf = 1.f; weight = v3(1, 1, 1);
-            } else {
-                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
-                bs_pdf = kInvPi * bs_wo.z;
-                weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
-            }
-            throughput = throughput * weight;
-            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
-            needs_intersection = true;
-            if (!is_null) {
-                depth += 1;
-                last_p = si.p;
-                last_pdf = bs_pdf;
-                specular_chain = false;
-            }
-            if (is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
-        }
-        active = active && (active_surface || active_medium);
+        escaped = !mei.valid;
+        active_medium = mei.valid;
+        bool null_scatter = false;
+        if (active_medium) null_scatter = rng.next_float() >= mei.sigma_t / mei.maj;
+        act_null = null_scatter && active_medium;
+        act_scatter = !act_null && active_medium;
+        if (spectral && act_null) throughput = throughput * ((mei.sigma_n * mei.maj) / mei.sigma_n);
+        if (act_scatter) { depth += 1; last_p = mei.p; }
     }
-    return active;
+    active = active && depth < in.max_depth;
+    act_scatter = act_scatter && active;
+    if (act_null) { ray.o = mei.p; si_t = si_t - mei.t; }
+    v.nee_kind = kNeeNone;
+    bool walk = false;
+    if (act_scatter) {
+        const DMedium &m = S.media[medium];
+        if (spectral) throughput = throughput * vdiv(mei.sigma_s * mei.maj, mei.sigma_t);
+        else throughput = throughput * vdiv(mei.sigma_s, mei.sigma_t);
+        const bool sample_emitters = !(m.flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+        specular_chain = !sample_emitters;
+        if (sample_emitters) {
+            walk = nee_begin(S, mei.p, v3(0, 0, 0), nullptr, rng, medium, v.ds, v.ns);
+            const float ph = phase_eval(m, mei_to_local(mei, v.ds.d));
+            v.pend = throughput * ph;
+            v.pend_w = mis_weight(v.ds.pdf, v.ds.delta ? 0.f : ph);
+            v.nee_kind = kNeeMedium;
+        }
+    }
+    // ---- surface interactions (volpath.cpp:254-326), up to the emitter sample
+    // (act_scatter paths are not surface paths: only escaped ones join)
+    active_surface = active_surface || escaped;
+    if (active_surface && needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+    if (active_surface) {
+        const bool count_direct = depth == 0 || specular_chain;
+        const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+        if (em != MH_INVALID && !(depth == 0 && in.hide_emitters)) {
+            float emitter_pdf = 1.f;
+            if (!count_direct) emitter_pdf = emitter_pdf_direction(S, em, si, last_p);
+            const V3 emitted = emitter_eval(S, em, si);
+            result = result + (count_direct ? throughput * emitted
+                                            : (throughput * mis_weight(last_pdf, emitter_pdf)) * emitted);
+        }
+    }
+    active_surface = active_surface && si.valid;
+    v.rho = v3(0, 0, 0);
+    if (active_surface) {
+        const uint32_t b = S.shapes[si.shape].bsdf;
+        const bool is_null = b == MH_INVALID || S.bsdf_type[b] == MH_BSDF_NULL;
+        if (!is_null) v.rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+        if (!is_null && depth + 1 < in.max_depth) {
+            walk = nee_begin(S, si.p, si.n, &si, rng, medium, v.ds, v.ns);
+            V3 bv;
+            float bp;
+            diffuse_eval_pdf(v.rho, si.wi, to_local(si, v.ds.d), true, bv, bp);
+            const float w = mis_weight(v.ds.pdf, v.ds.delta ? 0.f : bp);
+            v.pend = (throughput * bv) * w;
+            v.nee_kind = kNeeSurface;
+        }
+    }
+    v.active = active;
+    v.active_medium = active_medium;
+    v.active_surface = active_surface;
+    v.act_scatter = act_scatter;
+    if (v.nee_kind != kNeeNone && !walk) {   // ds.pdf == 0: emitted = 0
+        v.ns.transmittance = v3(0, 0, 0);
+        v.ns.emitter_val = v3(0, 0, 0);
+    }
+    v.mode = walk ? kVolNee : kVolPost;
+    return true;
+}
+
+// post: the emitter sample's contribution, then phase / BSDF sampling; false
+// when the path has ended
+MH_DEV bool volpath_post(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    V3 &throughput = v.throughput, &result = v.result;
+    if (v.nee_kind == kNeeMedium) result = result + (v.pend * nee_result(v.ns)) * v.pend_w;
+    else if (v.nee_kind == kNeeSurface) result = result + v.pend * nee_result(v.ns);
+    bool act_scatter = v.act_scatter;
+    const MEI &mei = v.mei;
+    if (act_scatter) {
+        const DMedium &m = S.media[v.medium];
+        (void)rng.next_float();
+        const float s2x = rng.next_float(), s2y = rng.next_float();
+        float ph_pdf;
+        V3 wo = phase_sample(m, s2x, s2y, ph_pdf);
+        act_scatter = act_scatter && ph_pdf > 0.f;
+        if (act_scatter) {
+            v.ray = spawn_ray(mei.p, v3(0, 0, 0), mei_to_world(mei, wo));
+            v.needs_intersection = true;
+            v.last_pdf = ph_pdf;
+        }
+    }
+    if (v.active_surface) {
+        const SI &si = v.si;
+        const uint32_t b = S.shapes[si.shape].bsdf;
+        const bool is_null = b == MH_INVALID || S.bsdf_type[b] == MH_BSDF_NULL;
+        (void)rng.next_float();
+        const float s2x = rng.next_float(), s2y = rng.next_float();
+        V3 bs_wo, weight;
+        float bs_pdf;
+        if (is_null) {
+            bs_wo = -si.wi; bs_pdf = 1.f; weight = v3(1, 1, 1);
+        } else {
+            bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+            bs_pdf = kInvPi * bs_wo.z;
+            weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? v.rho : v3(0, 0, 0);
+        }
+        throughput = throughput * weight;
+        v.ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+        v.needs_intersection = true;
+        if (!is_null) {
+            v.depth += 1;
+            v.last_p = si.p;
+            v.last_pdf = bs_pdf;
+            v.specular_chain = false;
+        }
+        if (is_medium_transition(S, si)) v.medium = target_medium(S, si, v.ray.d);
+    }
+    v.mode = kVolPre;
+    return v.active && (v.active_surface || v.active_medium);
+}
+
+// one unit of progress; false when the path has ended (v.result is final).
+// Scheduling (wave vote): lanes in a shadow walk take one step every trip;
+// the others run their main work (post of the finished walk, then pre of the
+// next loop trip) only once at least MH_VOL_MAIN_PCT % of the wave's live
+// lanes wait for it -- the main work is the heavy code, a walk step is
+// light, so running both every trip would make the walkers pay for it.
+#ifndef MH_VOL_MAIN_PCT
+#define MH_VOL_MAIN_PCT 75  // measured best of 25..100 on config 4 (tools/bench_volpath.py)
+#endif
+MH_DEV bool volpath_advance(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, VolState &v,
+                            uint32_t &n_closest, uint32_t &n_shadow) {
+    const bool walking = v.mode == kVolNee;
+    const uint32_t n_all = (uint32_t)__popcll(__ballot(true)), n_main = (uint32_t)__popcll(__ballot(!walking));
+    if (walking) {
+        if (!nee_step(S, B, rng, v.ds, v.ns, n_shadow)) v.mode = kVolPost;
+        return true;
+    }
+    if (n_main * 100u < n_all * (uint32_t)MH_VOL_MAIN_PCT) return true;
+    if (v.mode == kVolPost && !volpath_post(S, in, rng, v)) return false;
+    if (!volpath_pre(S, B, in, rng, v, n_closest)) return false;
+    if (v.mode == kVolPost) return volpath_post(S, in, rng, v);
+    return true;
 }
 
 MH_DEV V3 volpath_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
                          RayT ray, uint32_t &n_closest, uint32_t &n_shadow) {
     VolState v;
     volpath_init(S, in, rng, ray, v);
-    while (volpath_step(S, B, in, rng, v, n_closest, n_shadow)) {
+    while (volpath_advance(S, B, in, rng, v, n_closest, n_shadow)) {
     }
     return v.result;
 }
-
 
 // ===========================================================================
 // PRBVolpathIntegrator (python/ad/integrators/prbvolpath.py:91-431)
