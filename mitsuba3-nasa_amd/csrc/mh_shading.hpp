@@ -437,10 +437,41 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
                         Hit &hit, float &best) {
     for (uint32_t i = 0; i < count; ++i) {
         const Prim p = load_uniform(prims, first + i);
-        // Branch-free: all lanes test, the hit update is a per-lane select
-        float tt, u, v;
-        const bool ok = p.info.z == MH_SHAPE_RECTANGLE ? rect_test(p, r, tt, u, v) : tri_test(p, r, tt, u, v);
-        const bool take = lane_hit & ok & (Shadow ? hit.shape == MH_INVALID : closer(tt, p, hit));
+        // Branch-free per lane; the hit update is a per-lane select.  Each test
+        // computes the quantity that rejects most lanes first (the plane
+        // distance of a rectangle, u of a triangle) and skips the rest of the
+        // test when the wave's ballot is empty -- a uniform branch, and the
+        // values a surviving lane sees are computed exactly as in rect_test /
+        // tri_test.
+        float tt = 0.f, u = 0.f, v = 0.f;
+        bool ok;
+        if (p.info.z == MH_SHAPE_RECTANGLE) {
+            const float m[12] = {p.a.x, p.a.y, p.a.z, p.a.w, p.b.x, p.b.y, p.b.z, p.b.w,
+                                 p.c.x, p.c.y, p.c.z, p.c.w};
+            const float oz = __builtin_fmaf(m[10], r.o.z, __builtin_fmaf(m[9], r.o.y, __builtin_fmaf(m[8], r.o.x, m[11])));
+            const float dz = __builtin_fmaf(m[10], r.d.z, __builtin_fmaf(m[9], r.d.y, m[8] * r.d.x));
+            tt = -oz / dz;
+            ok = lane_hit & (tt >= 0.f) & (tt <= r.maxt);
+            if (!__any(ok)) continue;
+            const V3 o = xf_point(m, r.o), d = xf_vector(m, r.d);
+            const V3 local = fma3s(d, tt, o);
+            u = local.x;
+            v = local.y;
+            ok = ok & (__builtin_fabsf(local.x) <= 1.f) & (__builtin_fabsf(local.y) <= 1.f);
+        } else {
+            const V3 v0 = v3(p.a.x, p.a.y, p.a.z), e1 = v3(p.b.x, p.b.y, p.b.z), e2 = v3(p.c.x, p.c.y, p.c.z);
+            const V3 pvec = cross(r.d, e2);
+            const float inv_det = rcp(dot(e1, pvec));
+            const V3 tvec = r.o - v0;
+            u = dot(tvec, pvec) * inv_det;
+            ok = lane_hit & (u >= 0.f) & (u <= 1.f);
+            if (!__any(ok)) continue;
+            const V3 qvec = cross(tvec, e1);
+            v = dot(r.d, qvec) * inv_det;
+            tt = dot(e2, qvec) * inv_det;
+            ok = ok & (v >= 0.f) & (u + v <= 1.f) & (tt >= 0.f) & (tt <= r.maxt);
+        }
+        const bool take = ok & (Shadow ? hit.shape == MH_INVALID : closer(tt, p, hit));
         hit.t = take ? tt : hit.t;
         hit.u = take ? u : hit.u;
         hit.v = take ? v : hit.v;
