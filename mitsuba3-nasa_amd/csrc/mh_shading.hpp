@@ -445,13 +445,14 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
         // tri_test.
         float tt = 0.f, u = 0.f, v = 0.f;
         bool ok;
+        const bool live = lane_hit & (!Shadow || hit.shape == MH_INVALID);   // an occluded shadow lane is done
         if (p.info.z == MH_SHAPE_RECTANGLE) {
             const float m[12] = {p.a.x, p.a.y, p.a.z, p.a.w, p.b.x, p.b.y, p.b.z, p.b.w,
                                  p.c.x, p.c.y, p.c.z, p.c.w};
             const float oz = __builtin_fmaf(m[10], r.o.z, __builtin_fmaf(m[9], r.o.y, __builtin_fmaf(m[8], r.o.x, m[11])));
             const float dz = __builtin_fmaf(m[10], r.d.z, __builtin_fmaf(m[9], r.d.y, m[8] * r.d.x));
             tt = -oz / dz;
-            ok = lane_hit & (tt >= 0.f) & (tt <= r.maxt);
+            ok = live & (tt >= 0.f) & (tt <= r.maxt);
             if (!__any(ok)) continue;
             const V3 o = xf_point(m, r.o), d = xf_vector(m, r.d);
             const V3 local = fma3s(d, tt, o);
@@ -464,14 +465,14 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
             const float inv_det = rcp(dot(e1, pvec));
             const V3 tvec = r.o - v0;
             u = dot(tvec, pvec) * inv_det;
-            ok = lane_hit & (u >= 0.f) & (u <= 1.f);
+            ok = live & (u >= 0.f) & (u <= 1.f);
             if (!__any(ok)) continue;
             const V3 qvec = cross(tvec, e1);
             v = dot(r.d, qvec) * inv_det;
             tt = dot(e2, qvec) * inv_det;
             ok = ok & (v >= 0.f) & (u + v <= 1.f) & (tt >= 0.f) & (tt <= r.maxt);
         }
-        const bool take = ok & (Shadow ? hit.shape == MH_INVALID : closer(tt, p, hit));
+        const bool take = ok & (Shadow || closer(tt, p, hit));
         hit.t = take ? tt : hit.t;
         hit.u = take ? u : hit.u;
         hit.v = take ? v : hit.v;
