@@ -452,7 +452,8 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
             const float oz = __builtin_fmaf(m[10], r.o.z, __builtin_fmaf(m[9], r.o.y, __builtin_fmaf(m[8], r.o.x, m[11])));
             const float dz = __builtin_fmaf(m[10], r.d.z, __builtin_fmaf(m[9], r.d.y, m[8] * r.d.x));
             tt = -oz / dz;
-            ok = live & (tt >= 0.f) & (tt <= r.maxt);
+            // tt <= best (<= r.maxt): a farther plane cannot pass closer() below
+            ok = live & (tt >= 0.f) & (tt <= best);
             if (!__any(ok)) continue;
             const V3 o = xf_point(m, r.o), d = xf_vector(m, r.d);
             const V3 local = fma3s(d, tt, o);
