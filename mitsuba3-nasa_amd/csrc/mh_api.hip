@@ -83,7 +83,7 @@ struct mh_scene {
     bool own_stream = false;
     DScene S{};
     // device buffers
-    DevBuf nodes, prims, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
+    DevBuf nodes, nodes4, prims, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
@@ -379,6 +379,23 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.stack_size = bvh.depth + 2;
     const size_t bvh_bytes = bvh.nodes.size() + bvh.prims.size();
     S.lds_bytes_bvh = bvh_bytes <= 32768 ? (uint32_t)bvh_bytes : 0u;  // stage into LDS when small
+    // wide BVH for the stream engine when the BVH lives in global memory
+    // (mh_bvh.cpp collapse_bvh4; MH_BVH4=0 keeps BVH2 everywhere)
+    S.nodes4 = nullptr;
+    {
+        const char *e4 = getenv("MH_BVH4");
+        if (S.lds_bytes_bvh == 0 && bvh.n_prims > 64 && !(e4 && !strcmp(e4, "0"))) {
+            std::vector<uint8_t> n4;
+            uint32_t cnt4 = 0, depth4 = 0;
+            collapse_bvh4(bvh, n4, cnt4, depth4);
+            const uint32_t stack4 = 3u * depth4 + 2u;
+            if ((size_t)std::max(S.stack_size, stack4) * 256 * 4 <= 65536 &&
+                upload(s->nodes4, n4.data(), n4.size(), st) == hipSuccess) {
+                S.nodes4 = reinterpret_cast<const Node4 *>(s->nodes4.ptr);
+                S.stack_size = std::max(S.stack_size, stack4);
+            }
+        }
+    }
     if ((size_t)S.stack_size * 256 * 4 + S.lds_bytes_bvh > 65536)
         return fail(MH_ERR_UNSUPPORTED, "mh_scene_create: BVH too deep for the LDS traversal stack");
     memcpy(S.cam_to_world, sn.to_world, sizeof(S.cam_to_world));
@@ -402,7 +419,7 @@ int mh_scene_destroy(mh_scene *s) {
     if (!s) return MH_OK;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    for (DevBuf *b : {&s->nodes, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
+    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw})

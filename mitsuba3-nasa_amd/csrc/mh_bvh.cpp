@@ -223,4 +223,96 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf,
     }
 }
 
+namespace {
+constexpr uint32_t kLeafRef = 0x80000000u, kEmptyRef = 0xffffffffu;  // as mh_shading.hpp kLeafBit
+
+struct Entry {
+    float lo[3], hi[3];
+    uint32_t inner;   // BVH2 node index, or ~0u for a leaf
+    uint32_t first, count;
+    float area() const {
+        const float d[3] = {hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]};
+        return 2.f * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+    }
+};
+
+struct Collapser {
+    const Node *n2;
+    std::vector<Node4> out;
+    uint32_t depth = 0;
+    void entries_of(uint32_t i, Entry e[2]) const {
+        const Node &n = n2[i];
+        const float4 *lo[2] = {&n.lo0, &n.lo1}, *hi[2] = {&n.hi0, &n.hi1};
+        for (int c = 0; c < 2; ++c) {
+            uint32_t w, cnt;
+            memcpy(&w, &lo[c]->w, 4);
+            memcpy(&cnt, &hi[c]->w, 4);
+            e[c].lo[0] = lo[c]->x; e[c].lo[1] = lo[c]->y; e[c].lo[2] = lo[c]->z;
+            e[c].hi[0] = hi[c]->x; e[c].hi[1] = hi[c]->y; e[c].hi[2] = hi[c]->z;
+            e[c].inner = cnt ? ~0u : w;
+            e[c].first = w;
+            e[c].count = cnt;
+        }
+    }
+    uint32_t emit(uint32_t i, uint32_t d) {
+        depth = std::max(depth, d);
+        Entry e[4];
+        int k = 0;
+        entries_of(i, e);
+        k = 2;
+        while (k < 4) {   // open the inner child of largest area
+            int best = -1;
+            for (int c = 0; c < k; ++c)
+                if (e[c].inner != ~0u && (best < 0 || e[c].area() > e[best].area())) best = c;
+            if (best < 0) break;
+            Entry sub[2];
+            entries_of(e[best].inner, sub);
+            e[best] = sub[0];
+            e[k++] = sub[1];
+        }
+        const uint32_t me = (uint32_t)out.size();
+        out.push_back(Node4{});
+        Node4 n;
+        float lx[4], ly[4], lz[4], hx[4], hy[4], hz[4];
+        uint32_t ref[4];
+        for (int c = 0; c < 4; ++c) {
+            if (c >= k) {   // empty slot: a box no ray enters
+                lx[c] = ly[c] = lz[c] = FLT_MAX;
+                hx[c] = hy[c] = hz[c] = -FLT_MAX;
+                ref[c] = kEmptyRef;
+                continue;
+            }
+            lx[c] = e[c].lo[0]; ly[c] = e[c].lo[1]; lz[c] = e[c].lo[2];
+            hx[c] = e[c].hi[0]; hy[c] = e[c].hi[1]; hz[c] = e[c].hi[2];
+            ref[c] = e[c].inner == ~0u ? (kLeafRef | (e[c].first << 5) | e[c].count) : 0u;
+        }
+        for (int c = 0; c < k; ++c)
+            if (e[c].inner != ~0u) ref[c] = emit(e[c].inner, d + 1);
+        n.lox = make_float4(lx[0], lx[1], lx[2], lx[3]);
+        n.loy = make_float4(ly[0], ly[1], ly[2], ly[3]);
+        n.loz = make_float4(lz[0], lz[1], lz[2], lz[3]);
+        n.hix = make_float4(hx[0], hx[1], hx[2], hx[3]);
+        n.hiy = make_float4(hy[0], hy[1], hy[2], hy[3]);
+        n.hiz = make_float4(hz[0], hz[1], hz[2], hz[3]);
+        n.ref = make_uint4(ref[0], ref[1], ref[2], ref[3]);
+        n.pad = make_uint4(0, 0, 0, 0);
+        out[me] = n;
+        return me;
+    }
+};
+}  // namespace
+
+void collapse_bvh4(const BvhOut &b2, std::vector<uint8_t> &nodes4, uint32_t &n4, uint32_t &depth4) {
+    nodes4.clear();
+    n4 = depth4 = 0;
+    if (b2.n_nodes == 0) return;
+    Collapser c;
+    c.n2 = reinterpret_cast<const Node *>(b2.nodes.data());
+    c.emit(0, 1);
+    n4 = (uint32_t)c.out.size();
+    depth4 = c.depth;
+    nodes4.resize(sizeof(Node4) * n4);
+    memcpy(nodes4.data(), c.out.data(), nodes4.size());
+}
+
 }  // namespace mh

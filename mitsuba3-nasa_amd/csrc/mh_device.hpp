@@ -30,6 +30,15 @@ struct alignas(16) Node {       // 64 B: two child boxes (Aila-Laine BVH2 layout
     float4 lo0, hi0, lo1, hi1;  // .w of lo = child index / first prim, .w of hi = leaf count (0 = inner)
 };
 
+// 128 B: four child boxes in SoA (one float4 per plane), the per-lane stream
+// engine's wide node for large scenes (collapsed from the BVH2, mh_bvh.cpp).
+// ref: inner Node4 index, or kLeafBit | first << 5 | count, or kEmptyRef.
+struct alignas(16) Node4 {
+    float4 lox, loy, loz, hix, hiy, hiz;
+    uint4 ref;
+    uint4 pad;
+};
+
 struct alignas(16) Prim {       // 64 B primitive record
     float4 a, b, c;             // triangle: v0, e1 = v1 - v0, e2 = v2 - v0; rectangle: to_object rows
     uint4 info;                 // x: shape, y: prim index (face; ~0 for rectangles), z: type, w: scene-order key
@@ -88,6 +97,7 @@ struct DScene {                 // kernel argument (by value)
     const float *texels;
     const DMedium *media;
     const float *grid;             // volume grid data
+    const Node4 *nodes4;           // wide BVH of the stream engine (nullptr: BVH2 only)
     uint32_t n_nodes, n_prims, n_emitters, environment;
     uint32_t n_media, camera_medium;
     uint32_t vol_flags;            // prbvolpath prepare_scene flags (kVol*)

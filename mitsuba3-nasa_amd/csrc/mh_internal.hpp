@@ -45,6 +45,9 @@ struct BvhOut {
 };
 // max_leaf <= 31 (5-bit leaf count of the per-lane stream engine's stack entries)
 void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf = 4, float trav_cost = 1.0f);
+// BVH4 collapsed from a BVH2 (greedy: open the largest-area inner child until
+// four children); depth4 = max Node4 nesting
+void collapse_bvh4(const BvhOut &b2, std::vector<uint8_t> &nodes4, uint32_t &n4, uint32_t &depth4);
 
 // ---- kernel launchers (mh_kernels.hip) -------------------------------------
 size_t lds_bytes(const DScene &S, uint32_t block);

@@ -163,6 +163,7 @@ MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32
 // LDS staging of the BVH (nodes then prims) — one copy per workgroup.
 struct LdsBvh {
     const Node *nodes;
+    const Node4 *nodes4;  // wide BVH (global memory), nullptr when absent
     const Prim *prims;
     uint32_t *stack;  // this lane's column
     uint32_t stride;
@@ -187,6 +188,7 @@ MH_DEV LdsBvh stage_bvh(const DScene &S, uint4 *lds) {
         b.nodes = S.n_prims ? S.nodes : nullptr;
         b.prims = S.prims;
     }
+    b.nodes4 = InLds ? nullptr : S.nodes4;
     b.stack = reinterpret_cast<uint32_t *>(lds + nq) + threadIdx.x;
     b.stride = blockDim.x;
     return b;
@@ -348,6 +350,54 @@ MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint3
     }
 }
 
+// one inner step on the wide BVH: the four child boxes of a Node4 (one
+// 128-B record, SoA planes), the hit children sorted near to far, the nearest
+// taken and the others pushed far-first (at most 3 pushes per step)
+MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, uint32_t *stk, uint32_t stride) {
+    if (t.node == kNoNode) {
+        if (t.sp == 0) { t.node = kDone; return; }
+        --t.sp;
+        const uint32_t ref = stk[t.sp * stride];
+        trav_take(t, ref);
+        if (t.node == kNoNode || (t.node & kLeafBit)) return;
+    }
+    const Node4 n = nodes[t.node];
+    const float lx[4] = {n.lox.x, n.lox.y, n.lox.z, n.lox.w}, ly[4] = {n.loy.x, n.loy.y, n.loy.z, n.loy.w},
+                lz[4] = {n.loz.x, n.loz.y, n.loz.z, n.loz.w}, hx[4] = {n.hix.x, n.hix.y, n.hix.z, n.hix.w},
+                hy[4] = {n.hiy.x, n.hiy.y, n.hiy.z, n.hiy.w}, hz[4] = {n.hiz.x, n.hiz.y, n.hiz.z, n.hiz.w};
+    const uint32_t rf[4] = {n.ref.x, n.ref.y, n.ref.z, n.ref.w};
+    float tc[4];
+    uint32_t rc[4];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float a0 = __builtin_fmaf(lx[c], t.inv.x, -t.ood.x), b0 = __builtin_fmaf(hx[c], t.inv.x, -t.ood.x);
+        const float a1 = __builtin_fmaf(ly[c], t.inv.y, -t.ood.y), b1 = __builtin_fmaf(hy[c], t.inv.y, -t.ood.y);
+        const float a2 = __builtin_fmaf(lz[c], t.inv.z, -t.ood.z), b2 = __builtin_fmaf(hz[c], t.inv.z, -t.ood.z);
+        const float lo = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.f));
+        const float hi = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), t.best));
+        const bool h = lo <= hi && rf[c] != 0xffffffffu;
+        tc[c] = h ? lo : __builtin_huge_valf();
+        rc[c] = rf[c];
+        cnt += h ? 1u : 0u;
+    }
+    // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance
+#define MH_CSWAP(i, j)                                                           \
+    {                                                                            \
+        const bool sw = tc[j] < tc[i];                                           \
+        const float ta = sw ? tc[j] : tc[i], tb = sw ? tc[i] : tc[j];            \
+        const uint32_t ra = sw ? rc[j] : rc[i], rb = sw ? rc[i] : rc[j];         \
+        tc[i] = ta; tc[j] = tb; rc[i] = ra; rc[j] = rb;                          \
+    }
+    MH_CSWAP(0, 1) MH_CSWAP(2, 3) MH_CSWAP(0, 2) MH_CSWAP(1, 3) MH_CSWAP(1, 2)
+#undef MH_CSWAP
+    if (cnt == 0) { t.node = kNoNode; return; }
+    if (cnt > 3) { stk[t.sp * stride] = rc[3]; ++t.sp; }
+    if (cnt > 2) { stk[t.sp * stride] = rc[2]; ++t.sp; }
+    if (cnt > 1) { stk[t.sp * stride] = rc[1]; ++t.sp; }
+    trav_take(t, rc[0]);
+}
+
 template <bool Shadow>
 MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
     RayT r{t.o, t.d, t.maxt};
@@ -366,7 +416,7 @@ MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
 
 // Traces items [r0, r1) of this wave.  load(item) -> RayT, store(item, hit,
 // found).  Must be called by all 64 lanes of the wave (uniform r0, r1).
-template <bool Shadow, class Load, class Store>
+template <bool Shadow, bool Wide = false, class Load, class Store>
 MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, Store store) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool empty = B.nodes == nullptr;
@@ -381,7 +431,10 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
             const bool inner = has && trav_wants(t);
             const bool ready = !has || t.nleaf != 0 || t.node == kDone;
             if (!__any(inner) || __all(ready)) break;
-            if (inner) trav_inner_step(t, B.nodes, B.stack, B.stride);
+            if (inner) {
+                if (Wide) trav_inner_step4(t, B.nodes4, B.stack, B.stride);
+                else trav_inner_step(t, B.nodes, B.stack, B.stride);
+            }
         }
         // grouped leaf phase
         if (has && t.nleaf) trav_leaf<Shadow>(t, B.prims);

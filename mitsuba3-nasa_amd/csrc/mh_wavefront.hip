@@ -230,6 +230,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
         w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
     };
     if (Packet) trace_packet<false>(S.nodes, S.prims, B, r0, r1, load, store);
+    else if (B.nodes4) trace_stream<false, true>(B, r0, r1, load, store);
     else trace_stream<false>(B, r0, r1, load, store);
 }
 
@@ -533,6 +534,7 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
         out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
     };
     if (Packet) trace_packet<true>(S.nodes, S.prims, B, r0, r1, load, store);
+    else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
     else trace_stream<true>(B, r0, r1, load, store);
 }
 
@@ -1051,6 +1053,7 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
             }
     };
     if (Packet) trace_packet<true>(S.nodes, S.prims, B, r0, r1, load, store);
+    else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
     else trace_stream<true>(B, r0, r1, load, store);
     flush_partial(acc, q);
 }

@@ -476,3 +476,56 @@ def test_inverse_rendering_loop_recovers_albedo():
     # the loss bottoms out at the Monte Carlo noise floor; the parameter converges
     assert np.mean(losses[-10:]) < np.mean(losses[:3]), losses
     assert err < 0.35 * err0, (err, err0, params[key])
+
+
+# ---------------------------------------------------------------------------
+# large meshes (BVH in HBM/L2, not LDS): the per-lane stream engine on the
+# collapsed 4-wide BVH (mh_bvh.cpp collapse_bvh4) and on the binary BVH
+# ---------------------------------------------------------------------------
+def _blob_scene(mi, n_tri=6000, w=24, h=24, spp=8, max_depth=6):
+    m = max(8, int(np.sqrt(n_tri / 4)))
+    th = np.linspace(0, np.pi, m + 1)
+    ph = np.linspace(0, 2 * np.pi, 2 * m + 1)
+    T_, P_ = np.meshgrid(th, ph, indexing="ij")
+    r = 1.0 + 0.08 * np.sin(7 * T_) * np.cos(9 * P_)
+    V = np.stack([r * np.sin(T_) * np.cos(P_), r * np.cos(T_), r * np.sin(T_) * np.sin(P_)], -1).reshape(-1, 3)
+    a = (np.arange(m)[:, None] * (2 * m + 1) + np.arange(2 * m)[None, :]).reshape(-1)
+    F = np.concatenate([np.stack([a, a + 2 * m + 1, a + 1], 1), np.stack([a + 1, a + 2 * m + 1, a + 2 * m + 2], 1)])
+    d = mi.cornell_box()
+    d["sensor"]["film"].update(width=w, height=h)
+    d["sensor"]["sampler"]["sample_count"] = spp
+    d["integrator"]["max_depth"] = max_depth
+    T = mi.Transform4f
+    d["blob"] = {"type": "mesh", "vertex_positions": V.astype(np.float32), "faces": F.astype(np.uint32),
+                 "to_world": T.translate([0, -0.45, 0]) @ T.scale(0.45), "bsdf": {"type": "ref", "id": "white"}}
+    return mi.load_dict(d)
+
+
+@pytest.mark.parametrize("bvh4", ["1", "0"])
+def test_large_mesh_trace_parity(bvh4, monkeypatch):
+    monkeypatch.setenv("MH_BVH4", bvh4)
+    mi = _mi()
+    scene = _blob_scene(mi)
+    rays = random_rays(scene, 1 << 16, seed=4)
+    t, u, v, prim, shape, occ = gpu_trace(mi, scene, rays)
+    rt, ru, rv, rprim, rshape = O.trace_closest(scene, rays)
+    rocc = O.trace_shadow(scene, rays)
+    same = (shape == rshape) & (prim == rprim) & ((t == rt) | (np.isinf(t) & np.isinf(rt)))
+    assert same.mean() >= 0.9999, f"closest-hit mismatch fraction {1 - same.mean()}"
+    assert (occ == rocc).mean() >= 0.9999
+    assert (rshape == 8).mean() > 0.02      # the blob is hit
+
+
+@pytest.mark.parametrize("bvh4,fused", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_large_mesh_per_sample_parity(bvh4, fused, monkeypatch):
+    monkeypatch.setenv("MH_BVH4", bvh4)
+    monkeypatch.setenv("MH_WF_FUSED", fused)
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = _blob_scene(mi)
+    integ = scene.integrator()
+    L, pos = _gpu_samples(mi, scene, integ, 2, 8, A.FLAG_WAVEFRONT)
+    rL, rpos, _ = O.sample_range(scene, integ, 2, 8, 0, L.shape[0])
+    np.testing.assert_array_equal(pos, rpos)
+    exact = np.all(L == rL, axis=1)
+    assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
