@@ -151,8 +151,17 @@ struct Builder {
         uint32_t mid = split(b, e, depth);
         if (mid == e) {  // leaf
             uint32_t first = (uint32_t)order.size();
-            for (uint32_t i = b; i < e; ++i) order.push_back(idx[i]);
-            uint32_t cnt = e - b;
+            // primitives of one type together (scene order within a type): the
+            // packet engine tests same-type pairs on packed f32 (packet_leaf)
+            std::stable_sort(idx.begin() + b, idx.begin() + e, [&](uint32_t x, uint32_t y) {
+                return p[x].type != p[y].type ? p[x].type < p[y].type : x < y;
+            });
+            uint32_t nrect = 0;
+            for (uint32_t i = b; i < e; ++i) {
+                order.push_back(idx[i]);
+                nrect += p[idx[i]].type == MH_SHAPE_RECTANGLE ? 1u : 0u;
+            }
+            uint32_t cnt = (e - b) | nrect << kLeafRectShift;
             memcpy(&lo.w, &first, 4);
             memcpy(&hi.w, &cnt, 4);
             max_depth = std::max(max_depth, depth);
@@ -190,7 +199,7 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf,
         bld.order.push_back(0);
         Box bb = bld.bounds(0, 1);
         Builder::pad(bb);
-        uint32_t first = 0, cnt = 1;
+        uint32_t first = 0, cnt = 1u | (in[0].type == MH_SHAPE_RECTANGLE ? 1u : 0u) << kLeafRectShift;
         r.lo0 = make_float4(bb.lo[0], bb.lo[1], bb.lo[2], 0.f);
         r.hi0 = make_float4(bb.hi[0], bb.hi[1], bb.hi[2], 0.f);
         memcpy(&r.lo0.w, &first, 4);
@@ -247,6 +256,7 @@ struct Collapser {
             uint32_t w, cnt;
             memcpy(&w, &lo[c]->w, 4);
             memcpy(&cnt, &hi[c]->w, 4);
+            cnt &= kLeafCountMask;
             e[c].lo[0] = lo[c]->x; e[c].lo[1] = lo[c]->y; e[c].lo[2] = lo[c]->z;
             e[c].hi[0] = hi[c]->x; e[c].hi[1] = hi[c]->y; e[c].hi[2] = hi[c]->z;
             e[c].inner = cnt ? ~0u : w;

@@ -27,8 +27,11 @@ constexpr float kFloatMax = 3.40282346638528859812e+38f;      // dr::Largest<flo
 // Device scene layout (HBM; the BVH + primitive records are staged into LDS)
 // ---------------------------------------------------------------------------
 struct alignas(16) Node {       // 64 B: two child boxes (Aila-Laine BVH2 layout)
-    float4 lo0, hi0, lo1, hi1;  // .w of lo = child index / first prim, .w of hi = leaf count (0 = inner)
+    float4 lo0, hi0, lo1, hi1;  // .w of lo = child index / first prim, .w of hi = leaf word (0 = inner)
 };
+// leaf word: primitive count in the low 16 bits, number of rectangles (the
+// leaf's primitives are ordered rectangles first) from bit 16
+constexpr uint32_t kLeafCountMask = 0xffffu, kLeafRectShift = 16;
 
 // 128 B: four child boxes in SoA (one float4 per plane), the per-lane stream
 // engine's wide node for large scenes (collapsed from the BVH2, mh_bvh.cpp).

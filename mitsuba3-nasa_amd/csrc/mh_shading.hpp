@@ -114,8 +114,8 @@ MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32
         bool h0, h1;
         float t0, t1;
         box2(n, inv, ood, best, h0, h1, t0, t1);
-        uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
-        uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
+        uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w) & kLeafCountMask;
+        uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w) & kLeafCountMask;
         // leaves are tested immediately
         if (h0 && n0) {
             for (uint32_t i = 0; i < n0; ++i) {
@@ -332,8 +332,8 @@ MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint3
     bool h0, h1;
     float t0, t1;
     box2(n, t.inv, t.ood, t.best, h0, h1, t0, t1);
-    const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
-    const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
+    const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w) & kLeafCountMask;
+    const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w) & kLeafCountMask;
     const uint32_t r0 = n0 ? (kLeafBit | (c0 << 5) | n0) : c0;
     const uint32_t r1 = n1 ? (kLeafBit | (c1 << 5) | n1) : c1;
     if (h0 && h1) {
@@ -474,6 +474,10 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
 // primitive tests take them as SGPR operands; the visiting decisions are
 // ballots (SGPR masks) — the whole control path is scalar.
 typedef const __attribute__((address_space(4))) float CFloat;
+// wave vote as an SGPR mask: the compiler knows a ballot is wave-uniform, so
+// a branch on it stays a scalar branch (no exec-mask structurisation and no
+// copies of the values live across it)
+MH_DEV bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 template <class T>
 MH_DEV T load_uniform(const T *base, uint32_t i) {
     static_assert(sizeof(T) % 4 == 0, "dword records");
@@ -485,56 +489,151 @@ MH_DEV T load_uniform(const T *base, uint32_t i) {
     return r;
 }
 
+// Running hit of the packet engine.  t starts at the ray's maxt (every
+// accepted t is <= maxt), key is the scene-order key of the primitive held
+// (MH_INVALID: none yet) and pos its index in the leaf-ordered primitive
+// array; (shape, prim) are read from that record once, after the traversal.
+struct PHit {
+    float t, u, v;
+    uint32_t key, pos;
+};
+
+// closer() on (t, key): strict t, exact-t ties to the lower scene-order key.
+// With t starting at maxt this is also the t <= maxt test of the first hit.
 template <bool Shadow>
-MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool lane_hit, const RayT &r,
-                        Hit &hit, float &best) {
-    for (uint32_t i = 0; i < count; ++i) {
-        const Prim p = load_uniform(prims, first + i);
-        // Branch-free per lane; the hit update is a per-lane select.  Each test
-        // computes the quantity that rejects most lanes first (the plane
-        // distance of a rectangle, u of a triangle) and skips the rest of the
-        // test when the wave's ballot is empty -- a uniform branch, and the
-        // values a surviving lane sees are computed exactly as in rect_test /
-        // tri_test.
-        float tt = 0.f, u = 0.f, v = 0.f;
-        bool ok;
-        const bool live = lane_hit & (!Shadow || hit.shape == MH_INVALID);   // an occluded shadow lane is done
-        if (p.info.z == MH_SHAPE_RECTANGLE) {
-            const float m[12] = {p.a.x, p.a.y, p.a.z, p.a.w, p.b.x, p.b.y, p.b.z, p.b.w,
-                                 p.c.x, p.c.y, p.c.z, p.c.w};
-            const float oz = __builtin_fmaf(m[10], r.o.z, __builtin_fmaf(m[9], r.o.y, __builtin_fmaf(m[8], r.o.x, m[11])));
-            const float dz = __builtin_fmaf(m[10], r.d.z, __builtin_fmaf(m[9], r.d.y, m[8] * r.d.x));
-            tt = -oz / dz;
-            // tt <= best (<= r.maxt): a farther plane cannot pass closer() below
-            ok = live & (tt >= 0.f) & (tt <= best);
-            if (!__any(ok)) continue;
-            const V3 o = xf_point(m, r.o), d = xf_vector(m, r.d);
-            const V3 local = fma3s(d, tt, o);
-            u = local.x;
-            v = local.y;
-            ok = ok & (__builtin_fabsf(local.x) <= 1.f) & (__builtin_fabsf(local.y) <= 1.f);
-        } else {
-            const V3 v0 = v3(p.a.x, p.a.y, p.a.z), e1 = v3(p.b.x, p.b.y, p.b.z), e2 = v3(p.c.x, p.c.y, p.c.z);
-            const V3 pvec = cross(r.d, e2);
-            const float inv_det = rcp(dot(e1, pvec));
-            const V3 tvec = r.o - v0;
-            u = dot(tvec, pvec) * inv_det;
-            ok = live & (u >= 0.f) & (u <= 1.f);
-            if (!__any(ok)) continue;
-            const V3 qvec = cross(tvec, e1);
-            v = dot(r.d, qvec) * inv_det;
-            tt = dot(e2, qvec) * inv_det;
-            ok = ok & (v >= 0.f) & (u + v <= 1.f) & (tt >= 0.f) & (tt <= r.maxt);
-        }
-        const bool take = ok & (Shadow || closer(tt, p, hit));
-        hit.t = take ? tt : hit.t;
-        hit.u = take ? u : hit.u;
-        hit.v = take ? v : hit.v;
-        hit.prim = take ? p.info.y : hit.prim;
-        hit.shape = take ? p.info.x : hit.shape;
-        hit.key = take ? p.info.w : hit.key;
-        best = take ? tt : best;
+MH_DEV void packet_take(bool ok, float tt, float u, float v, uint32_t key, uint32_t pos, PHit &h) {
+    if (Shadow) {
+        h.key = ok ? key : h.key;  // any hit occludes
+        return;
     }
+    const bool take = ok & ((tt < h.t) | ((tt == h.t) & (key < h.key)));
+    h.t = take ? tt : h.t;
+    h.u = take ? u : h.u;
+    h.v = take ? v : h.v;
+    h.key = take ? key : h.key;
+    h.pos = take ? pos : h.pos;
+}
+
+// Two primitives of one type per step: their arithmetic runs on packed f32
+// pairs (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, two IEEE operations per
+// lane and instruction, bit-identical to the scalar fmaf/mul/add of
+// rect_test / tri_test); the ray's components are broadcast to both halves.
+typedef float F2 __attribute__((ext_vector_type(2)));
+MH_DEV F2 fma2(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
+MH_DEV F2 sp2(float a) { F2 r; r.x = a; r.y = a; return r; }
+MH_DEV F2 pair(float a, float b) { F2 r; r.x = a; r.y = b; return r; }
+
+// field k (dword) of primitive record i, read through the scalar cache at a
+// wave-uniform index (no Prim copy in registers / private memory)
+MH_DEV float pf(const Prim *P, uint32_t i, uint32_t k) { return ((CFloat *)(P + i))[k]; }
+MH_DEV uint32_t pu(const Prim *P, uint32_t i, uint32_t k) { return __float_as_uint(((CFloat *)(P + i))[k]); }
+
+template <bool Shadow>
+MH_DEV void rect_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    // rows of to_object: x = a, y = b, z = c (shapes/rectangle.cpp:446-470)
+    const F2 ox = sp2(r.o.x), oy = sp2(r.o.y), oz = sp2(r.o.z);
+    const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
+    const F2 c0 = pair(pf(P, pos, 8), pf(P, pos + 1u, 8)), c1 = pair(pf(P, pos, 9), pf(P, pos + 1u, 9)), c2 = pair(pf(P, pos, 10), pf(P, pos + 1u, 10));
+    const F2 lz = fma2(c2, oz, fma2(c1, oy, fma2(c0, ox, pair(pf(P, pos, 11), pf(P, pos + 1u, 11)))));
+    const F2 ldz = fma2(c2, dz, fma2(c1, dy, c0 * dx));
+    const F2 tt = pair(-lz.x / ldz.x, -lz.y / ldz.y);
+    const float bound = Shadow ? r.maxt : h.t;
+    bool okA = live & (tt.x >= 0.f) & (tt.x <= bound), okB = live & (tt.y >= 0.f) & (tt.y <= bound);
+    if (!wave_any(okA | okB)) return;
+    const F2 a0 = pair(pf(P, pos, 0), pf(P, pos + 1u, 0)), a1 = pair(pf(P, pos, 1), pf(P, pos + 1u, 1)), a2 = pair(pf(P, pos, 2), pf(P, pos + 1u, 2));
+    const F2 b0 = pair(pf(P, pos, 4), pf(P, pos + 1u, 4)), b1 = pair(pf(P, pos, 5), pf(P, pos + 1u, 5)), b2 = pair(pf(P, pos, 6), pf(P, pos + 1u, 6));
+    const F2 lox = fma2(a2, oz, fma2(a1, oy, fma2(a0, ox, pair(pf(P, pos, 3), pf(P, pos + 1u, 3)))));
+    const F2 loy = fma2(b2, oz, fma2(b1, oy, fma2(b0, ox, pair(pf(P, pos, 7), pf(P, pos + 1u, 7)))));
+    const F2 ldx = fma2(a2, dz, fma2(a1, dy, a0 * dx));
+    const F2 ldy = fma2(b2, dz, fma2(b1, dy, b0 * dx));
+    const F2 lx = fma2(ldx, tt, lox), ly = fma2(ldy, tt, loy);
+    okA = okA & (__builtin_fabsf(lx.x) <= 1.f) & (__builtin_fabsf(ly.x) <= 1.f);
+    okB = okB & (__builtin_fabsf(lx.y) <= 1.f) & (__builtin_fabsf(ly.y) <= 1.f);
+    packet_take<Shadow>(okA, tt.x, lx.x, ly.x, pu(P, pos, 15), pos, h);
+    packet_take<Shadow>(okB, tt.y, lx.y, ly.y, pu(P, pos + 1u, 15), pos + 1u, h);
+}
+
+template <bool Shadow>
+MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    // Moeller-Trumbore (render/mesh.h:430-453) on two triangles
+    const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
+    const F2 e1x = pair(pf(P, pos, 4), pf(P, pos + 1u, 4)), e1y = pair(pf(P, pos, 5), pf(P, pos + 1u, 5)), e1z = pair(pf(P, pos, 6), pf(P, pos + 1u, 6));
+    const F2 e2x = pair(pf(P, pos, 8), pf(P, pos + 1u, 8)), e2y = pair(pf(P, pos, 9), pf(P, pos + 1u, 9)), e2z = pair(pf(P, pos, 10), pf(P, pos + 1u, 10));
+    // pvec = cross(d, e2)
+    const F2 px = fma2(dy, e2z, -(dz * e2y)), py = fma2(dz, e2x, -(dx * e2z)), pz = fma2(dx, e2y, -(dy * e2x));
+    const F2 det = fma2(e1z, pz, fma2(e1y, py, e1x * px));
+    const F2 inv_det = pair(1.0f / det.x, 1.0f / det.y);
+    const F2 tx = sp2(r.o.x) - pair(pf(P, pos, 0), pf(P, pos + 1u, 0)), ty = sp2(r.o.y) - pair(pf(P, pos, 1), pf(P, pos + 1u, 1)),
+             tz = sp2(r.o.z) - pair(pf(P, pos, 2), pf(P, pos + 1u, 2));
+    const F2 u = fma2(tz, pz, fma2(ty, py, tx * px)) * inv_det;
+    bool okA = live & (u.x >= 0.f) & (u.x <= 1.f), okB = live & (u.y >= 0.f) & (u.y <= 1.f);
+    if (!wave_any(okA | okB)) return;
+    // qvec = cross(tvec, e1)
+    const F2 qx = fma2(ty, e1z, -(tz * e1y)), qy = fma2(tz, e1x, -(tx * e1z)), qz = fma2(tx, e1y, -(ty * e1x));
+    const F2 v = fma2(dz, qz, fma2(dy, qy, dx * qx)) * inv_det;
+    const F2 tt = fma2(e2z, qz, fma2(e2y, qy, e2x * qx)) * inv_det;
+    const F2 uv = u + v;
+    okA = okA & (v.x >= 0.f) & (uv.x <= 1.f) & (tt.x >= 0.f) & (tt.x <= r.maxt);
+    okB = okB & (v.y >= 0.f) & (uv.y <= 1.f) & (tt.y >= 0.f) & (tt.y <= r.maxt);
+    packet_take<Shadow>(okA, tt.x, u.x, v.x, pu(P, pos, 15), pos, h);
+    packet_take<Shadow>(okB, tt.y, u.y, v.y, pu(P, pos + 1u, 15), pos + 1u, h);
+}
+
+template <bool Shadow>
+MH_DEV void rect_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    const float oz = __builtin_fmaf(pf(P, pos, 10), r.o.z, __builtin_fmaf(pf(P, pos, 9), r.o.y, __builtin_fmaf(pf(P, pos, 8), r.o.x, pf(P, pos, 11))));
+    const float dz = __builtin_fmaf(pf(P, pos, 10), r.d.z, __builtin_fmaf(pf(P, pos, 9), r.d.y, pf(P, pos, 8) * r.d.x));
+    const float tt = -oz / dz;
+    bool ok = live & (tt >= 0.f) & (tt <= (Shadow ? r.maxt : h.t));
+    if (!wave_any(ok)) return;
+    // xf_point / xf_vector rows x, y, then fma(d, t, o)
+    const float ox = __builtin_fmaf(pf(P, pos, 2), r.o.z, __builtin_fmaf(pf(P, pos, 1), r.o.y, __builtin_fmaf(pf(P, pos, 0), r.o.x, pf(P, pos, 3))));
+    const float oy = __builtin_fmaf(pf(P, pos, 6), r.o.z, __builtin_fmaf(pf(P, pos, 5), r.o.y, __builtin_fmaf(pf(P, pos, 4), r.o.x, pf(P, pos, 7))));
+    const float dx = __builtin_fmaf(pf(P, pos, 2), r.d.z, __builtin_fmaf(pf(P, pos, 1), r.d.y, pf(P, pos, 0) * r.d.x));
+    const float dy = __builtin_fmaf(pf(P, pos, 6), r.d.z, __builtin_fmaf(pf(P, pos, 5), r.d.y, pf(P, pos, 4) * r.d.x));
+    const float lx = __builtin_fmaf(dx, tt, ox), ly = __builtin_fmaf(dy, tt, oy);
+    ok = ok & (__builtin_fabsf(lx) <= 1.f) & (__builtin_fabsf(ly) <= 1.f);
+    packet_take<Shadow>(ok, tt, lx, ly, pu(P, pos, 15), pos, h);
+}
+
+template <bool Shadow>
+MH_DEV void tri_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    const V3 v0 = v3(pf(P, pos, 0), pf(P, pos, 1), pf(P, pos, 2)), e1 = v3(pf(P, pos, 4), pf(P, pos, 5), pf(P, pos, 6)), e2 = v3(pf(P, pos, 8), pf(P, pos, 9), pf(P, pos, 10));
+    const V3 pvec = cross(r.d, e2);
+    const float inv_det = rcp(dot(e1, pvec));
+    const V3 tvec = r.o - v0;
+    const float u = dot(tvec, pvec) * inv_det;
+    bool ok = live & (u >= 0.f) & (u <= 1.f);
+    if (!wave_any(ok)) return;
+    const V3 qvec = cross(tvec, e1);
+    const float v = dot(r.d, qvec) * inv_det;
+    const float tt = dot(e2, qvec) * inv_det;
+    ok = ok & (v >= 0.f) & (u + v <= 1.f) & (tt >= 0.f) & (tt <= r.maxt);
+    packet_take<Shadow>(ok, tt, u, v, pu(P, pos, 15), pos, h);
+}
+
+// One leaf for the lanes whose ray overlapped its box (lane_hit).  The host
+// orders every leaf by primitive type (build_bvh), so primitives go in
+// same-type pairs with at most one single test per type.  Each test computes
+// the quantity that rejects most lanes first (the plane distance of a
+// rectangle, u of a triangle) and skips the rest when the wave's ballot is
+// empty -- a uniform branch; the values a surviving lane sees are computed
+// exactly as in rect_test / tri_test.
+template <bool Shadow>
+MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, uint32_t nrect, bool lane_hit,
+                        const RayT r, PHit &h) {
+    // rectangles [0, nrect), then triangles [nrect, count): straight-line
+    // loops (one body each) rather than one loop with a per-step type switch
+    uint32_t i = 0;
+    for (; i + 1u < nrect; i += 2u)
+        rect_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
+    if (i < nrect) {
+        rect_one<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
+        ++i;
+    }
+    for (; i + 1u < count; i += 2u)
+        tri_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
+    if (i < count) tri_one<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
 }
 
 // gnodes / gprims: the BVH in global memory (read via the scalar cache);
@@ -542,31 +641,35 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, bool 
 // One batch: the wave's 64 rays (act: lanes that hold a ray).  ws: the
 // wave-uniform stack (entry k at ws[k * stride]).
 template <bool Shadow>
-MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, uint32_t stride, const RayT &r,
+MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, uint32_t stride, const RayT r,
                         bool act) {
     const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
-    float best = r.maxt;
-    Hit hit;
-    hit.t = __builtin_huge_valf();
-    hit.u = hit.v = 0.f;
-    hit.prim = MH_INVALID;
-    hit.shape = MH_INVALID;
-    hit.key = MH_INVALID;
+    PHit ph;
+    ph.t = r.maxt;
+    ph.u = ph.v = 0.f;
+    ph.key = MH_INVALID;
+    ph.pos = 0;
     act = act && gnodes != nullptr;
     uint32_t node = 0, sp = 0;
-    while (__any(act)) {
+    while (wave_any(act)) {
         const Node n = load_uniform(gnodes, node);
         bool h0, h1;
         float t0, t1;
-        box2(n, inv, ood, best, h0, h1, t0, t1);
+        box2(n, inv, ood, ph.t, h0, h1, t0, t1);
         h0 = h0 && act;
         h1 = h1 && act;
-        const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w);
-        const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w);
-        bool any0 = __any(h0), any1 = __any(h1);
-        if (any0 && n0) { packet_leaf<Shadow>(gprims, c0, n0, h0, r, hit, best); any0 = false; }
-        if (any1 && n1) { packet_leaf<Shadow>(gprims, c1, n1, h1, r, hit, best); any1 = false; }
-        if (Shadow) act = act && hit.shape == MH_INVALID;
+        const uint32_t c0 = __float_as_uint(n.lo0.w), n0 = __float_as_uint(n.hi0.w) & kLeafCountMask;
+        const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w) & kLeafCountMask;
+        bool any0 = wave_any(h0), any1 = wave_any(h1);
+        if (any0 && n0) {
+            packet_leaf<Shadow>(gprims, c0, n0, __float_as_uint(n.hi0.w) >> kLeafRectShift, h0, r, ph);
+            any0 = false;
+        }
+        if (any1 && n1) {
+            packet_leaf<Shadow>(gprims, c1, n1, __float_as_uint(n.hi1.w) >> kLeafRectShift, h1, r, ph);
+            any1 = false;
+        }
+        if (Shadow) act = act && ph.key == MH_INVALID;
         if (any0 && any1) {
             const unsigned long long both = __ballot(h0 && h1), pref1 = __ballot(h0 && h1 && t1 < t0);
             const bool first1 = 2u * (uint32_t)__popcll(pref1) > (uint32_t)__popcll(both);
@@ -581,6 +684,22 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, ui
             if (sp == 0) break;
             --sp;
             node = __builtin_amdgcn_readfirstlane(ws[sp * stride]);
+        }
+    }
+    Hit hit;
+    hit.key = ph.key;
+    hit.prim = MH_INVALID;
+    hit.shape = MH_INVALID;
+    hit.t = __builtin_huge_valf();
+    hit.u = hit.v = 0.f;
+    if (ph.key != MH_INVALID) {
+        const uint4 info = gprims[ph.pos].info;
+        hit.shape = info.x;
+        hit.prim = info.y;
+        if (!Shadow) {
+            hit.t = ph.t;
+            hit.u = ph.u;
+            hit.v = ph.v;
         }
     }
     return hit;

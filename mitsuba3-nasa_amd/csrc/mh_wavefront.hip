@@ -412,6 +412,14 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             ray.maxt = w.mt[cur][j];
         }
         const Hit h = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, ray, has);
+#ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
+        {
+            RayT r2 = ray;
+            asm volatile("" : "+v"(r2.maxt));
+            const Hit h2 = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, r2, has);
+            asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.u));
+        }
+#endif
         if (has) {
             tp = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
             L = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
@@ -490,6 +498,14 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         }
         // ---- visibility of the NEE sample (scene.cpp:201-210)
         const Hit sh = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, sray, shadow);
+#ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
+        {
+            RayT r2 = sray;
+            asm volatile("" : "+v"(r2.maxt));
+            const Hit h2 = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, r2, shadow);
+            asm volatile("" ::"v"(h2.shape));
+        }
+#endif
         if (shadow && sh.shape == MH_INVALID) L = fma3(a_nee, b_nee, L);
         n_shadow += (uint32_t)__popcll(__ballot(shadow));
         // ---- compaction: survivors -> next queue; finished paths -> sample planes
