@@ -83,7 +83,7 @@ struct mh_scene {
     bool own_stream = false;
     DScene S{};
     // device buffers
-    DevBuf nodes, nodes4, prims, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
+    DevBuf nodes, nodes4, prims, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
@@ -226,8 +226,17 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     s->bvh_nodes = bvh.n_nodes;
     s->bvh_prims = bvh.n_prims;
     s->bvh_depth = bvh.depth;
+    // scene-order key -> (shape, prim) of every primitive (the packet engine
+    // carries only the key of its running hit)
+    std::vector<uint32_t> key_sp(2 * (size_t)bvh.n_prims);
+    for (uint32_t i = 0; i < bvh.n_prims; ++i) {
+        const Prim &q = reinterpret_cast<const Prim *>(bvh.prims.data())[i];
+        key_sp[2 * (size_t)q.info.w] = q.info.x;
+        key_sp[2 * (size_t)q.info.w + 1] = q.info.y;
+    }
     if (upload(s->nodes, bvh.nodes.data(), bvh.nodes.size(), st) != hipSuccess ||
-        upload(s->prims, bvh.prims.data(), bvh.prims.size(), st) != hipSuccess)
+        upload(s->prims, bvh.prims.data(), bvh.prims.size(), st) != hipSuccess ||
+        upload(s->key_sp, key_sp.data(), 4 * key_sp.size(), st) != hipSuccess)
         return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: BVH upload failed");
 
     // ---- shading-time records ----
@@ -342,6 +351,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     DScene &S = s->S;
     S.nodes = s->nodes.as<Node>();
     S.prims = s->prims.as<Prim>();
+    S.key_sp = s->key_sp.as<uint2>();
     S.shapes = s->shapes.as<DShape>();
     S.bsdf_type = s->bsdf_type.as<uint32_t>();
     S.bsdf_tex = s->bsdf_tex.as<uint32_t>();
@@ -419,7 +429,7 @@ int mh_scene_destroy(mh_scene *s) {
     if (!s) return MH_OK;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
+    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw})

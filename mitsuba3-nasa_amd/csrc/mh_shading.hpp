@@ -489,21 +489,30 @@ MH_DEV T load_uniform(const T *base, uint32_t i) {
     return r;
 }
 
+#ifdef MH_EXP_COUNT  // diagnostic build: per-wave event counters of the packet engine
+__device__ unsigned long long g_exp_cnt[16];
+#define MH_CNT(k) do { if ((threadIdx.x & 63u) == 0) atomicAdd(&g_exp_cnt[(k) + (Shadow ? 8 : 0)], 1ull); } while (0)
+#else
+#define MH_CNT(k) do { } while (0)
+#endif
+
 // Running hit of the packet engine.  t starts at the ray's maxt (every
-// accepted t is <= maxt), key is the scene-order key of the primitive held
-// (MH_INVALID: none yet) and pos its index in the leaf-ordered primitive
-// array; (shape, prim) are read from that record once, after the traversal.
+// accepted t is <= maxt) and key is the scene-order key of the primitive held
+// (MH_INVALID: none yet); (shape, prim) are looked up from the key once,
+// after the traversal (DScene::key_sp).  Shadow rays only track `occl`, a
+// lane mask the compiler keeps in SGPRs (no per-primitive vector selects).
 struct PHit {
     float t, u, v;
-    uint32_t key, pos;
+    uint32_t key;
+    bool occl;
 };
 
 // closer() on (t, key): strict t, exact-t ties to the lower scene-order key.
 // With t starting at maxt this is also the t <= maxt test of the first hit.
 template <bool Shadow>
-MH_DEV void packet_take(bool ok, float tt, float u, float v, uint32_t key, uint32_t pos, PHit &h) {
+MH_DEV void packet_take(bool ok, float tt, float u, float v, uint32_t key, PHit &h) {
     if (Shadow) {
-        h.key = ok ? key : h.key;  // any hit occludes
+        h.occl = h.occl | ok;  // any hit occludes
         return;
     }
     const bool take = ok & ((tt < h.t) | ((tt == h.t) & (key < h.key)));
@@ -511,7 +520,6 @@ MH_DEV void packet_take(bool ok, float tt, float u, float v, uint32_t key, uint3
     h.u = take ? u : h.u;
     h.v = take ? v : h.v;
     h.key = take ? key : h.key;
-    h.pos = take ? pos : h.pos;
 }
 
 // Two primitives of one type per step: their arithmetic runs on packed f32
@@ -530,6 +538,7 @@ MH_DEV uint32_t pu(const Prim *P, uint32_t i, uint32_t k) { return __float_as_ui
 
 template <bool Shadow>
 MH_DEV void rect_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    MH_CNT(0);
     // rows of to_object: x = a, y = b, z = c (shapes/rectangle.cpp:446-470)
     const F2 ox = sp2(r.o.x), oy = sp2(r.o.y), oz = sp2(r.o.z);
     const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
@@ -540,6 +549,7 @@ MH_DEV void rect_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit
     const float bound = Shadow ? r.maxt : h.t;
     bool okA = live & (tt.x >= 0.f) & (tt.x <= bound), okB = live & (tt.y >= 0.f) & (tt.y <= bound);
     if (!wave_any(okA | okB)) return;
+    MH_CNT(1);
     const F2 a0 = pair(pf(P, pos, 0), pf(P, pos + 1u, 0)), a1 = pair(pf(P, pos, 1), pf(P, pos + 1u, 1)), a2 = pair(pf(P, pos, 2), pf(P, pos + 1u, 2));
     const F2 b0 = pair(pf(P, pos, 4), pf(P, pos + 1u, 4)), b1 = pair(pf(P, pos, 5), pf(P, pos + 1u, 5)), b2 = pair(pf(P, pos, 6), pf(P, pos + 1u, 6));
     const F2 lox = fma2(a2, oz, fma2(a1, oy, fma2(a0, ox, pair(pf(P, pos, 3), pf(P, pos + 1u, 3)))));
@@ -549,12 +559,13 @@ MH_DEV void rect_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit
     const F2 lx = fma2(ldx, tt, lox), ly = fma2(ldy, tt, loy);
     okA = okA & (__builtin_fabsf(lx.x) <= 1.f) & (__builtin_fabsf(ly.x) <= 1.f);
     okB = okB & (__builtin_fabsf(lx.y) <= 1.f) & (__builtin_fabsf(ly.y) <= 1.f);
-    packet_take<Shadow>(okA, tt.x, lx.x, ly.x, pu(P, pos, 15), pos, h);
-    packet_take<Shadow>(okB, tt.y, lx.y, ly.y, pu(P, pos + 1u, 15), pos + 1u, h);
+    packet_take<Shadow>(okA, tt.x, lx.x, ly.x, pu(P, pos, 15), h);
+    packet_take<Shadow>(okB, tt.y, lx.y, ly.y, pu(P, pos + 1u, 15), h);
 }
 
 template <bool Shadow>
 MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    MH_CNT(2);
     // Moeller-Trumbore (render/mesh.h:430-453) on two triangles
     const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
     const F2 e1x = pair(pf(P, pos, 4), pf(P, pos + 1u, 4)), e1y = pair(pf(P, pos, 5), pf(P, pos + 1u, 5)), e1z = pair(pf(P, pos, 6), pf(P, pos + 1u, 6));
@@ -568,6 +579,7 @@ MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit 
     const F2 u = fma2(tz, pz, fma2(ty, py, tx * px)) * inv_det;
     bool okA = live & (u.x >= 0.f) & (u.x <= 1.f), okB = live & (u.y >= 0.f) & (u.y <= 1.f);
     if (!wave_any(okA | okB)) return;
+    MH_CNT(3);
     // qvec = cross(tvec, e1)
     const F2 qx = fma2(ty, e1z, -(tz * e1y)), qy = fma2(tz, e1x, -(tx * e1z)), qz = fma2(tx, e1y, -(ty * e1x));
     const F2 v = fma2(dz, qz, fma2(dy, qy, dx * qx)) * inv_det;
@@ -575,17 +587,19 @@ MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit 
     const F2 uv = u + v;
     okA = okA & (v.x >= 0.f) & (uv.x <= 1.f) & (tt.x >= 0.f) & (tt.x <= r.maxt);
     okB = okB & (v.y >= 0.f) & (uv.y <= 1.f) & (tt.y >= 0.f) & (tt.y <= r.maxt);
-    packet_take<Shadow>(okA, tt.x, u.x, v.x, pu(P, pos, 15), pos, h);
-    packet_take<Shadow>(okB, tt.y, u.y, v.y, pu(P, pos + 1u, 15), pos + 1u, h);
+    packet_take<Shadow>(okA, tt.x, u.x, v.x, pu(P, pos, 15), h);
+    packet_take<Shadow>(okB, tt.y, u.y, v.y, pu(P, pos + 1u, 15), h);
 }
 
 template <bool Shadow>
 MH_DEV void rect_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    MH_CNT(4);
     const float oz = __builtin_fmaf(pf(P, pos, 10), r.o.z, __builtin_fmaf(pf(P, pos, 9), r.o.y, __builtin_fmaf(pf(P, pos, 8), r.o.x, pf(P, pos, 11))));
     const float dz = __builtin_fmaf(pf(P, pos, 10), r.d.z, __builtin_fmaf(pf(P, pos, 9), r.d.y, pf(P, pos, 8) * r.d.x));
     const float tt = -oz / dz;
     bool ok = live & (tt >= 0.f) & (tt <= (Shadow ? r.maxt : h.t));
     if (!wave_any(ok)) return;
+    MH_CNT(4);
     // xf_point / xf_vector rows x, y, then fma(d, t, o)
     const float ox = __builtin_fmaf(pf(P, pos, 2), r.o.z, __builtin_fmaf(pf(P, pos, 1), r.o.y, __builtin_fmaf(pf(P, pos, 0), r.o.x, pf(P, pos, 3))));
     const float oy = __builtin_fmaf(pf(P, pos, 6), r.o.z, __builtin_fmaf(pf(P, pos, 5), r.o.y, __builtin_fmaf(pf(P, pos, 4), r.o.x, pf(P, pos, 7))));
@@ -593,11 +607,12 @@ MH_DEV void rect_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit 
     const float dy = __builtin_fmaf(pf(P, pos, 6), r.d.z, __builtin_fmaf(pf(P, pos, 5), r.d.y, pf(P, pos, 4) * r.d.x));
     const float lx = __builtin_fmaf(dx, tt, ox), ly = __builtin_fmaf(dy, tt, oy);
     ok = ok & (__builtin_fabsf(lx) <= 1.f) & (__builtin_fabsf(ly) <= 1.f);
-    packet_take<Shadow>(ok, tt, lx, ly, pu(P, pos, 15), pos, h);
+    packet_take<Shadow>(ok, tt, lx, ly, pu(P, pos, 15), h);
 }
 
 template <bool Shadow>
 MH_DEV void tri_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+    MH_CNT(5);
     const V3 v0 = v3(pf(P, pos, 0), pf(P, pos, 1), pf(P, pos, 2)), e1 = v3(pf(P, pos, 4), pf(P, pos, 5), pf(P, pos, 6)), e2 = v3(pf(P, pos, 8), pf(P, pos, 9), pf(P, pos, 10));
     const V3 pvec = cross(r.d, e2);
     const float inv_det = rcp(dot(e1, pvec));
@@ -605,11 +620,12 @@ MH_DEV void tri_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &
     const float u = dot(tvec, pvec) * inv_det;
     bool ok = live & (u >= 0.f) & (u <= 1.f);
     if (!wave_any(ok)) return;
+    MH_CNT(5);
     const V3 qvec = cross(tvec, e1);
     const float v = dot(r.d, qvec) * inv_det;
     const float tt = dot(e2, qvec) * inv_det;
     ok = ok & (v >= 0.f) & (u + v <= 1.f) & (tt >= 0.f) & (tt <= r.maxt);
-    packet_take<Shadow>(ok, tt, u, v, pu(P, pos, 15), pos, h);
+    packet_take<Shadow>(ok, tt, u, v, pu(P, pos, 15), h);
 }
 
 // One leaf for the lanes whose ray overlapped its box (lane_hit).  The host
@@ -626,14 +642,14 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, uint3
     // loops (one body each) rather than one loop with a per-step type switch
     uint32_t i = 0;
     for (; i + 1u < nrect; i += 2u)
-        rect_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
+        rect_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
     if (i < nrect) {
-        rect_one<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
+        rect_one<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
         ++i;
     }
     for (; i + 1u < count; i += 2u)
-        tri_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
-    if (i < count) tri_one<Shadow>(prims, first + i, lane_hit & (!Shadow || h.key == MH_INVALID), r, h);
+        tri_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
+    if (i < count) tri_one<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
 }
 
 // gnodes / gprims: the BVH in global memory (read via the scalar cache);
@@ -641,20 +657,21 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, uint3
 // One batch: the wave's 64 rays (act: lanes that hold a ray).  ws: the
 // wave-uniform stack (entry k at ws[k * stride]).
 template <bool Shadow>
-MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, uint32_t stride, const RayT r,
-                        bool act) {
+MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const uint2 *key_sp, uint32_t *ws, uint32_t stride,
+                        const RayT r, bool act) {
     const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
     PHit ph;
     ph.t = r.maxt;
     ph.u = ph.v = 0.f;
     ph.key = MH_INVALID;
-    ph.pos = 0;
+    ph.occl = false;
     act = act && gnodes != nullptr;
     uint32_t node = 0, sp = 0;
     while (wave_any(act)) {
         const Node n = load_uniform(gnodes, node);
         bool h0, h1;
         float t0, t1;
+        MH_CNT(6);
         box2(n, inv, ood, ph.t, h0, h1, t0, t1);
         h0 = h0 && act;
         h1 = h1 && act;
@@ -669,7 +686,7 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, ui
             packet_leaf<Shadow>(gprims, c1, n1, __float_as_uint(n.hi1.w) >> kLeafRectShift, h1, r, ph);
             any1 = false;
         }
-        if (Shadow) act = act && ph.key == MH_INVALID;
+        if (Shadow) act = act && !ph.occl;
         if (any0 && any1) {
             const unsigned long long both = __ballot(h0 && h1), pref1 = __ballot(h0 && h1 && t1 < t0);
             const bool first1 = 2u * (uint32_t)__popcll(pref1) > (uint32_t)__popcll(both);
@@ -686,27 +703,29 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, uint32_t *ws, ui
             node = __builtin_amdgcn_readfirstlane(ws[sp * stride]);
         }
     }
+    MH_CNT(7);
     Hit hit;
     hit.key = ph.key;
     hit.prim = MH_INVALID;
     hit.shape = MH_INVALID;
     hit.t = __builtin_huge_valf();
     hit.u = hit.v = 0.f;
-    if (ph.key != MH_INVALID) {
-        const uint4 info = gprims[ph.pos].info;
-        hit.shape = info.x;
-        hit.prim = info.y;
-        if (!Shadow) {
-            hit.t = ph.t;
-            hit.u = ph.u;
-            hit.v = ph.v;
-        }
+    if (Shadow) {
+        hit.shape = ph.occl ? 0u : MH_INVALID;  // occluded / not (the shadow consumers' test)
+    } else if (ph.key != MH_INVALID) {
+        const uint2 sp = key_sp[ph.key];
+        hit.shape = sp.x;
+        hit.prim = sp.y;
+        hit.t = ph.t;
+        hit.u = ph.u;
+        hit.v = ph.v;
     }
     return hit;
 }
 
 template <bool Shadow, class Load, class Store>
-MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const LdsBvh &B, uint32_t r0, uint32_t r1,
+MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const uint2 *key_sp, const LdsBvh &B, uint32_t r0,
+                         uint32_t r1,
                          Load load, Store store) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t *ws = B.stack - lane;  // wave-uniform stack: entry k at ws[k * stride]
@@ -716,7 +735,7 @@ MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const LdsBvh &B
         RayT r;
         if (has) r = load(item);
         else r = RayT{v3(0, 0, 0), v3(0, 0, 1), -1.f};
-        const Hit hit = packet_batch<Shadow>(gnodes, gprims, ws, B.stride, r, has);
+        const Hit hit = packet_batch<Shadow>(gnodes, gprims, key_sp, ws, B.stride, r, has);
         if (has) store(item, hit, hit.shape != MH_INVALID);
     }
 }

@@ -229,7 +229,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
         const uint32_t j = base + i;
         w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
     };
-    if (Packet) trace_packet<false>(S.nodes, S.prims, B, r0, r1, load, store);
+    if (Packet) trace_packet<false>(S.nodes, S.prims, S.key_sp, B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<false, true>(B, r0, r1, load, store);
     else trace_stream<false>(B, r0, r1, load, store);
 }
@@ -411,12 +411,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
             ray.maxt = w.mt[cur][j];
         }
-        const Hit h = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, ray, has);
+        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, ray, has);
 #ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
         {
             RayT r2 = ray;
             asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, r2, has);
+            const Hit h2 = packet_batch<false>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, r2, has);
             asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.u));
         }
 #endif
@@ -497,12 +497,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
         }
         // ---- visibility of the NEE sample (scene.cpp:201-210)
-        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, sray, shadow);
+        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, sray, shadow);
 #ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
         {
             RayT r2 = sray;
             asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, r2, shadow);
+            const Hit h2 = packet_batch<true>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, r2, shadow);
             asm volatile("" ::"v"(h2.shape));
         }
 #endif
@@ -549,7 +549,7 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
         L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
         out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
     };
-    if (Packet) trace_packet<true>(S.nodes, S.prims, B, r0, r1, load, store);
+    if (Packet) trace_packet<true>(S.nodes, S.prims, S.key_sp, B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
     else trace_stream<true>(B, r0, r1, load, store);
 }
@@ -906,7 +906,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
             ray.maxt = w.mt[cur][j];
         }
-        const Hit h = packet_batch<false>(S0.nodes, S0.prims, ws, 1u, ray, i < n);
+        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, ray, i < n);
         if (i < n) {
             beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
             prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
@@ -1003,7 +1003,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             alive = active_next;
         }
         // ---- visibility of the NEE sample; the record is charged if unoccluded
-        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, ws, 1u, sray, shadow);
+        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, sray, shadow);
         if (shadow && sh.shape == MH_INVALID) {
 #pragma unroll
             for (int kk = 0; kk < NR; ++kk)
@@ -1068,7 +1068,7 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
                 acc[kk][2] += q.G(kk * 3 + 2)[j];
             }
     };
-    if (Packet) trace_packet<true>(S.nodes, S.prims, B, r0, r1, load, store);
+    if (Packet) trace_packet<true>(S.nodes, S.prims, S.key_sp, B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
     else trace_stream<true>(B, r0, r1, load, store);
     flush_partial(acc, q);
@@ -1151,4 +1151,14 @@ hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n
     return hipGetLastError();
 }
 
+#ifdef MH_EXP_COUNT
+extern "C" int mh_exp_counters(unsigned long long *out, int reset) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_cnt), sizeof(g_exp_cnt));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_exp_cnt), z, sizeof(z));
+    }
+    return 0;
+}
+#endif
 }  // namespace mh
