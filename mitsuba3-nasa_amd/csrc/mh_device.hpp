@@ -155,8 +155,37 @@ MH_DEV V3 cross(V3 a, V3 b) {
     return V3{__builtin_fmaf(a.y, b.z, -(a.z * b.y)), __builtin_fmaf(a.z, b.x, -(a.x * b.z)),
               __builtin_fmaf(a.x, b.y, -(a.y * b.x))};
 }
-MH_DEV float rcp(float x) { return 1.0f / x; }
-MH_DEV float rsqrt_(float x) { return __builtin_sqrtf(1.0f / x); }
+// rcp(x) == 1.0f / x correctly rounded (the numerics contract),
+// in 3 VALU on the common path: v_rcp_f32 (<= 1 ulp) and one Newton step on
+// fma give RN(1/x) for every 2^-126 <= |x| < 2^126 -- checked bit for bit
+// against the IEEE division for all 2^32 inputs on gfx950
+// (tools/exp_rcp.hip).  Lanes outside that range (zero, denormals,
+// |x| >= 2^126, inf, NaN) take the full division behind a wave vote.
+MH_DEV bool rcp_fast_ok(float x) { return (__builtin_fabsf(x) >= 0x1p-126f) & (__builtin_fabsf(x) < 0x1p126f); }
+// some active lane is outside the fast range (two ballots straight off the
+// compares, so no lane mask is materialised in a VGPR)
+MH_DEV bool rcp_fast_any_bad(float x) {
+    const float a = __builtin_fabsf(x);
+    return (__builtin_amdgcn_ballot_w64(!(a >= 0x1p-126f)) | __builtin_amdgcn_ballot_w64(!(a < 0x1p126f))) != 0;
+}
+// the full division, kept behind its branch (a volatile asm cannot be
+// speculated, so the compiler does not if-convert it into every lane's path)
+MH_DEV float rcp_slow(float x) {
+    asm volatile("" : "+v"(x));
+    return 1.0f / x;
+}
+MH_DEV float rcp_core(float x) {
+    const float y = __builtin_amdgcn_rcpf(x);
+    return __builtin_fmaf(__builtin_fmaf(-x, y, 1.f), y, y);
+}
+MH_DEV float rcp(float x) {
+    float y = rcp_core(x);
+    if (rcp_fast_any_bad(x)) {
+        if (!rcp_fast_ok(x)) y = rcp_slow(x);
+    }
+    return y;
+}
+MH_DEV float rsqrt_(float x) { return __builtin_sqrtf(rcp(x)); }
 MH_DEV V3 normalize(V3 v) { return v * rsqrt_(dot(v, v)); }
 MH_DEV float norm(V3 v) { return __builtin_sqrtf(dot(v, v)); }
 MH_DEV float hmax(V3 v) { return fmaxf(fmaxf(v.x, v.y), v.z); }

@@ -61,7 +61,7 @@ MH_DEV bool prim_test(const Prim &p, const RayT &r, float &t, float &u, float &v
 // in outcome.  The primitive tests still use the true direction.
 MH_DEV float safe_rcp_dir(float d) {
     const float e = 0x1p-80f;
-    return 1.f / (__builtin_fabsf(d) > e ? d : __builtin_copysignf(e, d));
+    return rcp(__builtin_fabsf(d) > e ? d : __builtin_copysignf(e, d));
 }
 MH_DEV V3 safe_inv_dir(V3 d) { return v3(safe_rcp_dir(d.x), safe_rcp_dir(d.y), safe_rcp_dir(d.z)); }
 
@@ -530,6 +530,16 @@ typedef float F2 __attribute__((ext_vector_type(2)));
 MH_DEV F2 fma2(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
 MH_DEV F2 sp2(float a) { F2 r; r.x = a; r.y = a; return r; }
 MH_DEV F2 pair(float a, float b) { F2 r; r.x = a; r.y = b; return r; }
+// two rcp() (mh_device.hpp) with the Newton step on packed f32 and one vote
+MH_DEV F2 rcp2(F2 x) {
+    const F2 y0 = pair(__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y));
+    F2 y = fma2(fma2(-x, y0, sp2(1.f)), y0, y0);
+    if (rcp_fast_any_bad(x.x) | rcp_fast_any_bad(x.y)) {
+        if (!rcp_fast_ok(x.x)) y.x = rcp_slow(x.x);
+        if (!rcp_fast_ok(x.y)) y.y = rcp_slow(x.y);
+    }
+    return y;
+}
 
 // field k (dword) of primitive record i, read through the scalar cache at a
 // wave-uniform index (no Prim copy in registers / private memory)
@@ -573,7 +583,7 @@ MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit 
     // pvec = cross(d, e2)
     const F2 px = fma2(dy, e2z, -(dz * e2y)), py = fma2(dz, e2x, -(dx * e2z)), pz = fma2(dx, e2y, -(dy * e2x));
     const F2 det = fma2(e1z, pz, fma2(e1y, py, e1x * px));
-    const F2 inv_det = pair(1.0f / det.x, 1.0f / det.y);
+    const F2 inv_det = rcp2(det);
     const F2 tx = sp2(r.o.x) - pair(pf(P, pos, 0), pf(P, pos + 1u, 0)), ty = sp2(r.o.y) - pair(pf(P, pos, 1), pf(P, pos + 1u, 1)),
              tz = sp2(r.o.z) - pair(pf(P, pos, 2), pf(P, pos + 1u, 2));
     const F2 u = fma2(tz, pz, fma2(ty, py, tx * px)) * inv_det;
@@ -1656,7 +1666,7 @@ MH_DEV bool bbox_ray_intersect(const float *mn, const float *mx, const RayT &r, 
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         active = active && (d[i] != 0.f || (o[i] > mn[i] || o[i] < mx[i]));
-        const float rc = 1.f / d[i];
+        const float rc = rcp(d[i]);
         const float t1 = (mn[i] - o[i]) * rc, t2 = (mx[i] - o[i]) * rc;
         t1p[i] = fminf(t1, t2);
         t2p[i] = fmaxf(t1, t2);
