@@ -83,7 +83,7 @@ struct mh_scene {
     bool own_stream = false;
     DScene S{};
     // device buffers
-    DevBuf nodes, nodes4, prims, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
+    DevBuf nodes, nodes4, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
@@ -234,9 +234,22 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         key_sp[2 * (size_t)q.info.w] = q.info.x;
         key_sp[2 * (size_t)q.info.w + 1] = q.info.y;
     }
+    // pair records of the packet engine: record i interleaves the dwords of
+    // leaf-ordered primitives i and i + 1 (the last one with itself); only
+    // scenes small enough for that engine (wf_packet_max_prims) get them
+    std::vector<uint32_t> pairs(bvh.n_prims <= wf_packet_max_prims() ? 32 * (size_t)bvh.n_prims : 0);
+    for (uint32_t i = 0; i < pairs.size() / 32; ++i) {
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(bvh.prims.data()) + 16 * (size_t)i;
+        const uint32_t *b = reinterpret_cast<const uint32_t *>(bvh.prims.data()) + 16 * (size_t)std::min(i + 1, bvh.n_prims - 1);
+        for (int k = 0; k < 16; ++k) {
+            pairs[32 * (size_t)i + 2 * k] = a[k];
+            pairs[32 * (size_t)i + 2 * k + 1] = b[k];
+        }
+    }
     if (upload(s->nodes, bvh.nodes.data(), bvh.nodes.size(), st) != hipSuccess ||
+        upload(s->prim_pairs, pairs.data(), pairs.size(), st) != hipSuccess ||
         upload(s->prims, bvh.prims.data(), bvh.prims.size(), st) != hipSuccess ||
-        upload(s->key_sp, key_sp.data(), 4 * key_sp.size(), st) != hipSuccess)
+        upload(s->key_sp, key_sp.data(), key_sp.size(), st) != hipSuccess)
         return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: BVH upload failed");
 
     // ---- shading-time records ----
@@ -352,6 +365,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.nodes = s->nodes.as<Node>();
     S.prims = s->prims.as<Prim>();
     S.key_sp = s->key_sp.as<uint2>();
+    S.prim_pairs = s->prim_pairs.as<Prim>();
     S.shapes = s->shapes.as<DShape>();
     S.bsdf_type = s->bsdf_type.as<uint32_t>();
     S.bsdf_tex = s->bsdf_tex.as<uint32_t>();
@@ -429,7 +443,7 @@ int mh_scene_destroy(mh_scene *s) {
     if (!s) return MH_OK;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
+    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw})

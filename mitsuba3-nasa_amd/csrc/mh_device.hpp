@@ -102,6 +102,7 @@ struct DScene {                 // kernel argument (by value)
     const float *grid;             // volume grid data
     const Node4 *nodes4;           // wide BVH of the stream engine (nullptr: BVH2 only)
     const uint2 *key_sp;           // scene-order key -> (shape, prim) (packet engine)
+    const Prim *prim_pairs;        // interleaved pair records of the packet engine (mh_shading.hpp pp())
     uint32_t n_nodes, n_prims, n_emitters, environment;
     uint32_t n_media, camera_medium;
     uint32_t vol_flags;            // prbvolpath prepare_scene flags (kVol*)

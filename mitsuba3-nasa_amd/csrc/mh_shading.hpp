@@ -545,47 +545,59 @@ MH_DEV F2 rcp2(F2 x) {
 // wave-uniform index (no Prim copy in registers / private memory)
 MH_DEV float pf(const Prim *P, uint32_t i, uint32_t k) { return ((CFloat *)(P + i))[k]; }
 MH_DEV uint32_t pu(const Prim *P, uint32_t i, uint32_t k) { return __float_as_uint(((CFloat *)(P + i))[k]); }
+// Pair records of the packet engine (DScene::prim_pairs): the record at
+// leaf-ordered position i interleaves the 16 dwords of primitives i and i + 1
+// (dword 2k = field k of i, 2k + 1 = field k of i + 1; 128 B), so field k of
+// both is one SGPR pair, the direct operand of a v_pk_* instruction (no
+// scalar moves to assemble pairs).
+MH_DEV F2 pp(const Prim *Q, uint32_t i, uint32_t k) {
+    CFloat *p = (CFloat *)(Q + 2u * i) + 2u * k;
+    return pair(p[0], p[1]);
+}
 
 template <bool Shadow>
-MH_DEV void rect_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(0);
     // rows of to_object: x = a, y = b, z = c (shapes/rectangle.cpp:446-470)
     const F2 ox = sp2(r.o.x), oy = sp2(r.o.y), oz = sp2(r.o.z);
     const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
-    const F2 c0 = pair(pf(P, pos, 8), pf(P, pos + 1u, 8)), c1 = pair(pf(P, pos, 9), pf(P, pos + 1u, 9)), c2 = pair(pf(P, pos, 10), pf(P, pos + 1u, 10));
-    const F2 lz = fma2(c2, oz, fma2(c1, oy, fma2(c0, ox, pair(pf(P, pos, 11), pf(P, pos + 1u, 11)))));
+    const F2 c0 = pp(Q, pos, 8), c1 = pp(Q, pos, 9), c2 = pp(Q, pos, 10);
+    const F2 lz = fma2(c2, oz, fma2(c1, oy, fma2(c0, ox, pp(Q, pos, 11))));
     const F2 ldz = fma2(c2, dz, fma2(c1, dy, c0 * dx));
     const F2 tt = pair(-lz.x / ldz.x, -lz.y / ldz.y);
     const float bound = Shadow ? r.maxt : h.t;
     bool okA = live & (tt.x >= 0.f) & (tt.x <= bound), okB = live & (tt.y >= 0.f) & (tt.y <= bound);
     if (!wave_any(okA | okB)) return;
     MH_CNT(1);
-    const F2 a0 = pair(pf(P, pos, 0), pf(P, pos + 1u, 0)), a1 = pair(pf(P, pos, 1), pf(P, pos + 1u, 1)), a2 = pair(pf(P, pos, 2), pf(P, pos + 1u, 2));
-    const F2 b0 = pair(pf(P, pos, 4), pf(P, pos + 1u, 4)), b1 = pair(pf(P, pos, 5), pf(P, pos + 1u, 5)), b2 = pair(pf(P, pos, 6), pf(P, pos + 1u, 6));
-    const F2 lox = fma2(a2, oz, fma2(a1, oy, fma2(a0, ox, pair(pf(P, pos, 3), pf(P, pos + 1u, 3)))));
-    const F2 loy = fma2(b2, oz, fma2(b1, oy, fma2(b0, ox, pair(pf(P, pos, 7), pf(P, pos + 1u, 7)))));
+    const F2 a0 = pp(Q, pos, 0), a1 = pp(Q, pos, 1), a2 = pp(Q, pos, 2);
+    const F2 b0 = pp(Q, pos, 4), b1 = pp(Q, pos, 5), b2 = pp(Q, pos, 6);
+    const F2 lox = fma2(a2, oz, fma2(a1, oy, fma2(a0, ox, pp(Q, pos, 3))));
+    const F2 loy = fma2(b2, oz, fma2(b1, oy, fma2(b0, ox, pp(Q, pos, 7))));
     const F2 ldx = fma2(a2, dz, fma2(a1, dy, a0 * dx));
     const F2 ldy = fma2(b2, dz, fma2(b1, dy, b0 * dx));
     const F2 lx = fma2(ldx, tt, lox), ly = fma2(ldy, tt, loy);
     okA = okA & (__builtin_fabsf(lx.x) <= 1.f) & (__builtin_fabsf(ly.x) <= 1.f);
     okB = okB & (__builtin_fabsf(lx.y) <= 1.f) & (__builtin_fabsf(ly.y) <= 1.f);
-    packet_take<Shadow>(okA, tt.x, lx.x, ly.x, pu(P, pos, 15), h);
-    packet_take<Shadow>(okB, tt.y, lx.y, ly.y, pu(P, pos + 1u, 15), h);
+    const F2 key = pp(Q, pos, 15);
+    packet_take<Shadow>(okA, tt.x, lx.x, ly.x, __float_as_uint(key.x), h);
+    packet_take<Shadow>(okB, tt.y, lx.y, ly.y, __float_as_uint(key.y), h);
 }
 
 template <bool Shadow>
-MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
+MH_DEV void tri_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(2);
     // Moeller-Trumbore (render/mesh.h:430-453) on two triangles
     const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
-    const F2 e1x = pair(pf(P, pos, 4), pf(P, pos + 1u, 4)), e1y = pair(pf(P, pos, 5), pf(P, pos + 1u, 5)), e1z = pair(pf(P, pos, 6), pf(P, pos + 1u, 6));
-    const F2 e2x = pair(pf(P, pos, 8), pf(P, pos + 1u, 8)), e2y = pair(pf(P, pos, 9), pf(P, pos + 1u, 9)), e2z = pair(pf(P, pos, 10), pf(P, pos + 1u, 10));
+    const F2 e1x = pp(Q, pos, 4), e1y = pp(Q, pos, 5), e1z = pp(Q, pos, 6);
+    const F2 e2x = pp(Q, pos, 8), e2y = pp(Q, pos, 9), e2z = pp(Q, pos, 10);
     // pvec = cross(d, e2)
     const F2 px = fma2(dy, e2z, -(dz * e2y)), py = fma2(dz, e2x, -(dx * e2z)), pz = fma2(dx, e2y, -(dy * e2x));
     const F2 det = fma2(e1z, pz, fma2(e1y, py, e1x * px));
+    // tvec ahead of the reciprocal: its loads are issued before the
+    // reciprocal's (rare) slow-path branch splits the block
+    const F2 tx = sp2(r.o.x) - pp(Q, pos, 0), ty = sp2(r.o.y) - pp(Q, pos, 1),
+             tz = sp2(r.o.z) - pp(Q, pos, 2);
     const F2 inv_det = rcp2(det);
-    const F2 tx = sp2(r.o.x) - pair(pf(P, pos, 0), pf(P, pos + 1u, 0)), ty = sp2(r.o.y) - pair(pf(P, pos, 1), pf(P, pos + 1u, 1)),
-             tz = sp2(r.o.z) - pair(pf(P, pos, 2), pf(P, pos + 1u, 2));
     const F2 u = fma2(tz, pz, fma2(ty, py, tx * px)) * inv_det;
     bool okA = live & (u.x >= 0.f) & (u.x <= 1.f), okB = live & (u.y >= 0.f) & (u.y <= 1.f);
     if (!wave_any(okA | okB)) return;
@@ -597,8 +609,9 @@ MH_DEV void tri_pair(const Prim *P, uint32_t pos, bool live, const RayT r, PHit 
     const F2 uv = u + v;
     okA = okA & (v.x >= 0.f) & (uv.x <= 1.f) & (tt.x >= 0.f) & (tt.x <= r.maxt);
     okB = okB & (v.y >= 0.f) & (uv.y <= 1.f) & (tt.y >= 0.f) & (tt.y <= r.maxt);
-    packet_take<Shadow>(okA, tt.x, u.x, v.x, pu(P, pos, 15), h);
-    packet_take<Shadow>(okB, tt.y, u.y, v.y, pu(P, pos + 1u, 15), h);
+    const F2 key = pp(Q, pos, 15);
+    packet_take<Shadow>(okA, tt.x, u.x, v.x, __float_as_uint(key.x), h);
+    packet_take<Shadow>(okB, tt.y, u.y, v.y, __float_as_uint(key.y), h);
 }
 
 template <bool Shadow>
@@ -646,19 +659,19 @@ MH_DEV void tri_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &
 // empty -- a uniform branch; the values a surviving lane sees are computed
 // exactly as in rect_test / tri_test.
 template <bool Shadow>
-MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, uint32_t nrect, bool lane_hit,
+MH_DEV void packet_leaf(const Prim *prims, const Prim *pairs, uint32_t first, uint32_t count, uint32_t nrect, bool lane_hit,
                         const RayT r, PHit &h) {
     // rectangles [0, nrect), then triangles [nrect, count): straight-line
     // loops (one body each) rather than one loop with a per-step type switch
     uint32_t i = 0;
     for (; i + 1u < nrect; i += 2u)
-        rect_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
+        rect_pair<Shadow>(pairs, first + i, lane_hit & (!Shadow || !h.occl), r, h);
     if (i < nrect) {
         rect_one<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
         ++i;
     }
     for (; i + 1u < count; i += 2u)
-        tri_pair<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
+        tri_pair<Shadow>(pairs, first + i, lane_hit & (!Shadow || !h.occl), r, h);
     if (i < count) tri_one<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
 }
 
@@ -667,7 +680,7 @@ MH_DEV void packet_leaf(const Prim *prims, uint32_t first, uint32_t count, uint3
 // One batch: the wave's 64 rays (act: lanes that hold a ray).  ws: the
 // wave-uniform stack (entry k at ws[k * stride]).
 template <bool Shadow>
-MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const uint2 *key_sp, uint32_t *ws, uint32_t stride,
+MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpairs, const uint2 *key_sp, uint32_t *ws, uint32_t stride,
                         const RayT r, bool act) {
     const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
     PHit ph;
@@ -689,11 +702,11 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const uint2 *key
         const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w) & kLeafCountMask;
         bool any0 = wave_any(h0), any1 = wave_any(h1);
         if (any0 && n0) {
-            packet_leaf<Shadow>(gprims, c0, n0, __float_as_uint(n.hi0.w) >> kLeafRectShift, h0, r, ph);
+            packet_leaf<Shadow>(gprims, gpairs, c0, n0, __float_as_uint(n.hi0.w) >> kLeafRectShift, h0, r, ph);
             any0 = false;
         }
         if (any1 && n1) {
-            packet_leaf<Shadow>(gprims, c1, n1, __float_as_uint(n.hi1.w) >> kLeafRectShift, h1, r, ph);
+            packet_leaf<Shadow>(gprims, gpairs, c1, n1, __float_as_uint(n.hi1.w) >> kLeafRectShift, h1, r, ph);
             any1 = false;
         }
         if (Shadow) act = act && !ph.occl;
@@ -734,7 +747,7 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const uint2 *key
 }
 
 template <bool Shadow, class Load, class Store>
-MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const uint2 *key_sp, const LdsBvh &B, uint32_t r0,
+MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const Prim *gpairs, const uint2 *key_sp, const LdsBvh &B, uint32_t r0,
                          uint32_t r1,
                          Load load, Store store) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -745,7 +758,7 @@ MH_DEV void trace_packet(const Node *gnodes, const Prim *gprims, const uint2 *ke
         RayT r;
         if (has) r = load(item);
         else r = RayT{v3(0, 0, 0), v3(0, 0, 1), -1.f};
-        const Hit hit = packet_batch<Shadow>(gnodes, gprims, key_sp, ws, B.stride, r, has);
+        const Hit hit = packet_batch<Shadow>(gnodes, gprims, gpairs, key_sp, ws, B.stride, r, has);
         if (has) store(item, hit, hit.shape != MH_INVALID);
     }
 }

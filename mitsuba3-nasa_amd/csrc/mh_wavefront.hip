@@ -52,7 +52,7 @@ struct WfState {
 // Per bounce: kSeg x 32 uint32: [s*32 + 0] queue length, [s*32 + 1] shadow length.
 constexpr uint32_t kSeg = 64;
 #ifndef MH_BOUNCE_WAVES
-#define MH_BOUNCE_WAVES 4  // fused bounce kernels: waves per SIMD the register budget targets
+#define MH_BOUNCE_WAVES 5  // fused bounce kernels: waves per SIMD the register budget targets
 #endif
 constexpr uint32_t kCtrStride = kSeg * 32;
 constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
@@ -62,6 +62,7 @@ constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
 // per-lane stack, broadcast node reads), per-lane while-while otherwise.
 // MH_TRAVERSAL=packet|lane overrides (tests cover both).
 constexpr uint32_t kPacketMaxPrims = 64;
+uint32_t wf_packet_max_prims() { return kPacketMaxPrims; }
 static bool use_packet(const DScene &S) {
     const char *e = getenv("MH_TRAVERSAL");
     if (e && !strcmp(e, "packet")) return true;
@@ -229,7 +230,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
         const uint32_t j = base + i;
         w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
     };
-    if (Packet) trace_packet<false>(S.nodes, S.prims, S.key_sp, B, r0, r1, load, store);
+    if (Packet) trace_packet<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<false, true>(B, r0, r1, load, store);
     else trace_stream<false>(B, r0, r1, load, store);
 }
@@ -411,12 +412,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
             ray.maxt = w.mt[cur][j];
         }
-        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, ray, has);
+        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has);
 #ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
         {
             RayT r2 = ray;
             asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<false>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, r2, has);
+            const Hit h2 = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, has);
             asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.u));
         }
 #endif
@@ -497,12 +498,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
         }
         // ---- visibility of the NEE sample (scene.cpp:201-210)
-        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, sray, shadow);
+        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow);
 #ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
         {
             RayT r2 = sray;
             asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<true>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, r2, shadow);
+            const Hit h2 = packet_batch<true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, shadow);
             asm volatile("" ::"v"(h2.shape));
         }
 #endif
@@ -549,7 +550,7 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
         L = fma3(v3(w.sax[j], w.say[j], w.saz[j]), v3(w.sbx[j], w.sby[j], w.sbz[j]), L);
         out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
     };
-    if (Packet) trace_packet<true>(S.nodes, S.prims, S.key_sp, B, r0, r1, load, store);
+    if (Packet) trace_packet<true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
     else trace_stream<true>(B, r0, r1, load, store);
 }
@@ -906,7 +907,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
             ray.maxt = w.mt[cur][j];
         }
-        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, ray, i < n);
+        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n);
         if (i < n) {
             beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
             prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
@@ -1003,7 +1004,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             alive = active_next;
         }
         // ---- visibility of the NEE sample; the record is charged if unoccluded
-        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.key_sp, ws, 1u, sray, shadow);
+        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow);
         if (shadow && sh.shape == MH_INVALID) {
 #pragma unroll
             for (int kk = 0; kk < NR; ++kk)
@@ -1068,7 +1069,7 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
                 acc[kk][2] += q.G(kk * 3 + 2)[j];
             }
     };
-    if (Packet) trace_packet<true>(S.nodes, S.prims, S.key_sp, B, r0, r1, load, store);
+    if (Packet) trace_packet<true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
     else trace_stream<true>(B, r0, r1, load, store);
     flush_partial(acc, q);
