@@ -666,7 +666,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         if (wavefront) {
             MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
                                     s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
-                                    n_bounces, (uint32_t)cus * 8, ev + 2, st));
+                                    n_bounces, wf_blocks(cus), ev + 2, st));
         } else {
             MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
                                  s->counters.as<unsigned long long>(), st));
@@ -747,7 +747,7 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(n)));
         MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, 4 * (size_t)wf_counter_words(in->max_depth))));
         MH_HIP(launch_wavefront(s->S, *in, lm, s->S.sampler_seed + seed, n, n, dst, s->wf_ws.ptr, n,
-                                s->wf_ctr.as<uint32_t>(), in->max_depth, (uint32_t)cus * 8, nullptr, st));
+                                s->wf_ctr.as<uint32_t>(), in->max_depth, wf_blocks(cus), nullptr, st));
     } else {
         MH_HIP(launch_render(s->S, *in, lm, s->S.sampler_seed + seed, 1, n, n, dst,
                              s->counters.as<unsigned long long>(), st));
@@ -965,7 +965,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (wavefront) {
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
-        const uint32_t grid = wf_grid((uint32_t)cus * 8);
+        const uint32_t grid = wf_grid(wf_blocks(cus));
         const char *ec = getenv("MH_WF_CHUNK");
         const uint64_t max_samples = std::min<uint64_t>(
             wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 23));

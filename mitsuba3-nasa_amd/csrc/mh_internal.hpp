@@ -70,6 +70,7 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             hipEvent_t *trace_ev, hipStream_t st);
 size_t wf_prb_workspace_bytes(uint64_t cap);
 uint32_t wf_grid(uint32_t grid);
+uint32_t wf_blocks(int cus);  // wavefront workgroups for a device of `cus` CUs
 uint32_t wf_packet_max_prims();  // largest scene (primitives) the packet engine traces
 bool wf_fused(const DScene &S);  // launch_wavefront runs the fused bounce kernel  // grid rounded to whole queue segments
 hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,

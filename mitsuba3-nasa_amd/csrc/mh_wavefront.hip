@@ -1144,6 +1144,15 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
 bool wf_fused(const DScene &S) { return use_packet(S) && S.tab_bytes != 0 && !wf_unfused(); }
 
 uint32_t wf_grid(uint32_t grid) { return std::max<uint32_t>(kSeg, grid / kSeg * kSeg); }
+// Workgroups of the wavefront kernels.  A wave's share of a queue is fixed
+// (stride loop), and a CU holds 5 bounce workgroups at a time, so a grid of a
+// few resident rounds leaves CUs idle in its last round; many small rounds
+// even the tail out (MH_WF_BPC overrides for experiments: tools/exp_bpc.sh).
+uint32_t wf_blocks(int cus) {
+    uint32_t bpc = 30;  // measured: 8 -> 54.6, 20 -> 51.4, 30 -> 51.2, 60 -> 52.3 ms per bench step
+    if (const char *e = getenv("MH_WF_BPC")) bpc = std::max(1, atoi(e));
+    return (uint32_t)cus * bpc;
+}
 
 hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
                                  hipStream_t st) {
