@@ -179,9 +179,11 @@ def main():
             # fused bounce kernel: per path-bounce the state is read
             # (pd 4 + ray 28 + throughput 12 + prev_p 12 + prev_pdf 4 + PCG 8 + L 12
             # = 80 B) and written for survivors (80 B); a finished path writes L (12 B).
+            # The first bounce generates its camera rays in registers (no state read)
+            # and writes the film position (8 B) of every sample.
             # sum of queue lengths R = rays_closest, survivors R - N, deaths N = samples
             R, N = float(st_f.rays_closest), float(n_local)
-            bytes_launch = (80.0 * R + 80.0 * (R - N) + 12.0 * N) / launches
+            bytes_launch = (80.0 * (R - N) + 80.0 * (R - N) + 12.0 * N + 8.0 * N) / launches
             kname = "k_wf_bounce"
         else:
             bytes_launch = rays_per_launch * 48.0

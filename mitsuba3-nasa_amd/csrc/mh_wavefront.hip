@@ -381,12 +381,24 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
 // one wave overlapping the state streams of the others.
 // LDS: shading tables (tab_bytes) + one traversal stack per wave.
 // ---------------------------------------------------------------------------
+// Gen: the first bounce generates its paths (k_wf_raygen's camera ray, PCG32
+// state and film position) in registers instead of reading them from the
+// queue -- the 80-B path state of every camera ray never goes to HBM.  Slot j
+// of bounce 0 is path j; n_total: paths of the chunk.
+template <bool Gen>
 __global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane, float *out,
-            WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+            WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
-    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n;
+    if (Gen) {
+        const uint64_t b0 = (uint64_t)it.seg * seg_cap;
+        n = b0 >= n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, n_total - b0);
+        if (blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
+    } else {
+        n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!block_has_stride_work(it, n)) return;
     const DScene S = stage_tables(S0, lds);
     uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
@@ -404,13 +416,28 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         V3 tp, a_nee, b_nee, prev_p, L;
         float eta = 1.f, prev_pdf = 1.f;
         Pcg rng;
+        uint64_t gen_state = 0;
         if (has) {
-            const uint32_t pd = w.pd[cur][j];
-            pid = pd & kPidMask;
-            depth = pd >> kPidBits;
-            ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
-            ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
-            ray.maxt = w.mt[cur][j];
+            if (Gen) {  // k_wf_raygen (integrator.cpp:1139-1176, perspective.cpp:240-281)
+                pid = j;
+                uint32_t lane, px, py;
+                lane_of(lm, pid, lane, px, py);
+                Pcg g;
+                g.seed(seed_value, lane);
+                const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
+                ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
+                                 __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
+                gen_state = g.state;
+                out[3 * plane + pid] = sx;
+                out[4 * plane + pid] = sy;
+            } else {
+                const uint32_t pd = w.pd[cur][j];
+                pid = pd & kPidMask;
+                depth = pd >> kPidBits;
+                ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+                ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+                ray.maxt = w.mt[cur][j];
+            }
         }
         const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has);
 #ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
@@ -422,15 +449,23 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         }
 #endif
         if (has) {
-            tp = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
-            L = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
+            if (Gen) {
+                tp = v3(1.f, 1.f, 1.f);
+                L = v3(0.f, 0.f, 0.f);
+                prev_p = v3(0.f, 0.f, 0.f);
+                prev_pdf = 1.f;
+                rng.state = gen_state;
+            } else {
+                tp = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+                L = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
+                prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+                prev_pdf = w.ppdf[cur][j];
+                rng.state = w.rng[cur][j];
+            }
             eta = 1.f;  // diffuse / null BSDFs: eta stays 1, only the camera vertex is delta
             const bool prev_delta = depth == 0;
-            prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
-            prev_pdf = w.ppdf[cur][j];
             uint32_t lane, px, py;
             lane_of(lm, pid, lane, px, py);
-            rng.state = w.rng[cur][j];
             rng.inc = pcg_inc(seed_value, lane);
             SI si;
             compute_si(S, ray, h, si);
@@ -569,20 +604,25 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     WfState w = carve(ws, cap);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_wf_raygen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
-                       seed_value, n, plane, out, w, ctr);
     const size_t sh = lds_bytes(S, 256);
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
     const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
+    if (!fused)  // the fused first bounce generates its camera rays itself
+        hipLaunchKernelGGL(k_wf_raygen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
+                           seed_value, n, plane, out, w, ctr);
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
             if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
-            hipLaunchKernelGGL(k_wf_bounce, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S, in, lm,
-                               seed_value, plane, out, w, cur, seg_cap, c, cn);
+            if (b == 0)
+                hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S,
+                                   in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n);
+            else
+                hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st,
+                                   S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n);
             if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
             continue;
         }
