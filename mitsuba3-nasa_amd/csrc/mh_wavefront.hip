@@ -910,13 +910,27 @@ k_wf_shade_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, 
 // gradient record is charged at once (same operations and order as
 // k_wf_trace -> k_wf_shade_prb -> k_wf_shadow_prb; only the order in which
 // the per-thread gradient registers accumulate differs).
-template <int NR>
+// First-bounce generation for the fused PRB bounce (k_wf_raygen_prb in
+// registers): camera ray, PCG32 state and the dL gather of the sample.
+struct PrbGen {
+    uint64_t n_total;          // paths of the chunk (0: not the first bounce)
+    const float *grad_in;      // grad_in / W (common.py:936-965)
+    int coalesce;
+};
+template <int NR, bool Gen>
 __global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
-                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
-    const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n;
+    if (Gen) {
+        const uint64_t b0 = (uint64_t)it.seg * seg_cap;
+        n = b0 >= gen.n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, gen.n_total - b0);
+        if (blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
+    } else {
+        n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!block_has_stride_work(it, n)) return;
     const DScene S = stage_tables(S0, lds);
     uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
@@ -939,29 +953,52 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         float A[NR][3], G[NR][3];
         Pcg rng;
         const uint32_t j = sbase + i;
+        uint64_t gen_state = 0;
         if (i < n) {
-            const uint32_t pd = w.pd[cur][j];
-            pid = pd & kPidMask;
-            depth = pd >> kPidBits;
-            ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
-            ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
-            ray.maxt = w.mt[cur][j];
+            if (Gen) {  // k_wf_raygen_prb (integrator.cpp:1139-1176, common.py:936-965)
+                pid = j;
+                uint32_t lane, px, py;
+                lane_of(lm, pid, lane, px, py);
+                Pcg g;
+                g.seed(seed_value, lane);
+                const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
+                ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
+                                 __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
+                gen_state = g.state;
+                dL = gather_dL(S0, gen.coalesce, gen.grad_in, sx, sy);
+            } else {
+                const uint32_t pd = w.pd[cur][j];
+                pid = pd & kPidMask;
+                depth = pd >> kPidBits;
+                ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+                ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+                ray.maxt = w.mt[cur][j];
+            }
         }
         const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n);
         if (i < n) {
-            beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
-            prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
-            prev_pdf = w.ppdf[cur][j];
-            dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
+            if (Gen) {
+                beta = v3(1.f, 1.f, 1.f);
+                prev_p = v3(0.f, 0.f, 0.f);
+                prev_pdf = 1.f;
 #pragma unroll
-            for (int kk = 0; kk < NR; ++kk)
+                for (int kk = 0; kk < NR; ++kk) A[kk][0] = A[kk][1] = A[kk][2] = 0.f;
+                rng.state = gen_state;
+            } else {
+                beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+                prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+                prev_pdf = w.ppdf[cur][j];
+                dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
+                for (int kk = 0; kk < NR; ++kk)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
+                rng.state = w.rng[cur][j];
+            }
             const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
             const float eta = 1.f;
             uint32_t lane, px, py;
             lane_of(lm, pid, lane, px, py);
-            rng.state = w.rng[cur][j];
             rng.inc = pcg_inc(seed_value, lane);
             SI si;
             compute_si(S, ray, h, si);
@@ -1140,23 +1177,34 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     WfPrb q = carve_prb(ws_prb, cap, partial, slot_of_tex, n_rgb);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
-                       seed_value, n, coalesce, grad_in, weights, w, q, ctr);
     const size_t sh = lds_bytes(S, 256);
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
     const size_t sh_fused = S.tab_bytes + 16u * S.stack_size;
+    if (!fused)  // the fused first bounce generates its camera rays itself
+        hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
+                           seed_value, n, coalesce, grad_in, weights, w, q, ctr);
+    const PrbGen gen{n, grad_in, coalesce};
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
-            if (n_rgb == 1)
-                hipLaunchKernelGGL((k_wf_bounce_prb<1>), dim3(grid), dim3(256), sh_fused, st, S, in, lm, seed_value,
-                                   w, q, cur, seg_cap, c, cn);
-            else
-                hipLaunchKernelGGL((k_wf_bounce_prb<kMaxRgbParams>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,
-                                   seed_value, w, q, cur, seg_cap, c, cn);
+            if (n_rgb == 1) {
+                if (b == 0)
+                    hipLaunchKernelGGL((k_wf_bounce_prb<1, true>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,
+                                       seed_value, w, q, cur, seg_cap, c, cn, gen);
+                else
+                    hipLaunchKernelGGL((k_wf_bounce_prb<1, false>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,
+                                       seed_value, w, q, cur, seg_cap, c, cn, gen);
+            } else {
+                if (b == 0)
+                    hipLaunchKernelGGL((k_wf_bounce_prb<kMaxRgbParams, true>), dim3(grid), dim3(256), sh_fused, st, S,
+                                       in, lm, seed_value, w, q, cur, seg_cap, c, cn, gen);
+                else
+                    hipLaunchKernelGGL((k_wf_bounce_prb<kMaxRgbParams, false>), dim3(grid), dim3(256), sh_fused, st,
+                                       S, in, lm, seed_value, w, q, cur, seg_cap, c, cn, gen);
+            }
             continue;
         }
         MH_WF_DISPATCH(k_wf_trace, S, w, cur, seg_cap, c);
