@@ -194,10 +194,13 @@ def main():
         if os.path.exists(tpath):
             try:
                 ks = json.load(open(tpath)).get("kernels", {})
-                cand = [(v["calls"], k, v) for k, v in ks.items() if k.startswith(kname + "<") or k == kname]
-                if cand:
-                    _, kname, ent = max(cand)
-                    traffic = round(ent["hbm_bytes_per_call"])
+                # calls-weighted mean over the template instances of the family
+                # (k_wf_bounce<true> = first bounce, <false> = the others), the
+                # same launches the HIP-event average above covers
+                fam = [v for k, v in ks.items() if k.startswith(kname + "<") or k == kname]
+                if fam:
+                    calls = sum(v["calls"] for v in fam)
+                    traffic = round(sum(v["calls"] * v["hbm_bytes_per_call"] for v in fam) / calls)
             except Exception:
                 traffic = None
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
