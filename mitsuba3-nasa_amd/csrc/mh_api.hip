@@ -631,7 +631,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     uint64_t max_samples = 1ull << 25;
     if (wavefront) {
         const char *ec = getenv("MH_WF_CHUNK");
-        max_samples = std::min<uint64_t>(wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 23));
+        max_samples = std::min<uint64_t>(wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
     }
     uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
     const uint64_t plane = (uint64_t)chunk_px * per_pixel;
@@ -947,7 +947,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
 
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
     // grad_in / W once per pixel (the adjoint of develop)
-    MH_HIP(s->gw.alloc(n_px * 12));
+    MH_HIP(s->gw.alloc(n_px * 16));  // float4 per pixel (k_grad_over_w)
     MH_HIP(launch_grad_over_w(n_px, g_in, w, s->gw.as<float>(), st));
     g_in = s->gw.as<float>();
     const uint32_t S_ = L.s_end - L.s_begin;
@@ -968,7 +968,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         const uint32_t grid = wf_grid(wf_blocks(cus));
         const char *ec = getenv("MH_WF_CHUNK");
         const uint64_t max_samples = std::min<uint64_t>(
-            wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : (1ull << 23));
+            wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
         const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
         const uint64_t cap = (uint64_t)chunk_px * S_;
         const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);

@@ -9,8 +9,9 @@
 //                       writes L and sample_pos SoA.
 //   k_prb_primal        per-lane PRB primal (prb.py:59-257) for mi.render(prb).
 //   k_splat_px          ImageBlock::put, coalesced Gaussian (imageblock.cpp:418-531):
-//                       one lane per pixel, 5x5x4 partial sums in VGPRs, one
-//                       global atomic per footprint texel per pixel.
+//                       16 lanes per pixel, 5x5x4 partial sums in VGPRs summed
+//                       across the DPP row, one global atomic per footprint
+//                       texel per pixel.
 //   k_splat_generic     ImageBlock::put for every other filter/spp case.
 //   k_develop           HDRFilm::develop (hdrfilm.cpp:349-405).
 //   k_prb_weights       W image of render_backward (common.py:936-947).
@@ -134,13 +135,31 @@ MH_DEV void splat_one_atomic(const DScene &S, float *film, float px, float py, c
 
 // Mode 0: RGBW film from stored (L, pos); mode 1: W-only image from the RNG
 // jitter (PRB weights; film has 1 channel).
+//
+// kSplatLanes (16) lanes share a pixel: lane g of the group takes samples
+// g, g + 16, ... (16 consecutive floats per plane read: one 64-B segment),
+// and the 16 partial footprints are summed across the DPP row before one
+// lane issues the footprint's atomics.  (A lane per pixel left a chunk of
+// 32k pixels at 512 waves for 1024 SIMDs, each walking 256 samples alone.)
+constexpr uint32_t kSplatLanes = 16;
+
+// sum over the 16 lanes of a DPP row; every lane of the row gets the total
+MH_DEV float row16_sum(float x) {
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
+    return x;
+}
+
 template <int Mode>
 __global__ void __launch_bounds__(128)
 k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t n_passes,
            uint64_t n, uint64_t plane, const float *__restrict__ in, float *__restrict__ film,
            uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin) {
-    uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pl >= n_pix) return;
+    const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t pl = gl / kSplatLanes, g = gl % kSplatLanes;
+    if (pl >= n_pix) return;  // whole DPP rows leave together (n_pix granularity = 16 lanes)
     const uint32_t W = S.width, H = S.height;
     const uint32_t pixel = pixel_begin + pl;
     const uint32_t py = pixel / W, px = pixel - py * W;
@@ -152,16 +171,28 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc[i][j][c] = 0.f;
     for (uint32_t pass = 0; pass < n_passes; ++pass) {
-        for (uint32_t j = 0; j < Sn; ++j) {
+        // Mode 0: the next sample's five floats are in flight while this one
+        // is weighted (one wave has the SIMD to itself at this VGPR count)
+        const float *src = in + (uint64_t)pass * n + (uint64_t)pl * Sn;
+        float nv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+        if (Mode == 0 && g < Sn) {
+#pragma unroll
+            for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + g];
+        }
+        for (uint32_t j = g; j < Sn; j += kSplatLanes) {
             float sx, sy, vals[4];
             if (Mode == 0) {
-                uint64_t o = (uint64_t)pass * n + (uint64_t)pl * Sn + j;
-                vals[0] = in[o];
-                vals[1] = in[plane + o];
-                vals[2] = in[2 * plane + o];
+                vals[0] = nv[0];
+                vals[1] = nv[1];
+                vals[2] = nv[2];
                 vals[3] = 1.f;
-                sx = in[3 * plane + o];
-                sy = in[4 * plane + o];
+                sx = nv[3];
+                sy = nv[4];
+                const uint32_t jn = j + kSplatLanes;
+                if (jn < Sn) {
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + jn];
+                }
             } else {
                 Pcg rng;
                 rng.seed(seed_value, pixel * spp_pp + s_begin + j);
@@ -211,6 +242,13 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
                 }
         }
     }
+#pragma unroll
+    for (int ys = 0; ys < 5; ++ys)
+#pragma unroll
+        for (int xs = 0; xs < 5; ++xs)
+#pragma unroll
+            for (int c = (Mode == 0 ? 0 : 3); c < 4; ++c) acc[ys][xs][c] = row16_sum(acc[ys][xs][c]);
+    if (g != 0) return;
 #pragma unroll
     for (int ys = 0; ys < 5; ++ys) {
         uint32_t yy = py - 2 + ys;
@@ -310,9 +348,9 @@ __global__ void k_grad_over_w(uint64_t n_px, const float *__restrict__ grad_in, 
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_px) return;
     const float Wp = w[i] == 0.f ? 1.f : w[i];
-    out[3 * i] = grad_in[3 * i] / Wp;
-    out[3 * i + 1] = grad_in[3 * i + 1] / Wp;
-    out[3 * i + 2] = grad_in[3 * i + 2] / Wp;
+    // float4 per pixel: gather_dL reads a footprint texel with one load
+    reinterpret_cast<float4 *>(out)[i] =
+        make_float4(grad_in[3 * i] / Wp, grad_in[3 * i + 1] / Wp, grad_in[3 * i + 2] / Wp, 0.f);
 }
 
 // HDRFilm::develop (films/hdrfilm.cpp:349-405): rgb / w, or luminance(rgb) / w
@@ -494,12 +532,13 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, b
     if (n == 0) return hipSuccess;
     if (fast) {
         const uint32_t bs = 128;
+        const uint64_t lanes = (uint64_t)n_pix * kSplatLanes;
         if (weights_mode)
-            hipLaunchKernelGGL(k_splat_px<1>, dim3(blocks_for(n_pix, bs)), dim3(bs), 0, st, S,
+            hipLaunchKernelGGL(k_splat_px<1>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S,
                                lm.pixel_begin, n_pix, lm.S, n_passes, n, plane, in, film,
                                seed_value, lm.spp_pp, lm.s_begin);
         else
-            hipLaunchKernelGGL(k_splat_px<0>, dim3(blocks_for(n_pix, bs)), dim3(bs), 0, st, S,
+            hipLaunchKernelGGL(k_splat_px<0>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S,
                                lm.pixel_begin, n_pix, lm.S, n_passes, n, plane, in, film,
                                seed_value, lm.spp_pp, lm.s_begin);
     } else {

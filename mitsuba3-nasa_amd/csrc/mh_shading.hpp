@@ -1420,14 +1420,18 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
 // ---------------------------------------------------------------------------
 // gw: grad_in / (W == 0 ? 1 : W) per pixel (k_grad_over_w), i.e. the adjoint
 // of develop, which Dr.Jit also evaluates once per pixel.
+// gw: grad_in / W as one float4 (r, g, b, 0) per pixel (k_grad_over_w), so a
+// footprint texel is one 16-B load
 MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *__restrict__ gw, float px, float py) {
+    const float4 *__restrict__ g4 = reinterpret_cast<const float4 *>(gw);
     const uint32_t W = S.width, H = S.height;
     float o0 = 0.f, o1 = 0.f, o2 = 0.f;
     if (S.rfilter == MH_RFILTER_BOX) {
         uint32_t ux = (uint32_t)(int32_t)floorf(px), uy = (uint32_t)(int32_t)floorf(py);
         if (ux < W && uy < H) {
             uint64_t p = (uint64_t)uy * W + ux;
-            o0 = gw[3 * p]; o1 = gw[3 * p + 1]; o2 = gw[3 * p + 2];
+            const float4 g = g4[p];
+            o0 = g.x; o1 = g.y; o2 = g.z;
         }
         return v3(o0, o1, o2);
     }
@@ -1440,18 +1444,20 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *__restrict__ gw,
         float wxs[5];
 #pragma unroll
         for (int32_t xs = 0; xs < 5; ++xs) wxs[xs] = xs < count ? gaussian_eval(S.filter_coeff, relx + (float)xs) : 0.f;
-        for (int32_t ys = 0; ys < count; ++ys) {
+#pragma unroll
+        for (int32_t ys = 0; ys < 5; ++ys) {
+            if (ys >= count) break;
             float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
             uint32_t yy = (uint32_t)(piy + ys);
 #pragma unroll
             for (int32_t xs = 0; xs < 5; ++xs) {
                 uint32_t xx = (uint32_t)(pix + xs);
                 if (xs < count && xx < W && yy < H) {
-                    uint64_t p = (uint64_t)yy * W + xx;
+                    const float4 g = g4[(uint64_t)yy * W + xx];
                     float w = wy * wxs[xs];
-                    o0 += gw[3 * p] * w;
-                    o1 += gw[3 * p + 1] * w;
-                    o2 += gw[3 * p + 2] * w;
+                    o0 += g.x * w;
+                    o1 += g.y * w;
+                    o2 += g.z * w;
                 }
             }
         }
@@ -1469,11 +1475,11 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *__restrict__ gw,
                 float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
                 int32_t xx = a0x + (int32_t)xs, yy = a0y + (int32_t)ys;
                 if (xx <= a1x && yy <= a1y) {
-                    uint64_t p = (uint64_t)yy * W + xx;
+                    const float4 g = g4[(uint64_t)yy * W + xx];
                     float w = wy * wx;
-                    o0 += gw[3 * p] * w;
-                    o1 += gw[3 * p + 1] * w;
-                    o2 += gw[3 * p + 2] * w;
+                    o0 += g.x * w;
+                    o1 += g.y * w;
+                    o2 += g.z * w;
                 }
             }
         }

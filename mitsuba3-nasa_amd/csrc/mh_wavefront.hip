@@ -416,7 +416,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         V3 tp, a_nee, b_nee, prev_p, L;
         float eta = 1.f, prev_pdf = 1.f;
         Pcg rng;
-        uint64_t gen_state = 0;
+        uint64_t gen_state = 0, gen_inc = 0;
         if (has) {
             if (Gen) {  // k_wf_raygen (integrator.cpp:1139-1176, perspective.cpp:240-281)
                 pid = j;
@@ -428,6 +428,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
                                  __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
                 gen_state = g.state;
+                gen_inc = g.inc;  // the TEA of this lane, reused below
                 out[3 * plane + pid] = sx;
                 out[4 * plane + pid] = sy;
             } else {
@@ -466,7 +467,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             const bool prev_delta = depth == 0;
             uint32_t lane, px, py;
             lane_of(lm, pid, lane, px, py);
-            rng.inc = pcg_inc(seed_value, lane);
+            rng.inc = Gen ? gen_inc : pcg_inc(seed_value, lane);
             SI si;
             compute_si(S, ray, h, si);
 
@@ -953,7 +954,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         float A[NR][3], G[NR][3];
         Pcg rng;
         const uint32_t j = sbase + i;
-        uint64_t gen_state = 0;
+        uint64_t gen_state = 0, gen_inc = 0;
         if (i < n) {
             if (Gen) {  // k_wf_raygen_prb (integrator.cpp:1139-1176, common.py:936-965)
                 pid = j;
@@ -965,6 +966,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
                                  __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
                 gen_state = g.state;
+                gen_inc = g.inc;  // the TEA of this lane, reused below
                 dL = gather_dL(S0, gen.coalesce, gen.grad_in, sx, sy);
             } else {
                 const uint32_t pd = w.pd[cur][j];
@@ -999,7 +1001,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             const float eta = 1.f;
             uint32_t lane, px, py;
             lane_of(lm, pid, lane, px, py);
-            rng.inc = pcg_inc(seed_value, lane);
+            rng.inc = Gen ? gen_inc : pcg_inc(seed_value, lane);
             SI si;
             compute_si(S, ray, h, si);
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
