@@ -617,14 +617,18 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
-            if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
+            // timed as one span: an event between two launches costs a ~10 us
+            // gap (measured), so bounce 0 opens the span, the last bounce
+            // closes it and the remaining pairs are recorded empty after it
+            if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
             if (b == 0)
                 hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S,
                                    in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n);
             else
                 hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st,
                                    S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n);
-            if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
+            if (trace_ev && b + 1 == n_bounces)
+                for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
             continue;
         }
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
