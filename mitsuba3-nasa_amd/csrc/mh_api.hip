@@ -87,7 +87,7 @@ struct mh_scene {
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
-    DevBuf wf_ws_prb, wf_partial, gw;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
+    DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     std::vector<mh_medium> h_media;
@@ -446,7 +446,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -620,14 +620,16 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
     const uint32_t S_ = L.s_end - L.s_begin;
     const uint64_t per_pixel = (uint64_t)S_ * L.n_passes;
-    // execution mode: wavefront for `path` (single pass, bounded depth) unless forced
-    bool wavefront = in->type == MH_INTEGRATOR_PATH && L.n_passes == 1 && in->max_depth <= 64;
+    // execution mode: wavefront for `path` (bounded depth; several passes only
+    // on the fused bounce kernel, which carries each lane's PCG32 state from
+    // one pass to the next) unless forced
+    bool wavefront = in->type == MH_INTEGRATOR_PATH && in->max_depth <= 64 && (L.n_passes == 1 || wf_fused(s->S));
     const char *env_mode = getenv("MH_MODE");
     if (env_mode && !strcmp(env_mode, "mega")) wavefront = false;
     if (flags & MH_FLAG_MEGAKERNEL) wavefront = false;
     if ((flags & MH_FLAG_WAVEFRONT) && !wavefront)
-        return set_error(MH_ERR_UNSUPPORTED, "mh_render: the wavefront mode supports the single-pass "
-                                             "'path' integrator with max_depth <= 64");
+        return set_error(MH_ERR_UNSUPPORTED, "mh_render: the wavefront mode supports the 'path' integrator "
+                                             "with max_depth <= 64 (several passes: packet-engine scenes)");
     uint64_t max_samples = 1ull << 25;
     if (wavefront) {
         const char *ec = getenv("MH_WF_CHUNK");
@@ -649,12 +651,14 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         MH_HIP(hipEventCreate(&e));
         s->evpool.push_back(e);
     }
-    const size_t ctr_per_chunk = wavefront ? wf_counter_words(n_bounces) : 0;
+    const size_t ctr_words = wavefront ? wf_counter_words(n_bounces) : 0;  // per pass
+    const size_t ctr_per_chunk = ctr_words * L.n_passes;
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
     if (wavefront) {
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(plane)));
         MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, ctr_per_chunk * n_chunks * 4)));
+        if (L.n_passes > 1) MH_HIP(s->wf_carry.alloc((size_t)chunk_px * S_ * 8));
     }
     size_t chunk = 0;
     for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
@@ -666,7 +670,8 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         if (wavefront) {
             MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
                                     s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
-                                    n_bounces, wf_blocks(cus), ev + 2, st));
+                                    n_bounces, wf_blocks(cus), ev + 2, st, L.n_passes,
+                                    L.n_passes > 1 ? s->wf_carry.as<uint64_t>() : nullptr));
         } else {
             MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
                                  s->counters.as<unsigned long long>(), st));
@@ -697,13 +702,15 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         }
     }
     if (wavefront) {
-        const size_t per_bounce = ctr_per_chunk / (n_bounces + 1), nseg = per_bounce / 32;
+        const size_t per_bounce = ctr_words / (n_bounces + 1), nseg = per_bounce / 32;
         for (size_t c = 0; c < n_chunks; ++c)
-            for (uint32_t b = 0; b < n_bounces; ++b)
-                for (size_t sg = 0; sg < nseg; ++sg) {
-                    ctr[0] += wctr[ctr_per_chunk * c + per_bounce * b + 32 * sg + 0];
-                    ctr[1] += wctr[ctr_per_chunk * c + per_bounce * b + 32 * sg + 1];
-                }
+            for (uint32_t p = 0; p < L.n_passes; ++p)
+                for (uint32_t b = 0; b < n_bounces; ++b)
+                    for (size_t sg = 0; sg < nseg; ++sg) {
+                        const size_t o = ctr_per_chunk * c + ctr_words * p + per_bounce * b + 32 * sg;
+                        ctr[0] += wctr[o + 0];
+                        ctr[1] += wctr[o + 1];
+                    }
     }
     if (stats) {
         stats->samples = n_px * per_pixel;
@@ -713,7 +720,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         stats->ms_total = now_ms() - t_start;
         stats->ms_kernel = kernel_ms;
         stats->ms_trace = trace_ms;
-        stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces : 0;
+        stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces * L.n_passes : 0;
         stats->mode = wavefront ? (wf_fused(s->S) ? 2u : 1u) : 0u;
     }
     return MH_OK;

@@ -67,7 +67,8 @@ uint64_t wf_max_chunk();
 hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                             uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
-                            hipEvent_t *trace_ev, hipStream_t st);
+                            hipEvent_t *trace_ev, hipStream_t st, uint32_t n_passes = 1,
+                            uint64_t *carry = nullptr);  // carry: n PCG32 states (n_passes > 1)
 size_t wf_prb_workspace_bytes(uint64_t cap);
 uint32_t wf_grid(uint32_t grid);
 uint32_t wf_blocks(int cus);  // wavefront workgroups for a device of `cus` CUs

@@ -555,6 +555,12 @@ MH_DEV F2 pp(const Prim *Q, uint32_t i, uint32_t k) {
     return pair(p[0], p[1]);
 }
 
+#ifndef MH_TRI_EARLY
+#define MH_TRI_EARLY 1  // wave-level early exit of a triangle pair after u
+#endif
+#ifndef MH_RECT_EARLY
+#define MH_RECT_EARLY 1  // wave-level early exit of a rectangle pair after the plane distance
+#endif
 template <bool Shadow>
 MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(0);
@@ -567,7 +573,7 @@ MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit
     const F2 tt = pair(-lz.x / ldz.x, -lz.y / ldz.y);
     const float bound = Shadow ? r.maxt : h.t;
     bool okA = live & (tt.x >= 0.f) & (tt.x <= bound), okB = live & (tt.y >= 0.f) & (tt.y <= bound);
-    if (!wave_any(okA | okB)) return;
+    if (MH_RECT_EARLY && !wave_any(okA | okB)) return;
     MH_CNT(1);
     const F2 a0 = pp(Q, pos, 0), a1 = pp(Q, pos, 1), a2 = pp(Q, pos, 2);
     const F2 b0 = pp(Q, pos, 4), b1 = pp(Q, pos, 5), b2 = pp(Q, pos, 6);
@@ -600,7 +606,7 @@ MH_DEV void tri_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit 
     const F2 inv_det = rcp2(det);
     const F2 u = fma2(tz, pz, fma2(ty, py, tx * px)) * inv_det;
     bool okA = live & (u.x >= 0.f) & (u.x <= 1.f), okB = live & (u.y >= 0.f) & (u.y <= 1.f);
-    if (!wave_any(okA | okB)) return;
+    if (MH_TRI_EARLY && !wave_any(okA | okB)) return;
     MH_CNT(3);
     // qvec = cross(tvec, e1)
     const F2 qx = fma2(ty, e1z, -(tz * e1y)), qy = fma2(tz, e1x, -(tx * e1z)), qz = fma2(tx, e1y, -(ty * e1x));

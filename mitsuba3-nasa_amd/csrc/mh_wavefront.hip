@@ -388,7 +388,8 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
 template <bool Gen>
 __global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane, float *out,
-            WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total) {
+            WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total,
+            uint64_t *carry, uint32_t pass) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
     uint32_t n;
@@ -423,7 +424,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 uint32_t lane, px, py;
                 lane_of(lm, pid, lane, px, py);
                 Pcg g;
-                g.seed(seed_value, lane);
+                if (pass == 0) {
+                    g.seed(seed_value, lane);
+                } else {  // later pass: the lane's stream continues (integrator.cpp:353-357)
+                    g.state = carry[pid];
+                    g.inc = pcg_inc(seed_value, lane);
+                }
                 const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
                 ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
                                  __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
@@ -559,6 +565,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             w.lx[nxt][slot] = L.x; w.ly[nxt][slot] = L.y; w.lz[nxt][slot] = L.z;
         } else if (has) {
             out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
+            if (carry) carry[pid] = rng.state;  // multi-pass: the next pass continues the stream
         }
     }
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
@@ -596,12 +603,42 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
 // without host synchronisation.  trace_ev: optional event pairs bracketing
 // every k_wf_trace launch (roofline timing of the dominant kernel).
 // ---------------------------------------------------------------------------
+static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                        uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
+                                        uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
+                                        hipEvent_t *trace_ev, hipStream_t st, uint64_t *carry, uint32_t pass);
+
 hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                             uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
-                            hipEvent_t *trace_ev, hipStream_t st) {
+                            hipEvent_t *trace_ev, hipStream_t st, uint32_t n_passes, uint64_t *carry) {
     if (n == 0) return hipSuccess;
-    if (n > (1ull << kPidBits) || n_bounces > 255) return hipErrorInvalidValue;
+    if (n > (1ull << kPidBits) || n_bounces > 255 || n_passes == 0) return hipErrorInvalidValue;
+    if (n_passes == 1)
+        return launch_wavefront_pass(S, in, lm, seed_value, n, plane, out, ws, cap, ctr, n_bounces, grid, trace_ev,
+                                     st, nullptr, 0);
+    if (!wf_fused(S) || !carry) return hipErrorInvalidValue;
+    // passes of one chunk run back to back (integrator.cpp:350-360): pass p
+    // writes its samples at p * n of every plane and hands each lane's PCG32
+    // state to pass p + 1 through `carry`; counters per pass; the bounce
+    // launches of all passes are timed as one span
+    if (trace_ev) (void)hipEventRecord(trace_ev[0], st);
+    for (uint32_t p = 0; p < n_passes; ++p) {
+        hipError_t e = launch_wavefront_pass(S, in, lm, seed_value, n, plane, out + (uint64_t)p * n, ws, cap,
+                                             ctr + (size_t)p * wf_counter_words(n_bounces), n_bounces, grid,
+                                             nullptr, st, carry, p);
+        if (e != hipSuccess) return e;
+    }
+    if (trace_ev)
+        for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
+    return hipSuccess;
+}
+
+static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                        uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
+                                        uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
+                                        hipEvent_t *trace_ev, hipStream_t st, uint64_t *carry, uint32_t pass) {
+    const bool fused = wf_fused(S);
     WfState w = carve(ws, cap);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
@@ -609,7 +646,6 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
-    const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
     if (!fused)  // the fused first bounce generates its camera rays itself
         hipLaunchKernelGGL(k_wf_raygen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                            seed_value, n, plane, out, w, ctr);
@@ -623,10 +659,10 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
             if (b == 0)
                 hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S,
-                                   in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n);
+                                   in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass);
             else
                 hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st,
-                                   S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n);
+                                   S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass);
             if (trace_ev && b + 1 == n_bounces)
                 for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
             continue;

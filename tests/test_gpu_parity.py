@@ -366,6 +366,24 @@ def test_multipass_config5_slab_parity():
     assert ok, f"film parity {frac}"
 
 
+def test_multipass_wavefront_matches_megakernel():
+    """The fused wavefront runs the passes of a > 2^32-sample render back to
+    back, carrying each lane's PCG32 state (integrator.cpp:353-357); the
+    megakernel runs every pass of a lane in one thread.  Same samples."""
+    mi = _mi()
+    scene = cbox(mi, 2048, 2048, 1024)
+    integ = mi.load_dict({"type": "path", "max_depth": 8})
+    from mitsuba_hip import _abi as A
+    st = A.Stats()
+    wf = mi.render_film(scene, integ, seed=3, spp=1024, spp_begin=4, spp_end=6, mode="wavefront",
+                        stats=st).cpu().numpy()
+    assert st.mode == 2 and st.n_trace_launches == 2 * 8  # one chunk, two passes of 8 bounces
+    mega = mi.render_film(scene, integ, seed=3, spp=1024, spp_begin=4, spp_end=6, mode="mega").cpu().numpy()
+    assert mega[..., 3].sum() > 0
+    ok, frac = _film_close(wf, mega)
+    assert ok, f"film parity {frac}"
+
+
 # ---------------------------------------------------------------------------
 # path / prb with several emitters of different kinds (uniform emitter
 # selection, scene.cpp:227-250; constant environment; delta directional)
