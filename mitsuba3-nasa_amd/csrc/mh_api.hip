@@ -925,6 +925,12 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     ga.n_rgb = n_rgb;
     ga.sigma_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_sig) : nullptr;
     ga.albedo_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_alb) : nullptr;
+    // one bitmap parameter of <= 48 KiB: the replay kernel accumulates its
+    // texel gradients per workgroup in LDS (k_prb_backward)
+    if (n_bmp == 1 && counts[kMaxRgbParams] * 4 <= (48u << 10)) {
+        ga.lds_slot = kMaxRgbParams;
+        ga.lds_floats = (uint32_t)counts[kMaxRgbParams];
+    }
 
     // ---- grad_in / weights on the device ----
     const float *g_in = grad_in;

@@ -30,6 +30,9 @@ struct GradArgs {
                                  // rgb textures, medium albedo, homogeneous sigma_t
     const int32_t *sigma_slot;   // device: medium -> sigma_t slot or -1 (prbvolpath)
     const int32_t *albedo_slot;  // device: medium -> albedo slot or -1 (prbvolpath)
+    int32_t lds_slot = -1;       // bitmap slot accumulated per workgroup in LDS (k_prb_backward replay)
+    uint32_t lds_floats = 0;     // its size (floats)
+    uint32_t lds_offset = 0;     // byte offset of the accumulator in dynamic LDS (set by the launcher)
 };
 
 // ---- BVH builder (host, binned SAH) --------------------------------------

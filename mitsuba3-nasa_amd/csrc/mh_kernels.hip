@@ -17,6 +17,8 @@
 //   k_prb_weights       W image of render_backward (common.py:936-947).
 //   k_prb_backward      per-lane dL gather + PRB primal + adjoint replay with
 //                       wave/block-reduced gradient atomics (common.py:828-983).
+#include <algorithm>
+
 #include "mh_shading.hpp"
 
 namespace mh {
@@ -402,6 +404,8 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.is_rgb = ga.is_rgb;
     g.sigma_slot = ga.sigma_slot;
     g.albedo_slot = ga.albedo_slot;
+    g.lds_slot = -1;
+    g.lds_acc = nullptr;
 #pragma unroll
     for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
     return g;
@@ -410,17 +414,31 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
 // ---------------------------------------------------------------------------
 // PRB backward: dL gather + primal + adjoint per lane (common.py:900-983)
 // ---------------------------------------------------------------------------
+#ifndef MH_PRB_WAVES
+#define MH_PRB_WAVES 4  // replay backward: 127-128 VGPRs (4 waves/SIMD) instead of 129 (3), no spills
+#endif
 template <bool InLds, bool Fused>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, Fused ? 1 : MH_PRB_WAVES)
 k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n,
                int coalesce, const float *__restrict__ grad_in, const float *__restrict__ weights,
                GradArgs ga, unsigned long long *__restrict__ counters) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
     GradCtx g = make_grad_ctx(ga);
+    // one bitmap parameter small enough for LDS: texel gradients accumulate per
+    // workgroup (after the BVH staging region) and are flushed once at the end;
+    // the grid is then persistent (grid-stride over the samples)
+    float *tex_acc = nullptr;
+    if (!Fused && ga.lds_slot >= 0) {
+        tex_acc = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + ga.lds_offset);
+        for (uint32_t i = threadIdx.x; i < ga.lds_floats; i += blockDim.x) tex_acc[i] = 0.f;
+        __syncthreads();
+        g.lds_slot = ga.lds_slot;
+        g.lds_acc = tex_acc;
+    }
     uint32_t n_closest = 0, n_shadow = 0;
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) {
+    const uint64_t stride = tex_acc ? (uint64_t)gridDim.x * blockDim.x : n;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
         uint32_t lane, px, py;
         lane_of(lm, k, lane, px, py);
         Pcg rng;
@@ -437,6 +455,12 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
                                       n_closest, n_shadow);
             prb_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
         }
+    }
+    if (tex_acc) {
+        __syncthreads();
+        float *dst = ga.bufs[ga.lds_slot];
+        for (uint32_t i = threadIdx.x; i < ga.lds_floats; i += blockDim.x)
+            if (tex_acc[i] != 0.f) atomicAdd(dst + i, tex_acc[i]);
     }
     flush_small_slots(g, ga);
     if (counters) {
@@ -633,12 +657,25 @@ hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t
 
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
-                               const float *grad_in, const float *weights, const GradArgs &ga,
+                               const float *grad_in, const float *weights, const GradArgs &ga_in,
                                bool fused, unsigned long long *counters, hipStream_t st) {
     const uint32_t bs = 256;
     if (n == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
-    const dim3 g(blocks_for(n, bs)), b(bs);
+    dim3 g(blocks_for(n, bs)), b(bs);
+    GradArgs ga = ga_in;
+    if (in.type != MH_INTEGRATOR_PRBVOLPATH && !fused && ga.lds_slot >= 0) {
+        // persistent grid: as many workgroups as fit beside the texel accumulator
+        ga.lds_offset = (uint32_t)((sh + 15) / 16 * 16);
+        sh = ga.lds_offset + (size_t)ga.lds_floats * 4;
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160u << 10) / sh));
+        g = dim3(std::min<uint32_t>(blocks_for(n, bs), (uint32_t)cus * per_cu));
+    } else {
+        ga.lds_slot = -1;
+    }
     if (in.type == MH_INTEGRATOR_PRBVOLPATH) {
         if (S.lds_bytes_bvh)
             hipLaunchKernelGGL((k_prbvol_backward<true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters);

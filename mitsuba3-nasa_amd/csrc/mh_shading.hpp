@@ -1273,6 +1273,8 @@ struct GradCtx {
     float acc[kMaxRgbParams][3];  // per-lane accumulators for rgb params
     const int32_t *sigma_slot;    // prbvolpath: medium -> sigma_t slot or -1 (nullptr: none)
     const int32_t *albedo_slot;   // prbvolpath: medium -> albedo slot or -1 (nullptr: none)
+    int32_t lds_slot;             // bitmap slot whose texels accumulate in LDS (-1: none)
+    float *lds_acc;               // that slot's workgroup accumulator
 };
 
 // register accumulator of a small (rgb / scalar) parameter slot; the
@@ -1295,7 +1297,9 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
     }
     Taps tp;
     bitmap_taps(tx, uvx, uvy, tp);
-    float *buf = g.bufs[k];
+    // a lane-coherent wave adds to the same few texels: in LDS (ds_add_f32)
+    // those same-address adds cost a few cycles, at L2 a round trip each
+    float *buf = k == g.lds_slot ? g.lds_acc : g.bufs[k];
     float w[4] = {1.f, 0.f, 0.f, 0.f};
     if (tp.n == 1) { w[0] = 1.f; }
     else { w[0] = tp.w0y * tp.w0x; w[1] = tp.w0y * tp.w1x; w[2] = tp.w1y * tp.w0x; w[3] = tp.w1y * tp.w1x; }
