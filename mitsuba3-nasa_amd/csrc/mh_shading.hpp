@@ -1299,7 +1299,8 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
     bitmap_taps(tx, uvx, uvy, tp);
     // a lane-coherent wave adds to the same few texels: in LDS (ds_add_f32)
     // those same-address adds cost a few cycles, at L2 a round trip each
-    float *buf = k == g.lds_slot ? g.lds_acc : g.bufs[k];
+    const bool in_lds = k == g.lds_slot;
+    float *buf = in_lds ? g.lds_acc : g.bufs[k];
     float w[4] = {1.f, 0.f, 0.f, 0.f};
     if (tp.n == 1) { w[0] = 1.f; }
     else { w[0] = tp.w0y * tp.w0x; w[1] = tp.w0y * tp.w1x; w[2] = tp.w1y * tp.w0x; w[3] = tp.w1y * tp.w1x; }
@@ -1307,6 +1308,18 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
     for (uint32_t j = 0; j < 4; ++j) {
         if (j >= tp.n) break;
         uint64_t base = tp.idx[j] - tx.data_offset;
+        if (in_lds) {  // ds_add_f32 (an LDS-qualified pointer, not a flat atomic)
+            typedef __attribute__((address_space(3))) float LdsFloat;
+            LdsFloat *l = (LdsFloat *)(buf + base);
+            if (tx.channels == 3) {
+                __hip_atomic_fetch_add(l + 0, adj.x * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(l + 1, adj.y * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(l + 2, adj.z * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                __hip_atomic_fetch_add(l, (adj.x + adj.y + adj.z) * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            continue;
+        }
         if (tx.channels == 3) {
             atomicAdd(buf + base + 0, adj.x * w[j]);
             atomicAdd(buf + base + 1, adj.y * w[j]);
