@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--res", type=int, default=512)
     p.add_argument("--spp", type=int, default=256, help="samples per pixel per GPU")
     p.add_argument("--max-depth", type=int, default=8)
-    p.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=24.0, help="budget of the CPU baseline (3 timed runs)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     p.add_argument("--fwd-only", action="store_true")
     p.add_argument("--backend", default="nccl",
@@ -48,22 +48,41 @@ def parse():
     return p.parse_args()
 
 
-def cpu_threads():
+def cpu_info():
+    """(model name, nproc, affinity) of the host this runs on."""
+    model = "unknown"
     try:
-        n = len(os.sched_getaffinity(0))
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
     except Exception:
-        n = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    return max(1, min(n, cap, 64))
+        aff = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, aff
+
+
+def cpu_threads():
+    """Every core this process may run on, capped by OMP_NUM_THREADS where
+    the host sets it (the GPU box: 16, its CPU share of a larger machine)."""
+    _, _, aff = cpu_info()
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return max(1, min(aff, cap))
 
 
 def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
-    """Oracle (CPU restatement, kind 'port') on the box's host cores, on a
-    bounded sample of the same workload: the same scene/integrators at a
-    reduced spp chosen to fit ~budget_s of CPU work."""
+    """CPU baseline: the oracle -- the
+    CPU restatement of llvm_ad_rgb (scalar C, no SIMD), kind 'port' -- on the
+    host's cores, on a bounded sample of the same workload: the same scene and
+    integrators at a reduced spp sized so one run takes ~budget_s / 4.  One
+    warm-up run (the spp calibration), then the min of 3 timed runs."""
     import numpy as np
     import oracle_py as O
     threads = cpu_threads()
+    model, nproc, aff = cpu_info()
     H, W = scene.height, scene.width
     gi = np.full((H, W, 3), 1.0 / (H * W * 3), np.float32)
     tex = [scene.params[key][1]]
@@ -75,15 +94,50 @@ def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
             O.render_backward(scene, prb, 1, spp, gi, tex, [(3,)], threads=threads)
         return time.perf_counter() - t0
 
-    t1 = run(1)
-    spp = int(max(1, min(spp_gpu, budget_s / max(t1, 1e-3))))
+    t1 = run(1)  # warm-up + calibration
+    spp = int(max(1, min(spp_gpu, budget_s / 4 / max(t1, 1e-3))))
     spp = 1 << max(0, spp.bit_length() - 1)
-    if spp > 1:
-        t1 = run(spp)
-    rate = H * W * spp / t1 / 1e6
+    best = min(run(spp) for _ in range(3))
+    rate = H * W * spp / best / 1e6
     return {"value": round(rate, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"cornell_box {W}x{H} @ {spp} spp, path fwd" + ("" if fwd_only else " + prb grad")
-                      + f" (oracle/libmh_oracle.so, {threads} threads, {t1:.1f} s)"}
+                      + f"; min of 3 runs after 1 warm-up, {best:.2f} s each",
+            "label": "CPU restatement of llvm_ad_rgb (oracle/libmh_oracle.so: scalar C, no SIMD)",
+            "cpu_model": model, "nproc": nproc, "affinity": aff, "threads": threads}
+
+
+def build_step(res, spp, max_depth, rank, world, dev):
+    """The bench's hot-path wiring (also driven by tests/test_gpu_multirank.py):
+    cornell_box res^2, `path` forward + `prb` backward wrt white's rgb
+    reflectance, the rank's sample slab of a spp * world render, through the
+    HIP C-ABI wrappers of mitsuba_hip."""
+    import torch
+    import mitsuba_hip as mi
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip import distributed as D
+    mi.set_variant("hip_ad_rgb")
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"] = res
+    d["sensor"]["film"]["height"] = res
+    scene = mi.load_dict(d)
+    fwd = mi.load_dict({"type": "path", "max_depth": max_depth})
+    prb = mi.load_dict({"type": "prb", "max_depth": max_depth})
+    params = mi.traverse(scene)
+    key = "white.reflectance.value"
+    grad_in = torch.full((res, res, 3), 1.0 / (res * res * 3), dtype=torch.float32, device=dev)
+    st_f, st_b = A.Stats(), A.Stats()
+    film = torch.empty((res, res, 4), dtype=torch.float32, device=dev)
+    ops = D.StepOps(
+        render_film=lambda seed, spp_, b, e: mi.render_film(scene, fwd, seed=seed, spp=spp_, spp_begin=b,
+                                                            spp_end=e, film=film, stats=st_f),
+        develop=lambda f: mi.develop(scene, f),
+        prb_weights=lambda seed, spp_, b, e: mi.prb_weights(scene, seed, spp_, b, e),
+        render_backward=lambda seed, spp_, b, e, w: mi.render_backward(
+            scene, params, grad_in, [key], prb, seed=seed, spp=spp_, spp_begin=b, spp_end=e, weights=w,
+            stats=st_b),
+        seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0])
+    return {"scene": scene, "fwd": fwd, "prb": prb, "key": key, "ops": ops,
+            "slab": D.sample_slab(rank, world, spp), "st_f": st_f, "st_b": st_b}
 
 
 def main():
@@ -107,34 +161,13 @@ def main():
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
-    import mitsuba_hip as mi
     from mitsuba_hip import _abi as A
-    mi.set_variant("hip_ad_rgb")
-    d = mi.cornell_box()
-    d["sensor"]["film"]["width"] = args.res
-    d["sensor"]["film"]["height"] = args.res
-    scene = mi.load_dict(d)
-    fwd = mi.load_dict({"type": "path", "max_depth": args.max_depth})
-    prb = mi.load_dict({"type": "prb", "max_depth": args.max_depth})
-    params = mi.traverse(scene)
-    key = "white.reflectance.value"
+    from mitsuba_hip import distributed as D
+    w = build_step(args.res, args.spp, args.max_depth, rank, world, dev)
+    scene, fwd, prb, key, ops, slab, st_f, st_b = (w[k] for k in ("scene", "fwd", "prb", "key", "ops", "slab",
+                                                                   "st_f", "st_b"))
     H = W = args.res
     spp_total = args.spp * world
-    grad_in = torch.full((H, W, 3), 1.0 / (H * W * 3), dtype=torch.float32, device=dev)
-    st_f, st_b = A.Stats(), A.Stats()
-    film = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-
-    from mitsuba_hip import distributed as D
-    slab = D.sample_slab(rank, world, args.spp)
-    ops = D.StepOps(
-        render_film=lambda seed, spp, b, e: mi.render_film(scene, fwd, seed=seed, spp=spp, spp_begin=b,
-                                                           spp_end=e, film=film, stats=st_f),
-        develop=lambda f: mi.develop(scene, f),
-        prb_weights=lambda seed, spp, b, e: mi.prb_weights(scene, seed, spp, b, e),
-        render_backward=lambda seed, spp, b, e, w: mi.render_backward(
-            scene, params, grad_in, [key], prb, seed=seed, spp=spp, spp_begin=b, spp_end=e, weights=w,
-            stats=st_b),
-        seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0])
 
     def step(i):
         return D.fwd_grad_step(ops, slab, i, with_grad=not args.fwd_only)

@@ -302,12 +302,24 @@ int mh_render_backward(mh_scene *scene, const mh_integrator *integrator, uint32_
 
 /*
  * Ray-query sub-boundary (the OptiX slot).  Rays are SoA: ray[0..6][n] =
- * o.x o.y o.z d.x d.y d.z maxt (mint = 0).  Hits: t (+inf on miss), u, v
- * (prim_uv), prim (prim_index; 0xffffffff for rectangles) and shape
- * (shape index; 0xffffffff on miss) — the payload of scene_optix.inl:619-657.
+ * o.x o.y o.z d.x d.y d.z maxt (mint = 0).  Output = the payload of
+ * Scene::ray_intersect_preliminary_gpu (scene_optix.inl:592-657,
+ * optix/common.h:43-58, optix_rt.cu:9-17):
+ *   t         hit distance; +inf on a miss (the miss program)
+ *   u, v      prim_uv; (0, 0) on a miss (the payload's initial value)
+ *   prim      prim_index: the face index of a mesh triangle, 0 for a
+ *             rectangle (rectangle.cuh:42) and 0 on a miss
+ *   shape     shape index; 0xffffffff (null ShapePtr) on a miss
+ *   instance  (mh_trace_preliminary only; may be NULL) the instance of the
+ *             hit: always 0xffffffff (null) here, since hip_ad_rgb scenes have
+ *             no shapegroups / instances (payload_inst_index starts at 0 and
+ *             stays null when m_shapegroups is empty, scene_optix.inl:607-608)
  */
 int mh_trace_closest(mh_scene *scene, uint64_t n, const float *rays, float *t, float *u,
                      float *v, uint32_t *prim, uint32_t *shape, uint32_t flags, mh_stats *stats);
+int mh_trace_preliminary(mh_scene *scene, uint64_t n, const float *rays, float *t, float *u, float *v,
+                         uint32_t *prim, uint32_t *shape, uint32_t *instance, uint32_t flags,
+                         mh_stats *stats);
 int mh_trace_shadow(mh_scene *scene, uint64_t n, const float *rays, uint32_t *occluded,
                     uint32_t flags, mh_stats *stats);
 

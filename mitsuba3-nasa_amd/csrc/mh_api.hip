@@ -554,14 +554,23 @@ struct Layout {
     uint32_t W, H, spp, spp_pp, n_passes, s_begin, s_end;
 };
 
-static int make_layout(const mh_scene *s, uint32_t spp, uint32_t b, uint32_t e, Layout &L) {
+// ad: the Python ADIntegrator's single wavefront (prb / prbvolpath primal,
+// W image and render_backward): prepare() accepts up to exactly 2^32 samples
+// and raises beyond (common.py:571-578); lane indices [0, 2^32) are uint32.
+// Otherwise SamplingIntegrator::render's passes of <= 2^32 - 1 samples.
+static int make_layout(const mh_scene *s, uint32_t spp, uint32_t b, uint32_t e, Layout &L, bool ad) {
     L.W = s->S.width;
     L.H = s->S.height;
     L.spp = spp;
     uint64_t wf = (uint64_t)L.W * L.H * spp, lim = 0xffffffffull;
     L.spp_pp = spp;
     L.n_passes = 1;
-    if (wf > lim) {  // integrator.cpp:281-295
+    if (ad && wf > (1ull << 32))
+        return set_error(MH_ERR_INVALID_ARGUMENT,
+                         "The total number of Monte Carlo samples required by this rendering task (" +
+                             std::to_string(wf) + ") exceeds 2^32 = 4294967296. Please use fewer samples "
+                             "per pixel or render using multiple passes.");
+    if (!ad && wf > lim) {  // integrator.cpp:281-295
         L.spp_pp = spp / (uint32_t)((wf + lim - 1) / lim);
         L.n_passes = spp / L.spp_pp;
         if (L.spp_pp * L.n_passes != spp)
@@ -603,7 +612,8 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: spp must be > 0");
     double t_start = now_ms();
     Layout L;
-    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    const bool ad = in->type == MH_INTEGRATOR_PRB || in->type == MH_INTEGRATOR_PRBVOLPATH;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L, ad);
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
@@ -733,7 +743,8 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: unsupported integrator");
     if (spp == 0 || in->rr_depth == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: bad arguments");
     Layout L;
-    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    const bool ad = in->type == MH_INTEGRATOR_PRB || in->type == MH_INTEGRATOR_PRBVOLPATH;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L, ad);
     if (rc) return rc;
     if (L.n_passes != 1) return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: single pass only");
     MH_HIP(hipSetDevice(s->device));
@@ -793,13 +804,8 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     if (!s || !weights) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: NULL argument");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: spp must be > 0");
     Layout L;
-    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
     if (rc) return rc;
-    if (L.n_passes != 1)
-        return set_error(MH_ERR_INVALID_ARGUMENT,
-                         "The total number of Monte Carlo samples required by this rendering task "
-                         "exceeds 2^32 = 4294967296. Please use fewer samples per pixel or render "
-                         "using multiple passes.");
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
@@ -835,13 +841,8 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: spp must be > 0");
     double t_start = now_ms();
     Layout L;
-    int rc = make_layout(s, spp, spp_begin, spp_end, L);
+    int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
     if (rc) return rc;
-    if (L.n_passes != 1)
-        return set_error(MH_ERR_INVALID_ARGUMENT,
-                         "The total number of Monte Carlo samples required by this rendering task "
-                         "exceeds 2^32 = 4294967296. Please use fewer samples per pixel or render "
-                         "using multiple passes.");
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
@@ -927,7 +928,9 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     ga.albedo_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_alb) : nullptr;
     // one bitmap parameter of <= 48 KiB: the replay kernel accumulates its
     // texel gradients per workgroup in LDS (k_prb_backward)
-    if (n_bmp == 1 && counts[kMaxRgbParams] * 4 <= (48u << 10)) {
+    // (MH_PRB_LDS_TEX=0: global atomics, the parity tests' cross-check)
+    const char *env_lds = getenv("MH_PRB_LDS_TEX");
+    if (n_bmp == 1 && counts[kMaxRgbParams] * 4 <= (48u << 10) && !(env_lds && !strcmp(env_lds, "0"))) {
         ga.lds_slot = kMaxRgbParams;
         ga.lds_floats = (uint32_t)counts[kMaxRgbParams];
     }
@@ -1057,7 +1060,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
 // Ray-query sub-boundary
 // ---------------------------------------------------------------------------
 static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, float *t, float *u,
-                      float *v, uint32_t *prim, uint32_t *shape, uint32_t *occ, uint32_t flags,
+                      float *v, uint32_t *prim, uint32_t *shape, uint32_t *inst, uint32_t *occ, uint32_t flags,
                       mh_stats *stats) {
     if (!s || (n && !rays)) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace: NULL argument");
     if (n == 0) return MH_OK;
@@ -1067,16 +1070,17 @@ static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, f
     const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
     const float *r = rays;
     float *dt = t, *du = u, *dv = v;
-    uint32_t *dp = prim, *ds = shape, *doc = occ;
+    uint32_t *dp = prim, *ds = shape, *di = inst, *doc = occ;
     if (!dev) {
         MH_HIP(s->tmp_a.alloc(n * 28));
         MH_HIP(hipMemcpyAsync(s->tmp_a.ptr, rays, n * 28, hipMemcpyHostToDevice, st));
         r = s->tmp_a.as<float>();
-        MH_HIP(s->tmp_b.alloc(n * 20));
+        MH_HIP(s->tmp_b.alloc(n * 24));
         float *base = s->tmp_b.as<float>();
         dt = base; du = base + n; dv = base + 2 * n;
         dp = reinterpret_cast<uint32_t *>(base + 3 * n);
         ds = reinterpret_cast<uint32_t *>(base + 4 * n);
+        di = inst ? reinterpret_cast<uint32_t *>(base + 5 * n) : nullptr;
         doc = reinterpret_cast<uint32_t *>(base);
     }
     // persistent grid: 8 workgroups of 256 lanes per CU
@@ -1084,7 +1088,7 @@ static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, f
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
     uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 8);
     MH_HIP(hipEventRecord(s->ev0, st));
-    MH_HIP(launch_trace(s->S, shadow, n, r, dt, du, dv, dp, ds, doc, grid, st));
+    MH_HIP(launch_trace(s->S, shadow, n, r, dt, du, dv, dp, ds, di, doc, grid, st));
     MH_HIP(hipEventRecord(s->ev1, st));
     if (!dev) {
         if (shadow) {
@@ -1095,6 +1099,7 @@ static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, f
             MH_HIP(hipMemcpyAsync(v, dv, n * 4, hipMemcpyDeviceToHost, st));
             MH_HIP(hipMemcpyAsync(prim, dp, n * 4, hipMemcpyDeviceToHost, st));
             MH_HIP(hipMemcpyAsync(shape, ds, n * 4, hipMemcpyDeviceToHost, st));
+            if (inst) MH_HIP(hipMemcpyAsync(inst, di, n * 4, hipMemcpyDeviceToHost, st));
         }
     }
     if (!(flags & MH_FLAG_NO_SYNC) || !dev) MH_HIP(hipStreamSynchronize(st));
@@ -1114,15 +1119,20 @@ static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, f
 
 int mh_trace_closest(mh_scene *s, uint64_t n, const float *rays, float *t, float *u, float *v,
                      uint32_t *prim, uint32_t *shape, uint32_t flags, mh_stats *stats) {
+    return mh_trace_preliminary(s, n, rays, t, u, v, prim, shape, nullptr, flags, stats);
+}
+
+int mh_trace_preliminary(mh_scene *s, uint64_t n, const float *rays, float *t, float *u, float *v,
+                         uint32_t *prim, uint32_t *shape, uint32_t *instance, uint32_t flags, mh_stats *stats) {
     if (n && (!t || !u || !v || !prim || !shape))
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace_closest: NULL output");
-    return trace_impl(s, false, n, rays, t, u, v, prim, shape, nullptr, flags, stats);
+    return trace_impl(s, false, n, rays, t, u, v, prim, shape, instance, nullptr, flags, stats);
 }
 
 int mh_trace_shadow(mh_scene *s, uint64_t n, const float *rays, uint32_t *occluded, uint32_t flags,
                     mh_stats *stats) {
     if (n && !occluded) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace_shadow: NULL output");
-    return trace_impl(s, true, n, rays, nullptr, nullptr, nullptr, nullptr, nullptr, occluded, flags,
+    return trace_impl(s, true, n, rays, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, occluded, flags,
                       stats);
 }
 

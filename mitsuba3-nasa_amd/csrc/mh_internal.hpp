@@ -55,7 +55,7 @@ void collapse_bvh4(const BvhOut &b2, std::vector<uint8_t> &nodes4, uint32_t &n4,
 // ---- kernel launchers (mh_kernels.hip) -------------------------------------
 size_t lds_bytes(const DScene &S, uint32_t block);
 hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *rays, float *t,
-                        float *u, float *v, uint32_t *prim, uint32_t *shape, uint32_t *occ,
+                        float *u, float *v, uint32_t *prim, uint32_t *shape, uint32_t *inst, uint32_t *occ,
                         uint32_t grid, hipStream_t st);
 hipError_t launch_render(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                          uint32_t seed_value, uint32_t n_passes, uint64_t n, uint64_t plane,

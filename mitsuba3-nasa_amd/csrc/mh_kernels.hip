@@ -29,7 +29,7 @@ template <bool InLds>
 __global__ void __launch_bounds__(256)
 k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__restrict__ t_out,
                 float *__restrict__ u_out, float *__restrict__ v_out, uint32_t *__restrict__ prim_out,
-                uint32_t *__restrict__ shape_out) {
+                uint32_t *__restrict__ shape_out, uint32_t *__restrict__ inst_out) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -40,11 +40,17 @@ k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__r
         r.maxt = fminf(rays[6 * n + i], kFloatMax);
         Hit h;
         traverse<false>(B.nodes, B.prims, B.stack, B.stride, r, h);
+        // the OptiX payload (scene_optix.inl:602-657, optix/common.h:43-58):
+        // prim_index 0 for rectangles (rectangle.cuh:42) and for misses (the
+        // payload's initial value; the miss program sets only t and shape),
+        // prim_uv (0, 0) on a miss; no instancing: instance = null
+        const bool hit = h.shape != MH_INVALID;
         t_out[i] = h.t;
-        u_out[i] = h.u;
-        v_out[i] = h.v;
-        prim_out[i] = h.prim;
+        u_out[i] = hit ? h.u : 0.f;
+        v_out[i] = hit ? h.v : 0.f;
+        prim_out[i] = hit && h.prim != MH_INVALID ? h.prim : 0u;
         shape_out[i] = h.shape;
+        if (inst_out) inst_out[i] = MH_INVALID;
     }
 }
 
@@ -406,6 +412,7 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.albedo_slot = ga.albedo_slot;
     g.lds_slot = -1;
     g.lds_acc = nullptr;
+    g.lds_floats = 0;
 #pragma unroll
     for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
     return g;
@@ -435,6 +442,7 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
         __syncthreads();
         g.lds_slot = ga.lds_slot;
         g.lds_acc = tex_acc;
+        g.lds_floats = ga.lds_floats;
     }
     uint32_t n_closest = 0, n_shadow = 0;
     const uint64_t stride = tex_acc ? (uint64_t)gridDim.x * blockDim.x : n;
@@ -511,7 +519,7 @@ size_t lds_bytes(const DScene &S, uint32_t block) {
 }
 
 hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *rays, float *t,
-                        float *u, float *v, uint32_t *prim, uint32_t *shape, uint32_t *occ,
+                        float *u, float *v, uint32_t *prim, uint32_t *shape, uint32_t *inst, uint32_t *occ,
                         uint32_t grid, hipStream_t st) {
     const uint32_t bs = 256;
     uint32_t g = grid ? grid : blocks_for(n, bs);
@@ -522,8 +530,8 @@ hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *r
         if (lds) hipLaunchKernelGGL(k_trace_shadow<true>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
         else hipLaunchKernelGGL(k_trace_shadow<false>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
     } else {
-        if (lds) hipLaunchKernelGGL(k_trace_closest<true>, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape);
-        else hipLaunchKernelGGL(k_trace_closest<false>, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape);
+        if (lds) hipLaunchKernelGGL(k_trace_closest<true>, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape, inst);
+        else hipLaunchKernelGGL(k_trace_closest<false>, dim3(g), dim3(bs), sh, st, S, n, rays, t, u, v, prim, shape, inst);
     }
     return hipGetLastError();
 }
@@ -666,13 +674,24 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
     GradArgs ga = ga_in;
     if (in.type != MH_INTEGRATOR_PRBVOLPATH && !fused && ga.lds_slot >= 0) {
         // persistent grid: as many workgroups as fit beside the texel accumulator
-        ga.lds_offset = (uint32_t)((sh + 15) / 16 * 16);
-        sh = ga.lds_offset + (size_t)ga.lds_floats * 4;
-        int dev = 0, cus = 256;
+        // the accumulator must fit the device's per-workgroup LDS beside the
+        // BVH / stack staging; otherwise the texels take the global-atomic path
+        int dev = 0, cus = 256, max_wg = 64 << 10, per_cu_lds = 160 << 10;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160u << 10) / sh));
-        g = dim3(std::min<uint32_t>(blocks_for(n, bs), (uint32_t)cus * per_cu));
+        (void)hipDeviceGetAttribute(&max_wg, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+        (void)hipDeviceGetAttribute(&per_cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+        const uint32_t off = (uint32_t)((sh + 15) / 16 * 16);
+        const size_t total = off + (size_t)ga.lds_floats * 4;
+        if (total <= (size_t)max_wg) {
+            ga.lds_offset = off;
+            sh = total;
+            const size_t lds_cu = per_cu_lds > 0 ? (size_t)per_cu_lds : (size_t)max_wg;
+            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, lds_cu / sh));
+            g = dim3(std::min<uint32_t>(blocks_for(n, bs), (uint32_t)cus * per_cu));
+        } else {
+            ga.lds_slot = -1;
+        }
     } else {
         ga.lds_slot = -1;
     }

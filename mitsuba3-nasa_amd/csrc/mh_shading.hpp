@@ -1275,6 +1275,7 @@ struct GradCtx {
     const int32_t *albedo_slot;   // prbvolpath: medium -> albedo slot or -1 (nullptr: none)
     int32_t lds_slot;             // bitmap slot whose texels accumulate in LDS (-1: none)
     float *lds_acc;               // that slot's workgroup accumulator
+    uint32_t lds_floats;          // its size (floats; checked under MH_DEBUG)
 };
 
 // register accumulator of a small (rgb / scalar) parameter slot; the
@@ -1309,6 +1310,9 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
         if (j >= tp.n) break;
         uint64_t base = tp.idx[j] - tx.data_offset;
         if (in_lds) {  // ds_add_f32 (an LDS-qualified pointer, not a flat atomic)
+#ifdef MH_DEBUG
+            assert(base + tx.channels <= g.lds_floats);
+#endif
             typedef __attribute__((address_space(3))) float LdsFloat;
             LdsFloat *l = (LdsFloat *)(buf + base);
             if (tx.channels == 3) {

@@ -281,9 +281,11 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
             SI si;
             compute_si(S, ray, h, si);
 
-            // ---- direct emission (path.cpp:158-174)
+            // ---- direct emission (path.cpp:158-174); a camera ray that escapes
+            // with the environment hidden returns 0 (valid_ray, path.cpp:115, 256, 284)
             const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
-            if (em != MH_INVALID) {
+            const bool hidden = depth == 0 && !si.valid && in.hide_emitters;
+            if (em != MH_INVALID && !hidden) {
                 float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
                 float mis_bsdf = mis_weight(prev_pdf, em_pdf);
                 V3 le = v3(0, 0, 0);
@@ -477,9 +479,11 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             SI si;
             compute_si(S, ray, h, si);
 
-            // ---- direct emission (path.cpp:158-174)
+            // ---- direct emission (path.cpp:158-174); a camera ray that escapes
+            // with the environment hidden returns 0 (valid_ray, path.cpp:115, 256, 284)
             const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
-            if (em != MH_INVALID) {
+            const bool hidden = depth == 0 && !si.valid && in.hide_emitters;
+            if (em != MH_INVALID && !hidden) {
                 float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
                 float mis_bsdf = mis_weight(prev_pdf, em_pdf);
                 V3 le = v3(0, 0, 0);

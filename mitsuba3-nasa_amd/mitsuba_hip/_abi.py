@@ -111,7 +111,7 @@ EXPORTS = [
     "mh_last_error", "mh_abi_version", "mh_device_count", "mh_scene_create", "mh_scene_destroy",
     "mh_scene_set_stream", "mh_scene_update_rgb", "mh_scene_update_texture", "mh_render",
     "mh_develop", "mh_prb_weights", "mh_render_backward", "mh_trace_closest", "mh_trace_shadow",
-    "mh_scene_bvh_info", "mh_render_samples", "mh_scene_update_medium",
+    "mh_scene_bvh_info", "mh_render_samples", "mh_scene_update_medium", "mh_trace_preliminary",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -159,6 +159,7 @@ def lib():
                                      PU, C.POINTER(vp), u32, C.POINTER(Stats)]
     L.mh_trace_closest.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, u32, C.POINTER(Stats)]
     L.mh_trace_shadow.argtypes = [vp, u64, vp, vp, u32, C.POINTER(Stats)]
+    L.mh_trace_preliminary.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, C.POINTER(Stats)]
     L.mh_scene_bvh_info.argtypes = [vp, PU, PU, PU]
     for name in EXPORTS:
         if name not in ("mh_last_error", "mh_abi_version"):

@@ -540,7 +540,12 @@ int oracle_trace_closest(const mh_scene_desc *desc, uint64_t n, const float *ray
                   V3(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]), rays[6 * n + i]};
         pi_rec pi;
         trace_closest(&sv, &r, &pi);
-        t[i] = pi.t; u[i] = pi.u; v[i] = pi.v; prim[i] = pi.prim; shape[i] = pi.shape;
+        /* the OptiX payload: prim_index 0 for rectangles and misses
+         * (rectangle.cuh:42, scene_optix.inl:602-606), prim_uv 0 on a miss */
+        const int hit = pi.shape != MH_INVALID;
+        t[i] = pi.t; u[i] = hit ? pi.u : 0.f; v[i] = hit ? pi.v : 0.f;
+        prim[i] = hit && pi.prim != MH_INVALID ? pi.prim : 0u;
+        shape[i] = pi.shape;
     }
     scene_view_free(&sv);
     return 0;
@@ -1185,20 +1190,26 @@ typedef struct {
     uint32_t W, H, spp, spp_pp, n_passes, log_spp; /* log_spp = 32 if not pow2 */
 } wf_layout;
 
-static void wf_init(const mh_sensor *s, uint32_t spp, wf_layout *L) {
+/* ad: ADIntegrator.prepare's single wavefront of <= 2^32 samples
+ * (common.py:571-578; prb / prbvolpath primal, W image, render_backward);
+ * otherwise SamplingIntegrator::render's passes (integrator.cpp:281-295).
+ * Returns nonzero when an ad wavefront exceeds 2^32. */
+static int wf_init(const mh_sensor *s, uint32_t spp, wf_layout *L, int ad) {
     L->W = s->width;
     L->H = s->height;
     L->spp = spp;
     uint64_t wf = (uint64_t)L->W * L->H * spp, lim = 0xffffffffull;
     L->spp_pp = spp;
     L->n_passes = 1;
-    if (wf > lim) {
+    if (ad && wf > (1ull << 32)) return 1;
+    if (!ad && wf > lim) {
         L->spp_pp = spp / (uint32_t)((wf + lim - 1) / lim);
         L->n_passes = spp / L->spp_pp;
     }
     L->log_spp = 32;
     for (uint32_t k = 0; k < 32; ++k)
         if ((1u << k) == L->spp_pp) L->log_spp = k;
+    return 0;
 }
 
 /* lane -> pixel (integrator.cpp:323-340) */
@@ -2076,7 +2087,8 @@ int oracle_sample_range(const mh_scene_desc *desc, const mh_integrator *integ, u
     if (scene_view_init(&sv, desc)) return 1;
     if (spp == 0) spp = desc->sensor.sample_count;
     wf_layout L;
-    wf_init(&desc->sensor, spp, &L);
+    const int ad = integ->type == MH_INTEGRATOR_PRB || integ->type == MH_INTEGRATOR_PRBVOLPATH;
+    if (wf_init(&desc->sensor, spp, &L, ad)) { scene_view_free(&sv); return fail("wavefront exceeds 2^32 samples"); }
     if (L.n_passes != 1) { scene_view_free(&sv); return fail("oracle_sample_range: multi-pass not supported"); }
     uint32_t seed_value = desc->sensor.sampler_seed + seed;
     for (uint64_t i = idx_begin; i < idx_end; ++i) {
@@ -2240,20 +2252,29 @@ static size_t param_count(const mh_scene_desc *desc, uint32_t id) {
     return tx->type == MH_TEX_RGB ? 3 : (size_t)tx->width * tx->height * tx->channels;
 }
 
+/* rows [row_lo, row_hi) of pixels whose samples are run (0, 0: all rows) */
 static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kind kind,
                      uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
                      int n_threads, float *film, const float *grad_in, const float *weights,
-                     uint32_t n_params, const uint32_t *param_tex, float *const *grads) {
+                     uint32_t n_params, const uint32_t *param_tex, float *const *grads,
+                     uint32_t row_lo, uint32_t row_hi) {
     scene_view sv;
     if (scene_view_init(&sv, desc)) return 1;
     const mh_sensor *s = &desc->sensor;
     if (spp == 0) spp = s->sample_count;
     wf_layout L;
-    wf_init(s, spp, &L);
+    const int ad = kind != JOB_RENDER || in->type == MH_INTEGRATOR_PRB || in->type == MH_INTEGRATOR_PRBVOLPATH;
+    if (wf_init(s, spp, &L, ad)) {
+        scene_view_free(&sv);
+        return fail("The total number of Monte Carlo samples required by this rendering task exceeds 2^32");
+    }
     if (spp_end == 0 && spp_begin == 0) spp_end = L.spp_pp;
     if (spp_end > L.spp_pp || spp_begin >= spp_end) { scene_view_free(&sv); return fail("invalid sample slab"); }
+    if (row_lo == 0 && row_hi == 0) row_hi = L.H;
+    if (row_hi > L.H || row_lo >= row_hi) { scene_view_free(&sv); return fail("invalid row range"); }
+    const uint32_t n_rows = row_hi - row_lo;
     if (n_threads < 1) n_threads = 1;
-    if ((uint32_t)n_threads > L.H) n_threads = (int)L.H;
+    if ((uint32_t)n_threads > n_rows) n_threads = (int)n_rows;
     uint32_t margin = splat_margin(s);
     band_job *jobs = (band_job *)calloc((size_t)n_threads, sizeof(band_job));
     pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
@@ -2264,8 +2285,8 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
         j->sv = &sv; j->in = in; j->L = &L; j->kind = kind;
         j->seed_value = s->sampler_seed + seed;
         j->spp_begin = spp_begin; j->spp_end = spp_end;
-        j->row_begin = (uint32_t)((uint64_t)L.H * t / n_threads);
-        j->row_end = (uint32_t)((uint64_t)L.H * (t + 1) / n_threads);
+        j->row_begin = row_lo + (uint32_t)((uint64_t)n_rows * t / n_threads);
+        j->row_end = row_lo + (uint32_t)((uint64_t)n_rows * (t + 1) / n_threads);
         j->grad_in = grad_in; j->weights = weights;
         if (kind != JOB_BACKWARD) {
             int32_t r0 = (int32_t)j->row_begin - (int32_t)margin;
@@ -2329,14 +2350,24 @@ int oracle_render(const mh_scene_desc *desc, const mh_integrator *integ, uint32_
                   uint32_t spp, uint32_t spp_begin, uint32_t spp_end, int n_threads,
                   float *film_rgbw) {
     return run_bands(desc, integ, JOB_RENDER, seed, spp, spp_begin, spp_end, n_threads,
-                     film_rgbw, NULL, NULL, 0, NULL, NULL);
+                     film_rgbw, NULL, NULL, 0, NULL, NULL, 0, 0);
 }
 
 int oracle_prb_weights(const mh_scene_desc *desc, uint32_t seed, uint32_t spp,
                        uint32_t spp_begin, uint32_t spp_end, int n_threads, float *weights) {
     mh_integrator dummy = {MH_INTEGRATOR_PRB, 1, 1, 0};
     return run_bands(desc, &dummy, JOB_WEIGHTS, seed, spp, spp_begin, spp_end, n_threads,
-                     weights, NULL, NULL, 0, NULL, NULL);
+                     weights, NULL, NULL, 0, NULL, NULL, 0, 0);
+}
+
+/* W image from the samples of pixel rows [row_lo, row_hi) only (test helper
+ * for films too large to sweep: rows [row_lo + 2, row_hi - 2) -- and the
+ * image border rows inside the range -- equal oracle_prb_weights) */
+int oracle_prb_weights_rows(const mh_scene_desc *desc, uint32_t seed, uint32_t spp, uint32_t row_lo,
+                            uint32_t row_hi, int n_threads, float *weights) {
+    mh_integrator dummy = {MH_INTEGRATOR_PRB, 1, 1, 0};
+    return run_bands(desc, &dummy, JOB_WEIGHTS, seed, spp, 0, 0, n_threads, weights, NULL, NULL, 0, NULL,
+                     NULL, row_lo, row_hi);
 }
 
 int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ,
@@ -2361,7 +2392,7 @@ int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ
         weights = w_local;
     }
     int rc = run_bands(desc, integ, JOB_BACKWARD, seed, spp, spp_begin, spp_end, n_threads, NULL,
-                       grad_in, weights, n_params, param_textures, grads);
+                       grad_in, weights, n_params, param_textures, grads, 0, 0);
     free(w_local);
     return rc;
 }

@@ -71,6 +71,8 @@ void oracle_develop_format(uint32_t w, uint32_t h, uint32_t pixel_format, const 
 /* PRB: per-pixel filter-weight image W (H*W) of the backward pass. */
 int oracle_prb_weights(const mh_scene_desc *desc, uint32_t seed, uint32_t spp,
                        uint32_t spp_begin, uint32_t spp_end, int n_threads, float *weights);
+int oracle_prb_weights_rows(const mh_scene_desc *desc, uint32_t seed, uint32_t spp, uint32_t row_lo,
+                            uint32_t row_hi, int n_threads, float *weights);
 /* PRB render_backward: grads[k] accumulated (double precision internally). */
 int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ,
                            uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,

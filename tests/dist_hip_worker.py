@@ -1,0 +1,35 @@
+"""Rank worker of tests/test_gpu_multirank.py, launched by
+`python -m torch.distributed.run --nproc-per-node 2 ...`: one bench step
+(bench.build_step: the HIP C-ABI path, forward + W all-reduce + PRB
+gradient) on this rank's sample slab, every rank on cuda:0 over gloo (the
+driver's N-GPU run uses one device per rank over RCCL).  Saves the
+all-reduced image and gradient to <out>/r<rank>.npz."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mitsuba3-nasa_amd")]
+
+
+def main():
+    out, res, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import bench
+    from mitsuba_hip import distributed as D
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    w = bench.build_step(res, spp, 6, rank, world, torch.device("cuda:0"))
+    img, grads = D.fwd_grad_step(w["ops"], w["slab"], seed=11)
+    torch.cuda.synchronize()
+    t = D.max_over_ranks(float(rank) + 0.25, torch.device("cuda:0"))
+    np.savez(os.path.join(out, f"r{rank}.npz"), img=img.cpu().numpy(), g=grads[0].cpu().numpy(), t=t,
+             begin=w["slab"].begin, end=w["slab"].end)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -49,6 +49,8 @@ def lib():
     L.oracle_develop_format.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]
     L.oracle_prb_weights.argtypes = [C.POINTER(A.SceneDesc), C.c_uint32, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.c_int, vp]
+    L.oracle_prb_weights_rows.argtypes = [C.POINTER(A.SceneDesc), C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, C.c_int, vp]
     L.oracle_render_backward.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32,
                                          C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint32,
                                          vp, C.POINTER(C.c_void_p), C.c_int]
@@ -67,7 +69,15 @@ def check(rc):
 
 
 def nthreads():
-    return max(1, min(os.cpu_count() or 1, 64))
+    """Host threads of the oracle: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS where it is set (the GPU box's share is 16 of a larger
+    machine) and by 64."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 64
+    return max(1, min(n, cap, 64))
 
 
 def render(scene, integrator=None, seed=0, spp=0, spp_begin=0, spp_end=0, threads=None):
@@ -118,6 +128,15 @@ def prb_weights(scene, seed, spp, spp_begin=0, spp_end=0, threads=None):
     w = np.zeros((scene.height, scene.width), np.float32)
     check(lib().oracle_prb_weights(C.byref(scene.desc), seed, spp, spp_begin, spp_end,
                                    threads or nthreads(), _p(w)))
+    return w
+
+
+def prb_weights_rows(scene, seed, spp, row_lo, row_hi, threads=None):
+    """W image from the samples of pixel rows [row_lo, row_hi) only: exact on
+    rows [row_lo + 2, row_hi - 2) and on image-border rows inside the range."""
+    w = np.zeros((scene.height, scene.width), np.float32)
+    check(lib().oracle_prb_weights_rows(C.byref(scene.desc), seed, spp, row_lo, row_hi, threads or nthreads(),
+                                        _p(w)))
     return w
 
 

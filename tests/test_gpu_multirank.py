@@ -1,0 +1,49 @@
+"""The N > 1 path of bench.py on one GPU: 2 ranks (torch.distributed.run,
+gloo, both on cuda:0) through the real HIP StepOps (bench.build_step), vs the
+single-process HIP result of the same sample set.  Sample-slab sharding
+(SURVEY.md §8(e)): rank r renders samples [8 r, 8 r + 8) of a 16-spp render
+with unchanged lane indices, so the all-reduced film / W / gradient equal the
+one-process run up to float summation order."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
+    import torch
+    sys.path[:0] = [ROOT]
+    import bench
+    from mitsuba_hip import distributed as D
+    res, spp = 48, 8
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_hip_worker.py"), str(tmp_path), str(res), str(spp)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, timeout=100, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    r0, r1 = (np.load(tmp_path / f"r{i}.npz") for i in range(2))
+    assert (int(r0["begin"]), int(r0["end"]), int(r1["begin"]), int(r1["end"])) == (0, 8, 8, 16)
+    assert float(r0["t"]) == float(r1["t"]) == 1.25  # max over ranks
+    np.testing.assert_array_equal(r0["img"], r1["img"])
+    np.testing.assert_array_equal(r0["g"], r1["g"])
+    w = bench.build_step(res, 2 * spp, 6, 0, 1, torch.device("cuda:0"))
+    img, grads = D.fwd_grad_step(w["ops"], w["slab"], seed=11)
+    img, g = img.cpu().numpy(), grads[0].cpu().numpy()
+    assert img.mean() > 0 and np.abs(g).min() > 0
+    np.testing.assert_allclose(r0["img"], img, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(r0["g"], g, rtol=1e-4)

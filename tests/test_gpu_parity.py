@@ -72,6 +72,27 @@ def test_trace_parity():
     assert hit.mean() > 0.3
     np.testing.assert_array_equal(u[same & hit], ru[same & hit])
     np.testing.assert_array_equal(v[same & hit], rv[same & hit])
+    # the OptiX payload (scene_optix.inl:602-657): rectangles report
+    # prim_index 0 (rectangle.cuh:42); a miss leaves prim_index 0, prim_uv
+    # (0, 0), t = +inf and a null shape (optix_rt.cu:9-17)
+    is_rect = np.isin(shape, [i for i in range(scene.desc.n_shapes)
+                              if scene.desc.shapes[i].type == 0])
+    assert is_rect.sum() > 1000 and (~is_rect & hit).sum() > 1000
+    assert np.all(prim[is_rect & hit] == 0)
+    miss = shape == 0xFFFFFFFF
+    assert miss.sum() > 0
+    assert np.all(prim[miss] == 0) and np.all(u[miss] == 0) and np.all(v[miss] == 0) and np.all(np.isinf(t[miss]))
+    # instance payload: null for every ray (no shapegroups, scene_optix.inl:607-608)
+    from mitsuba_hip import _abi as A
+    n = rays.shape[1]
+    t2, u2, v2 = (np.zeros(n, np.float32) for _ in range(3))
+    prim2, shape2, inst = (np.zeros(n, np.uint32) for _ in range(3))
+    p = lambda a: a.ctypes.data_as(C.c_void_p)
+    A.check(A.lib().mh_trace_preliminary(scene.handle(0), n, p(np.ascontiguousarray(rays)), p(t2), p(u2), p(v2),
+                                         p(prim2), p(shape2), p(inst), 0, None))
+    assert np.all(inst == 0xFFFFFFFF)
+    np.testing.assert_array_equal(prim2, prim)
+    np.testing.assert_array_equal(shape2, shape)
 
 
 def _gpu_samples(mi, scene, integrator, seed, spp, flags=0):
@@ -366,6 +387,54 @@ def test_multipass_config5_slab_parity():
     assert ok, f"film parity {frac}"
 
 
+@pytest.mark.slow
+def test_config5_prb_gradient_slab_parity():
+    """Config 5's gradient leg: 2048^2 @ 1024 = 2^32 samples is ONE AD
+    wavefront (ADIntegrator.prepare raises only above 2^32, common.py:571-578;
+    lane indices [0, 2^32) in uint32).  The W image sums all 2^32 jitters; the
+    gradient of the top slab [1022, 1024) of every pixel (the last lane is
+    2^32 - 1) vs the oracle with the same W."""
+    mi = _mi()
+    import torch
+    scene = cbox(mi, 2048, 2048, 1024)
+    integ = mi.load_dict({"type": "prb", "max_depth": 4})
+    params = mi.traverse(scene)
+    key = "white.reflectance.value"
+    seed = mi.sample_tea_32(2, 1)[0]
+    w = mi.prb_weights(scene, seed, 1024)
+    wn = w.cpu().numpy()
+    top = O.prb_weights_rows(scene, seed, 1024, 0, 6)
+    bot = O.prb_weights_rows(scene, seed, 1024, 2042, 2048)
+    np.testing.assert_allclose(wn[:4], top[:4], rtol=1e-4)
+    np.testing.assert_allclose(wn[-4:], bot[-4:], rtol=1e-4)
+    gi = np.full((2048, 2048, 3), 1.0 / (2048 * 2048 * 3), np.float32)
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), [key], integ, seed=seed, spp=1024,
+                           spp_begin=1022, spp_end=1024, weights=w)[0].cpu().numpy()
+    ref = O.render_backward(scene, integ, seed, 1024, gi, [params.texture_of(key)], [(3,)], weights=wn,
+                            spp_begin=1022, spp_end=1024)[0]
+    assert np.abs(ref).max() > 0
+    np.testing.assert_allclose(g, ref, rtol=1e-3, atol=1e-9)
+
+
+def test_ad_wavefront_limit():
+    """prepare() raises above 2^32 samples (common.py:571-578); the C++
+    SamplingIntegrator (path) splits into passes instead."""
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = cbox(mi, 2048, 2048, 1536)   # 1.5 * 2^32 samples
+    with pytest.raises(A.MitsubaHipError, match="exceeds 2\\^32"):
+        mi.prb_weights(scene, 1, 1536)
+    with pytest.raises(A.MitsubaHipError, match="exceeds 2\\^32"):
+        mi.render_film(scene, mi.load_dict({"type": "prb"}), seed=0, spp=1536, spp_begin=0, spp_end=1)
+    st = A.Stats()
+    film = mi.render_film(scene, mi.load_dict({"type": "path", "max_depth": 2}), seed=0, spp=1536,
+                          spp_begin=0, spp_end=1, stats=st)   # 4 passes of 384
+    assert float(film[..., 3].sum()) > 0 and st.samples == 2048 * 2048 * 4
+    # integrator.cpp:281-295 + the spp_per_pass divisibility error
+    with pytest.raises(A.MitsubaHipError, match="multiple of samples_per_wavefront"):
+        mi.render_film(scene, mi.load_dict({"type": "path"}), seed=0, spp=2048, spp_begin=0, spp_end=1)
+
+
 def test_multipass_wavefront_matches_megakernel():
     """The fused wavefront runs the passes of a > 2^32-sample render back to
     back, carrying each lane's PCG32 state (integrator.cpp:353-357); the
@@ -409,6 +478,29 @@ def test_multi_emitter_per_sample_parity(itype, mode):
     exact = np.all(L == rL, axis=1)
     assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
     assert rL.mean() > 0
+
+
+@pytest.mark.parametrize("mode", ["wavefront", "mega", "wavefront-unfused"])
+def test_hide_emitters_path_parity(mode, monkeypatch):
+    """path with hide_emitters and an environment: camera rays that escape
+    return 0 (valid_ray, path.cpp:115, 256, 284); later escapes still see the
+    environment."""
+    if mode == "wavefront-unfused":
+        monkeypatch.setenv("MH_WF_FUSED", "0")
+        mode = "wavefront"
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"], d["sensor"]["film"]["height"] = 24, 20
+    d.pop("back")   # open box: camera rays escape
+    d["sky"] = {"type": "constant", "radiance": {"type": "rgb", "value": [0.3, 0.4, 0.5]}}
+    scene = mi.load_dict(d)
+    integ = mi.load_dict({"type": "path", "max_depth": 6, "hide_emitters": True})
+    L, pos = _gpu_samples(mi, scene, integ, 5, 8, A.FLAG_WAVEFRONT if mode == "wavefront" else 0)
+    rL, rpos, _ = O.sample_range(scene, integ, 5, 8, 0, L.shape[0])
+    exact = np.all(L == rL, axis=1)
+    assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
+    assert (rL.sum(1) == 0).mean() > 0.05 and rL.mean() > 0
 
 
 def test_multi_emitter_prb_backward_parity():
@@ -547,3 +639,69 @@ def test_large_mesh_per_sample_parity(bvh4, fused, monkeypatch):
     np.testing.assert_array_equal(pos, rpos)
     exact = np.all(L == rL, axis=1)
     assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
+
+
+# ---------------------------------------------------------------------------
+# smooth shading frames on the device: a height-field mesh with
+# interpolated vertex normals (meshio.recompute_vertex_normals, the
+# reference's angle-weighted normals) and uvs driving a bitmap texture
+# (mesh.cpp:1368-1460 compute_surface_interaction: shading frame from the
+# interpolated normal, uv from the texcoords)
+# ---------------------------------------------------------------------------
+def _smooth_mesh_scene(mi, n, w=32, h=28, spp=8):
+    from mitsuba_hip import meshio
+    x, y = np.meshgrid(np.linspace(-0.8, 0.8, n), np.linspace(-0.8, 0.8, n))
+    z = 0.15 * np.sin(3 * x) * np.cos(2 * y)
+    V = np.stack([x, y, z], -1).reshape(-1, 3).astype(np.float32)
+    UV = np.stack([(x + 0.8) / 1.6, (y + 0.8) / 1.6], -1).reshape(-1, 2).astype(np.float32)
+    i = np.arange(n - 1)
+    a = (i[:, None] * n + i[None, :]).reshape(-1)
+    F = np.concatenate([np.stack([a, a + 1, a + n + 1], 1), np.stack([a, a + n + 1, a + n], 1)]).astype(np.uint32)
+    T = mi.Transform4f
+    to_world = T.translate([0, 0.1, 0]) @ T.rotate([1, 0, 0], -70)
+    Vw = (V.astype(np.float64) @ to_world.matrix[:3, :3].T + to_world.matrix[:3, 3]).astype(np.float32)
+    N = meshio.recompute_vertex_normals(Vw, F)
+    tex = np.random.default_rng(5).uniform(0.2, 0.9, (8, 8, 3)).astype(np.float32)
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"], d["sensor"]["film"]["height"] = w, h
+    d["sensor"]["sampler"]["sample_count"] = spp
+    d.pop("small-box")
+    d.pop("large-box")
+    d["bumpy"] = {"type": "mesh", "vertex_positions": Vw, "faces": F, "vertex_normals": N, "vertex_texcoords": UV,
+                  "bsdf": {"type": "diffuse", "reflectance": {"type": "bitmap", "data": tex, "raw": True,
+                                                              "filter_type": "bilinear"}}}
+    return mi.load_dict(d)
+
+
+@pytest.mark.parametrize("n,mode", [(5, "wavefront"), (5, "mega"), (12, "wavefront"), (12, "mega")])
+def test_smooth_normals_per_sample_parity(n, mode):
+    """n = 5: 32 triangles + 6 rectangles (packet engine, fused bounce);
+    n = 12: 242 triangles (per-lane stream engine, unfused wavefront)."""
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = _smooth_mesh_scene(mi, n)
+    assert scene.desc.normals and scene.desc.texcoords
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+    L, pos = _gpu_samples(mi, scene, integ, 4, 8, A.FLAG_WAVEFRONT if mode == "wavefront" else 0)
+    rL, rpos, _ = O.sample_range(scene, integ, 4, 8, 0, L.shape[0])
+    np.testing.assert_array_equal(pos, rpos)
+    exact = np.all(L == rL, axis=1)
+    assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
+    assert rL.mean() > 0
+
+
+def test_smooth_normals_prb_gradient_parity():
+    mi = _mi()
+    import torch
+    scene = _smooth_mesh_scene(mi, 5, 24, 20, 8)
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    keys = ["bumpy.bsdf.reflectance.data", "red.reflectance.value"]
+    gi = np.random.default_rng(1).random((20, 24, 3)).astype(np.float32) / (20 * 24 * 3)
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=6, spp=8)
+    ref = O.render_backward(scene, integ, 6, 8, gi, [params.texture_of(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    for k, a, b in zip(keys, g, ref):
+        a = a.cpu().numpy()
+        assert np.abs(b).max() > 0, k
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max(), err_msg=k)
