@@ -68,7 +68,10 @@ enum { MH_BSDF_DIFFUSE = 0, MH_BSDF_NULL = 1 };               /* diffuse.cpp, nu
 enum { MH_TEX_RGB = 0, MH_TEX_BITMAP = 1 };                   /* srgb.cpp, bitmap.cpp */
 enum { MH_EMITTER_AREA = 0, MH_EMITTER_CONSTANT = 1, MH_EMITTER_DIRECTIONAL = 2 };
 enum { MH_RFILTER_BOX = 0, MH_RFILTER_GAUSSIAN = 1 };         /* box.cpp, gaussian.cpp */
-enum { MH_PIXEL_RGB = 0, MH_PIXEL_Y = 1, MH_PIXEL_XYZ = 2 };   /* Bitmap::PixelFormat rgb / luminance / xyz */
+/* Bitmap::PixelFormat of hdrfilm's 'pixel_format': rgb / luminance / xyz, and
+ * the alpha variants rgba / ya / xyza (films with FilmFlags::Alpha) */
+enum { MH_PIXEL_RGB = 0, MH_PIXEL_Y = 1, MH_PIXEL_XYZ = 2, MH_PIXEL_RGBA = 3, MH_PIXEL_YA = 4,
+       MH_PIXEL_XYZA = 5 };
 enum { MH_MEDIUM_HETEROGENEOUS = 0, MH_MEDIUM_HOMOGENEOUS = 1 };
 enum { MH_PHASE_ISOTROPIC = 0, MH_PHASE_HG = 1 };
 enum { MH_MEDIUM_NO_EMITTER_SAMPLING = 1u,        /* medium.cpp:29 sample_emitters = false */
@@ -254,7 +257,12 @@ int mh_scene_update_medium(mh_scene *scene, uint32_t medium, const float *albedo
 int mh_scene_update_texture(mh_scene *scene, uint32_t texture, const float *data, uint64_t n_floats);
 
 /*
- * Forward render into an un-developed RGBW film (H*W*4 floats).
+ * Forward render into the un-developed film storage: RGBW (H*W*4 floats), or
+ * R G B A W (H*W*5) when the film has an alpha channel (MH_PIXEL_RGBA / YA /
+ * XYZA; hdrfilm.cpp:327-330 base_ch = 5).  A sample's alpha is 1 where the
+ * integrator reports a valid ray, else 0 (integrator.cpp:1229-1231; path
+ * valid_ray, prb depth != 0, volpath / prbvolpath valid_ray), splatted with
+ * the sample's filter weights like the colour.
  *   seed      : render seed (Integrator::render `seed`)
  *   spp       : samples per pixel (0 = sensor sample_count)
  *   spp_begin/spp_end : sample-slab [begin, end) of every pixel rendered by this call
@@ -269,22 +277,26 @@ int mh_render(mh_scene *scene, const mh_integrator *integrator, uint32_t seed, u
  * Per-sample outputs of the integrator (the value `sample()` returns per lane,
  * path.cpp:283-286 / prb.py:253-257) and the splat position, for sample-level
  * parity tests.  out = 5 SoA planes of n = W*H*(spp_end-spp_begin) floats:
- * L.r, L.g, L.b, pos.x, pos.y, lane order idx = pixel * S + s.  Single pass only.
+ * L.r, L.g, L.b, pos.x, pos.y, lane order idx = pixel * S + s, plus a 6th
+ * plane (alpha: 1 valid, 0 not) when the film has alpha.  Single pass only.
  */
 int mh_render_samples(mh_scene *scene, const mh_integrator *integrator, uint32_t seed,
                       uint32_t spp, uint32_t spp_begin, uint32_t spp_end, float *out,
                       uint32_t flags);
 
-/* RGBW film -> developed image (HDRFilm::develop, hdrfilm.cpp:304-405):
+/* film -> developed image (HDRFilm::develop, hdrfilm.cpp:304-405):
  * H*W*3 for MH_PIXEL_RGB (rgb / w) and MH_PIXEL_XYZ (srgb_to_xyz(rgb) / w),
- * H*W*1 for MH_PIXEL_Y (luminance(rgb) / w); w == 0 divides by 1. */
+ * H*W*1 for MH_PIXEL_Y (luminance(rgb) / w); the alpha formats append a / w:
+ * H*W*4 (RGBA, XYZA), H*W*2 (YA).  w == 0 divides by 1. */
 int mh_develop(mh_scene *scene, const float *film_rgbw, float *image_rgb, uint32_t flags);
 
 /*
  * Reverse-mode derivative of render(): accumulates d(loss)/d(param) for each
  * listed parameter into grads[k] (3 floats for MH_TEX_RGB, W*H*C for
- * MH_TEX_BITMAP; medium ids: see MH_PARAM_*).  `grad_in` is d(loss)/d(image),
- * H*W*3.  integrator: MH_INTEGRATOR_PRB (prb.py) or MH_INTEGRATOR_PRBVOLPATH
+ * MH_TEX_BITMAP; medium ids: see MH_PARAM_*).  `grad_in` is d(loss)/d(rgb
+ * before the colour conversion of develop), H*W*3: the caller applies the
+ * adjoint of luminance / srgb_to_xyz and drops the alpha channel, whose
+ * value (a validity mask) carries no derivative.  integrator: MH_INTEGRATOR_PRB (prb.py) or MH_INTEGRATOR_PRBVOLPATH
  * (prbvolpath.py: primal + adjoint replay per lane; grid gradients are
  * scattered with float atomics, so their summation order is not fixed).
  *   weights_rgbw (optional, device flag applies): the per-pixel filter-weight

@@ -85,7 +85,7 @@ struct mh_scene {
     // device buffers
     DevBuf nodes, nodes4, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
-    DevBuf work, film_tmp, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
+    DevBuf work, film_tmp, film4, alpha_px, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     // host mirrors (parameter updates)
@@ -295,7 +295,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         if (a.phase == MH_PHASE_HG && !(a.g > -1.f && a.g < 1.f))
             return fail(MH_ERR_INVALID_ARGUMENT, "The asymmetry parameter must lie in the interval (-1, 1)!");
     }
-    if (desc->sensor.pixel_format > MH_PIXEL_XYZ)
+    if (desc->sensor.pixel_format > MH_PIXEL_XYZA)
         return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: unknown pixel format");
     s->pixel_format = desc->sensor.pixel_format;
     // density grids in the 4^3-brick device layout (grid_index)
@@ -445,7 +445,7 @@ int mh_scene_destroy(mh_scene *s) {
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
-                      &s->media, &s->grid, &s->work, &s->film_tmp, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
+                      &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -550,6 +550,14 @@ int mh_scene_update_medium(mh_scene *s, uint32_t medium, const float *albedo, co
 // ---------------------------------------------------------------------------
 // Render
 // ---------------------------------------------------------------------------
+static bool has_alpha(uint32_t fmt) {
+    return fmt == MH_PIXEL_RGBA || fmt == MH_PIXEL_YA || fmt == MH_PIXEL_XYZA;
+}
+// channels of the developed image (hdrfilm.cpp:349-372: color_ch + alpha)
+static uint32_t image_channels(uint32_t fmt) {
+    const uint32_t c = (fmt == MH_PIXEL_Y || fmt == MH_PIXEL_YA) ? 1u : 3u;
+    return c + (has_alpha(fmt) ? 1u : 0u);
+}
 struct Layout {
     uint32_t W, H, spp, spp_pp, n_passes, s_begin, s_end;
 };
@@ -618,14 +626,27 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
+    // film storage: RGBW, or R G B A W for alpha films; the kernels splat into
+    // an RGBW film (+ an alpha plane) that an alpha film receives at the end
+    const bool alpha = has_alpha(s->pixel_format);
+    const size_t film_bytes = n_px * (alpha ? 20 : 16);
     float *film = film_rgbw;
     if (!(flags & MH_FLAG_DEVICE_POINTERS)) {
-        MH_HIP(s->film_tmp.alloc(n_px * 16));
+        MH_HIP(s->film_tmp.alloc(film_bytes));
         film = s->film_tmp.as<float>();
     }
     if (!(flags & MH_FLAG_ACCUMULATE) || !(flags & MH_FLAG_DEVICE_POINTERS)) {
-        if (!(flags & MH_FLAG_ACCUMULATE)) MH_HIP(hipMemsetAsync(film, 0, n_px * 16, st));
-        else MH_HIP(hipMemcpyAsync(film, film_rgbw, n_px * 16, hipMemcpyHostToDevice, st));
+        if (!(flags & MH_FLAG_ACCUMULATE)) MH_HIP(hipMemsetAsync(film, 0, film_bytes, st));
+        else MH_HIP(hipMemcpyAsync(film, film_rgbw, film_bytes, hipMemcpyHostToDevice, st));
+    }
+    float *film4 = film, *film_a = nullptr;
+    if (alpha) {
+        MH_HIP(s->film4.alloc(n_px * 16));
+        MH_HIP(s->alpha_px.alloc(n_px * 4));
+        film4 = s->film4.as<float>();
+        film_a = s->alpha_px.as<float>();
+        MH_HIP(hipMemsetAsync(film4, 0, n_px * 16, st));
+        MH_HIP(hipMemsetAsync(film_a, 0, n_px * 4, st));
     }
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
     const uint32_t S_ = L.s_end - L.s_begin;
@@ -647,7 +668,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     }
     uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
     const uint64_t plane = (uint64_t)chunk_px * per_pixel;
-    MH_HIP(s->work.alloc(plane * 5 * sizeof(float)));
+    MH_HIP(s->work.alloc(plane * (alpha ? 6 : 5) * sizeof(float)));
     const bool fast_splat = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN &&
                             s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
     const int coalesce = L.spp_pp >= 4;
@@ -681,17 +702,21 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
             MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
                                     s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
                                     n_bounces, wf_blocks(cus), ev + 2, st, L.n_passes,
-                                    L.n_passes > 1 ? s->wf_carry.as<uint64_t>() : nullptr));
+                                    L.n_passes > 1 ? s->wf_carry.as<uint64_t>() : nullptr, alpha));
         } else {
             MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
-                                 s->counters.as<unsigned long long>(), st));
+                                 s->counters.as<unsigned long long>(), st, alpha));
         }
         MH_HIP(hipEventRecord(ev[1], st));
-        MH_HIP(launch_splat(s->S, lm, false, fast_splat, npx, L.n_passes, n, plane,
-                            s->work.as<float>(), film, seed_value, coalesce, st));
+        MH_HIP(launch_splat(s->S, lm, kSplatFilm, fast_splat, npx, L.n_passes, n, plane,
+                            s->work.as<float>(), film4, seed_value, coalesce, st));
+        if (alpha)
+            MH_HIP(launch_splat(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane,
+                                s->work.as<float>(), film_a, seed_value, coalesce, st));
     }
+    if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
-        MH_HIP(hipMemcpyAsync(film_rgbw, film, n_px * 16, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
     unsigned long long ctr[2] = {0, 0};
     std::vector<uint32_t> wctr;
     if (wavefront) {
@@ -750,9 +775,11 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const uint64_t n = (uint64_t)L.W * L.H * (L.s_end - L.s_begin);
+    const bool alpha = has_alpha(s->pixel_format);
+    const size_t out_bytes = n * (alpha ? 24 : 20);
     float *dst = out;
     if (!(flags & MH_FLAG_DEVICE_POINTERS)) {
-        MH_HIP(s->tmp_a.alloc(n * 20));
+        MH_HIP(s->tmp_a.alloc(out_bytes));
         dst = s->tmp_a.as<float>();
     }
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
@@ -765,13 +792,14 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(n)));
         MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, 4 * (size_t)wf_counter_words(in->max_depth))));
         MH_HIP(launch_wavefront(s->S, *in, lm, s->S.sampler_seed + seed, n, n, dst, s->wf_ws.ptr, n,
-                                s->wf_ctr.as<uint32_t>(), in->max_depth, wf_blocks(cus), nullptr, st));
+                                s->wf_ctr.as<uint32_t>(), in->max_depth, wf_blocks(cus), nullptr, st, 1, nullptr,
+                                alpha));
     } else {
         MH_HIP(launch_render(s->S, *in, lm, s->S.sampler_seed + seed, 1, n, n, dst,
-                             s->counters.as<unsigned long long>(), st));
+                             s->counters.as<unsigned long long>(), st, alpha));
     }
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
-        MH_HIP(hipMemcpyAsync(out, dst, n * 20, hipMemcpyDeviceToHost, st));
+        MH_HIP(hipMemcpyAsync(out, dst, out_bytes, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
     return MH_OK;
 }
@@ -781,15 +809,16 @@ int mh_develop(mh_scene *s, const float *film_rgbw, float *image_rgb, uint32_t f
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)s->S.width * s->S.height;
-    const uint32_t fmt = s->pixel_format, ch = fmt == MH_PIXEL_Y ? 1 : 3;
+    const uint32_t fmt = s->pixel_format, ch = image_channels(fmt);
+    const size_t film_bytes = n_px * (has_alpha(fmt) ? 20 : 16);
     if (flags & MH_FLAG_DEVICE_POINTERS) {
         MH_HIP(launch_develop(n_px, film_rgbw, image_rgb, fmt, st));
         if (!(flags & MH_FLAG_NO_SYNC)) MH_HIP(hipStreamSynchronize(st));
         return MH_OK;
     }
-    MH_HIP(s->tmp_a.alloc(n_px * 16));
+    MH_HIP(s->tmp_a.alloc(film_bytes));
     MH_HIP(s->tmp_b.alloc(n_px * 4 * ch));
-    MH_HIP(hipMemcpyAsync(s->tmp_a.ptr, film_rgbw, n_px * 16, hipMemcpyHostToDevice, st));
+    MH_HIP(hipMemcpyAsync(s->tmp_a.ptr, film_rgbw, film_bytes, hipMemcpyHostToDevice, st));
     MH_HIP(launch_develop(n_px, s->tmp_a.as<float>(), s->tmp_b.as<float>(), fmt, st));
     MH_HIP(hipMemcpyAsync(image_rgb, s->tmp_b.ptr, n_px * 4 * ch, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
@@ -819,7 +848,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
                       s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
     LaneMap lm = lane_map(L, 0);
     const uint32_t S_ = L.s_end - L.s_begin;
-    MH_HIP(launch_splat(s->S, lm, true, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w,
+    MH_HIP(launch_splat(s->S, lm, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w,
                         s->S.sampler_seed + seed, L.spp_pp >= 4, st));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
@@ -952,7 +981,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         Lall.s_begin = 0;
         Lall.s_end = L.spp_pp;
         LaneMap lmw = lane_map(Lall, 0);
-        MH_HIP(launch_splat(s->S, lmw, true, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
+        MH_HIP(launch_splat(s->S, lmw, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
                             s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st));
         w = s->weights_tmp.as<float>();
     } else if (!dev) {

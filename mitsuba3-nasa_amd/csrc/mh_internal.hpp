@@ -59,11 +59,15 @@ hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *r
                         uint32_t grid, hipStream_t st);
 hipError_t launch_render(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                          uint32_t seed_value, uint32_t n_passes, uint64_t n, uint64_t plane,
-                         float *out, unsigned long long *counters, hipStream_t st);
-hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, bool fast,
+                         float *out, unsigned long long *counters, hipStream_t st, int alpha = 0);
+// splat modes: RGBW film from (L, pos) planes; W image from the RNG jitter;
+// alpha channel from (alpha, pos) planes (plane 5)
+enum { kSplatFilm = 0, kSplatWeights = 1, kSplatAlpha = 2 };
+hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
                         hipStream_t st);
+hipError_t launch_film_rgbaw(uint64_t n_px, const float *rgbw, const float *a, float *out, hipStream_t st);
 size_t wf_workspace_bytes(uint64_t cap);
 uint32_t wf_counter_words(uint32_t n_bounces);
 uint64_t wf_max_chunk();
@@ -71,7 +75,8 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
                             hipEvent_t *trace_ev, hipStream_t st, uint32_t n_passes = 1,
-                            uint64_t *carry = nullptr);  // carry: n PCG32 states (n_passes > 1)
+                            uint64_t *carry = nullptr,   // carry: n PCG32 states (n_passes > 1)
+                            int alpha = 0);              // alpha: write the validity plane (plane 5)
 size_t wf_prb_workspace_bytes(uint64_t cap);
 uint32_t wf_grid(uint32_t grid);
 uint32_t wf_blocks(int cus);  // wavefront workgroups for a device of `cus` CUs

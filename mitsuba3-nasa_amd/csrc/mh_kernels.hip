@@ -81,7 +81,8 @@ k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *_
 template <int Kind, bool InLds>
 __global__ void __launch_bounds__(256, (Kind == MH_INTEGRATOR_VOLPATH || Kind == MH_INTEGRATOR_PRBVOLPATH) ? MH_VOL_WAVES : 1)
 k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_t n_passes,
-         uint64_t n, uint64_t plane, float *__restrict__ out, unsigned long long *__restrict__ counters) {
+         uint64_t n, uint64_t plane, float *__restrict__ out, unsigned long long *__restrict__ counters,
+         int alpha) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -97,20 +98,24 @@ k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_
             float sx = (float)px + jx, sy = (float)py + jy;
             RayT r = camera_ray(S, __builtin_fmaf(sx, sw, -0.f), __builtin_fmaf(sy, sh, -0.f));
             V3 L;
+            bool valid = false;
             if (Kind == MH_INTEGRATOR_PRB)
-                L = prb_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow);
+                L = prb_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow,
+                                      &valid);
             else if (Kind == MH_INTEGRATOR_VOLPATH)
-                L = volpath_sample(S, B, in, rng, r, n_closest, n_shadow);
+                L = volpath_sample(S, B, in, rng, r, n_closest, n_shadow, &valid);
             else if (Kind == MH_INTEGRATOR_PRBVOLPATH)
-                L = prbvol_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow);
+                L = prbvol_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow,
+                                         &valid);
             else
-                L = path_sample(S, B, in, rng, r, n_closest, n_shadow);
+                L = path_sample(S, B, in, rng, r, n_closest, n_shadow, &valid);
             uint64_t o = (uint64_t)pass * n + k;
             out[o] = L.x;
             out[plane + o] = L.y;
             out[2 * plane + o] = L.z;
             out[3 * plane + o] = sx;
             out[4 * plane + o] = sy;
+            if (alpha) out[5 * plane + o] = valid ? 1.f : 0.f;  // aovs[3] (integrator.cpp:1229-1231)
         }
     }
     if (counters) {
@@ -142,7 +147,8 @@ MH_DEV void splat_one_atomic(const DScene &S, float *film, float px, float py, c
 }
 
 // Mode 0: RGBW film from stored (L, pos); mode 1: W-only image from the RNG
-// jitter (PRB weights; film has 1 channel).
+// jitter (PRB weights; film has 1 channel); mode 2: the alpha channel of an
+// rgba / ya / xyza film from the stored (alpha, pos) (1 channel).
 //
 // kSplatLanes (16) lanes share a pixel: lane g of the group takes samples
 // g, g + 16, ... (16 consecutive floats per plane read: one 64-B segment),
@@ -187,6 +193,11 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 #pragma unroll
             for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + g];
         }
+        if (Mode == 2 && g < Sn) {
+            nv[0] = src[5 * plane + g];
+            nv[3] = src[3 * plane + g];
+            nv[4] = src[4 * plane + g];
+        }
         for (uint32_t j = g; j < Sn; j += kSplatLanes) {
             float sx, sy, vals[4];
             if (Mode == 0) {
@@ -201,6 +212,17 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 #pragma unroll
                     for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + jn];
                 }
+            } else if (Mode == 2) {
+                vals[0] = vals[1] = vals[2] = 0.f;
+                vals[3] = nv[0];
+                sx = nv[3];
+                sy = nv[4];
+                const uint32_t jn = j + kSplatLanes;
+                if (jn < Sn) {
+                    nv[0] = src[5 * plane + jn];
+                    nv[3] = src[3 * plane + jn];
+                    nv[4] = src[4 * plane + jn];
+                }
             } else {
                 Pcg rng;
                 rng.seed(seed_value, pixel * spp_pp + s_begin + j);
@@ -213,8 +235,8 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
             if (fx != (int32_t)px || fy != (int32_t)py) {  // jitter rounded onto the next pixel
                 if (Mode == 0) splat_one_atomic(S, film, sx, sy, vals, 4, 0);
                 else {
-                    float one = 1.f;
-                    // W image is 1 channel: reuse the RGBW path on a 1-channel film
+                    const float one = vals[3];  // 1 (W image) or the sample's alpha
+                    // 1-channel film (W image / alpha): the footprint of one sample
                     const uint32_t Wd = S.width, Hd = S.height;
                     int32_t pix = fx - 2, piy = fy - 2;
                     float relx = ((float)pix + 0.5f) - sx, rely = ((float)piy + 0.5f) - sy;
@@ -297,6 +319,10 @@ k_splat_generic(DScene S, LaneMap lm, uint32_t n_passes, uint64_t n, uint64_t pl
             uint64_t o = (uint64_t)pass * n + k;
             vals[0] = in[o]; vals[1] = in[plane + o]; vals[2] = in[2 * plane + o]; vals[3] = 1.f;
             px = in[3 * plane + o]; py = in[4 * plane + o];
+        } else if (Mode == 2) {
+            uint64_t o = (uint64_t)pass * n + k;
+            vals[0] = in[5 * plane + o];
+            px = in[3 * plane + o]; py = in[4 * plane + o];
         } else {
             px = (float)pxi + rng.next_float();
             py = (float)pyi + rng.next_float();
@@ -363,15 +389,25 @@ __global__ void k_grad_over_w(uint64_t n_px, const float *__restrict__ grad_in, 
 
 // HDRFilm::develop (films/hdrfilm.cpp:349-405): rgb / w, or luminance(rgb) / w
 // (spectrum.h:431-434), or srgb_to_xyz(rgb) / w (spectrum.h:396-402, matrix
-// product as column fmadds)
-template <int Fmt>
+// product as column fmadds); with alpha (rgba / ya / xyza) the film holds
+// R G B A W and the image gets the alpha channel after the colour channels
+template <int Fmt, bool Alpha>
 __global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *__restrict__ out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_px) return;
-    float4 v = reinterpret_cast<const float4 *>(film)[i];
+    float4 v;
+    float al = 0.f;
+    if (Alpha) {
+        const float *f = film + 5 * i;
+        v = make_float4(f[0], f[1], f[2], f[4]);
+        al = f[3];
+    } else {
+        v = reinterpret_cast<const float4 *>(film)[i];
+    }
     float d = v.w == 0.f ? 1.f : v.w;
     if (Fmt == MH_PIXEL_Y) {
-        out[i] = ((v.x * 0.212671f + v.y * 0.715160f) + v.z * 0.072169f) / d;
+        out[(Alpha ? 2 : 1) * i] = ((v.x * 0.212671f + v.y * 0.715160f) + v.z * 0.072169f) / d;
+        if (Alpha) out[2 * i + 1] = al / d;
         return;
     }
     float a = v.x, b = v.y, c = v.z;
@@ -380,9 +416,11 @@ __global__ void k_develop(uint64_t n_px, const float *__restrict__ film, float *
         b = __builtin_fmaf(0.072169f, v.z, __builtin_fmaf(0.715160f, v.y, 0.212671f * v.x));
         c = __builtin_fmaf(0.950227f, v.z, __builtin_fmaf(0.119193f, v.y, 0.019334f * v.x));
     }
-    out[3 * i] = a / d;
-    out[3 * i + 1] = b / d;
-    out[3 * i + 2] = c / d;
+    const uint32_t ch = Alpha ? 4 : 3;
+    out[ch * i] = a / d;
+    out[ch * i + 1] = b / d;
+    out[ch * i + 2] = c / d;
+    if (Alpha) out[4 * i + 3] = al / d;
 }
 
 // small (register-accumulated) gradient slots: wave butterfly, then one
@@ -538,7 +576,7 @@ hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *r
 
 hipError_t launch_render(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                          uint32_t seed_value, uint32_t n_passes, uint64_t n, uint64_t plane,
-                         float *out, unsigned long long *counters, hipStream_t st) {
+                         float *out, unsigned long long *counters, hipStream_t st, int alpha) {
     const uint32_t bs = 256;
     size_t sh = lds_bytes(S, bs);
     if (n == 0) return hipSuccess;
@@ -546,8 +584,8 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
     const dim3 g(blocks_for(n, bs)), b(bs);
 #define MH_LAUNCH_RENDER(K)                                                                                   \
     do {                                                                                                      \
-        if (lds) hipLaunchKernelGGL((k_render<K, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters); \
-        else hipLaunchKernelGGL((k_render<K, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters);    \
+        if (lds) hipLaunchKernelGGL((k_render<K, true>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters, alpha); \
+        else hipLaunchKernelGGL((k_render<K, false>), g, b, sh, st, S, in, lm, seed_value, n_passes, n, plane, out, counters, alpha);    \
     } while (0)
     if (in.type == MH_INTEGRATOR_PRB) MH_LAUNCH_RENDER(MH_INTEGRATOR_PRB);
     else if (in.type == MH_INTEGRATOR_VOLPATH) MH_LAUNCH_RENDER(MH_INTEGRATOR_VOLPATH);
@@ -557,31 +595,52 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
     return hipGetLastError();
 }
 
-hipError_t launch_splat(const DScene &S, const LaneMap &lm, bool weights_mode, bool fast,
+hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
                         hipStream_t st) {
     if (n == 0) return hipSuccess;
+#define MH_SPLAT_PX(M)                                                                                          \
+    hipLaunchKernelGGL(k_splat_px<M>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S, lm.pixel_begin, n_pix, \
+                       lm.S, n_passes, n, plane, in, film, seed_value, lm.spp_pp, lm.s_begin)
+#define MH_SPLAT_GEN(M)                                                                                         \
+    hipLaunchKernelGGL(k_splat_generic<M>, dim3(blocks_for(n, bs)), dim3(bs), 0, st, S, lm, n_passes, n, plane, \
+                       in, film, seed_value, coalesce)
     if (fast) {
         const uint32_t bs = 128;
         const uint64_t lanes = (uint64_t)n_pix * kSplatLanes;
-        if (weights_mode)
-            hipLaunchKernelGGL(k_splat_px<1>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S,
-                               lm.pixel_begin, n_pix, lm.S, n_passes, n, plane, in, film,
-                               seed_value, lm.spp_pp, lm.s_begin);
-        else
-            hipLaunchKernelGGL(k_splat_px<0>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S,
-                               lm.pixel_begin, n_pix, lm.S, n_passes, n, plane, in, film,
-                               seed_value, lm.spp_pp, lm.s_begin);
+        if (mode == kSplatWeights) MH_SPLAT_PX(1);
+        else if (mode == kSplatAlpha) MH_SPLAT_PX(2);
+        else MH_SPLAT_PX(0);
     } else {
         const uint32_t bs = 256;
-        if (weights_mode)
-            hipLaunchKernelGGL(k_splat_generic<1>, dim3(blocks_for(n, bs)), dim3(bs), 0, st, S,
-                               lm, n_passes, n, plane, in, film, seed_value, coalesce);
-        else
-            hipLaunchKernelGGL(k_splat_generic<0>, dim3(blocks_for(n, bs)), dim3(bs), 0, st, S,
-                               lm, n_passes, n, plane, in, film, seed_value, coalesce);
+        if (mode == kSplatWeights) MH_SPLAT_GEN(1);
+        else if (mode == kSplatAlpha) MH_SPLAT_GEN(2);
+        else MH_SPLAT_GEN(0);
     }
+#undef MH_SPLAT_PX
+#undef MH_SPLAT_GEN
+    return hipGetLastError();
+}
+
+// an alpha film's storage (hdrfilm.cpp:304-327: base_ch = 5, R G B A W) from
+// the RGBW film and the alpha plane the splat kernels accumulate
+__global__ void k_film_rgbaw(uint64_t n_px, const float *__restrict__ rgbw, const float *__restrict__ a,
+                             float *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    const float4 v = reinterpret_cast<const float4 *>(rgbw)[i];
+    float *o = out + 5 * i;
+    o[0] += v.x;
+    o[1] += v.y;
+    o[2] += v.z;
+    o[3] += a[i];
+    o[4] += v.w;
+}
+
+hipError_t launch_film_rgbaw(uint64_t n_px, const float *rgbw, const float *a, float *out, hipStream_t st) {
+    if (n_px == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_film_rgbaw, dim3(blocks_for(n_px, 256)), dim3(256), 0, st, n_px, rgbw, a, out);
     return hipGetLastError();
 }
 
@@ -657,9 +716,14 @@ hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st) {
     if (n_px == 0) return hipSuccess;
     const dim3 g(blocks_for(n_px, 256)), b(256);
-    if (fmt == MH_PIXEL_Y) hipLaunchKernelGGL(k_develop<MH_PIXEL_Y>, g, b, 0, st, n_px, film, rgb);
-    else if (fmt == MH_PIXEL_XYZ) hipLaunchKernelGGL(k_develop<MH_PIXEL_XYZ>, g, b, 0, st, n_px, film, rgb);
-    else hipLaunchKernelGGL(k_develop<MH_PIXEL_RGB>, g, b, 0, st, n_px, film, rgb);
+    switch (fmt) {
+    case MH_PIXEL_Y: hipLaunchKernelGGL((k_develop<MH_PIXEL_Y, false>), g, b, 0, st, n_px, film, rgb); break;
+    case MH_PIXEL_XYZ: hipLaunchKernelGGL((k_develop<MH_PIXEL_XYZ, false>), g, b, 0, st, n_px, film, rgb); break;
+    case MH_PIXEL_RGBA: hipLaunchKernelGGL((k_develop<MH_PIXEL_RGB, true>), g, b, 0, st, n_px, film, rgb); break;
+    case MH_PIXEL_YA: hipLaunchKernelGGL((k_develop<MH_PIXEL_Y, true>), g, b, 0, st, n_px, film, rgb); break;
+    case MH_PIXEL_XYZA: hipLaunchKernelGGL((k_develop<MH_PIXEL_XYZ, true>), g, b, 0, st, n_px, film, rgb); break;
+    default: hipLaunchKernelGGL((k_develop<MH_PIXEL_RGB, false>), g, b, 0, st, n_px, film, rgb);
+    }
     return hipGetLastError();
 }
 

@@ -1175,7 +1175,7 @@ MH_DEV void wave_count(unsigned long long *ctr, uint32_t v) {
 // PathIntegrator::sample, JIT semantics (integrators/path.cpp:95-287)
 // ===========================================================================
 MH_DEV V3 path_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                      RayT ray, uint32_t &n_closest, uint32_t &n_shadow) {
+                      RayT ray, uint32_t &n_closest, uint32_t &n_shadow, bool *valid_out = nullptr) {
     if (in.max_depth == 0) return v3(0, 0, 0);
     V3 throughput = v3(1, 1, 1), result = v3(0, 0, 0);
     float eta = 1.f;
@@ -1259,6 +1259,7 @@ MH_DEV V3 path_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &
         if (rr_active) throughput = throughput * rcp(rr_prob);
         active = active_next && (!rr_active || rr_continue) && tmax != 0.f;
     }
+    if (valid_out) *valid_out = valid_ray;  // alpha (integrator.cpp:1229-1231)
     return valid_ray ? result : v3(0, 0, 0);
 }
 
@@ -1336,7 +1337,8 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
 
 template <bool Grad>
 MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                     RayT ray, V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow) {
+                     RayT ray, V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow,
+                     bool *valid_out = nullptr) {
     uint32_t depth = 0;
     if (!Grad) L = v3(0, 0, 0);
     V3 beta = v3(1, 1, 1);
@@ -1437,6 +1439,7 @@ MH_DEV V3 prb_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &i
         if (si.valid) depth += 1;
         active = active_next;
     }
+    if (valid_out) *valid_out = depth != 0;  // "ray validity flag for alpha blending" (prb.py:253-257)
     return L;
 }
 
@@ -1911,7 +1914,7 @@ struct VolState {
     SI si;
     float si_t, last_pdf, eta;
     uint32_t medium, depth;
-    bool specular_chain, needs_intersection;
+    bool specular_chain, needs_intersection, valid;
     // between pre and post
     uint32_t mode, nee_kind;
     bool active, active_medium, active_surface, act_scatter;
@@ -1929,6 +1932,7 @@ MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, 
     v.result = v3(0, 0, 0);
     v.medium = S.camera_medium;
     v.specular_chain = !in.hide_emitters;
+    v.valid = !in.hide_emitters && S.environment != MH_INVALID;  // valid_ray (volpath.cpp:105)
     v.depth = 0;
     (void)fminf(rng.next_float() * 3.f, 2.f);  // RGB channel (scalar majorants: all channels alike)
     v.si.valid = false;
@@ -1996,6 +2000,7 @@ MH_DEV bool volpath_pre(const DScene &S, const LdsBvh &B, const IntegratorParams
         else throughput = throughput * vdiv(mei.sigma_s, mei.sigma_t);
         const bool sample_emitters = !(m.flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
         specular_chain = !sample_emitters;
+        v.valid = true;  // valid_ray |= act_medium_scatter (volpath.cpp:223)
         if (sample_emitters) {
             walk = nee_begin(S, mei.p, v3(0, 0, 0), nullptr, rng, medium, v.ds, v.ns);
             const float ph = phase_eval(m, mei_to_local(mei, v.ds.d));
@@ -2091,6 +2096,7 @@ MH_DEV bool volpath_post(const DScene &S, const IntegratorParams &in, Pcg &rng, 
             v.last_p = si.p;
             v.last_pdf = bs_pdf;
             v.specular_chain = false;
+            v.valid = true;  // valid_ray |= non_null_bsdf (volpath.cpp:320)
         }
         if (is_medium_transition(S, si)) v.medium = target_medium(S, si, v.ray.d);
     }
@@ -2123,11 +2129,12 @@ MH_DEV bool volpath_advance(const DScene &S, const LdsBvh &B, const IntegratorPa
 }
 
 MH_DEV V3 volpath_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                         RayT ray, uint32_t &n_closest, uint32_t &n_shadow) {
+                         RayT ray, uint32_t &n_closest, uint32_t &n_shadow, bool *valid_out = nullptr) {
     VolState v;
     volpath_init(S, in, rng, ray, v);
     while (volpath_advance(S, B, in, rng, v, n_closest, n_shadow)) {
     }
+    if (valid_out) *valid_out = v.valid;
     return v.result;
 }
 
@@ -2257,7 +2264,8 @@ MH_DEV V3 pvp_sample_emitter(const DScene &S, const LdsBvh &B, const MEI &mei_re
 
 template <bool Adj>
 MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, RayT ray,
-                        V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow) {
+                        V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow,
+                        bool *valid_out = nullptr) {
     const bool handle_null = S.vol_flags & kVolHandleNull;
     uint32_t depth = 0;
     if (!Adj) L = v3(0.f, 0.f, 0.f);
@@ -2268,6 +2276,7 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
     si.valid = false;
     float si_t = 0.f;
     uint32_t medium = MH_INVALID;   // "TODO: support sensors inside media" (prbvolpath.py:123-124)
+    bool valid_ray = false;         // (prbvolpath.py:128, 274, 327)
     (void)fminf(3.f * rng.next_float(), 2.f);   // RGB channel (scalar majorants: all channels alike)
     while (active) {
         // ---- Russian roulette (:142-149)
@@ -2397,6 +2406,7 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
         }
 
         // ---- phase function sampling (:274-294)
+        valid_ray = valid_ray || act_scatter;
         if (act_scatter) {
             (void)rng.next_float();
             const float s2x = rng.next_float(), s2y = rng.next_float();
@@ -2435,12 +2445,13 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
                 throughput = throughput * bw;
                 ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
                 needs_intersection = true;
-                if (smooth) depth += 1;
+                if (smooth) { depth += 1; valid_ray = true; }
                 if (is_medium_transition(S, si)) medium = target_medium(S, si, ray.d);
             }
         }
         active = active && (active_surface || active_medium);
     }
+    if (valid_out) *valid_out = valid_ray;
     return L;
 }
 

@@ -240,7 +240,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
 template <bool Staged>
 __global__ void __launch_bounds__(256, 5)
 k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane,
-           float *out, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next) {
+           float *out, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, int alpha) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
     const uint32_t n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -295,6 +295,10 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
                 L = fma3(tp, le * mis_bsdf, L);
                 out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
             }
+            // alpha: valid_ray (path.cpp:115, 256); a path ends at its first miss,
+            // so the camera vertex decides it
+            if (alpha && depth == 0)
+                out[5 * plane + pid] = (si.valid || (!in.hide_emitters && S.environment != MH_INVALID)) ? 1.f : 0.f;
             const bool active_next = (depth + 1 < in.max_depth) && si.valid;
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
             const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
@@ -391,7 +395,7 @@ template <bool Gen>
 __global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane, float *out,
             WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total,
-            uint64_t *carry, uint32_t pass) {
+            uint64_t *carry, uint32_t pass, int alpha) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
     uint32_t n;
@@ -490,6 +494,8 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 if (prev_pdf > 0.f) le = emitter_eval(S, em, si);
                 L = fma3(tp, le * mis_bsdf, L);
             }
+            if (Gen && alpha)  // valid_ray (path.cpp:115, 256): decided at the camera vertex
+                out[5 * plane + pid] = (si.valid || (!in.hide_emitters && S.environment != MH_INVALID)) ? 1.f : 0.f;
             const bool active_next = (depth + 1 < in.max_depth) && si.valid;
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
             const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
@@ -610,17 +616,19 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
 static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                         uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                                         uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
-                                        hipEvent_t *trace_ev, hipStream_t st, uint64_t *carry, uint32_t pass);
+                                        hipEvent_t *trace_ev, hipStream_t st, uint64_t *carry, uint32_t pass,
+                                        int alpha);
 
 hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                             uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                             uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
-                            hipEvent_t *trace_ev, hipStream_t st, uint32_t n_passes, uint64_t *carry) {
+                            hipEvent_t *trace_ev, hipStream_t st, uint32_t n_passes, uint64_t *carry,
+                            int alpha) {
     if (n == 0) return hipSuccess;
     if (n > (1ull << kPidBits) || n_bounces > 255 || n_passes == 0) return hipErrorInvalidValue;
     if (n_passes == 1)
         return launch_wavefront_pass(S, in, lm, seed_value, n, plane, out, ws, cap, ctr, n_bounces, grid, trace_ev,
-                                     st, nullptr, 0);
+                                     st, nullptr, 0, alpha);
     if (!wf_fused(S) || !carry) return hipErrorInvalidValue;
     // passes of one chunk run back to back (integrator.cpp:350-360): pass p
     // writes its samples at p * n of every plane and hands each lane's PCG32
@@ -630,7 +638,7 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
     for (uint32_t p = 0; p < n_passes; ++p) {
         hipError_t e = launch_wavefront_pass(S, in, lm, seed_value, n, plane, out + (uint64_t)p * n, ws, cap,
                                              ctr + (size_t)p * wf_counter_words(n_bounces), n_bounces, grid,
-                                             nullptr, st, carry, p);
+                                             nullptr, st, carry, p, alpha);
         if (e != hipSuccess) return e;
     }
     if (trace_ev)
@@ -641,7 +649,8 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
 static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                         uint32_t seed_value, uint64_t n, uint64_t plane, float *out, void *ws,
                                         uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
-                                        hipEvent_t *trace_ev, hipStream_t st, uint64_t *carry, uint32_t pass) {
+                                        hipEvent_t *trace_ev, hipStream_t st, uint64_t *carry, uint32_t pass,
+                                        int alpha) {
     const bool fused = wf_fused(S);
     WfState w = carve(ws, cap);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
@@ -663,10 +672,10 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
             if (b == 0)
                 hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S,
-                                   in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass);
+                                   in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass, alpha);
             else
                 hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st,
-                                   S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass);
+                                   S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass, alpha);
             if (trace_ev && b + 1 == n_bounces)
                 for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
             continue;
@@ -676,10 +685,10 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b + 1], st);
         if (S.tab_bytes)
             hipLaunchKernelGGL(k_wf_shade<true>, dim3(grid), dim3(256), S.tab_bytes, st, S, in, lm, seed_value,
-                               plane, out, w, cur, seg_cap, c, cn);
+                               plane, out, w, cur, seg_cap, c, cn, alpha);
         else
             hipLaunchKernelGGL(k_wf_shade<false>, dim3(grid), dim3(256), 0, st, S, in, lm, seed_value, plane, out,
-                               w, cur, seg_cap, c, cn);
+                               w, cur, seg_cap, c, cn, alpha);
         MH_WF_DISPATCH(k_wf_shadow, S, w, plane, out, seg_cap, c);
     }
     return hipGetLastError();

@@ -21,7 +21,27 @@ BSDF_DIFFUSE, BSDF_NULL = 0, 1
 TEX_RGB, TEX_BITMAP = 0, 1
 EMITTER_AREA, EMITTER_CONSTANT, EMITTER_DIRECTIONAL = 0, 1, 2
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
-PIXEL_RGB, PIXEL_Y, PIXEL_XYZ = 0, 1, 2
+PIXEL_RGB, PIXEL_Y, PIXEL_XYZ, PIXEL_RGBA, PIXEL_YA, PIXEL_XYZA = 0, 1, 2, 3, 4, 5
+
+
+def pixel_has_alpha(fmt: int) -> bool:
+    return fmt in (PIXEL_RGBA, PIXEL_YA, PIXEL_XYZA)
+
+
+def film_channels(fmt: int) -> int:
+    """Channels of the film storage: RGBW, or RGBAW with alpha (hdrfilm.cpp:327-330)."""
+    return 5 if pixel_has_alpha(fmt) else 4
+
+
+def image_channels(fmt: int) -> int:
+    """Channels of the developed image: colour (1 or 3) + alpha."""
+    return (1 if fmt in (PIXEL_Y, PIXEL_YA) else 3) + (1 if pixel_has_alpha(fmt) else 0)
+
+
+def image_channel_names(fmt: int):
+    """Bitmap channel names of hdrfilm's output (EXR layers)."""
+    return {PIXEL_RGB: ["R", "G", "B"], PIXEL_Y: ["Y"], PIXEL_XYZ: ["X", "Y", "Z"],
+            PIXEL_RGBA: ["R", "G", "B", "A"], PIXEL_YA: ["Y", "A"], PIXEL_XYZA: ["X", "Y", "Z", "A"]}[fmt]
 MEDIUM_HETEROGENEOUS, MEDIUM_HOMOGENEOUS = 0, 1
 PHASE_ISOTROPIC, PHASE_HG = 0, 1
 MEDIUM_NO_EMITTER_SAMPLING, MEDIUM_NO_SPECTRAL_EXTINCTION = 1, 2

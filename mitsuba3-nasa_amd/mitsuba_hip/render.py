@@ -179,7 +179,8 @@ def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int
     spp = spp or scene.sample_count()
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
     if film is None:
-        film = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device=f"cuda:{dev}")
+        film = torch.empty((scene.height, scene.width, A.film_channels(scene.desc.sensor.pixel_format)),
+                           dtype=torch.float32, device=f"cuda:{dev}")
     flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_ACCUMULATE if accumulate else 0)
     flags |= {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "wavefront": A.FLAG_WAVEFRONT}[mode]
     ic = integrator.c()
@@ -192,7 +193,7 @@ def develop(scene: Scene, film, device=None):
     torch = _torch()
     dev = film.device.index or 0
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
-    ch = 1 if scene.desc.sensor.pixel_format == A.PIXEL_Y else 3
+    ch = A.image_channels(scene.desc.sensor.pixel_format)
     out = torch.empty((scene.height, scene.width, ch), dtype=torch.float32, device=film.device)
     A.check(A.lib().mh_develop(h, _ptr(film.contiguous()), _ptr(out), A.FLAG_DEVICE_POINTERS))
     return out
@@ -214,15 +215,21 @@ _SRGB_TO_XYZ = [[0.412453, 0.357580, 0.180423], [0.212671, 0.715160, 0.072169], 
 def _grad_to_rgb(scene: Scene, grad_in):
     """Adjoint of the develop colour conversion: d loss / d (weighted rgb)
     from d loss / d image for luminance / xyz films (the 1/W factor is
-    applied by mh_render_backward)."""
+    applied by mh_render_backward).  An alpha channel (rgba / ya / xyza) is
+    a select of the ray validity mask, which carries no derivative: its
+    gradient is dropped."""
     torch = _torch()
     fmt = scene.desc.sensor.pixel_format
-    if fmt == A.PIXEL_RGB:
-        return grad_in
+    ch = A.image_channels(fmt)
+    g = grad_in.reshape(scene.height, scene.width, ch)
+    if A.pixel_has_alpha(fmt):
+        g = g[..., :ch - 1]
+    if fmt in (A.PIXEL_RGB, A.PIXEL_RGBA):
+        return g.contiguous()
     M = torch.tensor(_SRGB_TO_XYZ, dtype=torch.float32, device=grad_in.device)
-    if fmt == A.PIXEL_Y:
-        return grad_in.reshape(scene.height, scene.width, 1) * M[1]
-    return grad_in.reshape(scene.height, scene.width, 3) @ M
+    if fmt in (A.PIXEL_Y, A.PIXEL_YA):
+        return g * M[1]
+    return g @ M
 
 
 def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],

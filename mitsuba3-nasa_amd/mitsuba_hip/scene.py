@@ -655,10 +655,12 @@ def _sensor(spec: Dict[str, Any]) -> A.Sensor:
         raise RuntimeError(f'Film plugin "{film.get("type")}" is not available in the hip_ad_rgb variant')
     W, H = int(film.get("width", 768)), int(film.get("height", 576))
     pf = film.get("pixel_format", "rgb").lower()
-    pix = {"rgb": A.PIXEL_RGB, "luminance": A.PIXEL_Y, "xyz": A.PIXEL_XYZ}.get(pf)
+    # hdrfilm.cpp:160-188
+    pix = {"rgb": A.PIXEL_RGB, "luminance": A.PIXEL_Y, "xyz": A.PIXEL_XYZ, "rgba": A.PIXEL_RGBA,
+           "luminance_alpha": A.PIXEL_YA, "xyza": A.PIXEL_XYZA}.get(pf)
     if pix is None:
-        raise RuntimeError(f'hdrfilm: pixel_format "{pf}" is not available in the hip_ad_rgb variant '
-                           '(rgb, luminance, xyz; alpha films are not)')
+        raise RuntimeError('The "pixel_format" parameter must either be equal to "luminance", '
+                           f'"luminance_alpha", "rgb", "rgba",  "xyz", "xyza". Found {pf}.')
     if "crop_offset_x" in film or "crop_width" in film:
         raise RuntimeError("hdrfilm: crop windows are not available in the hip_ad_rgb variant")
     rf = film.get("rfilter", {"type": "gaussian"})

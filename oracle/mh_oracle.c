@@ -273,21 +273,24 @@ static inline float rfilter_eval(const mh_sensor *s, float x) {
 
 /* ------------------------------------------------------------------------ */
 /* ImageBlock::put (src/render/imageblock.cpp:174-532)                      */
-/* values[4] = R G B W; `film` is H x W x 4 (row range [row0, row0+rows))   */
+/* values = R G B W (or R G B A W for alpha films, hdrfilm.cpp:327-330);     */
+/* `film` is H x W x ch (row range [row0, row0+rows))                        */
 /* ------------------------------------------------------------------------ */
 typedef struct {
     float *data;
     uint32_t width, height; /* full film size */
     int32_t row0;           /* first row stored in `data` */
     uint32_t rows;          /* number of rows stored */
+    uint32_t ch;            /* channels per pixel: 4 (RGBW) or 5 (RGBAW) */
 } film_band;
 
 static inline void band_add(film_band *f, uint32_t x, uint32_t y, const float *vals, float w,
                             int nch) {
+    (void)nch;
     int32_t r = (int32_t)y - f->row0;
     if (r < 0 || r >= (int32_t)f->rows) return; /* caller sized the band to cover it */
-    float *p = f->data + ((size_t)r * f->width + x) * 4;
-    for (int k = 0; k < nch; ++k) p[k] += vals[k] * w;
+    float *p = f->data + ((size_t)r * f->width + x) * f->ch;
+    for (uint32_t k = 0; k < f->ch; ++k) p[k] += vals[k] * w;
 }
 
 static void splat(const mh_sensor *s, film_band *f, float px, float py, const float *vals,
@@ -352,23 +355,35 @@ void oracle_develop(uint32_t w, uint32_t h, const float *film, float *rgb) {
 
 /* HDRFilm::develop (hdrfilm.cpp:313-401): luminance / srgb_to_xyz of the
    weighted sums (spectrum.h:396-402, 431-434), then the weight division */
+static int fmt_alpha(uint32_t fmt) {
+    return fmt == MH_PIXEL_RGBA || fmt == MH_PIXEL_YA || fmt == MH_PIXEL_XYZA;
+}
+
+/* alpha films: the film holds R G B A W and the image gets a / w after the
+   colour channels (hdrfilm.cpp:327-372: target_ch = color_ch + alpha) */
 void oracle_develop_format(uint32_t w, uint32_t h, uint32_t fmt, const float *film, float *out) {
     size_t n = (size_t)w * h;
+    const int alpha = fmt_alpha(fmt);
+    const uint32_t fch = alpha ? 5 : 4;
+    const int to_y = fmt == MH_PIXEL_Y || fmt == MH_PIXEL_YA, to_xyz = fmt == MH_PIXEL_XYZ || fmt == MH_PIXEL_XYZA;
+    const uint32_t och = (to_y ? 1 : 3) + (alpha ? 1 : 0);
     for (size_t i = 0; i < n; ++i) {
-        const float *v = film + 4 * i;
-        float W = v[3];
+        const float *v = film + fch * i;
+        float W = v[fch - 1];
         float d = (W == 0.f) ? 1.f : W;
-        if (fmt == MH_PIXEL_Y) {
-            out[i] = ((v[0] * 0.212671f + v[1] * 0.715160f) + v[2] * 0.072169f) / d;
-            continue;
+        float *o = out + och * i;
+        if (to_y) {
+            o[0] = ((v[0] * 0.212671f + v[1] * 0.715160f) + v[2] * 0.072169f) / d;
+        } else {
+            float c[3] = {v[0], v[1], v[2]};
+            if (to_xyz) {
+                c[0] = fmaf(0.180423f, v[2], fmaf(0.357580f, v[1], 0.412453f * v[0]));
+                c[1] = fmaf(0.072169f, v[2], fmaf(0.715160f, v[1], 0.212671f * v[0]));
+                c[2] = fmaf(0.950227f, v[2], fmaf(0.119193f, v[1], 0.019334f * v[0]));
+            }
+            for (int k = 0; k < 3; ++k) o[k] = c[k] / d;
         }
-        float c[3] = {v[0], v[1], v[2]};
-        if (fmt == MH_PIXEL_XYZ) {
-            c[0] = fmaf(0.180423f, v[2], fmaf(0.357580f, v[1], 0.412453f * v[0]));
-            c[1] = fmaf(0.072169f, v[2], fmaf(0.715160f, v[1], 0.212671f * v[0]));
-            c[2] = fmaf(0.950227f, v[2], fmaf(0.119193f, v[1], 0.019334f * v[0]));
-        }
-        for (int k = 0; k < 3; ++k) out[3 * i + k] = c[k] / d;
+        if (alpha) o[och - 1] = v[3] / d;
     }
 }
 
@@ -2208,7 +2223,9 @@ static void *band_worker(void *arg) {
                     int valid;
                     if (j->kind == JOB_RENDER) {
                         v3 l = lane_sample(j->sv, j->in, L, &rng, lane, pos, &valid, NULL);
-                        float vals[4] = {l.x, l.y, l.z, 1.f};
+                        /* aovs (integrator.cpp:1216-1233): alpha = valid ? 1 : 0 */
+                        float vals[5] = {l.x, l.y, l.z, 1.f, 1.f};
+                        if (j->band.ch == 5) vals[3] = valid ? 1.f : 0.f;
                         splat(s, &j->band, pos[0], pos[1], vals, coalesce);
                     } else if (j->kind == JOB_WEIGHTS) {
                         float jx = pcg_float(&rng), jy = pcg_float(&rng);
@@ -2278,8 +2295,7 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
     uint32_t margin = splat_margin(s);
     band_job *jobs = (band_job *)calloc((size_t)n_threads, sizeof(band_job));
     pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
-    int nch = kind == JOB_WEIGHTS ? 1 : 4;
-    (void)nch;
+    const uint32_t fch = fmt_alpha(s->pixel_format) ? 5 : 4; /* film channels of JOB_RENDER */
     for (int t = 0; t < n_threads; ++t) {
         band_job *j = &jobs[t];
         j->sv = &sv; j->in = in; j->L = &L; j->kind = kind;
@@ -2295,7 +2311,8 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
             if (r1 > (int32_t)L.H) r1 = (int32_t)L.H;
             j->band.width = L.W; j->band.height = L.H; j->band.row0 = r0;
             j->band.rows = (uint32_t)(r1 - r0);
-            j->band.data = (float *)calloc((size_t)j->band.rows * L.W * 4, sizeof(float));
+            j->band.ch = kind == JOB_RENDER ? fch : 4;
+            j->band.data = (float *)calloc((size_t)j->band.rows * L.W * j->band.ch, sizeof(float));
         } else {
             j->sink.n_params = n_params;
             j->sink.tex = param_tex;
@@ -2321,17 +2338,18 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
         }
     } else {
         size_t npx = (size_t)L.W * L.H;
-        if (kind == JOB_RENDER) memset(film, 0, npx * 4 * sizeof(float));
+        if (kind == JOB_RENDER) memset(film, 0, npx * fch * sizeof(float));
         else memset(film, 0, npx * sizeof(float));
         for (int t = 0; t < n_threads; ++t) {
             band_job *j = &jobs[t];
+            const uint32_t bc = j->band.ch;
             for (uint32_t r = 0; r < j->band.rows; ++r) {
                 size_t row = (size_t)(j->band.row0 + (int32_t)r);
                 for (uint32_t x = 0; x < L.W; ++x) {
-                    const float *src = j->band.data + ((size_t)r * L.W + x) * 4;
+                    const float *src = j->band.data + ((size_t)r * L.W + x) * bc;
                     if (kind == JOB_RENDER) {
-                        float *dst = film + (row * L.W + x) * 4;
-                        for (int c = 0; c < 4; ++c) dst[c] += src[c];
+                        float *dst = film + (row * L.W + x) * bc;
+                        for (uint32_t c = 0; c < bc; ++c) dst[c] += src[c];
                     } else {
                         film[row * L.W + x] += src[3];
                     }

@@ -82,7 +82,8 @@ def nthreads():
 
 def render(scene, integrator=None, seed=0, spp=0, spp_begin=0, spp_end=0, threads=None):
     integrator = integrator or scene.integrator()
-    film = np.zeros((scene.height, scene.width, 4), np.float32)
+    from mitsuba_hip import _abi as A
+    film = np.zeros((scene.height, scene.width, A.film_channels(scene.desc.sensor.pixel_format)), np.float32)
     ic = integrator.c()
     check(lib().oracle_render(C.byref(scene.desc), C.byref(ic), seed, spp or scene.sample_count(),
                               spp_begin, spp_end, threads or nthreads(), _p(film)))
@@ -90,8 +91,9 @@ def render(scene, integrator=None, seed=0, spp=0, spp_begin=0, spp_end=0, thread
 
 
 def develop(film, pixel_format=0):
+    from mitsuba_hip import _abi as A
     h, w = film.shape[:2]
-    out = np.zeros((h, w, 1 if pixel_format == 1 else 3), np.float32)
+    out = np.zeros((h, w, A.image_channels(pixel_format)), np.float32)
     lib().oracle_develop_format(w, h, pixel_format, _p(np.ascontiguousarray(film)), _p(out))
     return out
 

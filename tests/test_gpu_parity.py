@@ -428,8 +428,8 @@ def test_ad_wavefront_limit():
         mi.render_film(scene, mi.load_dict({"type": "prb"}), seed=0, spp=1536, spp_begin=0, spp_end=1)
     st = A.Stats()
     film = mi.render_film(scene, mi.load_dict({"type": "path", "max_depth": 2}), seed=0, spp=1536,
-                          spp_begin=0, spp_end=1, stats=st)   # 4 passes of 384
-    assert float(film[..., 3].sum()) > 0 and st.samples == 2048 * 2048 * 4
+                          spp_begin=0, spp_end=1, stats=st)   # 2 passes of 768
+    assert float(film[..., 3].sum()) > 0 and st.samples == 2048 * 2048 * 2
     # integrator.cpp:281-295 + the spp_per_pass divisibility error
     with pytest.raises(A.MitsubaHipError, match="multiple of samples_per_wavefront"):
         mi.render_film(scene, mi.load_dict({"type": "path"}), seed=0, spp=2048, spp_begin=0, spp_end=1)
@@ -705,3 +705,77 @@ def test_smooth_normals_prb_gradient_parity():
         a = a.cpu().numpy()
         assert np.abs(b).max() > 0, k
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max(), err_msg=k)
+
+
+# ---------------------------------------------------------------------------
+# alpha films (hdrfilm rgba / luminance_alpha / xyza, hdrfilm.cpp:160-188,
+# 304-405): the film stores R G B A W, a sample's alpha is its ray validity
+# (integrator.cpp:1229-1231; prb: depth != 0, prb.py:253-257)
+# ---------------------------------------------------------------------------
+def _open_box(mi, pf, w=32, h=24, spp=8, env=False):
+    d = mi.cornell_box()
+    d["sensor"]["film"].update(width=w, height=h, pixel_format=pf)
+    d["sensor"]["sampler"]["sample_count"] = spp
+    d.pop("back")   # camera rays escape through the back: alpha 0 there
+    if env:
+        d["sky"] = {"type": "constant", "radiance": {"type": "rgb", "value": [0.3, 0.4, 0.5]}}
+    return mi.load_dict(d)
+
+
+@pytest.mark.parametrize("pf,itype,mode", [("rgba", "path", "auto"), ("rgba", "path", "mega"),
+                                           ("luminance_alpha", "path", "auto"), ("xyza", "prb", "auto"),
+                                           ("rgba", "volpath", "auto")])
+def test_alpha_film_parity(pf, itype, mode):
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = _open_box(mi, pf)
+    fmt = scene.desc.sensor.pixel_format
+    assert A.pixel_has_alpha(fmt)
+    integ = mi.load_dict({"type": itype, "max_depth": 6})
+    film = mi.render_film(scene, integ, seed=2, spp=8, mode=mode).cpu().numpy()
+    ref = O.render(scene, integ, seed=2, spp=8)
+    assert film.shape == ref.shape == (24, 32, 5)
+    ok, frac = _film_close(film, ref)
+    assert ok, f"film parity {frac}"
+    assert 0.05 < (ref[..., 3] / ref[..., 4]).mean() < 0.95       # partly transparent
+    img = mi.develop(scene, mi.render_film(scene, integ, seed=2, spp=8, mode=mode)).cpu().numpy()
+    rimg = O.develop(ref, fmt)
+    assert img.shape == rimg.shape == (24, 32, A.image_channels(fmt))
+    ok, frac = _film_close(img, rimg)
+    assert ok, f"image parity {frac}"
+
+
+@pytest.mark.parametrize("itype,mode", [("path", "wavefront"), ("path", "mega"), ("prb", "mega"),
+                                        ("volpath", "mega")])
+def test_alpha_per_sample_validity(itype, mode):
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = _open_box(mi, "rgba", 24, 20, 8, env=(itype == "path"))
+    integ = mi.load_dict({"type": itype, "max_depth": 6, "hide_emitters": itype == "path"})
+    n = 24 * 20 * 8
+    out = np.zeros(6 * n, np.float32)
+    ic = integ.c()
+    A.check(A.lib().mh_render_samples(scene.handle(0), C.byref(ic), 3, 8, 0, 0, out.ctypes.data_as(C.c_void_p),
+                                      A.FLAG_WAVEFRONT if mode == "wavefront" else 0))
+    rL, rpos, rvalid = O.sample_range(scene, integ, 3, 8, 0, n)
+    alpha = out[5 * n:]
+    np.testing.assert_array_equal(alpha, rvalid.astype(np.float32))
+    assert 0.05 < alpha.mean() < 0.95
+    exact = np.all(out[:3 * n].reshape(3, n).T == rL, axis=1)
+    assert exact.mean() >= 0.999
+
+
+def test_alpha_film_prb_backward():
+    """d loss / d rho through an rgba film: the alpha channel carries no
+    derivative, the colour channels are the rgb adjoint."""
+    mi = _mi()
+    import torch
+    scene = _open_box(mi, "rgba", 24, 20, 8)
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    key = "white.reflectance.value"
+    gi = np.random.default_rng(2).random((20, 24, 4)).astype(np.float32)
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), [key], integ, seed=5, spp=8)[0].cpu().numpy()
+    ref = O.render_backward(scene, integ, 5, 8, np.ascontiguousarray(gi[..., :3]), [params.texture_of(key)],
+                            [(3,)])[0]
+    np.testing.assert_allclose(g, ref, rtol=1e-3)

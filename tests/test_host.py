@@ -118,3 +118,43 @@ def test_bitmap_texture_params(mi):
     params[key] = np.full((4, 8, 3), 0.25, np.float32)
     params.update()
     assert np.allclose(scene.texture_data(scene.params[key][1]), 0.25)
+
+
+def test_hdrfilm_pixel_formats():
+    """hdrfilm.cpp:160-188: the six pixel formats, their film / image
+    channel counts, and the reference's error for anything else."""
+    import mitsuba_hip as mi
+    from mitsuba_hip import _abi as A
+    want = {"rgb": (A.PIXEL_RGB, 4, 3), "luminance": (A.PIXEL_Y, 4, 1), "xyz": (A.PIXEL_XYZ, 4, 3),
+            "rgba": (A.PIXEL_RGBA, 5, 4), "luminance_alpha": (A.PIXEL_YA, 5, 2), "xyza": (A.PIXEL_XYZA, 5, 4)}
+    for pf, (fmt, fch, ich) in want.items():
+        d = mi.cornell_box()
+        d["sensor"]["film"]["pixel_format"] = pf.upper() if pf == "rgba" else pf
+        s = mi.load_dict(d)
+        assert s.desc.sensor.pixel_format == fmt
+        assert (A.film_channels(fmt), A.image_channels(fmt)) == (fch, ich)
+    d = mi.cornell_box()
+    d["sensor"]["film"]["pixel_format"] = "rgbe"
+    with pytest.raises(RuntimeError, match="luminance_alpha"):
+        mi.load_dict(d)
+
+
+def test_oracle_alpha_develop():
+    """oracle develop of R G B A W films: colour / w, then alpha / w."""
+    import numpy as np
+    import oracle_py as O
+    from mitsuba_hip import _abi as A
+    rng = np.random.default_rng(0)
+    f = rng.random((3, 4, 5)).astype(np.float32) + 0.1
+    f[0, 0, 4] = 0.0
+    rgba = O.develop(f, A.PIXEL_RGBA)
+    d = np.where(f[..., 4:] == 0, 1, f[..., 4:])
+    np.testing.assert_allclose(rgba[..., :3], f[..., :3] / d, rtol=1e-6)
+    np.testing.assert_allclose(rgba[..., 3], f[..., 3] / d[..., 0], rtol=1e-6)
+    ya = O.develop(f, A.PIXEL_YA)
+    y = O.develop(np.concatenate([f[..., :3], f[..., 4:]], -1), A.PIXEL_Y)
+    np.testing.assert_array_equal(ya[..., :1], y)
+    np.testing.assert_array_equal(ya[..., 1], rgba[..., 3])
+    xyza = O.develop(f, A.PIXEL_XYZA)
+    xyz = O.develop(np.concatenate([f[..., :3], f[..., 4:]], -1), A.PIXEL_XYZ)
+    np.testing.assert_array_equal(xyza[..., :3], xyz)

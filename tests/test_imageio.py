@@ -79,7 +79,7 @@ def test_develop_pixel_formats(pf):
         want = want[..., 1:2]
     np.testing.assert_allclose(out, want, rtol=1e-5, atol=1e-7)
     with pytest.raises(RuntimeError, match="pixel_format"):
-        d["sensor"]["film"]["pixel_format"] = "rgba"
+        d["sensor"]["film"]["pixel_format"] = "rgbe"
         mi.load_dict(d)
 
 
