@@ -490,10 +490,14 @@ MH_DEV T load_uniform(const T *base, uint32_t i) {
 }
 
 #ifdef MH_EXP_COUNT  // diagnostic build: per-wave event counters of the packet engine
-__device__ unsigned long long g_exp_cnt[16];
+__device__ unsigned long long g_exp_cnt[32];
 #define MH_CNT(k) do { if ((threadIdx.x & 63u) == 0) atomicAdd(&g_exp_cnt[(k) + (Shadow ? 8 : 0)], 1ull); } while (0)
+// slots 16+: lane sums (k: 0 rect_pair live lanes, 1 tri_pair live lanes, 2 rect accepted, 3 tri accepted)
+#define MH_CNTL(k, p) do { const unsigned long long _m = __ballot(p); \
+    if ((threadIdx.x & 63u) == 0) atomicAdd(&g_exp_cnt[16 + (k) + (Shadow ? 8 : 0)], (unsigned long long)__popcll(_m)); } while (0)
 #else
 #define MH_CNT(k) do { } while (0)
+#define MH_CNTL(k, p) do { } while (0)
 #endif
 
 // Running hit of the packet engine.  t starts at the ray's maxt (every
@@ -564,6 +568,7 @@ MH_DEV F2 pp(const Prim *Q, uint32_t i, uint32_t k) {
 template <bool Shadow>
 MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(0);
+    MH_CNTL(0, live);
     // rows of to_object: x = a, y = b, z = c (shapes/rectangle.cpp:446-470)
     const F2 ox = sp2(r.o.x), oy = sp2(r.o.y), oz = sp2(r.o.z);
     const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
@@ -584,6 +589,8 @@ MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit
     const F2 lx = fma2(ldx, tt, lox), ly = fma2(ldy, tt, loy);
     okA = okA & (__builtin_fabsf(lx.x) <= 1.f) & (__builtin_fabsf(ly.x) <= 1.f);
     okB = okB & (__builtin_fabsf(lx.y) <= 1.f) & (__builtin_fabsf(ly.y) <= 1.f);
+    MH_CNTL(2, okA);
+    MH_CNTL(2, okB);
     const F2 key = pp(Q, pos, 15);
     packet_take<Shadow>(okA, tt.x, lx.x, ly.x, __float_as_uint(key.x), h);
     packet_take<Shadow>(okB, tt.y, lx.y, ly.y, __float_as_uint(key.y), h);
@@ -592,6 +599,7 @@ MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit
 template <bool Shadow>
 MH_DEV void tri_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(2);
+    MH_CNTL(1, live);
     // Moeller-Trumbore (render/mesh.h:430-453) on two triangles
     const F2 dx = sp2(r.d.x), dy = sp2(r.d.y), dz = sp2(r.d.z);
     const F2 e1x = pp(Q, pos, 4), e1y = pp(Q, pos, 5), e1z = pp(Q, pos, 6);
@@ -615,6 +623,8 @@ MH_DEV void tri_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit 
     const F2 uv = u + v;
     okA = okA & (v.x >= 0.f) & (uv.x <= 1.f) & (tt.x >= 0.f) & (tt.x <= r.maxt);
     okB = okB & (v.y >= 0.f) & (uv.y <= 1.f) & (tt.y >= 0.f) & (tt.y <= r.maxt);
+    MH_CNTL(3, okA);
+    MH_CNTL(3, okB);
     const F2 key = pp(Q, pos, 15);
     packet_take<Shadow>(okA, tt.x, u.x, v.x, __float_as_uint(key.x), h);
     packet_take<Shadow>(okB, tt.y, u.y, v.y, __float_as_uint(key.y), h);

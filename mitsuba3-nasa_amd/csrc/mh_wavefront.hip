@@ -1308,7 +1308,7 @@ hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n
 extern "C" int mh_exp_counters(unsigned long long *out, int reset) {
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_cnt), sizeof(g_exp_cnt));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[32] = {0};
         hipMemcpyToSymbol(HIP_SYMBOL(g_exp_cnt), z, sizeof(z));
     }
     return 0;

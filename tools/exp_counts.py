@@ -28,7 +28,8 @@ def main():
     L = _abi.lib()
     fn = L.mh_exp_counters
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 32)()
+    nb = C.c_uint32(); npr = C.c_uint32(); dep = C.c_uint32()
     mi.render_film(scene, integ, seed=0, spp=spp)
     torch.cuda.synchronize()
     fn(buf, 1)
@@ -39,6 +40,12 @@ def main():
         b = max(buf[7], 1), max(buf[15], 1)
         print(f"{name:18s} closest {buf[k]:14d} ({buf[k] / b[0]:7.2f}/batch)   shadow {buf[8 + k]:14d} "
               f"({buf[8 + k] / b[1]:7.2f}/batch)")
+    # live lanes per pair test (of 64) and accepted primitives per ray-batch
+    for k, name, den in ((0, "rect_pair live lanes/call", 0), (1, "tri_pair live lanes/call", 2),
+                         (2, "rect accepts/batch", 7), (3, "tri accepts/batch", 7)):
+        print(f"{name:26s} closest {buf[16 + k] / max(buf[den], 1):7.2f}   shadow {buf[24 + k] / max(buf[8 + den], 1):7.2f}")
+    L.mh_scene_bvh_info(scene.handle(0), C.byref(nb), C.byref(npr), C.byref(dep))
+    print("bvh nodes", nb.value, "prims", npr.value, "depth", dep.value)
 
 
 if __name__ == "__main__":
