@@ -691,13 +691,180 @@ MH_DEV void packet_leaf(const Prim *prims, const Prim *pairs, uint32_t first, ui
     if (i < count) tri_one<Shadow>(prims, first + i, lane_hit & (!Shadow || !h.occl), r, h);
 }
 
+// ---------------------------------------------------------------------------
+// Sparse-leaf compaction (the fused bounce kernels).  A triangle run whose
+// leaf box only a few lanes of the wave overlap (the two cubes of the cornell
+// box: 16 of 64 closest rays, 7 of 64 shadow rays) wastes most of the packet
+// test's lanes.  Such a run is deferred: its overlapping lanes are listed in
+// the wave's LDS scratch (ballot + mbcnt compaction), and after the traversal
+// the (ray, triangle pair) items of every deferred run are packed densely
+// into the 64 lanes: lane j tests item j with per-lane operands (the ray by
+// ds_bpermute from its owner lane, the pair record from the LDS copy of the
+// pair table).  Results merge into the owner's hit through a 64-bit LDS
+// atomic min on (t, scene-order key) -- the lexicographic order of
+// packet_take -- and the winner writes its (u, v).  The arithmetic of a test
+// is tri_pair's, so hits are bit-identical to the dense packet test.
+// ---------------------------------------------------------------------------
+#ifndef MH_DEFER_DENSE_MIN
+#define MH_DEFER_DENSE_MIN 40  // lanes at or above which a triangle run is tested densely
+#endif
+constexpr uint32_t kMaxDefer = 2;        // deferred runs per batch (more: tested densely)
+constexpr uint32_t kPairRecFloats = 20;  // v0, e1, e2, key of both primitives, interleaved
+constexpr uint32_t kDeferScratch = 1536; // per wave: slot u64[64] | uv float2[64] | lists u32[2][64]
+// field k of a pair record (mh_api.hip pair records: dword 2k / 2k+1) -> compact slot
+MH_DEV void stage_pair_records(const DScene &S, float *dst) {
+    const CFloat *src = (CFloat *)S.prim_pairs;
+    const uint32_t total = S.n_prims * kPairRecFloats;
+    for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) {
+        const uint32_t rec = i / kPairRecFloats, w = i - rec * kPairRecFloats, j = w >> 1;
+        const uint32_t f = j < 9u ? j + j / 3u : 15u;  // fields 0 1 2 4 5 6 8 9 10 15
+        dst[i] = src[rec * 32u + 2u * f + (w & 1u)];
+    }
+}
+__host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+// dynamic LDS of the fused bounce kernels: tables | stacks | pair records | scratch
+__host__ __device__ inline uint32_t fused_pairs_offset(const DScene &S) {
+    return align16(S.tab_bytes + 16u * S.stack_size);
+}
+__host__ __device__ inline uint32_t fused_scratch_offset(const DScene &S) {
+    return fused_pairs_offset(S) + align16(S.n_prims * kPairRecFloats * 4u);
+}
+__host__ __device__ inline uint32_t fused_lds_bytes(const DScene &S) {
+    return fused_scratch_offset(S) + 4u * kDeferScratch;
+}
+
+struct Defer {
+    const float *recs;   // LDS pair records (nullptr: no deferral)
+    uint8_t *scratch;    // this wave's kDeferScratch bytes
+    uint32_t n;          // deferred runs so far
+    uint32_t first[kMaxDefer], ntri[kMaxDefer], pc[kMaxDefer];
+};
+
+MH_DEV uint32_t lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The triangle run [first, first + count) for the lanes `live`: dense packet
+// test, or deferred when few lanes overlap the leaf.
+template <bool Shadow, bool Def>
+MH_DEV void packet_tris(const Prim *prims, const Prim *pairs, uint32_t first, uint32_t count, bool live,
+                        const RayT r, PHit &h, Defer &df) {
+    if (Def && df.n < kMaxDefer) {
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(live);
+        const uint32_t pc = (uint32_t)__popcll(m);
+        if (pc < MH_DEFER_DENSE_MIN) {
+            uint32_t *list = reinterpret_cast<uint32_t *>(df.scratch + 1024) + 64u * df.n;
+            if (live) list[lane_rank(m)] = threadIdx.x & 63u;
+#pragma unroll
+            for (uint32_t k = 0; k < kMaxDefer; ++k)
+                if (k == df.n) { df.first[k] = first; df.ntri[k] = count; df.pc[k] = pc; }
+            ++df.n;
+            return;
+        }
+    }
+    uint32_t i = 0;
+    for (; i + 1u < count; i += 2u) tri_pair<Shadow>(pairs, first + i, live, r, h);
+    if (i < count) tri_one<Shadow>(prims, first + i, live, r, h);
+}
+
+// the deferred items: (ray, pair) of every deferred run, 64 per step
+template <bool Shadow>
+MH_DEV void run_deferred(const Defer &df, const RayT r, bool act, PHit &h) {
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long *slot = reinterpret_cast<unsigned long long *>(df.scratch);
+    float2 *uv = reinterpret_cast<float2 *>(df.scratch + 512);
+    const uint32_t *lists = reinterpret_cast<const uint32_t *>(df.scratch + 1024);
+    // the owner's hit so far: (t, key) as one ordered 64-bit key (t >= 0; -0 -> +0)
+    if (Shadow) {
+        reinterpret_cast<uint32_t *>(slot)[lane] = h.occl ? 1u : 0u;
+    } else if (act) {
+        slot[lane] = ((unsigned long long)__float_as_uint(h.t + 0.f) << 32) | h.key;
+        uv[lane] = make_float2(h.u, h.v);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k = 0; k < df.n; ++k) {
+        uint32_t first = 0, ntri = 0, pc = 1;
+#pragma unroll
+        for (uint32_t q = 0; q < kMaxDefer; ++q)
+            if (q == k) { first = df.first[q]; ntri = df.ntri[q]; pc = df.pc[q]; }
+        const uint32_t np = (ntri + 1u) >> 1, total = pc * np;
+        const float inv_pc = 1.f / (float)pc;
+        for (uint32_t base = 0; base < total; base += 64u) {
+            const uint32_t g = base + lane;
+            const bool on = g < total;
+            const uint32_t p = on ? (uint32_t)(((float)g + 0.5f) * inv_pc) : 0u;  // exact: g < 2^16, pc <= 64
+            const uint32_t rank = on ? g - p * pc : 0u;
+            const uint32_t owner = lists[64u * k + rank];
+            RayT q;
+            q.o = v3(__shfl(r.o.x, owner), __shfl(r.o.y, owner), __shfl(r.o.z, owner));
+            q.d = v3(__shfl(r.d.x, owner), __shfl(r.d.y, owner), __shfl(r.d.z, owner));
+            q.maxt = __shfl(r.maxt, owner);
+            const float *rec = df.recs + (first + 2u * p) * kPairRecFloats;
+            const float4 a = *reinterpret_cast<const float4 *>(rec), b = *reinterpret_cast<const float4 *>(rec + 4),
+                         c = *reinterpret_cast<const float4 *>(rec + 8), d = *reinterpret_cast<const float4 *>(rec + 12),
+                         e = *reinterpret_cast<const float4 *>(rec + 16);
+            // fields: (v0x v0y v0z e1x e1y e1z e2x e2y e2z key) x (A, B), interleaved
+            const F2 v0x = pair(a.x, a.y), v0y = pair(a.z, a.w), v0z = pair(b.x, b.y);
+            const F2 e1x = pair(b.z, b.w), e1y = pair(c.x, c.y), e1z = pair(c.z, c.w);
+            const F2 e2x = pair(d.x, d.y), e2y = pair(d.z, d.w), e2z = pair(e.x, e.y);
+            const bool hasB = 2u * p + 1u < ntri;
+            // Moeller-Trumbore (render/mesh.h:430-453): tri_pair's operations
+            const F2 dx = sp2(q.d.x), dy = sp2(q.d.y), dz = sp2(q.d.z);
+            const F2 px = fma2(dy, e2z, -(dz * e2y)), py = fma2(dz, e2x, -(dx * e2z)), pz = fma2(dx, e2y, -(dy * e2x));
+            const F2 det = fma2(e1z, pz, fma2(e1y, py, e1x * px));
+            const F2 tx = sp2(q.o.x) - v0x, ty = sp2(q.o.y) - v0y, tz = sp2(q.o.z) - v0z;
+            const F2 inv_det = rcp2(det);
+            const F2 u = fma2(tz, pz, fma2(ty, py, tx * px)) * inv_det;
+            bool okA = on & (u.x >= 0.f) & (u.x <= 1.f), okB = on & hasB & (u.y >= 0.f) & (u.y <= 1.f);
+            if (!wave_any(okA | okB)) continue;
+            const F2 qx = fma2(ty, e1z, -(tz * e1y)), qy = fma2(tz, e1x, -(tx * e1z)), qz = fma2(tx, e1y, -(ty * e1x));
+            const F2 v = fma2(dz, qz, fma2(dy, qy, dx * qx)) * inv_det;
+            const F2 tt = fma2(e2z, qz, fma2(e2y, qy, e2x * qx)) * inv_det;
+            const F2 uvs = u + v;
+            okA = okA & (v.x >= 0.f) & (uvs.x <= 1.f) & (tt.x >= 0.f) & (tt.x <= q.maxt);
+            okB = okB & (v.y >= 0.f) & (uvs.y <= 1.f) & (tt.y >= 0.f) & (tt.y <= q.maxt);
+            if (Shadow) {
+                if (okA | okB) reinterpret_cast<uint32_t *>(slot)[owner] = 1u;
+                continue;
+            }
+            // the better of A and B (packet_take's order), then the merge
+            PHit ch;
+            ch.t = q.maxt;
+            ch.u = ch.v = 0.f;
+            ch.key = MH_INVALID;
+            ch.occl = false;
+            packet_take<false>(okA, tt.x, u.x, v.x, __float_as_uint(e.z), ch);
+            packet_take<false>(okB, tt.y, u.y, v.y, __float_as_uint(e.w), ch);
+            const bool cand = ch.key != MH_INVALID;
+            const unsigned long long key64 = ((unsigned long long)__float_as_uint(ch.t + 0.f) << 32) | ch.key;
+            if (cand) __hip_atomic_fetch_min(slot + owner, key64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_wave_barrier();
+            if (cand && slot[owner] == key64) uv[owner] = make_float2(ch.u, ch.v);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (Shadow) {
+        h.occl = reinterpret_cast<const uint32_t *>(slot)[lane] != 0u;
+    } else if (act) {
+        const unsigned long long s = slot[lane];
+        const float2 w = uv[lane];
+        h.t = __uint_as_float((uint32_t)(s >> 32));
+        h.key = (uint32_t)s;
+        h.u = w.x;
+        h.v = w.y;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // gnodes / gprims: the BVH in global memory (read via the scalar cache);
 // B provides the LDS stack region (one wave-uniform stack per wave).
 // One batch: the wave's 64 rays (act: lanes that hold a ray).  ws: the
-// wave-uniform stack (entry k at ws[k * stride]).
-template <bool Shadow>
+// wave-uniform stack (entry k at ws[k * stride]).  Def: sparse triangle runs
+// are deferred and compacted (dfr: LDS pair records + the wave's scratch).
+template <bool Shadow, bool Def = false>
 MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpairs, const uint2 *key_sp, uint32_t *ws, uint32_t stride,
-                        const RayT r, bool act) {
+                        const RayT r, bool act, const float *dfr_recs = nullptr, uint8_t *dfr_scratch = nullptr) {
     const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
     PHit ph;
     ph.t = r.maxt;
@@ -705,7 +872,23 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpai
     ph.key = MH_INVALID;
     ph.occl = false;
     act = act && gnodes != nullptr;
+    Defer df;
+    df.recs = dfr_recs;
+    df.scratch = dfr_scratch;
+    df.n = 0;
+    const bool act0 = act;
     uint32_t node = 0, sp = 0;
+    auto leaf = [&](uint32_t c, uint32_t cnt, uint32_t nrect, bool hit) {
+        // rectangles [0, nrect) densely (nearly every ray overlaps the room),
+        // then the triangle run
+        uint32_t i = 0;
+        for (; i + 1u < nrect; i += 2u) rect_pair<Shadow>(gpairs, c + i, hit & (!Shadow || !ph.occl), r, ph);
+        if (i < nrect) {
+            rect_one<Shadow>(gprims, c + i, hit & (!Shadow || !ph.occl), r, ph);
+            ++i;
+        }
+        if (i < cnt) packet_tris<Shadow, Def>(gprims, gpairs, c + i, cnt - i, hit & (!Shadow || !ph.occl), r, ph, df);
+    };
     while (wave_any(act)) {
         const Node n = load_uniform(gnodes, node);
         bool h0, h1;
@@ -718,11 +901,11 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpai
         const uint32_t c1 = __float_as_uint(n.lo1.w), n1 = __float_as_uint(n.hi1.w) & kLeafCountMask;
         bool any0 = wave_any(h0), any1 = wave_any(h1);
         if (any0 && n0) {
-            packet_leaf<Shadow>(gprims, gpairs, c0, n0, __float_as_uint(n.hi0.w) >> kLeafRectShift, h0, r, ph);
+            leaf(c0, n0, __float_as_uint(n.hi0.w) >> kLeafRectShift, h0);
             any0 = false;
         }
         if (any1 && n1) {
-            packet_leaf<Shadow>(gprims, gpairs, c1, n1, __float_as_uint(n.hi1.w) >> kLeafRectShift, h1, r, ph);
+            leaf(c1, n1, __float_as_uint(n.hi1.w) >> kLeafRectShift, h1);
             any1 = false;
         }
         if (Shadow) act = act && !ph.occl;
@@ -742,6 +925,7 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpai
             node = __builtin_amdgcn_readfirstlane(ws[sp * stride]);
         }
     }
+    if (Def && df.n) run_deferred<Shadow>(df, r, act0, ph);
     MH_CNT(7);
     Hit hit;
     hit.key = ph.key;

@@ -65,6 +65,7 @@ constexpr uint32_t kPacketMaxPrims = 64;
 uint32_t wf_packet_max_prims() { return kPacketMaxPrims; }
 static bool use_packet(const DScene &S) {
     const char *e = getenv("MH_TRAVERSAL");
+    if (S.n_prims > kPacketMaxPrims) return false;  // no pair records beyond (mh_api.hip)
     if (e && !strcmp(e, "packet")) return true;
     if (e && !strcmp(e, "lane")) return false;
     return S.n_prims <= kPacketMaxPrims;
@@ -407,9 +408,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!block_has_stride_work(it, n)) return;
+    float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
+    stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
     const DScene S = stage_tables(S0, lds);
     uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
                    (threadIdx.x >> 6) * S0.stack_size;
+    uint8_t *dscr = reinterpret_cast<uint8_t *>(lds) + fused_scratch_offset(S0) + (threadIdx.x >> 6) * kDeferScratch;
     const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
     uint32_t n_shadow = 0;
@@ -452,7 +456,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 ray.maxt = w.mt[cur][j];
             }
         }
-        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has);
+        const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has, recs, dscr);
 #ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
         {
             RayT r2 = ray;
@@ -550,7 +554,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
         }
         // ---- visibility of the NEE sample (scene.cpp:201-210)
-        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow);
+        const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
 #ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
         {
             RayT r2 = sray;
@@ -671,10 +675,10 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
             // closes it and the remaining pairs are recorded empty after it
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
             if (b == 0)
-                hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st, S,
+                hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), fused_lds_bytes(S), st, S,
                                    in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass, alpha);
             else
-                hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), S.tab_bytes + 16u * S.stack_size, st,
+                hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), fused_lds_bytes(S), st,
                                    S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass, alpha);
             if (trace_ev && b + 1 == n_bounces)
                 for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
@@ -986,9 +990,12 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!block_has_stride_work(it, n)) return;
+    float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
+    stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
     const DScene S = stage_tables(S0, lds);
     uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
                    (threadIdx.x >> 6) * S0.stack_size;
+    uint8_t *dscr = reinterpret_cast<uint8_t *>(lds) + fused_scratch_offset(S0) + (threadIdx.x >> 6) * kDeferScratch;
     uint32_t n_shadow = 0;
     const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
@@ -1030,7 +1037,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 ray.maxt = w.mt[cur][j];
             }
         }
-        const Hit h = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n);
+        const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n, recs, dscr);
         if (i < n) {
             if (Gen) {
                 beta = v3(1.f, 1.f, 1.f);
@@ -1136,7 +1143,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             alive = active_next;
         }
         // ---- visibility of the NEE sample; the record is charged if unoccluded
-        const Hit sh = packet_batch<true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow);
+        const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
         if (shadow && sh.shape == MH_INVALID) {
 #pragma unroll
             for (int kk = 0; kk < NR; ++kk)
@@ -1236,7 +1243,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
     const uint32_t seg_cap = seg_len(n);
     const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
-    const size_t sh_fused = S.tab_bytes + 16u * S.stack_size;
+    const size_t sh_fused = fused_lds_bytes(S);
     if (!fused)  // the fused first bounce generates its camera rays itself
         hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                            seed_value, n, coalesce, grad_in, weights, w, q, ctr);
