@@ -54,6 +54,9 @@ constexpr uint32_t kSeg = 64;
 #ifndef MH_BOUNCE_WAVES
 #define MH_BOUNCE_WAVES 5  // fused bounce kernels: waves per SIMD the register budget targets
 #endif
+#ifndef MH_BOUNCE_PRB_WAVES
+#define MH_BOUNCE_PRB_WAVES MH_BOUNCE_WAVES  // the fused PRB bounce kernel's
+#endif
 constexpr uint32_t kCtrStride = kSeg * 32;
 constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
 
@@ -123,6 +126,32 @@ static WfState carve(void *ws, uint64_t cap) {
         p += align_up(cap * 8);
     }
     return w;
+}
+
+// Path state of the fused bounce kernels: 16-B records, one plane per record
+// field group (SoA of float4), ping-pong buffers b = 0, 1 -- five 16-B loads
+// and stores per path-bounce instead of twenty 4-B ones, and two base
+// addresses instead of a pointer per plane (kernel-argument SGPRs):
+//   plane 0: o.x o.y o.z maxt        plane 3: prev_p.x .y .z rng.lo
+//   plane 1: d.x d.y d.z pd          plane 4: L.x L.y L.z rng.hi    (PRB: dL.x .y .z rng.hi)
+//   plane 2: tp.x tp.y tp.z prev_pdf
+// (The PRB bounce kernel keeps the 4-B planes of WfState / WfPrb: packed, its
+// extra registers cost more than the fewer memory instructions saved, measured
+// bwd 20.0 -> 20.7 ms per bench step.)
+constexpr uint32_t kPkPlanes = 5, kPkExt = 3;
+struct WfPacked {
+    float4 *base, *ext;
+    uint64_t stride;  // float4 per plane
+    MH_DEV float4 *pl(int b, uint32_t k) const { return base + (uint64_t)(b * (int)kPkPlanes + (int)k) * stride; }
+    MH_DEV float4 *ex(int b, uint32_t k) const { return ext + (uint64_t)(b * (int)kPkExt + (int)k) * stride; }
+};
+static WfPacked carve_packed(void *ws, void *ws_ext, uint64_t cap) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    WfPacked p;
+    p.stride = align_up(cap * 16) / 16;
+    p.base = reinterpret_cast<float4 *>(ws);
+    p.ext = reinterpret_cast<float4 *>(ws_ext);
+    return p;
 }
 
 MH_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
@@ -395,7 +424,7 @@ k_wf_shade(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint
 template <bool Gen>
 __global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
 k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t plane, float *out,
-            WfState w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total,
+            WfPacked w, int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total,
             uint64_t *carry, uint32_t pass, int alpha) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
@@ -448,12 +477,13 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 out[3 * plane + pid] = sx;
                 out[4 * plane + pid] = sy;
             } else {
-                const uint32_t pd = w.pd[cur][j];
+                const float4 q0 = w.pl(cur, 0)[j], q1 = w.pl(cur, 1)[j];
+                const uint32_t pd = __float_as_uint(q1.w);
                 pid = pd & kPidMask;
                 depth = pd >> kPidBits;
-                ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
-                ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
-                ray.maxt = w.mt[cur][j];
+                ray.o = v3(q0.x, q0.y, q0.z);
+                ray.d = v3(q1.x, q1.y, q1.z);
+                ray.maxt = q0.w;
             }
         }
         const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has, recs, dscr);
@@ -461,7 +491,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         {
             RayT r2 = ray;
             asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<false>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, has);
+            const Hit h2 = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, has, recs, dscr);
             asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.u));
         }
 #endif
@@ -473,11 +503,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 prev_pdf = 1.f;
                 rng.state = gen_state;
             } else {
-                tp = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
-                L = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
-                prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
-                prev_pdf = w.ppdf[cur][j];
-                rng.state = w.rng[cur][j];
+                const float4 q2 = w.pl(cur, 2)[j], q3 = w.pl(cur, 3)[j], q4 = w.pl(cur, 4)[j];
+                tp = v3(q2.x, q2.y, q2.z);
+                prev_pdf = q2.w;
+                prev_p = v3(q3.x, q3.y, q3.z);
+                L = v3(q4.x, q4.y, q4.z);
+                rng.state = (uint64_t)__float_as_uint(q3.w) | ((uint64_t)__float_as_uint(q4.w) << 32);
             }
             eta = 1.f;  // diffuse / null BSDFs: eta stays 1, only the camera vertex is delta
             const bool prev_delta = depth == 0;
@@ -553,33 +584,35 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             if (rr_active) tp = tp * rcp(rr_prob);
             alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
         }
+        // ---- compaction: the survivor's next-bounce state leaves registers
+        // before the shadow trace (only L and the NEE product stay live across it)
+        const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        const float rng_hi = __uint_as_float((uint32_t)(rng.state >> 32));
+        if (alive) {
+            w.pl(nxt, 0)[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
+            w.pl(nxt, 1)[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(pid | (depth << kPidBits)));
+            w.pl(nxt, 2)[slot] = make_float4(tp.x, tp.y, tp.z, prev_pdf);
+            w.pl(nxt, 3)[slot] = make_float4(prev_p.x, prev_p.y, prev_p.z, __uint_as_float((uint32_t)rng.state));
+        } else if (has && carry) {
+            carry[pid] = rng.state;  // multi-pass: the next pass continues the stream
+        }
         // ---- visibility of the NEE sample (scene.cpp:201-210)
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
 #ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
         {
             RayT r2 = sray;
             asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, shadow);
+            const Hit h2 = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, shadow, recs, dscr);
             asm volatile("" ::"v"(h2.shape));
         }
 #endif
         if (shadow && sh.shape == MH_INVALID) L = fma3(a_nee, b_nee, L);
         n_shadow += (uint32_t)__popcll(__ballot(shadow));
-        // ---- compaction: survivors -> next queue; finished paths -> sample planes
-        const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        // ---- radiance: survivors carry it on, finished paths -> sample planes
         if (alive) {
-            w.pd[nxt][slot] = pid | (depth << kPidBits);
-            w.ox[nxt][slot] = ray.o.x; w.oy[nxt][slot] = ray.o.y; w.oz[nxt][slot] = ray.o.z;
-            w.dx[nxt][slot] = ray.d.x; w.dy[nxt][slot] = ray.d.y; w.dz[nxt][slot] = ray.d.z;
-            w.mt[nxt][slot] = ray.maxt;
-            w.bx[nxt][slot] = tp.x; w.by[nxt][slot] = tp.y; w.bz[nxt][slot] = tp.z;
-            w.ppx[nxt][slot] = prev_p.x; w.ppy[nxt][slot] = prev_p.y; w.ppz[nxt][slot] = prev_p.z;
-            w.ppdf[nxt][slot] = prev_pdf;
-            w.rng[nxt][slot] = rng.state;
-            w.lx[nxt][slot] = L.x; w.ly[nxt][slot] = L.y; w.lz[nxt][slot] = L.z;
+            w.pl(nxt, 4)[slot] = make_float4(L.x, L.y, L.z, rng_hi);
         } else if (has) {
             out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
-            if (carry) carry[pid] = rng.state;  // multi-pass: the next pass continues the stream
         }
     }
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
@@ -657,6 +690,7 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
                                         int alpha) {
     const bool fused = wf_fused(S);
     WfState w = carve(ws, cap);
+    const WfPacked pk = carve_packed(ws, nullptr, cap);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
     const size_t sh = lds_bytes(S, 256);
@@ -676,10 +710,10 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
             if (b == 0)
                 hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), fused_lds_bytes(S), st, S,
-                                   in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass, alpha);
+                                   in, lm, seed_value, plane, out, pk, cur, seg_cap, c, cn, n, carry, pass, alpha);
             else
                 hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), fused_lds_bytes(S), st,
-                                   S, in, lm, seed_value, plane, out, w, cur, seg_cap, c, cn, n, carry, pass, alpha);
+                                   S, in, lm, seed_value, plane, out, pk, cur, seg_cap, c, cn, n, carry, pass, alpha);
             if (trace_ev && b + 1 == n_bounces)
                 for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
             continue;
@@ -976,7 +1010,7 @@ struct PrbGen {
     int coalesce;
 };
 template <int NR, bool Gen>
-__global__ void __launch_bounds__(256, MH_BOUNCE_WAVES)
+__global__ void __launch_bounds__(256, MH_BOUNCE_PRB_WAVES)
 k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
                 int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen) {
     extern __shared__ uint4 lds[];
@@ -1142,18 +1176,6 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             if (si.valid) depth += 1;
             alive = active_next;
         }
-        // ---- visibility of the NEE sample; the record is charged if unoccluded
-        const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
-        if (shadow && sh.shape == MH_INVALID) {
-#pragma unroll
-            for (int kk = 0; kk < NR; ++kk)
-                if ((uint32_t)kk < n_rgb) {
-                    acc[kk][0] += G[kk][0];
-                    acc[kk][1] += G[kk][1];
-                    acc[kk][2] += G[kk][2];
-                }
-        }
-        n_shadow += (uint32_t)__popcll(__ballot(shadow));
         const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
         if (alive) {
             w.pd[nxt][slot_n] = pid | (depth << kPidBits);
@@ -1173,6 +1195,18 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                     q.A(nxt, kk * 3 + 2)[slot_n] = A[kk][2];
                 }
         }
+        // ---- visibility of the NEE sample; the record is charged if unoccluded
+        const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
+        if (shadow && sh.shape == MH_INVALID) {
+#pragma unroll
+            for (int kk = 0; kk < NR; ++kk)
+                if ((uint32_t)kk < n_rgb) {
+                    acc[kk][0] += G[kk][0];
+                    acc[kk][1] += G[kk][1];
+                    acc[kk][2] += G[kk][2];
+                }
+        }
+        n_shadow += (uint32_t)__popcll(__ballot(shadow));
     }
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
     flush_partial(acc, q);
