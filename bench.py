@@ -195,54 +195,72 @@ def main():
     value = samples_step / (ms_step / 1e3) / 1e6
 
     if rank == 0:
-        # ---- roofline of the dominant kernel.  With the fused wavefront
-        # (stats.mode 2) that is k_wf_bounce: one launch = one bounce of every
-        # live path (closest trace + shading + NEE visibility), ~88% of the
-        # forward pass.  mh_render times every launch with HIP events on the
-        # scene's stream (stats.ms_trace / n_trace_launches).  Algorithmic
-        # bytes per launch are stated below and in DESIGN.md §4; the BVH and
-        # shading tables are LDS / scalar-cache resident (no HBM bytes).
+        # ---- rooflines of the two bounce-kernel families, the dominant one as
+        # `roofline`.  One launch = one bounce of every live path
+        # of a 2^24-path chunk (closest trace + shading + NEE visibility).
+        # mh_render / mh_render_backward time the bounce launches with HIP
+        # events on the scene's stream (stats.ms_trace / n_trace_launches).
+        # Algorithmic bytes: the path state streamed per path-bounce (the BVH,
+        # pair records and shading tables are LDS / scalar-cache resident):
+        #   k_wf_bounce      80 B state (pd 4, ray 28, throughput 12, prev_p 12,
+        #                    prev_pdf 4, PCG32 8, L 12) read by every non-first
+        #                    bounce and written by every survivor; a finished
+        #                    path writes L (12 B); the first bounce writes the
+        #                    film position (8 B) of every sample
+        #   k_wf_bounce_prb  104 B (the same without L, + dL 12 + A_s 12) read and
+        #                    written alike; the first bounce reads the sample's
+        #                    grad / W texel (16 B)
+        # with R = rays (sum of queue lengths), N = samples: survivors R - N.
+        # traffic / VALU issue from the PMC passes of profiles/r2_pmc.json
+        # (tools/profile_r2.sh: FETCH/WRITE corrected by the calib_fetch factors
+        # for the kernel's access width; VALU issue = SQ_INSTS_VALU x 2 cycles /
+        # (1024 SIMDs x launch time x measured clock)).
         avg_f = sum(fwd_ms) / len(fwd_ms)
         avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
         n_local = H * W * args.spp
-        launches = max(1, st_f.n_trace_launches)
-        rays_per_launch = st_f.rays_closest / launches
-        us_per_launch = st_f.ms_trace / launches * 1e3
-        if st_f.mode == 2:
-            # fused bounce kernel: per path-bounce the state is read
-            # (pd 4 + ray 28 + throughput 12 + prev_p 12 + prev_pdf 4 + PCG 8 + L 12
-            # = 80 B) and written for survivors (80 B); a finished path writes L (12 B).
-            # The first bounce generates its camera rays in registers (no state read)
-            # and writes the film position (8 B) of every sample.
-            # sum of queue lengths R = rays_closest, survivors R - N, deaths N = samples
-            R, N = float(st_f.rays_closest), float(n_local)
-            bytes_launch = (80.0 * (R - N) + 80.0 * (R - N) + 12.0 * N + 8.0 * N) / launches
-            kname = "k_wf_bounce"
-        else:
-            bytes_launch = rays_per_launch * 48.0
-            kname = "k_wf_trace" if st_f.mode == 1 else "k_render"
-        achieved = bytes_launch / (us_per_launch / 1e6) / 1e9
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tpath):
+        pmc = {}
+        ppath = os.path.join(ROOT, "profiles", "r2_pmc.json")
+        if os.path.exists(ppath):
             try:
-                ks = json.load(open(tpath)).get("kernels", {})
-                # calls-weighted mean over the template instances of the family
-                # (k_wf_bounce<true> = first bounce, <false> = the others), the
-                # same launches the HIP-event average above covers
-                fam = [v for k, v in ks.items() if k.startswith(kname + "<") or k == kname]
-                if fam:
-                    calls = sum(v["calls"] for v in fam)
-                    traffic = round(sum(v["calls"] * v["hbm_bytes_per_call"] for v in fam) / calls)
+                pmc = json.load(open(ppath)).get("kernels", {})
             except Exception:
-                traffic = None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": kname, "kernel_avg_us": round(us_per_launch, 1),
-                    "algorithmic_bytes_per_launch": round(bytes_launch),
-                    "note": "BVH traversal of a 30-primitive scene is bound by the primitive tests (VALU), "
-                            "not by HBM (DESIGN.md §3); "
-                            "traffic = PMC FETCH_SIZE*2+WRITE_SIZE per launch from profiles/pmc_traffic.json"}
+                pmc = {}
+
+        def family(kname):
+            fam = [v for k, v in pmc.items() if k.startswith(kname + "<") and
+                   not (kname == "k_wf_bounce" and k.startswith("k_wf_bounce_prb"))]
+            calls = sum(v["calls"] for v in fam)
+            if not calls:
+                return None, None, None
+            mean = lambda f: sum(v["calls"] * v[f] for v in fam if v.get(f) is not None) / calls
+            return round(mean("hbm_bytes_per_call")), mean("valu_insts_per_call"), mean("clock_ghz")
+
+        def roof(kname, st, state_b, per_death, per_sample):
+            launches = max(1, st.n_trace_launches)
+            us = st.ms_trace / launches * 1e3
+            R, N = float(st.rays_closest), float(n_local)
+            bytes_launch = (2.0 * state_b * (R - N) + per_death * N + per_sample * N) / launches
+            achieved = bytes_launch / (us / 1e6) / 1e9
+            traffic, valu, clk = family(kname)
+            r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+                 "kernel_avg_us": round(us, 1), "algorithmic_bytes_per_launch": round(bytes_launch)}
+            if valu and clk:
+                r["valu_issue_frac"] = round(valu * 2.0 / (1024 * us * 1e-6 * clk * 1e9), 4)
+                r["valu_insts_per_launch"] = round(valu)
+                r["clock_ghz"] = round(clk, 3)
+                r["limiter"] = ("VALU issue + latency of the packet primitive tests, not HBM: "
+                                f"valu_issue_frac {r['valu_issue_frac']} vs hbm frac {r['frac']}")
+            return r
+
+        roofs = []
+        if st_f.mode == 2:
+            roofs.append((st_f.ms_trace, roof("k_wf_bounce", st_f, 80.0, 12.0, 8.0)))
+        if not args.fwd_only and st_b.mode == 1 and st_b.n_trace_launches:
+            roofs.append((st_b.ms_trace, roof("k_wf_bounce_prb", st_b, 104.0, 0.0, 16.0)))
+        roofs.sort(key=lambda x: -x[0])
+        roofline = roofs[0][1] if roofs else None
+        roofline_other = roofs[1][1] if len(roofs) > 1 else None
         cpu = None
         if not args.no_cpu:
             cpu = cpu_baseline(scene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)
@@ -259,7 +277,7 @@ def main():
             "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
             "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
             "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "roofline_other": roofline_other, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -1024,6 +1024,11 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
         MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));
         MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, (size_t)grid * kMaxRgbParams * 3 * 4, st));
+        while (s->evpool.size() < 2 * n_chunks) {
+            hipEvent_t e;
+            MH_HIP(hipEventCreate(&e));
+            s->evpool.push_back(e);
+        }
         size_t chunk = 0;
         for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
             const uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
@@ -1031,7 +1036,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                                         (uint64_t)npx * S_, L.spp_pp >= 4, g_in, w, ga.slot_of_tex, n_rgb,
                                         s->wf_ws.ptr, s->wf_ws_prb.ptr, cap,
                                         s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
-                                        s->wf_partial.as<float>(), st));
+                                        s->wf_partial.as<float>(), st, &s->evpool[2 * chunk]));
         }
         MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
         wf_ctr_words = ctr_per_chunk;
@@ -1072,8 +1077,16 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                 }
     }
     if (stats) {
-        float ms = 0.f;
+        float ms = 0.f, trace_ms = 0.f;
         MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        for (size_t c = 0; wavefront && c < wf_chunks; ++c) {
+            float t = 0.f;
+            MH_HIP(hipEventElapsedTime(&t, s->evpool[2 * c], s->evpool[2 * c + 1]));
+            trace_ms += t;
+        }
+        // the bounce-kernel span (fused: k_wf_bounce_prb launches only)
+        stats->ms_trace = trace_ms;
+        stats->n_trace_launches = wavefront ? (uint64_t)wf_chunks * in->max_depth : 0;
         stats->mode = wavefront ? 1u : 0u;
         stats->samples = n;
         stats->rays_closest = ctr[0];

@@ -86,7 +86,8 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
                                 const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
-                                uint32_t grid, float *partial, hipStream_t st);
+                                uint32_t grid, float *partial, hipStream_t st,
+                                hipEvent_t *span = nullptr);  // span: 2 events around the bounce launches
 hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
                                  hipStream_t st);
 // max of a float array (gridvolume max for the majorant), as an order-preserving

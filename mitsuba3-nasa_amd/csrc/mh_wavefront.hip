@@ -1266,7 +1266,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
                                 const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
-                                uint32_t grid, float *partial, hipStream_t st) {
+                                uint32_t grid, float *partial, hipStream_t st, hipEvent_t *span) {
     if (n == 0) return hipSuccess;
     if (n > (1ull << kPidBits) || n_bounces > 255 || n_rgb > (uint32_t)kMaxRgbParams) return hipErrorInvalidValue;
     WfState w = carve(ws, cap);
@@ -1282,6 +1282,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                            seed_value, n, coalesce, grad_in, weights, w, q, ctr);
     const PrbGen gen{n, grad_in, coalesce};
+    if (span) (void)hipEventRecord(span[0], st);
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
@@ -1322,6 +1323,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         if (n_rgb == 1) MH_WF_DISPATCH_NR(k_wf_shadow_prb, 1, S, w, q, seg_cap, c);
         else MH_WF_DISPATCH_NR(k_wf_shadow_prb, kMaxRgbParams, S, w, q, seg_cap, c);
     }
+    if (span) (void)hipEventRecord(span[1], st);
     return hipGetLastError();
 }
 
