@@ -221,7 +221,8 @@ typedef struct mh_stats {
     double   ms_kernel;         /* device time of the dominant kernel (hipEvents, ms) */
     double   ms_trace;          /* wavefront: device time of all k_wf_trace (mode 1) / k_wf_bounce (mode 2) launches (ms) */
     uint64_t n_trace_launches;  /* wavefront: number of those launches */
-    uint32_t mode;              /* 0 megakernel, 1 wavefront (trace/shade/shadow), 2 wavefront fused bounce kernel */
+    uint32_t mode;              /* 0 megakernel, 1 wavefront (trace/shade/shadow), 2 wavefront fused bounce kernel,
+                                   3 volpath wavefront (main / walk rounds) */
     uint32_t pad0;
 } mh_stats;
 

@@ -358,7 +358,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
               upload(s->texels, desc->texels, desc->n_texels, st) == hipSuccess &&
               upload(s->media, meds.data(), meds.size(), st) == hipSuccess &&
               upload(s->grid, bricked.data(), bricked.size(), st) == hipSuccess &&
-              s->counters.alloc(64) == hipSuccess;
+              s->counters.alloc(256) == hipSuccess;
     if (!ok) return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: device upload failed");
 
     DScene &S = s->S;
@@ -648,20 +648,23 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         MH_HIP(hipMemsetAsync(film4, 0, n_px * 16, st));
         MH_HIP(hipMemsetAsync(film_a, 0, n_px * 4, st));
     }
-    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 256, st));
     const uint32_t S_ = L.s_end - L.s_begin;
     const uint64_t per_pixel = (uint64_t)S_ * L.n_passes;
     // execution mode: wavefront for `path` (bounded depth; several passes only
     // on the fused bounce kernel, which carries each lane's PCG32 state from
     // one pass to the next) unless forced
     bool wavefront = in->type == MH_INTEGRATOR_PATH && in->max_depth <= 64 && (L.n_passes == 1 || wf_fused(s->S));
+    // volpath: main / walk rounds (mh_volwave.hip), single pass
+    bool volwave = vw_supported(s->S, *in) && L.n_passes == 1;
     const char *env_mode = getenv("MH_MODE");
-    if (env_mode && !strcmp(env_mode, "mega")) wavefront = false;
-    if (flags & MH_FLAG_MEGAKERNEL) wavefront = false;
-    if ((flags & MH_FLAG_WAVEFRONT) && !wavefront)
+    if (env_mode && !strcmp(env_mode, "mega")) wavefront = volwave = false;
+    if (flags & MH_FLAG_MEGAKERNEL) wavefront = volwave = false;
+    if ((flags & MH_FLAG_WAVEFRONT) && !wavefront && !volwave)
         return set_error(MH_ERR_UNSUPPORTED, "mh_render: the wavefront mode supports the 'path' integrator "
-                                             "with max_depth <= 64 (several passes: packet-engine scenes)");
-    uint64_t max_samples = 1ull << 25;
+                                             "with max_depth <= 64 (several passes: packet-engine scenes) and "
+                                             "'volpath' with max_depth <= 1024 (one pass)");
+    uint64_t max_samples = volwave ? vw_max_chunk() : 1ull << 25;
     if (wavefront) {
         const char *ec = getenv("MH_WF_CHUNK");
         max_samples = std::min<uint64_t>(wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
@@ -691,6 +694,10 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, ctr_per_chunk * n_chunks * 4)));
         if (L.n_passes > 1) MH_HIP(s->wf_carry.alloc((size_t)chunk_px * S_ * 8));
     }
+    if (volwave && !vol_sched_mode()) {
+        MH_HIP(s->wf_ws.alloc(vw_workspace_bytes(plane)));
+        MH_HIP(s->wf_ctr.alloc((size_t)vw_counter_words(vw_rounds(*in)) * 4));
+    }
     size_t chunk = 0;
     for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
         uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
@@ -703,6 +710,13 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                                     s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
                                     n_bounces, wf_blocks(cus), ev + 2, st, L.n_passes,
                                     L.n_passes > 1 ? s->wf_carry.as<uint64_t>() : nullptr, alpha));
+        } else if (volwave && vol_sched_mode()) {
+            MH_HIP(launch_vol_sched(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), vs_blocks(cus),
+                                    s->counters.as<unsigned long long>(), st, alpha));
+        } else if (volwave) {
+            MH_HIP(launch_volwave(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), s->wf_ws.ptr, plane,
+                                  s->wf_ctr.as<uint32_t>(), vw_blocks(cus), s->counters.as<unsigned long long>(),
+                                  st, alpha));
         } else {
             MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
                                  s->counters.as<unsigned long long>(), st, alpha));
@@ -747,6 +761,33 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                         ctr[1] += wctr[o + 1];
                     }
     }
+    if (volwave && vol_sched_mode() && getenv("MH_VW_DEBUG")) {  // MH_EXP_VSCNT builds: wave trips per phase
+        unsigned long long c[32];
+        MH_HIP(hipMemcpy(c, s->counters.ptr, sizeof(c), hipMemcpyDeviceToHost));
+        const char *nm[7] = {"free", "head", "trace", "scatter", "surf", "walk", "post"};
+        for (int g = 0; g < 7; ++g)
+            fprintf(stderr, "vs phase %-8s wave trips %llu, lanes %llu (%.1f per trip), cycles %.3e (%.0f per trip)\n",
+                    nm[g], c[2 + g], c[9 + g], c[2 + g] ? (double)c[9 + g] / c[2 + g] : 0.0, (double)c[16 + g],
+                    c[2 + g] ? (double)c[16 + g] / c[2 + g] : 0.0);
+    }
+    if (volwave && !vol_sched_mode() && getenv("MH_VW_DEBUG")) {  // per-round queue sizes (+ MH_EXP_VWCNT builds: trips / steps)
+        const uint32_t R = vw_rounds(*in), W = vw_counter_words(R) / (R + 1);
+        std::vector<uint32_t> c((size_t)W * (R + 1));
+        MH_HIP(hipMemcpy(c.data(), s->wf_ctr.ptr, c.size() * 4, hipMemcpyDeviceToHost));
+        for (uint32_t r = 1; r <= R; ++r) {
+            unsigned long long q = 0, trips = 0, steps = 0, it_m = 0, it_w = 0;
+            for (uint32_t g = 0; g < W / 32; ++g) {
+                const uint32_t *w = &c[(size_t)W * r + 32 * g];
+                q += w[0];
+                trips += w[2] | ((unsigned long long)w[3] << 32);
+                steps += w[4] | ((unsigned long long)w[5] << 32);
+                it_m += w[6];
+                it_w += w[7];
+            }
+            if (q || trips) fprintf(stderr, "vw round %u: walks %llu, main trips %llu (wave iters %llu), walk steps %llu (wave iters %llu)\n",
+                                    r - 1, q, trips, it_m, steps, it_w);
+        }
+    }
     if (stats) {
         stats->samples = n_px * per_pixel;
         stats->rays_closest = ctr[0];
@@ -756,7 +797,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         stats->ms_kernel = kernel_ms;
         stats->ms_trace = trace_ms;
         stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces * L.n_passes : 0;
-        stats->mode = wavefront ? (wf_fused(s->S) ? 2u : 1u) : 0u;
+        stats->mode = wavefront ? (wf_fused(s->S) ? 2u : 1u) : volwave ? 3u : 0u;
     }
     return MH_OK;
 }
@@ -782,11 +823,25 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         MH_HIP(s->tmp_a.alloc(out_bytes));
         dst = s->tmp_a.as<float>();
     }
-    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 256, st));
     LaneMap lm = lane_map(L, 0);
-    if (flags & MH_FLAG_WAVEFRONT) {
+    if ((flags & MH_FLAG_WAVEFRONT) && vw_supported(s->S, *in) && vol_sched_mode()) {
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+        MH_HIP(launch_vol_sched(s->S, *in, lm, s->S.sampler_seed + seed, n, n, dst, vs_blocks(cus),
+                                s->counters.as<unsigned long long>(), st, alpha));
+    } else if ((flags & MH_FLAG_WAVEFRONT) && vw_supported(s->S, *in)) {
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+        MH_HIP(s->wf_ws.alloc(vw_workspace_bytes(n)));
+        MH_HIP(s->wf_ctr.alloc((size_t)vw_counter_words(vw_rounds(*in)) * 4));
+        MH_HIP(launch_volwave(s->S, *in, lm, s->S.sampler_seed + seed, n, n, dst, s->wf_ws.ptr, n,
+                              s->wf_ctr.as<uint32_t>(), vw_blocks(cus), s->counters.as<unsigned long long>(), st,
+                              alpha));
+    } else if (flags & MH_FLAG_WAVEFRONT) {
         if (in->type != MH_INTEGRATOR_PATH || in->max_depth > 64)
-            return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: wavefront mode needs 'path', max_depth <= 64");
+            return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: wavefront mode needs 'path' (max_depth <= 64) "
+                                                 "or 'volpath' (max_depth <= 1024)");
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(n)));
@@ -990,7 +1045,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         w = s->tmp_e.as<float>();
     }
 
-    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 64, st));
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 256, st));
     // grad_in / W once per pixel (the adjoint of develop)
     MH_HIP(s->gw.alloc(n_px * 16));  // float4 per pixel (k_grad_over_w)
     MH_HIP(launch_grad_over_w(n_px, g_in, w, s->gw.as<float>(), st));

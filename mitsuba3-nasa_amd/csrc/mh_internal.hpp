@@ -109,5 +109,20 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
                                uint32_t seed_value, uint64_t n, int coalesce,
                                const float *grad_in, const float *weights, const GradArgs &ga,
                                bool fused, unsigned long long *counters, hipStream_t st);
+// wavefront volpath (mh_volwave.hip): k_vw_main / k_vw_walk rounds
+uint64_t vw_max_chunk();
+size_t vw_workspace_bytes(uint64_t cap);
+uint32_t vw_counter_words(uint32_t rounds);
+uint32_t vw_rounds(const IntegratorParams &in);
+bool vw_supported(const DScene &S, const IntegratorParams &in);
+uint32_t vw_blocks(int cus);
+bool vol_sched_mode();
+uint32_t vs_blocks(int cus);
+hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                            uint64_t n, uint64_t plane, float *out, uint32_t grid, unsigned long long *counters,
+                            hipStream_t st, int alpha);
+hipError_t launch_volwave(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                          uint64_t n, uint64_t plane, float *out, void *ws, uint64_t cap, uint32_t *ctr,
+                          uint32_t grid, unsigned long long *counters, hipStream_t st, int alpha);
 
 }  // namespace mh

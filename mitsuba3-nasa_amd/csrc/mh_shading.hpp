@@ -1890,6 +1890,9 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     const int32_t x0 = min(max(ix, 0), rx - 1), x1 = min(max(ix + 1, 0), rx - 1);
     const int32_t y0 = min(max(iy, 0), ry - 1), y1 = min(max(iy + 1, 0), ry - 1);
     const int32_t z0 = min(max(iz, 0), rz - 1), z1 = min(max(iz + 1, 0), rz - 1);
+#ifdef MH_EXP_NOGRID  // timing experiment: no grid memory traffic (wrong results)
+    return w0x * 0.3f + w1y * 0.2f + w0z * 0.1f + (float)(x0 + y1 + z0) * 1e-9f;
+#endif
     const float *g = S.grid + m.grid_offset;
     float v000 = g[grid_index(x0, y0, z0, rx, ry)], v100 = g[grid_index(x1, y0, z0, rx, ry)];
     float v010 = g[grid_index(x0, y1, z0, rx, ry)], v110 = g[grid_index(x1, y1, z0, rx, ry)];
@@ -1988,9 +1991,15 @@ MH_DEV uint32_t target_medium(const DScene &S, const SI &si, V3 d) {
     return dot(d, si.n) > 0.f ? sh.exterior : sh.interior;
 }
 
+// Pk: the wave-coherent packet engine (small scenes with pair records; the
+// lanes that reach this call trace together, control stays scalar) instead
+// of the per-lane traversal; same hits (closest, exact-t ties to the lower key)
+template <bool Pk = false>
 MH_DEV void trace_si(const DScene &S, const LdsBvh &B, const RayT &ray, SI &si, float &si_t) {
     Hit h;
-    traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
+    if (Pk) h = packet_batch<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B.stack - (threadIdx.x & 63u), B.stride,
+                                    ray, true);
+    else traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
     compute_si(S, ray, h, si);
     si_t = si.valid ? h.t : __builtin_huge_valf();
 }
@@ -2030,6 +2039,7 @@ MH_DEV bool nee_begin(const DScene &S, V3 ref_p, V3 ref_n, const SI *si_ref, Pcg
 MH_DEV V3 nee_result(const NeeState &ns) { return ns.transmittance * ns.emitter_val; }
 
 // one trip of the transmittance loop; false when the loop has ended
+template <bool Pk = false>
 MH_DEV bool nee_step(const DScene &S, const LdsBvh &B, Pcg &rng, const DirS &ds, NeeState &ns, uint32_t &n_shadow) {
     RayT &ray = ns.ray;
     SI &si = ns.si;
@@ -2048,7 +2058,7 @@ MH_DEV bool nee_step(const DScene &S, const LdsBvh &B, Pcg &rng, const DirS &ds,
         MEI mei;
         sample_interaction(S, medium, ray, rng.next_float(), mei);
         if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = fminf(mei.t, remaining_dist);
-        if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+        if (needs_intersection) { trace_si<Pk>(S, B, ray, si, si_t); ++n_shadow; }
         if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
         needs_intersection = needs_intersection && !si.valid;
         const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
@@ -2070,7 +2080,7 @@ MH_DEV bool nee_step(const DScene &S, const LdsBvh &B, Pcg &rng, const DirS &ds,
         }
     }
     const bool intersect = active_surface && needs_intersection;
-    if (intersect) { trace_si(S, B, ray, si, si_t); ++n_shadow; }
+    if (intersect) { trace_si<Pk>(S, B, ray, si, si_t); ++n_shadow; }
     needs_intersection = needs_intersection && !intersect;
     active_surface = active_surface || escaped_medium;
     if (active_surface) total_dist += si_t;
@@ -2138,6 +2148,7 @@ MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, 
 }
 
 // pre: false when the path ends at the loop head
+template <bool Pk = false>
 MH_DEV bool volpath_pre(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, VolState &v,
                         uint32_t &n_closest) {
     RayT &ray = v.ray;
@@ -2164,7 +2175,7 @@ MH_DEV bool volpath_pre(const DScene &S, const LdsBvh &B, const IntegratorParams
         const DMedium &m = S.media[medium];
         sample_interaction(S, medium, ray, rng.next_float(), mei);
         if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ray.maxt = mei.t;
-        if (needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+        if (needs_intersection) { trace_si<Pk>(S, B, ray, si, si_t); ++n_closest; }
         needs_intersection = needs_intersection && !si.valid;
         if (si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
         spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
@@ -2206,7 +2217,7 @@ MH_DEV bool volpath_pre(const DScene &S, const LdsBvh &B, const IntegratorParams
     // ---- surface interactions (volpath.cpp:254-326), up to the emitter sample
     // (act_scatter paths are not surface paths: only escaped ones join)
     active_surface = active_surface || escaped;
-    if (active_surface && needs_intersection) { trace_si(S, B, ray, si, si_t); ++n_closest; }
+    if (active_surface && needs_intersection) { trace_si<Pk>(S, B, ray, si, si_t); ++n_closest; }
     if (active_surface) {
         const bool count_direct = depth == 0 || specular_chain;
         const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
@@ -2307,17 +2318,18 @@ MH_DEV bool volpath_post(const DScene &S, const IntegratorParams &in, Pcg &rng, 
 #ifndef MH_VOL_MAIN_PCT
 #define MH_VOL_MAIN_PCT 75  // measured best of 25..100 on config 4 (tools/bench_volpath.py)
 #endif
+template <bool Pk = false>
 MH_DEV bool volpath_advance(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, VolState &v,
                             uint32_t &n_closest, uint32_t &n_shadow) {
     const bool walking = v.mode == kVolNee;
     const uint32_t n_all = (uint32_t)__popcll(__ballot(true)), n_main = (uint32_t)__popcll(__ballot(!walking));
     if (walking) {
-        if (!nee_step(S, B, rng, v.ds, v.ns, n_shadow)) v.mode = kVolPost;
+        if (!nee_step<Pk>(S, B, rng, v.ds, v.ns, n_shadow)) v.mode = kVolPost;
         return true;
     }
     if (n_main * 100u < n_all * (uint32_t)MH_VOL_MAIN_PCT) return true;
     if (v.mode == kVolPost && !volpath_post(S, in, rng, v)) return false;
-    if (!volpath_pre(S, B, in, rng, v, n_closest)) return false;
+    if (!volpath_pre<Pk>(S, B, in, rng, v, n_closest)) return false;
     if (v.mode == kVolPost) return volpath_post(S, in, rng, v);
     return true;
 }

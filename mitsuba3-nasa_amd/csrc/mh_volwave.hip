@@ -1,0 +1,923 @@
+// mh_volwave.hip — wavefront execution of the `volpath` integrator
+// (integrators/volpath.cpp:95-450) for configuration 4.
+//
+// The per-lane megakernel (k_render<VOLPATH>) runs at 10-12 % lane
+// utilisation: a lane's loop trips are mostly null collisions
+// (volpath.cpp:161-205; ~17.5 trips per sample on config 4) and its emitter
+// samples walk ratio-tracked shadow rays of very different lengths
+// (volpath.cpp:361-448; ~25 steps per sample), so the 64 lanes of a wave sit
+// in different loops most of the time.  Here the loop is cut at its one
+// long inner loop, the NEE transmittance walk, into two persistent kernels
+// that alternate in rounds:
+//
+//   k_vw_main  runs a path's loop trips (volpath_post of the previous trip,
+//              then volpath_pre) until the path either ends -- it writes its
+//              sample -- or starts a shadow walk: then it appends its state
+//              to the next round's queue and the walk to the walk queue;
+//   k_vw_walk  runs every queued walk to its end (nee_step until the
+//              transmittance loop exits) and hands the transmittance x
+//              emitter value and the lane's advanced PCG32 state back.
+//
+// Both kernels keep every lane busy with per-lane refill: a lane whose path
+// suspends or ends (or whose walk ends) takes the wave's next item at once
+// (the while-while scheme of trace_stream), so a wave no longer waits for
+// its longest lane.  A path walks at most once per real scatter and depth <
+// max_depth bounds those, so at most max_depth + 1 main rounds exist.
+//
+// Every per-lane operation and random draw is the megakernel's (the same
+// volpath_pre / volpath_post / nee_step device functions in the same
+// order, with the state a walk needs carried through HBM bit for bit), so
+// samples are bit-identical to k_render<VOLPATH> and to the CPU oracle.
+//
+// HBM layout: 15 planes of 16-B records per path slot and side (ping-pong),
+// slot-indexed by queue position; queues are split into kVwSeg static
+// segments (a path never changes segment, each segment's counter has its
+// own 128-B line; workgroup b serves segment b % kVwSeg).
+//   path record    C0 d.xyz last_pdf      C1 throughput.xyz pid
+//                  C2 result.xyz bits     C3 last_p.xyz pend_w
+//                  C4 pend.xyz pcg_v1     C5 mei.p.xyz depth
+//   surface NEE    X0 si.p.xyz wi.z       X1 si.n.xyz shape
+//                  X2 si.s.xyz rho.x      X3 si.t.xyz rho.y    X4 si.sn.xyz rho.z
+//   walk item      W0 o.xyz max_dist      W1 d.xyz medium
+//                  W2 emitter_val.xyz ds.dist  (walk result: nee.xyz)
+//                  W3 pcg.state lo hi, pcg_v1
+#include <algorithm>
+#include <cstring>
+
+#include "mh_internal.hpp"
+#include "mh_shading.hpp"
+
+namespace mh {
+namespace {
+
+constexpr uint32_t kVwSeg = 64;
+constexpr uint32_t kVwCtr = kVwSeg * 32;  // counter words per round
+constexpr uint32_t kVwPlanes = 15;        // per side
+constexpr uint32_t kVwWaveRounds = 6;     // main / walk rounds before the finish launch (MH_VW_ROUNDS)
+enum : uint32_t { kC0 = 0, kC1, kC2, kC3, kC4, kC5, kX0, kX1, kX2, kX3, kX4, kW0, kW1, kW2, kW3 };
+
+// bits of C2.w
+enum : uint32_t {
+    kBitActScatter = 1u << 10, kBitActSurface = 1u << 11, kBitActMedium = 1u << 12, kBitActive = 1u << 13,
+    kBitSpecChain = 1u << 14, kBitValid = 1u << 15
+};
+
+struct VwPlanes {
+    float4 *p;     // side base: plane k at p + k * cap
+    uint64_t cap;
+    MH_DEV float4 &at(uint32_t k, uint64_t i) const { return p[k * cap + i]; }
+};
+
+MH_DEV uint32_t vw_lane() { return threadIdx.x & 63u; }
+
+struct VwSeg {
+    uint32_t seg, wave, nwaves;
+};
+MH_DEV VwSeg vw_seg() {
+    VwSeg it;
+    it.seg = blockIdx.x % kVwSeg;
+    const uint32_t wpb = blockDim.x / 64u;
+    it.wave = (blockIdx.x / kVwSeg) * wpb + threadIdx.x / 64u;
+    it.nwaves = (gridDim.x / kVwSeg) * wpb;
+    return it;
+}
+
+// ballot-compacted append to a segment counter; reached by the whole wave
+MH_DEV uint32_t vw_append(uint32_t *count, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    const uint32_t tot = (uint32_t)__popcll(m);
+    uint32_t base = 0;
+    if (vw_lane() == 0 && tot) base = atomicAdd(count, tot);
+    base = __builtin_amdgcn_readfirstlane(base);
+    return base + (uint32_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
+}
+
+MH_DEV float4 f4(V3 a, float w) { return make_float4(a.x, a.y, a.z, w); }
+MH_DEV float4 f4u(V3 a, uint32_t w) { return make_float4(a.x, a.y, a.z, __uint_as_float(w)); }
+MH_DEV V3 xyz(const float4 &a) { return v3(a.x, a.y, a.z); }
+
+// ---- the state a suspended path carries through HBM ------------------------
+MH_DEV void vw_store_path(const VwPlanes &P, uint64_t i, const VolState &v, uint32_t pid, uint32_t v1) {
+    const uint32_t med = v.medium == MH_INVALID ? 0xffu : v.medium;
+    const uint32_t bits = med | (v.nee_kind << 8) | (v.act_scatter ? kBitActScatter : 0u) |
+                          (v.active_surface ? kBitActSurface : 0u) | (v.active_medium ? kBitActMedium : 0u) |
+                          (v.active ? kBitActive : 0u) | (v.specular_chain ? kBitSpecChain : 0u) |
+                          (v.valid ? kBitValid : 0u);
+    P.at(kC0, i) = f4(v.ray.d, v.last_pdf);
+    P.at(kC1, i) = f4u(v.throughput, pid);
+    P.at(kC2, i) = f4u(v.result, bits);
+    P.at(kC3, i) = f4(v.last_p, v.pend_w);
+    P.at(kC4, i) = f4u(v.pend, v1);
+    P.at(kC5, i) = f4u(v.mei.p, v.depth);
+    if (v.active_surface) {
+        // a surface walk only starts from a non-null BSDF, whose sampling in
+        // volpath_post reads wi.z alone (the null branch's -wi never runs)
+        P.at(kX0, i) = f4(v.si.p, v.si.wi.z);
+        P.at(kX1, i) = f4u(v.si.n, v.si.shape);
+        P.at(kX2, i) = f4(v.si.s, v.rho.x);
+        P.at(kX3, i) = f4(v.si.t_, v.rho.y);
+        P.at(kX4, i) = f4(v.si.sn, v.rho.z);
+    }
+}
+
+MH_DEV void vw_store_walk(const VwPlanes &P, uint64_t i, const VolState &v, const Pcg &rng, uint32_t v1) {
+    const NeeState &ns = v.ns;
+    P.at(kW0, i) = f4(ns.ray.o, ns.max_dist);
+    P.at(kW1, i) = f4u(ns.ray.d, ns.medium);
+    P.at(kW2, i) = f4(ns.emitter_val, v.ds.dist);
+    P.at(kW3, i) = make_float4(__uint_as_float((uint32_t)rng.state), __uint_as_float((uint32_t)(rng.state >> 32)),
+                               __uint_as_float(v1), 0.f);
+}
+
+// resume a suspended path in kVolPost mode with its walk's result
+MH_DEV void vw_load_path(const DScene &S, const VwPlanes &P, uint64_t i, VolState &v, Pcg &rng, uint32_t &pid,
+                         uint32_t &v1) {
+    const float4 c0 = P.at(kC0, i), c1 = P.at(kC1, i), c2 = P.at(kC2, i), c3 = P.at(kC3, i), c4 = P.at(kC4, i),
+                 c5 = P.at(kC5, i), w2 = P.at(kW2, i), w3 = P.at(kW3, i);
+    const uint32_t bits = __float_as_uint(c2.w);
+    v.ray.d = xyz(c0);
+    v.last_pdf = c0.w;
+    v.throughput = xyz(c1);
+    pid = __float_as_uint(c1.w);
+    v.result = xyz(c2);
+    v.last_p = xyz(c3);
+    v.pend_w = c3.w;
+    v.pend = xyz(c4);
+    v1 = __float_as_uint(c4.w);
+    v.mei.p = xyz(c5);
+    v.depth = __float_as_uint(c5.w);
+    const uint32_t med = bits & 0xffu;
+    v.medium = med == 0xffu ? MH_INVALID : med;
+    v.nee_kind = (bits >> 8) & 3u;
+    v.act_scatter = bits & kBitActScatter;
+    v.active_surface = bits & kBitActSurface;
+    v.active_medium = bits & kBitActMedium;
+    v.active = bits & kBitActive;
+    v.specular_chain = bits & kBitSpecChain;
+    v.valid = bits & kBitValid;
+    v.eta = 1.f;
+    // the medium interaction's frame: Frame3f(ray.d) of sample_interaction
+    v.mei.fn = v.ray.d;
+    coordinate_system(v.ray.d, v.mei.fs, v.mei.ft);
+    // the walk's transmittance x emitter value (x 1 keeps it exact)
+    v.ns.transmittance = xyz(w2);
+    v.ns.emitter_val = v3(1.f, 1.f, 1.f);
+    rng.state = (uint64_t)__float_as_uint(w3.x) | ((uint64_t)__float_as_uint(w3.y) << 32);
+    rng.inc = ((uint64_t)v1 << 1) | 1u;
+    if (v.active_surface) {
+        const float4 x0 = P.at(kX0, i), x1 = P.at(kX1, i), x2 = P.at(kX2, i), x3 = P.at(kX3, i), x4 = P.at(kX4, i);
+        v.si.valid = true;
+        v.si.p = xyz(x0);
+        v.si.wi = v3(0.f, 0.f, x0.w);
+        v.si.n = xyz(x1);
+        v.si.shape = __float_as_uint(x1.w);
+        v.si.s = xyz(x2);
+        v.si.t_ = xyz(x3);
+        v.si.sn = xyz(x4);
+        v.rho = v3(x2.w, x3.w, x4.w);
+    }
+    v.mode = kVolPost;
+}
+
+MH_DEV void vw_write_sample(float *out, uint64_t plane, uint32_t pid, const VolState &v, int alpha) {
+    out[pid] = v.result.x;
+    out[plane + pid] = v.result.y;
+    out[2 * plane + pid] = v.result.z;
+    if (alpha) out[5 * plane + pid] = v.valid ? 1.f : 0.f;  // aovs[3] (integrator.cpp:1229-1231)
+}
+
+MH_DEV void vw_range(const VwSeg &it, uint32_t n, uint32_t &r0, uint32_t &r1) {
+    const uint32_t per = (n + it.nwaves - 1) / it.nwaves;
+    r0 = min(n, it.wave * per);
+    r1 = min(n, r0 + per);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// k_vw_main: the loop trips of every queued path up to its next shadow walk.
+// Fresh (round 0): item j of segment s is path s * seg_cap + j, generated
+// here exactly as k_render does (TEA/PCG32 seed, jitter, camera ray,
+// volpath_init); film positions go to the sample planes.
+// ---------------------------------------------------------------------------
+#ifndef MH_VW_MAIN_WAVES
+#define MH_VW_MAIN_WAVES 2
+#endif
+template <bool Fresh, bool InLds, bool Pk>
+__global__ void __launch_bounds__(256, MH_VW_MAIN_WAVES)
+k_vw_main(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane,
+          float *__restrict__ out, VwPlanes cur, VwPlanes nxt, uint32_t seg_cap, const uint32_t *__restrict__ ctr_in,
+          uint32_t *__restrict__ ctr_out, unsigned long long *__restrict__ counters, int alpha) {
+    const VwSeg it = vw_seg();
+    uint32_t count;
+    if (Fresh) {
+        const uint64_t b = (uint64_t)it.seg * seg_cap;
+        count = b >= n ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, n - b);
+    } else {
+        count = ctr_in[it.seg * 32];
+    }
+    {   // workgroups without items leave before staging anything
+        const uint32_t first_wave = (blockIdx.x / kVwSeg) * (blockDim.x / 64u);
+        const uint32_t per = (count + it.nwaves - 1) / it.nwaves;
+        if (first_wave * per >= count) return;
+    }
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    uint32_t r0, r1;
+    vw_range(it, count, r0, r1);
+    const uint64_t base = (uint64_t)it.seg * seg_cap;
+    uint32_t *ctr_next = ctr_out + it.seg * 32;
+    const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
+    uint32_t n_closest = 0;
+#ifdef MH_EXP_VWCNT  // diagnostic build: loop trips / walk steps / wave iterations per round
+    uint32_t n_trips = 0, n_iter = 0;
+#endif
+
+    VolState v;
+    Pcg rng;
+    uint32_t pid = 0, v1 = 0;
+    auto load = [&](uint32_t item) {
+        if (Fresh) {
+            pid = (uint32_t)(base + item);
+            uint32_t lane, px, py;
+            lane_of(lm, pid, lane, px, py);
+            rng.seed(seed_value, lane);
+            v1 = (uint32_t)(rng.inc >> 1);
+            const float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+            const RayT r = camera_ray(S, __builtin_fmaf(sx, sw, -0.f), __builtin_fmaf(sy, sh, -0.f));
+            out[3 * plane + pid] = sx;
+            out[4 * plane + pid] = sy;
+            volpath_init(S, in, rng, r, v);
+        } else {
+            vw_load_path(S, cur, base + item, v, rng, pid, v1);
+        }
+    };
+    uint32_t fetched = r0 + 64u;  // wave-uniform
+    bool has = r0 + vw_lane() < r1;
+    if (has) load(r0 + vw_lane());
+    while (__builtin_amdgcn_ballot_w64(has) != 0) {
+        bool ended = false, susp = false;
+#ifdef MH_EXP_VWCNT
+        ++n_iter;
+#endif
+        if (has) {
+            bool alive = true;
+#ifdef MH_EXP_VWCNT
+            ++n_trips;
+#endif
+            if (v.mode == kVolPost) alive = volpath_post(S, in, rng, v);
+            if (alive) alive = volpath_pre<Pk>(S, B, in, rng, v, n_closest);
+            if (!alive) ended = true;
+            else susp = v.mode == kVolNee;
+        }
+        const uint32_t pos = vw_append(ctr_next, susp);
+        if (susp) {
+            vw_store_path(nxt, base + pos, v, pid, v1);
+            vw_store_walk(nxt, base + pos, v, rng, v1);
+        }
+        if (ended) vw_write_sample(out, plane, pid, v, alpha);
+        const bool need = !has || ended || susp;
+        const unsigned long long m = __ballot(need);
+        if (need) {
+            const uint32_t cand = fetched + (uint32_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
+            has = cand < r1;
+            if (has) load(cand);
+        }
+        fetched += (uint32_t)__popcll(m);
+    }
+    if (counters) wave_count(&counters[0], n_closest);
+#ifdef MH_EXP_VWCNT
+    wave_count(reinterpret_cast<unsigned long long *>(ctr_out + it.seg * 32 + 2), n_trips);
+    if (vw_lane() == 0) atomicAdd(ctr_out + it.seg * 32 + 6, n_iter);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_vw_finish: the tail.  After the first rounds few paths remain, and a
+// round costs its longest walk or trip chain however few items it holds, so
+// the remaining paths run to their end in one launch: each lane resumes a
+// suspended path and advances it through its remaining trips and walks
+// (volpath_advance, the megakernel's state machine), refilled per lane.
+// ---------------------------------------------------------------------------
+template <bool InLds, bool Pk>
+__global__ void __launch_bounds__(256, MH_VW_MAIN_WAVES)
+k_vw_finish(DScene S, IntegratorParams in, uint64_t plane, float *__restrict__ out, VwPlanes cur, uint32_t seg_cap,
+            const uint32_t *__restrict__ ctr_in, unsigned long long *__restrict__ counters, int alpha) {
+    const VwSeg it = vw_seg();
+    const uint32_t count = ctr_in[it.seg * 32];
+    {
+        const uint32_t first_wave = (blockIdx.x / kVwSeg) * (blockDim.x / 64u);
+        const uint32_t per = (count + it.nwaves - 1) / it.nwaves;
+        if (first_wave * per >= count) return;
+    }
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    uint32_t r0, r1;
+    vw_range(it, count, r0, r1);
+    const uint64_t base = (uint64_t)it.seg * seg_cap;
+    uint32_t n_closest = 0, n_shadow = 0;
+    VolState v;
+    Pcg rng;
+    uint32_t pid = 0, v1 = 0;
+    uint32_t fetched = r0 + 64u;
+    bool has = r0 + vw_lane() < r1;
+    if (has) vw_load_path(S, cur, base + r0 + vw_lane(), v, rng, pid, v1);
+    while (__builtin_amdgcn_ballot_w64(has) != 0) {
+        bool ended = false;
+        if (has && !volpath_advance<Pk>(S, B, in, rng, v, n_closest, n_shadow)) {
+            ended = true;
+            vw_write_sample(out, plane, pid, v, alpha);
+        }
+        const bool need = !has || ended;
+        const unsigned long long m = __ballot(need);
+        if (need) {
+            const uint32_t cand = fetched + (uint32_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
+            has = cand < r1;
+            if (has) vw_load_path(S, cur, base + cand, v, rng, pid, v1);
+        }
+        fetched += (uint32_t)__popcll(m);
+    }
+    if (counters) {
+        wave_count(&counters[0], n_closest);
+        wave_count(&counters[1], n_shadow);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_vw_walk: every queued shadow walk to its end (volpath.cpp:361-448,
+// nee_step), starting from nee_begin's state; writes transmittance x
+// emitter value and the lane's PCG32 state back into the walk record.
+// ---------------------------------------------------------------------------
+#ifndef MH_VW_WALK_WAVES
+#define MH_VW_WALK_WAVES 4
+#endif
+template <bool InLds, bool Pk>
+__global__ void __launch_bounds__(256, MH_VW_WALK_WAVES)
+k_vw_walk(DScene S, VwPlanes P, uint32_t seg_cap, const uint32_t *__restrict__ ctr,
+          unsigned long long *__restrict__ counters) {
+    const VwSeg it = vw_seg();
+    const uint32_t count = ctr[it.seg * 32];
+    {
+        const uint32_t first_wave = (blockIdx.x / kVwSeg) * (blockDim.x / 64u);
+        const uint32_t per = (count + it.nwaves - 1) / it.nwaves;
+        if (first_wave * per >= count) return;
+    }
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    uint32_t r0, r1;
+    vw_range(it, count, r0, r1);
+    const uint64_t base = (uint64_t)it.seg * seg_cap;
+    uint32_t n_shadow = 0;
+#ifdef MH_EXP_VWCNT
+    uint32_t n_steps = 0, n_iter = 0;
+#endif
+    NeeState ns;
+    DirS ds;
+    Pcg rng;
+    uint64_t slot = 0;
+    auto load = [&](uint32_t item) {
+        slot = base + item;
+        const float4 w0 = P.at(kW0, slot), w1 = P.at(kW1, slot), w2 = P.at(kW2, slot), w3 = P.at(kW3, slot);
+        // nee_begin's state after the emitter sample (mh_shading.hpp)
+        ns.ray = RayT{xyz(w0), xyz(w1), w0.w};
+        ns.max_dist = w0.w;
+        ns.medium = __float_as_uint(w1.w);
+        ns.emitter_val = xyz(w2);
+        ds.dist = w2.w;
+        ns.transmittance = v3(1.f, 1.f, 1.f);
+        ns.total_dist = 0.f;
+        ns.si.valid = false;
+        ns.si_t = 0.f;
+        ns.needs_intersection = true;
+        rng.state = (uint64_t)__float_as_uint(w3.x) | ((uint64_t)__float_as_uint(w3.y) << 32);
+        rng.inc = ((uint64_t)__float_as_uint(w3.z) << 1) | 1u;
+    };
+    uint32_t fetched = r0 + 64u;
+    bool has = r0 + vw_lane() < r1;
+    if (has) load(r0 + vw_lane());
+    while (__builtin_amdgcn_ballot_w64(has) != 0) {
+        bool fin = false;
+#ifdef MH_EXP_VWCNT
+        n_steps += has;
+        ++n_iter;
+#endif
+        if (has && !nee_step<Pk>(S, B, rng, ds, ns, n_shadow)) {
+            fin = true;
+            const V3 r = nee_result(ns);
+            P.at(kW2, slot) = f4(r, 0.f);
+            P.at(kW3, slot) = make_float4(__uint_as_float((uint32_t)rng.state),
+                                          __uint_as_float((uint32_t)(rng.state >> 32)), 0.f, 0.f);
+        }
+        const bool need = !has || fin;
+        const unsigned long long m = __ballot(need);
+        if (need) {
+            const uint32_t cand = fetched + (uint32_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
+            has = cand < r1;
+            if (has) load(cand);
+        }
+        fetched += (uint32_t)__popcll(m);
+    }
+    if (counters) wave_count(&counters[1], n_shadow);
+#ifdef MH_EXP_VWCNT
+    wave_count(reinterpret_cast<unsigned long long *>(const_cast<uint32_t *>(ctr) + it.seg * 32 + 4), n_steps);
+    if (vw_lane() == 0) atomicAdd(const_cast<uint32_t *>(ctr) + it.seg * 32 + 7, n_iter);
+#endif
+}
+
+// ===========================================================================
+// Phase-scheduled volpath (k_vol_sched): one persistent launch, no rounds.
+//
+// The loop of volpath.cpp:139-330 and its NEE walk (:361-448) are cut into
+// phases at every point where the work changes kind:
+//   HEAD     loop head: Russian roulette, free-flight sampling in the medium
+//            (sample_interaction), the null / real decision of a null
+//            collision -- the light, frequent trip;
+//   TRACE    a closest-hit query (medium segment, surface, or walk segment);
+//   SCATTER  a real medium scatter: albedo weight, emitter sample, phase eval;
+//   SURF     a surface interaction: emission + MIS, BSDF NEE setup;
+//   WALK     one step of the ratio-tracked transmittance walk;
+//   POST     after a walk: the sample's contribution, phase / BSDF sampling;
+//   FREE     a lane without a path takes the wave's next sample (camera ray).
+// Each trip of the wave runs ONE phase -- the one whose pending lanes times
+// its weight is largest (a ballot per phase) -- for exactly the lanes pending
+// in it; lanes of other phases wait.  Heavy, rare work (scatter, surface,
+// traces) therefore runs for many lanes at once instead of costing the whole
+// wave at a few active lanes per instruction, the light phases run nearly
+// full, and a finished lane is refilled at once (no wave waits for its
+// longest path, no barrier between rounds, no path state through HBM).
+// Per lane, the operations and random draws are those of volpath_pre /
+// volpath_post / nee_step in their order (bit-identical samples).
+// ===========================================================================
+enum : uint32_t {
+    kPhFree = 0, kPhHead, kPhTraceM, kPhTraceS, kPhTraceWM, kPhTraceWS, kPhScatter, kPhSurf, kPhWalk, kPhPost
+};
+enum : uint32_t { kGFree = 0, kGHead, kGTrace, kGScatter, kGSurf, kGWalk, kGPost, kNGroups };
+MH_DEV uint32_t ph_group(uint32_t ph) {
+    return ph == kPhFree ? kGFree : ph == kPhHead ? kGHead : ph <= kPhTraceWS ? kGTrace : ph == kPhScatter ? kGScatter
+         : ph == kPhSurf ? kGSurf : ph == kPhWalk ? kGWalk : kGPost;
+}
+
+// the walk's own medium interaction across its trace (nee_step's local mei)
+struct WMei {
+    float t, mint, maj, sigma_n;
+    V3 p;
+    bool valid;
+};
+
+// end of a trip that needs no walk (volpath_pre's tail + volpath_post)
+MH_DEV uint32_t vs_no_walk(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    if (v.nee_kind != kNeeNone) {  // ds.pdf == 0: emitted = 0
+        v.ns.transmittance = v3(0, 0, 0);
+        v.ns.emitter_val = v3(0, 0, 0);
+    }
+    return volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
+}
+
+// the medium block of volpath_pre after its (optional) intersection, up to
+// the scatter / surface split (volpath.cpp:166-223)
+MH_DEV uint32_t vs_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    MEI &mei = v.mei;
+    v.needs_intersection = v.needs_intersection && !v.si.valid;
+    if (v.si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+    const DMedium &m = S.media[v.medium];
+    const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+    if (spectral) {
+        const float t = fminf(mei.t, v.si_t) - mei.mint;
+        const float tr = exp_dr((-t) * mei.maj);
+        const float pdf = v.si_t < mei.t ? tr : tr * mei.maj;
+        v.throughput = v.throughput * (pdf > 0.f ? tr / pdf : 0.f);
+    }
+    const bool escaped = !mei.valid;
+    v.active_medium = mei.valid;
+    bool null_scatter = false;
+    if (v.active_medium) null_scatter = rng.next_float() >= mei.sigma_t / mei.maj;
+    const bool act_null = null_scatter && v.active_medium;
+    bool act_scatter = !act_null && v.active_medium;
+    if (spectral && act_null) v.throughput = v.throughput * ((mei.sigma_n * mei.maj) / mei.sigma_n);
+    if (act_scatter) { v.depth += 1; v.last_p = mei.p; }
+    v.active = v.active && v.depth < in.max_depth;
+    act_scatter = act_scatter && v.active;
+    if (act_null) { v.ray.o = mei.p; v.si_t = v.si_t - mei.t; }
+    v.nee_kind = kNeeNone;
+    v.act_scatter = act_scatter;
+    if (act_scatter) return kPhScatter;
+    v.active_surface = v.active_surface || escaped;
+    if (v.active_surface) return v.needs_intersection ? kPhTraceS : kPhSurf;
+    // a null collision (or a scatter cut by max_depth): volpath_post's test
+    v.active_surface = false;
+    v.rho = v3(0, 0, 0);
+    return (v.active && v.active_medium) ? kPhHead : kPhFree;
+}
+
+// HEAD: Russian roulette and free-flight sampling (volpath.cpp:143-165)
+MH_DEV uint32_t vs_head(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    bool active = nonzero(v.throughput);
+    const float q = fminf(hmax(v.throughput) * (v.eta * v.eta), 0.95f);
+    const bool perform_rr = v.depth > in.rr_depth;
+    if (active) active = rng.next_float() < q || !perform_rr;
+    if (perform_rr) v.throughput = v.throughput * rcp(q);
+    active = active && v.depth < in.max_depth;
+    if (!active) return kPhFree;
+    v.active = true;
+    v.active_medium = v.medium != MH_INVALID;
+    v.active_surface = !v.active_medium;
+    v.act_scatter = false;
+    v.nee_kind = kNeeNone;
+    v.mei.valid = false;
+    v.mei.t = __builtin_huge_valf();
+    if (v.active_medium) {
+        const DMedium &m = S.media[v.medium];
+        sample_interaction(S, v.medium, v.ray, rng.next_float(), v.mei);
+        if (m.type == MH_MEDIUM_HOMOGENEOUS && v.mei.valid) v.ray.maxt = v.mei.t;
+        if (v.needs_intersection) return kPhTraceM;
+        return vs_med_rest(S, in, rng, v);
+    }
+    return v.needs_intersection ? kPhTraceS : kPhSurf;
+}
+
+// SCATTER: a real medium interaction (volpath.cpp:224-252)
+MH_DEV uint32_t vs_scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    const DMedium &m = S.media[v.medium];
+    const MEI &mei = v.mei;
+    const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+    if (spectral) v.throughput = v.throughput * vdiv(mei.sigma_s * mei.maj, mei.sigma_t);
+    else v.throughput = v.throughput * vdiv(mei.sigma_s, mei.sigma_t);
+    const bool sample_emitters = !(m.flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+    v.specular_chain = !sample_emitters;
+    v.valid = true;  // valid_ray |= act_medium_scatter (volpath.cpp:223)
+    bool walk = false;
+    if (sample_emitters) {
+        walk = nee_begin(S, mei.p, v3(0, 0, 0), nullptr, rng, v.medium, v.ds, v.ns);
+        const float ph = phase_eval(m, mei_to_local(mei, v.ds.d));
+        v.pend = v.throughput * ph;
+        v.pend_w = mis_weight(v.ds.pdf, v.ds.delta ? 0.f : ph);
+        v.nee_kind = kNeeMedium;
+    }
+    v.active_surface = false;
+    v.rho = v3(0, 0, 0);
+    return walk ? kPhWalk : vs_no_walk(S, in, rng, v);
+}
+
+// SURF: a surface interaction after its intersection (volpath.cpp:254-300)
+MH_DEV uint32_t vs_surf(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    const SI &si = v.si;
+    const bool count_direct = v.depth == 0 || v.specular_chain;
+    const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+    if (em != MH_INVALID && !(v.depth == 0 && in.hide_emitters)) {
+        float emitter_pdf = 1.f;
+        if (!count_direct) emitter_pdf = emitter_pdf_direction(S, em, si, v.last_p);
+        const V3 emitted = emitter_eval(S, em, si);
+        v.result = v.result + (count_direct ? v.throughput * emitted
+                                            : (v.throughput * mis_weight(v.last_pdf, emitter_pdf)) * emitted);
+    }
+    v.active_surface = v.active_surface && si.valid;
+    v.rho = v3(0, 0, 0);
+    bool walk = false;
+    if (v.active_surface) {
+        const uint32_t b = S.shapes[si.shape].bsdf;
+        const bool is_null = b == MH_INVALID || S.bsdf_type[b] == MH_BSDF_NULL;
+        if (!is_null) v.rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+        if (!is_null && v.depth + 1 < in.max_depth) {
+            walk = nee_begin(S, si.p, si.n, &si, rng, v.medium, v.ds, v.ns);
+            V3 bv;
+            float bp;
+            diffuse_eval_pdf(v.rho, si.wi, to_local(si, v.ds.d), true, bv, bp);
+            const float w = mis_weight(v.ds.pdf, v.ds.delta ? 0.f : bp);
+            v.pend = (v.throughput * bv) * w;
+            v.nee_kind = kNeeSurface;
+        }
+    }
+    return walk ? kPhWalk : vs_no_walk(S, in, rng, v);
+}
+
+// ---- the walk (nee_step, volpath.cpp:361-448) cut at its intersection ------
+// common tail of a walk step; false when the walk has ended
+MH_DEV bool walk_tail(const DScene &S, NeeState &ns, bool active_medium, bool escaped, bool active_surface0,
+                      bool intersect, float remaining) {
+    ns.needs_intersection = ns.needs_intersection && !intersect;
+    bool active_surface = active_surface0 || escaped;
+    if (active_surface) ns.total_dist += ns.si_t;
+    active_surface = active_surface && ns.si.valid && !active_medium;
+    if (active_surface) {
+        const uint32_t b = S.shapes[ns.si.shape].bsdf;
+        const float tn = (b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f;
+        ns.transmittance = ns.transmittance * tn;
+        ns.ray = spawn_ray(ns.si.p, ns.si.n, ns.ray.d);
+    }
+    ns.ray.maxt = remaining;
+    ns.needs_intersection = ns.needs_intersection || active_surface;
+    const bool active = (active_medium || active_surface) && nonzero(ns.transmittance);
+    if (active_surface && is_medium_transition(S, ns.si)) ns.medium = target_medium(S, ns.si, ns.ray.d);
+    return active;
+}
+
+// the medium part of a walk step after its (optional) intersection
+MH_DEV bool walk_med_rest(const DScene &S, const DirS &ds, NeeState &ns, WMei &wm) {
+    const float remaining = ns.max_dist - ns.total_dist;
+    const DMedium &m = S.media[ns.medium];
+    if (ns.si_t < wm.t) { wm.t = __builtin_huge_valf(); wm.valid = false; }
+    ns.needs_intersection = ns.needs_intersection && !ns.si.valid;
+    const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
+    if (spectral) {
+        const float t = fminf(remaining, fminf(wm.t, ns.si_t)) - wm.mint;
+        const float tr = exp_dr((-t) * wm.maj);
+        const float pdf = (ns.si_t < wm.t || wm.t > remaining) ? tr : tr * wm.maj;
+        ns.transmittance = ns.transmittance * (pdf > 0.f ? tr / pdf : 0.f);
+    }
+    if (wm.t > remaining && wm.valid) ns.total_dist = ds.dist;
+    if (wm.t > remaining) { wm.t = __builtin_huge_valf(); wm.valid = false; }
+    const bool escaped = !wm.valid, active_medium = wm.valid;
+    if (active_medium) {
+        ns.total_dist += wm.t;
+        ns.ray.o = wm.p;
+        ns.si_t = ns.si_t - wm.t;
+        ns.transmittance = ns.transmittance * (spectral ? wm.sigma_n : wm.sigma_n / wm.maj);
+    }
+    return walk_tail(S, ns, active_medium, escaped, false, false, remaining);
+}
+
+// WALK: the start of a walk step, up to its intersection
+MH_DEV uint32_t vs_walk(const DScene &S, Pcg &rng, const DirS &ds, NeeState &ns, WMei &wm) {
+    const float remaining = ns.max_dist - ns.total_dist;
+    ns.ray.maxt = remaining;
+    if (!(remaining > 0.f)) return kPhPost;
+    if (ns.medium != MH_INVALID) {
+        const DMedium &m = S.media[ns.medium];
+        MEI mei;
+        sample_interaction(S, ns.medium, ns.ray, rng.next_float(), mei);
+        if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ns.ray.maxt = fminf(mei.t, remaining);
+        wm.t = mei.t; wm.mint = mei.mint; wm.maj = mei.maj; wm.sigma_n = mei.sigma_n; wm.p = mei.p;
+        wm.valid = mei.valid;
+        if (ns.needs_intersection) return kPhTraceWM;
+        return walk_med_rest(S, ds, ns, wm) ? kPhWalk : kPhPost;
+    }
+    if (ns.needs_intersection) return kPhTraceWS;
+    return walk_tail(S, ns, false, false, true, false, remaining) ? kPhWalk : kPhPost;
+}
+
+// TRACE: every lane pending an intersection traces it; then its continuation
+template <bool Pk>
+MH_DEV uint32_t vs_trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, uint32_t ph,
+                         VolState &v, WMei &wm, uint32_t &n_closest, uint32_t &n_shadow) {
+    const bool walk = ph == kPhTraceWM || ph == kPhTraceWS;
+    const RayT ray = walk ? v.ns.ray : v.ray;
+    SI si;
+    float si_t;
+    trace_si<Pk>(S, B, ray, si, si_t);
+    if (walk) {
+        v.ns.si = si;
+        v.ns.si_t = si_t;
+        ++n_shadow;
+        if (ph == kPhTraceWM) return walk_med_rest(S, v.ds, v.ns, wm) ? kPhWalk : kPhPost;
+        const float remaining = v.ns.max_dist - v.ns.total_dist;
+        return walk_tail(S, v.ns, false, false, true, true, remaining) ? kPhWalk : kPhPost;
+    }
+    v.si = si;
+    v.si_t = si_t;
+    ++n_closest;
+    if (ph == kPhTraceM) return vs_med_rest(S, in, rng, v);
+    return kPhSurf;
+}
+
+#ifndef MH_VS_WAVES
+#define MH_VS_WAVES 2
+#endif
+// phase weights (x16): a phase runs when its pending lanes x weight is the
+// largest; heavy phases wait for more lanes
+#ifndef MH_VS_W
+#define MH_VS_W 8, 16, 8, 6, 6, 16, 10   // free, head, trace, scatter, surf, walk, post
+#endif
+// Tab: the shading tables (stage_tables) and the media records staged into
+// LDS: every trip reads the medium record (transform, bbox, majorant,
+// albedo) and the surface trips walk shape -> bsdf -> texture / emitter
+// chains; from global memory each of those is a dependent L2 round trip
+// (~20 per trip), from LDS ~100 cycles.
+__host__ __device__ inline uint32_t vs_media_bytes(const DScene &S) { return (S.n_media * (uint32_t)sizeof(DMedium) + 15u) & ~15u; }
+__host__ __device__ inline uint32_t vs_tab_bytes(const DScene &S) { return ((S.tab_bytes + 15u) & ~15u) + vs_media_bytes(S); }
+
+template <bool InLds, bool Pk, bool Tab>
+__global__ void __launch_bounds__(256, MH_VS_WAVES)
+k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane,
+            float *__restrict__ out, unsigned long long *__restrict__ counters, unsigned long long *__restrict__ work,
+            int alpha) {
+    // samples are handed out in batches of 64 from one device counter (work)
+    extern __shared__ uint4 lds[];
+    DScene S = S0;
+    uint32_t tab = 0;
+    if (Tab) {
+        S = stage_tables(S0, lds);
+        const uint32_t mo = (S0.tab_bytes + 15u) & ~15u;
+        uint8_t *mb = reinterpret_cast<uint8_t *>(lds) + mo;
+        lds_copy(mb, S0.media, S0.n_media * (uint32_t)sizeof(DMedium));
+        __syncthreads();
+        S.media = reinterpret_cast<const DMedium *>(mb);
+        tab = vs_tab_bytes(S0) / 16u;
+    }
+    LdsBvh B = stage_bvh<InLds>(S0, lds + tab);
+    constexpr uint32_t W[kNGroups] = {MH_VS_W};
+    const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
+    uint32_t n_closest = 0, n_shadow = 0;
+    VolState v;
+    WMei wm;
+    Pcg rng;
+    uint32_t pid = 0, ph = kPhFree;
+    uint64_t next = 0, end = 0;  // wave-uniform: the wave's current batch [next, end)
+    bool drained = false;        // wave-uniform: the device counter has passed n
+#ifdef MH_EXP_VSCNT
+    unsigned long long d_trips[kNGroups] = {}, d_lanes[kNGroups] = {}, d_ticks[kNGroups] = {};
+#endif
+    while (true) {
+        uint32_t cnt[kNGroups];
+        const uint32_t g = ph_group(ph);
+#pragma unroll
+        for (uint32_t k = 0; k < kNGroups; ++k) cnt[k] = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(g == k));
+        if (drained && next >= end) cnt[kGFree] = 0;
+        uint32_t sel = kNGroups, best = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kNGroups; ++k)
+            if (cnt[k] * W[k] > best) { best = cnt[k] * W[k]; sel = k; }
+        if (sel == kNGroups) break;  // no lane holds a path and the range is done
+#ifdef MH_EXP_VSCNT  // diagnostic build: wave trips, lanes and shader cycles per phase (in registers)
+#pragma unroll
+        for (uint32_t k = 0; k < kNGroups; ++k)
+            if (sel == k) { d_trips[k] += 1; d_lanes[k] += cnt[k]; }
+        const uint64_t t_phase = __builtin_amdgcn_s_memtime();
+#endif
+        bool ended = false;
+        if (sel == kGFree) {
+            if (next >= end) {  // take the next batch of 64 samples
+                uint64_t b = 0;
+                if (vw_lane() == 0) b = atomicAdd(work, 64ull);
+                b = __builtin_amdgcn_readfirstlane((uint32_t)b) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32);
+                next = std::min<uint64_t>(b, n);
+                end = std::min<uint64_t>(b + 64u, n);
+                drained = b + 64u >= n;
+            }
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(ph == kPhFree);
+            if (ph == kPhFree) {
+                const uint64_t k = next + (uint64_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
+                if (k < end) {
+                    pid = (uint32_t)k;
+                    uint32_t lane, px, py;
+                    lane_of(lm, k, lane, px, py);
+                    rng.seed(seed_value, lane);
+                    const float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+                    const RayT r = camera_ray(S, __builtin_fmaf(sx, sw, -0.f), __builtin_fmaf(sy, sh, -0.f));
+                    out[3 * plane + k] = sx;
+                    out[4 * plane + k] = sy;
+                    volpath_init(S, in, rng, r, v);
+                    ph = kPhHead;
+                }
+            }
+            next = std::min<uint64_t>(end, next + (uint64_t)__popcll(m));
+        } else if (sel == kGHead) {
+            if (ph == kPhHead) { ph = vs_head(S, in, rng, v); ended = ph == kPhFree; }
+        } else if (sel == kGTrace) {
+            if (g == kGTrace) {
+                ph = vs_trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
+                ended = ph == kPhFree;
+            }
+        } else if (sel == kGScatter) {
+            if (ph == kPhScatter) { ph = vs_scatter(S, in, rng, v); ended = ph == kPhFree; }
+        } else if (sel == kGSurf) {
+            if (ph == kPhSurf) { ph = vs_surf(S, in, rng, v); ended = ph == kPhFree; }
+        } else if (sel == kGWalk) {
+            if (ph == kPhWalk) ph = vs_walk(S, rng, v.ds, v.ns, wm);
+        } else {
+            if (ph == kPhPost) { ph = volpath_post(S, in, rng, v) ? kPhHead : kPhFree; ended = ph == kPhFree; }
+        }
+        if (ended) vw_write_sample(out, plane, pid, v, alpha);
+#ifdef MH_EXP_VSCNT
+        {
+            const uint64_t dt = __builtin_amdgcn_s_memtime() - t_phase;
+#pragma unroll
+            for (uint32_t k = 0; k < kNGroups; ++k)
+                if (sel == k) d_ticks[k] += dt;
+        }
+#endif
+    }
+    if (counters) {
+        wave_count(&counters[0], n_closest);
+        wave_count(&counters[1], n_shadow);
+    }
+#ifdef MH_EXP_VSCNT
+    if (vw_lane() == 0 && counters)
+        for (uint32_t k = 0; k < kNGroups; ++k) {
+            atomicAdd(&counters[2 + k], d_trips[k]);
+            atomicAdd(&counters[9 + k], d_lanes[k]);
+            atomicAdd(&counters[16 + k], d_ticks[k]);
+        }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+// volpath execution: phase-scheduled persistent kernel (default) or
+// main / walk rounds (MH_VOL_MODE=rounds)
+bool vol_sched_mode() {
+    const char *e = getenv("MH_VOL_MODE");
+    return !(e && !strcmp(e, "rounds"));
+}
+uint32_t vs_blocks(int cus) {
+    uint32_t bpc = MH_VS_WAVES;  // one resident round of 256-lane workgroups (a wave per SIMD each)
+    if (const char *e = getenv("MH_VS_BPC")) bpc = std::max(1, atoi(e));
+    return (uint32_t)cus * bpc;
+}
+uint64_t vw_max_chunk() { return 1ull << 23; }
+size_t vw_workspace_bytes(uint64_t cap) { return (size_t)2 * kVwPlanes * 16 * cap; }
+uint32_t vw_counter_words(uint32_t rounds) { return kVwCtr * (rounds + 1); }
+uint32_t vw_rounds(const IntegratorParams &in) { return in.max_depth + 1; }
+bool vw_supported(const DScene &S, const IntegratorParams &in) {
+    return in.type == MH_INTEGRATOR_VOLPATH && in.max_depth <= 1024 && S.n_media < 255;
+}
+uint32_t vw_blocks(int cus) {
+    uint32_t bpc = 8;
+    if (const char *e = getenv("MH_VW_BPC")) bpc = std::max(1, atoi(e));
+    return std::max<uint32_t>(kVwSeg, (uint32_t)cus * bpc / kVwSeg * kVwSeg);
+}
+
+hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                            uint64_t n, uint64_t plane, float *out, uint32_t grid, unsigned long long *counters,
+                            hipStream_t st, int alpha) {
+    if (n == 0) return hipSuccess;
+    const size_t sh = lds_bytes(S, 256);
+    const bool lds = S.lds_bytes_bvh != 0;
+    const char *te = getenv("MH_TRAVERSAL");
+    const bool pk = S.n_prims > 0 && S.n_prims <= wf_packet_max_prims() && !(te && !strcmp(te, "lane"));
+    const bool tab = S.tab_bytes != 0 && !getenv("MH_VS_NOTAB");
+#define MH_VS(L, P, T)                                                                                        \
+    hipLaunchKernelGGL((k_vol_sched<L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), st, S, in, \
+                       lm, seed_value, n, plane, out, counters, work, alpha)
+    unsigned long long *work = counters + 31;  // the batch counter of this launch
+    hipError_t e = hipMemsetAsync(work, 0, sizeof(*work), st);
+    if (e != hipSuccess) return e;
+    if (pk && tab) MH_VS(false, true, true);
+    else if (pk) MH_VS(false, true, false);
+    else if (lds) MH_VS(true, false, false);
+    else MH_VS(false, false, false);
+#undef MH_VS
+    return hipGetLastError();
+}
+
+// one chunk of n paths (single pass), all rounds queued on `st` without host
+// synchronisation; rounds without work exit at their first instructions
+hipError_t launch_volwave(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                          uint64_t n, uint64_t plane, float *out, void *ws, uint64_t cap, uint32_t *ctr,
+                          uint32_t grid, unsigned long long *counters, hipStream_t st, int alpha) {
+    if (n == 0) return hipSuccess;
+    if (n > cap || n > 0xffffffffull) return hipErrorInvalidValue;
+    const uint32_t rounds = vw_rounds(in);
+    hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * vw_counter_words(rounds), st);
+    if (e != hipSuccess) return e;
+    VwPlanes side[2];
+    for (int k = 0; k < 2; ++k) {
+        side[k].p = reinterpret_cast<float4 *>(ws) + (size_t)k * kVwPlanes * cap;
+        side[k].cap = cap;
+    }
+    const uint32_t seg_cap = (uint32_t)((n + kVwSeg - 1) / kVwSeg);
+    const size_t sh = lds_bytes(S, 256);
+    const bool lds = S.lds_bytes_bvh != 0;
+    // packet engine for scenes with pair records (MH_TRAVERSAL=lane: per-lane)
+    const char *te = getenv("MH_TRAVERSAL");
+    const bool pk = S.n_prims > 0 && S.n_prims <= wf_packet_max_prims() && !(te && !strcmp(te, "lane"));
+    // main / walk rounds while many paths are live, then one finish launch
+    uint32_t wave_rounds = kVwWaveRounds;
+    if (const char *e = getenv("MH_VW_ROUNDS")) wave_rounds = (uint32_t)std::max(1, atoi(e));
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const VwPlanes &c = side[r & 1], &x = side[(r + 1) & 1];
+        const uint32_t *cin = ctr + (size_t)kVwCtr * r;
+        uint32_t *cout = ctr + (size_t)kVwCtr * (r + 1);
+        if (r == wave_rounds) {
+#define MH_VW_FIN(L, P) \
+    hipLaunchKernelGGL((k_vw_finish<L, P>), dim3(grid), dim3(256), sh, st, S, in, plane, out, c, seg_cap, cin, counters, alpha)
+            if (pk) MH_VW_FIN(false, true);
+            else if (lds) MH_VW_FIN(true, false);
+            else MH_VW_FIN(false, false);
+#undef MH_VW_FIN
+            break;
+        }
+#define MH_VW_MAIN(F, L, P)                                                                                   \
+    hipLaunchKernelGGL((k_vw_main<F, L, P>), dim3(grid), dim3(256), sh, st, S, in, lm, seed_value, n, plane, out, \
+                       c, x, seg_cap, cin, cout, counters, alpha)
+#define MH_VW_WALK(L, P) \
+    hipLaunchKernelGGL((k_vw_walk<L, P>), dim3(grid), dim3(256), sh, st, S, x, seg_cap, cout, counters)
+        if (pk) {
+            if (r == 0) MH_VW_MAIN(true, false, true);
+            else MH_VW_MAIN(false, false, true);
+        } else if (r == 0) {
+            if (lds) MH_VW_MAIN(true, true, false); else MH_VW_MAIN(true, false, false);
+        } else {
+            if (lds) MH_VW_MAIN(false, true, false); else MH_VW_MAIN(false, false, false);
+        }
+        if (r + 1 == rounds) break;  // depth < max_depth: no walk after the last round
+        if (pk) MH_VW_WALK(false, true);
+        else if (lds) MH_VW_WALK(true, false);
+        else MH_VW_WALK(false, false);
+#undef MH_VW_MAIN
+#undef MH_VW_WALK
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mh

@@ -242,13 +242,44 @@ def _vol_scene(mi, w=24, h=20, spp=8, **kw):
     return mi.load_dict(mi.volume_cube(w, h, spp, **kw))
 
 
-@pytest.mark.parametrize("kw", [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0},
-                                {"max_depth": 8, "g": -0.3, "albedo": [0.9, 0.5, 0.2]}])
-def test_volpath_per_sample_parity(kw):
+def _vol_floor_scene(mi, w=24, h=20, spp=8, **kw):
+    """volume_cube + a diffuse floor below it: surface NEE walks through the
+    medium (suspended surface paths carry their interaction through HBM)."""
+    kw.setdefault("grid", mi.fbm_grid(16))
+    kw.setdefault("scale", 4.0)
+    d = mi.volume_cube(w, h, spp, **kw)
+    T = mi.Transform4f
+    d["floor"] = {"type": "rectangle",
+                  "to_world": T.translate([0, -1.2, 0]) @ T.rotate([1, 0, 0], -90) @ T.scale([3, 3, 3]),
+                  "bsdf": {"type": "diffuse", "reflectance": {"type": "rgb", "value": [0.6, 0.5, 0.4]}}}
+    return mi.load_dict(d)
+
+
+VOL_CASES = [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0},
+             {"max_depth": 8, "g": -0.3, "albedo": [0.9, 0.5, 0.2]}, {"floor": True}, {"floor": True, "max_depth": 3},
+             {"max_depth": 1}, {"max_depth": 0}]
+
+
+@pytest.mark.parametrize("mode", ["mega", "wavefront", "wavefront-rounds", "wavefront-finish1", "wavefront-rounds100"])
+@pytest.mark.parametrize("kw", VOL_CASES)
+def test_volpath_per_sample_parity(kw, mode, monkeypatch):
+    """mega: k_render<VOLPATH>; wavefront: the phase-scheduled persistent
+    kernel k_vol_sched (mh_volwave.hip); -rounds: k_vw_main / k_vw_walk
+    rounds then k_vw_finish; -rounds100: rounds only; -finish1: one round,
+    then the finish kernel.  Bit-identical per sample."""
     mi = _mi()
-    scene = _vol_scene(mi, **kw)
+    from mitsuba_hip import _abi as A
+    if mode != "wavefront" and mode != "mega":
+        monkeypatch.setenv("MH_VOL_MODE", "rounds")
+    if mode == "wavefront-rounds100":
+        monkeypatch.setenv("MH_VW_ROUNDS", "100000")
+    if mode == "wavefront-finish1":
+        monkeypatch.setenv("MH_VW_ROUNDS", "1")
+    mode = mode.split("-")[0]
+    kw = dict(kw)
+    scene = _vol_floor_scene(mi, **kw) if kw.pop("floor", False) else _vol_scene(mi, **kw)
     integ = scene.integrator()
-    L, pos = _gpu_samples(mi, scene, integ, 3, 8)
+    L, pos = _gpu_samples(mi, scene, integ, 3, 8, A.FLAG_WAVEFRONT if mode == "wavefront" else 0)
     rL, rpos, _ = O.sample_range(scene, integ, 3, 8, 0, L.shape[0])
     np.testing.assert_array_equal(pos, rpos)
     exact = np.all(L == rL, axis=1)
@@ -257,13 +288,29 @@ def test_volpath_per_sample_parity(kw):
     assert close.mean() >= 0.999
 
 
-def test_volpath_film_parity():
+@pytest.mark.parametrize("mode", ["mega", "wavefront"])
+def test_volpath_film_parity(mode):
     mi = _mi()
     scene = _vol_scene(mi, 40, 32, 16)
-    film = mi.render_film(scene, seed=5, spp=16).cpu().numpy()
+    film = mi.render_film(scene, seed=5, spp=16, mode=mode).cpu().numpy()
     ref = O.render(scene, seed=5, spp=16)
     ok, frac = _film_close(film, ref)
     assert ok, f"film parity {frac}"
+
+
+def test_volpath_wavefront_matches_megakernel_stats():
+    """The two execution modes trace the same rays (closest / shadow counts)
+    and produce the same samples on a 64^3 grid at 64 x 48 @ 16 spp."""
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = _vol_scene(mi, 64, 48, 16, grid=mi.fbm_grid(64))
+    sm, sw = A.Stats(), A.Stats()
+    fm = mi.render_film(scene, seed=9, spp=16, mode="mega", stats=sm).cpu().numpy()
+    fw = mi.render_film(scene, seed=9, spp=16, mode="wavefront", stats=sw).cpu().numpy()
+    assert sw.mode == 3 and sm.mode == 0
+    assert (sw.rays_closest, sw.rays_shadow) == (sm.rays_closest, sm.rays_shadow)
+    ok, frac = _film_close(fw, fm, 0.999)
+    assert ok, f"film agreement {frac}"
 
 
 def test_volpath_white_furnace_gpu():
@@ -746,8 +793,14 @@ def test_alpha_film_parity(pf, itype, mode):
 
 
 @pytest.mark.parametrize("itype,mode", [("path", "wavefront"), ("path", "mega"), ("prb", "mega"),
-                                        ("volpath", "mega")])
-def test_alpha_per_sample_validity(itype, mode):
+                                        ("volpath", "mega"), ("volpath", "wavefront"), ("volpath", "wavefront-lane"),
+                                        ("volpath", "wavefront-rounds")])
+def test_alpha_per_sample_validity(itype, mode, monkeypatch):
+    if mode == "wavefront-lane":
+        monkeypatch.setenv("MH_TRAVERSAL", "lane")
+    if mode == "wavefront-rounds":
+        monkeypatch.setenv("MH_VOL_MODE", "rounds")
+    mode = mode.split("-")[0]
     mi = _mi()
     from mitsuba_hip import _abi as A
     scene = _open_box(mi, "rgba", 24, 20, 8, env=(itype == "path"))
