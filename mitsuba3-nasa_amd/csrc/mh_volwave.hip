@@ -685,7 +685,7 @@ MH_DEV uint32_t vs_trace(const DScene &S, const LdsBvh &B, const IntegratorParam
 // phase weights (x16): a phase runs when its pending lanes x weight is the
 // largest; heavy phases wait for more lanes
 #ifndef MH_VS_W
-#define MH_VS_W 8, 16, 8, 6, 6, 16, 10   // free, head, trace, scatter, surf, walk, post
+#define MH_VS_W 8, 16, 12, 8, 8, 6, 12   // free, head, trace, scatter, surf, walk, post (swept on config 4: 194 -> 214 Msamples/s)
 #endif
 // Tab: the shading tables (stage_tables) and the media records staged into
 // LDS: every trip reads the medium record (transform, bbox, majorant,
