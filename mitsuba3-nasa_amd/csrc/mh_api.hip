@@ -88,6 +88,7 @@ struct mh_scene {
     DevBuf work, film_tmp, film4, alpha_px, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
+    DevBuf wf_ws_bmp;  // wavefront PRB with a bitmap parameter: vertex records (WfBmp)
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     std::vector<mh_medium> h_media;
@@ -446,7 +447,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -941,7 +942,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     std::vector<float *> bufs(kMaxParams, nullptr);
     std::vector<size_t> counts(kMaxParams, 0);
     std::vector<uint32_t> slot_of_param(n_params);
-    uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0;
+    uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0, bmp_tex = 0;
     for (uint32_t k = 0; k < n_params; ++k) {
         const uint32_t kind = param_tex[k] & MH_PARAM_KIND_MASK, idx = param_tex[k] & ~MH_PARAM_KIND_MASK;
         int32_t *owner;
@@ -978,6 +979,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         } else {
             if (n_bmp >= (uint32_t)kMaxBitmapParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many bitmap parameters");
             slot = kMaxRgbParams + (int)n_bmp++;
+            if (kind == 0) bmp_tex = idx;
         }
         counts[slot] = cnt;
         *owner = slot;
@@ -1057,9 +1059,16 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     // fused form runs as wavefront kernels unless MH_FLAG_MEGAKERNEL / MH_MODE=mega
     const char *env_replay = getenv("MH_PRB_REPLAY");
     const char *env_mode = getenv("MH_MODE");
-    const bool fused = !vol && n_bmp == 0 && !(flags & MH_FLAG_PRB_REPLAY) && !(env_replay && !strcmp(env_replay, "1"));
-    const bool wavefront = fused && in->max_depth <= 64 && !(flags & MH_FLAG_MEGAKERNEL) &&
-                           !(env_mode && !strcmp(env_mode, "mega"));
+    const bool replay = (flags & MH_FLAG_PRB_REPLAY) || (env_replay && !strcmp(env_replay, "1"));
+    const bool mega = (flags & MH_FLAG_MEGAKERNEL) || (env_mode && !strcmp(env_mode, "mega"));
+    const bool fused = !vol && n_bmp == 0 && !replay;
+    // one bitmap parameter: the fused PRB wavefront logs its vertices and a
+    // scatter pass charges the texels (WfBmp, mh_wavefront.hip) -- packet-engine
+    // scenes, max_depth <= 32 (MH_PRB_BMP_WF=0: the replay megakernel)
+    const char *env_bwf = getenv("MH_PRB_BMP_WF");
+    const bool bmp_wf = !vol && n_bmp == 1 && !replay && !mega && wf_fused(s->S) && in->max_depth >= 1 &&
+                        in->max_depth <= 32 && !(env_bwf && !strcmp(env_bwf, "0"));
+    const bool wavefront = ((fused && in->max_depth <= 64 && !mega) || bmp_wf);
     size_t wf_ctr_words = 0, wf_chunks = 0;
     MH_HIP(hipEventRecord(s->ev0, st));
     if (wavefront) {
@@ -1067,8 +1076,11 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
         const uint32_t grid = wf_grid(wf_blocks(cus));
         const char *ec = getenv("MH_WF_CHUNK");
-        const uint64_t max_samples = std::min<uint64_t>(
+        uint64_t max_samples = std::min<uint64_t>(
             wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
+        const uint32_t n_depth = std::max<uint32_t>(1, in->max_depth - 1);
+        if (bmp_wf)  // vertex records: 48 B per path and depth; at most 8 GiB of them per chunk
+            max_samples = std::min<uint64_t>(max_samples, std::max<uint64_t>(1 << 16, (8ull << 30) / (48ull * n_depth)));
         const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
         const uint64_t cap = (uint64_t)chunk_px * S_;
         const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
@@ -1076,6 +1088,23 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         const size_t ctr_per_chunk = wf_counter_words(n_bounces);
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(cap)));
         MH_HIP(s->wf_ws_prb.alloc(wf_prb_workspace_bytes(cap)));
+        WfBitmapArgs bmp;
+        if (bmp_wf) {
+            MH_HIP(s->wf_ws_bmp.alloc(wf_bmp_workspace_bytes(cap, n_depth)));
+            int max_wg = 64 << 10, per_cu_lds = 160 << 10;
+            (void)hipDeviceGetAttribute(&max_wg, hipDeviceAttributeMaxSharedMemoryPerBlock, s->device);
+            (void)hipDeviceGetAttribute(&per_cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, s->device);
+            bmp.ws = s->wf_ws_bmp.ptr;
+            bmp.n_depth = n_depth;
+            bmp.slot = kMaxRgbParams;
+            bmp.tex = bmp_tex;
+            bmp.grad = bufs[kMaxRgbParams];
+            bmp.n_floats = (uint32_t)counts[kMaxRgbParams];
+            bmp.lds_max = (env_lds && !strcmp(env_lds, "0")) ? 0u : (uint32_t)std::min(max_wg, 64 << 10);
+            const size_t per_wg = std::max<size_t>((size_t)bmp.n_floats * 4, 1);
+            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (size_t)per_cu_lds / per_wg));
+            bmp.blocks = (uint32_t)cus * per_cu;
+        }
         MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
         MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));
         MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, (size_t)grid * kMaxRgbParams * 3 * 4, st));
@@ -1091,7 +1120,8 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                                         (uint64_t)npx * S_, L.spp_pp >= 4, g_in, w, ga.slot_of_tex, n_rgb,
                                         s->wf_ws.ptr, s->wf_ws_prb.ptr, cap,
                                         s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
-                                        s->wf_partial.as<float>(), st, &s->evpool[2 * chunk]));
+                                        s->wf_partial.as<float>(), st, &s->evpool[2 * chunk],
+                                        bmp_wf ? &bmp : nullptr));
         }
         MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
         wf_ctr_words = ctr_per_chunk;

@@ -82,12 +82,27 @@ uint32_t wf_grid(uint32_t grid);
 uint32_t wf_blocks(int cus);  // wavefront workgroups for a device of `cus` CUs
 uint32_t wf_packet_max_prims();  // largest scene (primitives) the packet engine traces
 bool wf_fused(const DScene &S);  // launch_wavefront runs the fused bounce kernel  // grid rounded to whole queue segments
+// One bitmap parameter on the fused PRB wavefront: the bounce kernel logs a
+// record per bitmap vertex, a scatter pass turns the records into texel
+// gradients once the chunk's paths have ended (mh_wavefront.hip).
+struct WfBitmapArgs {
+    void *ws = nullptr;      // wf_bmp_workspace_bytes(cap, n_depth)
+    uint32_t n_depth = 0;    // vertex records per path: max_depth - 1
+    int32_t slot = -1;       // the bitmap's gradient slot (its slot_of_tex value)
+    uint32_t tex = 0;        // its texture index
+    float *grad = nullptr;   // its gradient buffer (device)
+    uint32_t n_floats = 0;   // texels x channels
+    uint32_t lds_max = 0;    // per-workgroup LDS accumulation when n_floats * 4 <= lds_max
+    uint32_t blocks = 0;     // scatter workgroups (persistent grid)
+};
+size_t wf_bmp_workspace_bytes(uint64_t cap, uint32_t n_depth);
 hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                 uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
                                 const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
                                 uint32_t grid, float *partial, hipStream_t st,
-                                hipEvent_t *span = nullptr);  // span: 2 events around the bounce launches
+                                hipEvent_t *span = nullptr,               // span: 2 events around the bounce launches
+                                const WfBitmapArgs *bmp = nullptr);      // one bitmap parameter (or none)
 hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
                                  hipStream_t st);
 // max of a float array (gridvolume max for the majorant), as an order-preserving

@@ -1481,6 +1481,51 @@ MH_DEV void acc_add(GradCtx &g, int32_t k, V3 a) {
         if (kk == k) { g.acc[kk][0] += a.x; g.acc[kk][1] += a.y; g.acc[kk][2] += a.z; }
 }
 
+// ---------------------------------------------------------------------------
+// Texel gradients of a wave, grouped by address.  The lanes of a coherent wave
+// (the samples of one pixel at their camera vertex) add to the same few
+// texels, and same-address ds_add_f32 of one instruction serialize lane by
+// lane.  The largest group (the first pending lane's address and every lane
+// sharing it) is summed across the wave (__ockl_wfred_add_f32, a DPP
+// reduction) and added by one lane; the next group follows while groups stay
+// large (>= kGroupMin lanes), and the remaining, incoherent lanes add on their
+// own.  The whole wave must be active (the DPP reduction reads every lane:
+// measured wrong sums from the divergent replay loop), hence `on` masks.
+// ---------------------------------------------------------------------------
+extern "C" __device__ float __ockl_wfred_add_f32(float);
+typedef __attribute__((address_space(3))) float LdsFloat;
+#ifndef MH_GROUP_MIN
+#define MH_GROUP_MIN 6
+#endif
+constexpr int kGroupMin = MH_GROUP_MIN, kGroupIters = 4;
+
+template <int C>
+MH_DEV void lds_add_grouped(LdsFloat *acc, uint32_t key, bool on, const float (&v)[C]) {
+    const uint32_t me = __lane_id();
+    for (int it = 0; it < kGroupIters; ++it) {
+        const uint64_t m = __ballot(on);
+        if (m == 0) return;
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+        const uint32_t kl = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)leader);
+        const bool mine = on && key == kl;
+        if (__popcll(__ballot(mine)) < kGroupMin) break;
+        float s[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) s[c] = __ockl_wfred_add_f32(mine ? v[c] : 0.f);
+        if (me == leader) {
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                __hip_atomic_fetch_add(acc + kl + c, s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        on = on && !mine;
+    }
+    if (on) {
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            __hip_atomic_fetch_add(acc + key + c, v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
 MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3 adj, GradCtx &g) {
     int32_t k = g.slot_of_tex[tex];
     if (k < 0) return;
@@ -1508,7 +1553,7 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
 #ifdef MH_DEBUG
             assert(base + tx.channels <= g.lds_floats);
 #endif
-            typedef __attribute__((address_space(3))) float LdsFloat;
+            // (not lds_add_grouped: the replay's lanes are divergent here)
             LdsFloat *l = (LdsFloat *)(buf + base);
             if (tx.channels == 3) {
                 __hip_atomic_fetch_add(l + 0, adj.x * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

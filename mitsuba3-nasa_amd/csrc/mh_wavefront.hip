@@ -1009,10 +1009,57 @@ struct PrbGen {
     const float *grad_in;      // grad_in / W (common.py:936-965)
     int coalesce;
 };
-template <int NR, bool Gen>
-__global__ void __launch_bounds__(256, MH_BOUNCE_PRB_WAVES)
+
+// ---------------------------------------------------------------------------
+// A bitmap parameter on the fused wavefront (Bm).  Its texels differ from
+// vertex to vertex, so the A_s regrouping of the rgb slots does not apply;
+// the replay's adjoint at a bitmap vertex k (prb.py:203-248),
+//     adj_k = D_k + dL (L_total - P_k) q_k / pi,
+// D_k = the NEE term (dL em_weight beta mis cos / pi, zero when occluded),
+// q_k = cos / (rho pdf) of the sampled direction, P_k = the primal radiance
+// through vertex k (Le and Lr_dir included, as prb.py's `L - Le - Lr_dir`),
+// needs L_total, known only when the path ends.  The bounce kernel carries the
+// running radiance L, logs (P_k, uv) (q_k) (D_k) per bitmap vertex under the
+// path id, and writes (L_total, depth mask) (dL) when the path ends; after the
+// chunk's last bounce k_wf_bitmap_scatter turns the records into texel
+// gradients (bilinear taps of bitmap.cpp, per-workgroup LDS accumulator).
+// ---------------------------------------------------------------------------
+struct WfBmp {
+    float4 *fin;         // [2][stride]: (L_total, mask as bits), (dL, 0) per path id
+    float4 *rec;         // [n_depth][3][stride]: (P, uvx), (q, uvy), (D, 0) per path id
+    uint32_t *mask[2];   // per queue slot, ping-pong: depths holding a record
+    uint64_t stride;     // float4 per plane
+    uint32_t n_depth;
+    int32_t slot;        // gradient slot of the bitmap (-1: no bitmap on this launch)
+    MH_DEV float4 *r(uint32_t d, uint32_t k) const { return rec + (uint64_t)(d * 3u + k) * stride; }
+};
+
+size_t wf_bmp_workspace_bytes(uint64_t cap, uint32_t n_depth) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    return (size_t)(2 + 3 * n_depth) * align_up(cap * 16) + 2 * align_up(cap * 4);
+}
+
+static WfBmp carve_bmp(void *ws, uint64_t cap, uint32_t n_depth, int32_t slot) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    WfBmp b;
+    b.stride = align_up(cap * 16) / 16;
+    b.fin = reinterpret_cast<float4 *>(ws);
+    b.rec = b.fin + 2 * b.stride;
+    uint8_t *m = reinterpret_cast<uint8_t *>(b.rec + (uint64_t)3 * n_depth * b.stride);
+    b.mask[0] = reinterpret_cast<uint32_t *>(m);
+    b.mask[1] = reinterpret_cast<uint32_t *>(m + align_up(cap * 4));
+    b.n_depth = n_depth;
+    b.slot = slot;
+    return b;
+}
+
+#ifndef MH_BOUNCE_BMP_WAVES
+#define MH_BOUNCE_BMP_WAVES 4  // the Bm instance carries ~20 more live values across the shadow trace
+#endif
+template <int NR, bool Gen, bool Bm>
+__global__ void __launch_bounds__(256, Bm ? MH_BOUNCE_BMP_WAVES : MH_BOUNCE_PRB_WAVES)
 k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
-                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen) {
+                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen, WfBmp bm) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
     uint32_t n;
@@ -1049,6 +1096,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         Pcg rng;
         const uint32_t j = sbase + i;
         uint64_t gen_state = 0, gen_inc = 0;
+        // Bm: running radiance, this vertex's Le / potential Lr_dir / record
+        V3 Lrun = v3(0, 0, 0), Le_b = v3(0, 0, 0), Lr_pot = v3(0, 0, 0), D_pot = v3(0, 0, 0), q_ind = v3(0, 0, 0);
+        float b_uvx = 0.f, b_uvy = 0.f;
+        uint32_t vmask = 0, depth_v = 0;
+        bool bvtx = false;
         if (i < n) {
             if (Gen) {  // k_wf_raygen_prb (integrator.cpp:1139-1176, common.py:936-965)
                 pid = j;
@@ -1090,6 +1142,10 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 #pragma unroll
                     for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
                 rng.state = w.rng[cur][j];
+                if (Bm) {
+                    Lrun = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
+                    vmask = bm.mask[cur][j];
+                }
             }
             const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
             const float eta = 1.f;
@@ -1110,7 +1166,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 V3 le = v3(0, 0, 0);
                 if (active_next)
                     le = emitter_eval(S, em, si);
-                charge(acc, A, n_rgb, dL * ((beta * mis) * le));
+                const V3 Le = (beta * mis) * le;
+                charge(acc, A, n_rgb, dL * Le);
+                if (Bm) Le_b = Le;
             }
             active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
             const bool active_em0 = active_next && smooth;
@@ -1132,6 +1190,12 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             V3 rho = v3(0, 0, 0);
             if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
             const int32_t slot = smooth ? q.slot_of_tex[S.bsdf_tex[b]] : -1;
+            if (Bm) {
+                bvtx = slot >= 0 && slot == bm.slot && depth < bm.n_depth;
+                depth_v = depth;
+                b_uvx = si.uvx;
+                b_uvy = si.uvy;
+            }
             if (shadow) {  // as if unoccluded; applied after the visibility test
                 V3 wo_em = to_local(si, ds.d);
                 V3 bsdf_value_em;
@@ -1139,7 +1203,8 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 diffuse_eval_pdf(rho, si.wi, wo_em, true, bsdf_value_em, bsdf_pdf_em);
                 float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
                 V3 beta_mis_em = beta * mis_em;
-                V3 dLe = dL * ((beta_mis_em * bsdf_value_em) * em_weight);
+                const V3 Lr = (beta_mis_em * bsdf_value_em) * em_weight;
+                V3 dLe = dL * Lr;
 #pragma unroll
                 for (int kk = 0; kk < NR; ++kk) {
                     G[kk][0] = (dLe.x * (A[kk][0] * kInvPi));
@@ -1148,6 +1213,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 }
                 if (slot >= 0 && si.wi.z > 0.f && wo_em.z > 0.f)
                     add_slot(G, slot, (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi);
+                if (Bm) {
+                    Lr_pot = Lr;
+                    if (bvtx && si.wi.z > 0.f && wo_em.z > 0.f)
+                        D_pot = (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi;
+                }
             }
 
             // ---- BSDF sampling, RR (prb.py:181-278)
@@ -1171,8 +1241,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             if (rr_active) beta = beta * rcp(rr_prob);
             bool rr_continue = rng.next_float() < rr_prob;
             active_next = active_next && (!rr_active || rr_continue);
-            if (slot >= 0)
-                add_slot(A, slot, prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf));
+            if (slot >= 0) {
+                const V3 c = prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf);
+                add_slot(A, slot, c);
+                if (Bm && bvtx) q_ind = c;
+            }
             if (si.valid) depth += 1;
             alive = active_next;
         }
@@ -1197,7 +1270,8 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         }
         // ---- visibility of the NEE sample; the record is charged if unoccluded
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
-        if (shadow && sh.shape == MH_INVALID) {
+        const bool unocc = shadow && sh.shape == MH_INVALID;
+        if (unocc) {
 #pragma unroll
             for (int kk = 0; kk < NR; ++kk)
                 if ((uint32_t)kk < n_rgb) {
@@ -1206,10 +1280,102 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                     acc[kk][2] += G[kk][2];
                 }
         }
+        if (Bm && i < n) {
+            // primal state update L = (L + Le) + Lr_dir (prb.py:174-199), then the vertex record
+            Lrun = (Lrun + Le_b) + (unocc ? Lr_pot : v3(0, 0, 0));
+            const V3 D = unocc ? D_pot : v3(0, 0, 0);
+            if (bvtx && (nonzero(q_ind) || nonzero(D))) {
+                bm.r(depth_v, 0)[pid] = make_float4(Lrun.x, Lrun.y, Lrun.z, b_uvx);
+                bm.r(depth_v, 1)[pid] = make_float4(q_ind.x, q_ind.y, q_ind.z, b_uvy);
+                bm.r(depth_v, 2)[pid] = make_float4(D.x, D.y, D.z, 0.f);
+                vmask |= 1u << depth_v;
+            }
+            if (alive) {
+                w.lx[nxt][slot_n] = Lrun.x; w.ly[nxt][slot_n] = Lrun.y; w.lz[nxt][slot_n] = Lrun.z;
+                bm.mask[nxt][slot_n] = vmask;
+            } else {  // the path ends: L_total and the record mask under its id
+                bm.fin[pid] = make_float4(Lrun.x, Lrun.y, Lrun.z, __uint_as_float(vmask));
+                if (vmask) bm.fin[bm.stride + pid] = make_float4(dL.x, dL.y, dL.z, 0.f);
+            }
+        }
         n_shadow += (uint32_t)__popcll(__ballot(shadow));
     }
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
     flush_partial(acc, q);
+}
+
+// Texel gradients of the logged bitmap vertices of one chunk (see WfBmp):
+// adj_k = D_k + dL (L_total - P_k) q_k / pi per record, spread over the
+// bilinear taps (tex_backward's weights).  Item t of each 4096-path block is
+// path (t & 63) * 64 + (t >> 6) of the block, so the 64 lanes of a wave take
+// paths 64 apart -- 64 different pixels at 64 spp -- instead of the samples
+// of one pixel, whose camera vertices all land on the same texels.  InLds: a
+// persistent grid accumulating into a per-workgroup LDS copy of the texture
+// (grouped ds_add_f32), flushed once with one global atomic per non-zero
+// texel; otherwise global atomics.
+template <bool InLds>
+__global__ void __launch_bounds__(256)
+k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restrict__ grad, uint32_t n_floats) {
+    extern __shared__ uint4 lds[];
+    LdsFloat *acc = (LdsFloat *)reinterpret_cast<float *>(lds);
+    if (InLds) {
+        for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x) acc[i] = 0.f;
+        __syncthreads();
+    }
+    const DTexture tx = S.textures[tex];
+    const uint32_t full = n & ~4095u;
+    const uint32_t n_pad = (n + 63u) & ~63u;  // whole waves iterate together (grouped adds)
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_pad; t += stride) {
+        const uint32_t pid = t < full ? (t & ~4095u) | ((t & 63u) << 6) | ((t >> 6) & 63u) : t;
+        uint32_t mask = 0;
+        float4 f0 = make_float4(0.f, 0.f, 0.f, 0.f), f1 = f0;
+        if (pid < n) {
+            f0 = bm.fin[pid];
+            mask = __float_as_uint(f0.w);
+            if (mask) f1 = bm.fin[bm.stride + pid];
+        }
+        const V3 Ltot = v3(f0.x, f0.y, f0.z), dL = v3(f1.x, f1.y, f1.z);
+        while (__ballot(mask != 0)) {
+            const bool on = mask != 0;
+            const uint32_t d = on ? (uint32_t)__ffs(mask) - 1u : 0u;
+            mask &= mask - 1u;
+            V3 adj = v3(0, 0, 0);
+            float uvx = 0.f, uvy = 0.f;
+            if (on) {
+                const float4 r0 = bm.r(d, 0)[pid], r1 = bm.r(d, 1)[pid], r2 = bm.r(d, 2)[pid];
+                const V3 Lsuf = Ltot - v3(r0.x, r0.y, r0.z);  // prb.py: L - Le - Lr_dir
+                adj = v3(r2.x, r2.y, r2.z) + ((dL * Lsuf) * v3(r1.x, r1.y, r1.z)) * kInvPi;
+                uvx = r0.w;
+                uvy = r1.w;
+            }
+            Taps tp;
+            bitmap_taps(tx, uvx, uvy, tp);
+            float w4[4] = {1.f, 0.f, 0.f, 0.f};
+            if (tp.n != 1) {
+                w4[0] = tp.w0y * tp.w0x; w4[1] = tp.w0y * tp.w1x; w4[2] = tp.w1y * tp.w0x; w4[3] = tp.w1y * tp.w1x;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const bool tap = on && k < tp.n;
+                const uint32_t base = (uint32_t)(tp.idx[k] - tx.data_offset);
+                if (tx.channels == 3) {
+                    const float v[3] = {adj.x * w4[k], adj.y * w4[k], adj.z * w4[k]};
+                    if (InLds) lds_add_grouped<3>(acc, base, tap, v);
+                    else if (tap) { atomicAdd(grad + base, v[0]); atomicAdd(grad + base + 1, v[1]); atomicAdd(grad + base + 2, v[2]); }
+                } else {
+                    const float v[1] = {(adj.x + adj.y + adj.z) * w4[k]};
+                    if (InLds) lds_add_grouped<1>(acc, base, tap, v);
+                    else if (tap) atomicAdd(grad + base, v[0]);
+                }
+            }
+        }
+    }
+    if (InLds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x)
+            if (acc[i] != 0.f) atomicAdd(grad + i, acc[i]);
+    }
 }
 
 template <bool InLds, bool Packet, int NR>
@@ -1266,7 +1432,8 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 uint32_t seed_value, uint64_t n, int coalesce, const float *grad_in,
                                 const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
-                                uint32_t grid, float *partial, hipStream_t st, hipEvent_t *span) {
+                                uint32_t grid, float *partial, hipStream_t st, hipEvent_t *span,
+                                const WfBitmapArgs *bmp) {
     if (n == 0) return hipSuccess;
     if (n > (1ull << kPidBits) || n_bounces > 255 || n_rgb > (uint32_t)kMaxRgbParams) return hipErrorInvalidValue;
     WfState w = carve(ws, cap);
@@ -1278,29 +1445,32 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     const uint32_t seg_cap = seg_len(n);
     const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
     const size_t sh_fused = fused_lds_bytes(S);
+    const bool with_bmp = bmp != nullptr;
+    if (with_bmp && (!fused || bmp->n_depth > 31 || bmp->n_depth + 1 < n_bounces || !bmp->ws)) return hipErrorInvalidValue;
+    const WfBmp bm = with_bmp ? carve_bmp(bmp->ws, cap, bmp->n_depth, bmp->slot) : WfBmp{};
     if (!fused)  // the fused first bounce generates its camera rays itself
         hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                            seed_value, n, coalesce, grad_in, weights, w, q, ctr);
     const PrbGen gen{n, grad_in, coalesce};
     if (span) (void)hipEventRecord(span[0], st);
+#define MH_BOUNCE_PRB(NR, GEN, BM)                                                                             \
+    hipLaunchKernelGGL((k_wf_bounce_prb<NR, GEN, BM>), dim3(grid), dim3(256), sh_fused, st, S, in, lm, seed_value, \
+                       w, q, cur, seg_cap, c, cn, gen, bm)
+#define MH_BOUNCE_PRB_NR(GEN, BM)                                                                              \
+    do {                                                                                                       \
+        if (n_rgb <= 1) MH_BOUNCE_PRB(1, GEN, BM);                                                             \
+        else MH_BOUNCE_PRB(kMaxRgbParams, GEN, BM);                                                            \
+    } while (0)
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
-            if (n_rgb == 1) {
-                if (b == 0)
-                    hipLaunchKernelGGL((k_wf_bounce_prb<1, true>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,
-                                       seed_value, w, q, cur, seg_cap, c, cn, gen);
-                else
-                    hipLaunchKernelGGL((k_wf_bounce_prb<1, false>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,
-                                       seed_value, w, q, cur, seg_cap, c, cn, gen);
+            if (with_bmp) {
+                if (b == 0) MH_BOUNCE_PRB_NR(true, true);
+                else MH_BOUNCE_PRB_NR(false, true);
             } else {
-                if (b == 0)
-                    hipLaunchKernelGGL((k_wf_bounce_prb<kMaxRgbParams, true>), dim3(grid), dim3(256), sh_fused, st, S,
-                                       in, lm, seed_value, w, q, cur, seg_cap, c, cn, gen);
-                else
-                    hipLaunchKernelGGL((k_wf_bounce_prb<kMaxRgbParams, false>), dim3(grid), dim3(256), sh_fused, st,
-                                       S, in, lm, seed_value, w, q, cur, seg_cap, c, cn, gen);
+                if (b == 0) MH_BOUNCE_PRB_NR(true, false);
+                else MH_BOUNCE_PRB_NR(false, false);
             }
             continue;
         }
@@ -1322,6 +1492,18 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         }
         if (n_rgb == 1) MH_WF_DISPATCH_NR(k_wf_shadow_prb, 1, S, w, q, seg_cap, c);
         else MH_WF_DISPATCH_NR(k_wf_shadow_prb, kMaxRgbParams, S, w, q, seg_cap, c);
+    }
+#undef MH_BOUNCE_PRB_NR
+#undef MH_BOUNCE_PRB
+    if (with_bmp) {
+        const bool in_lds = (size_t)bmp->n_floats * 4 <= bmp->lds_max;
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->blocks, (uint32_t)((n + 255) / 256)));
+        if (in_lds)
+            hipLaunchKernelGGL(k_wf_bitmap_scatter<true>, dim3(blocks), dim3(256), (size_t)bmp->n_floats * 4, st, S,
+                               bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
+        else
+            hipLaunchKernelGGL(k_wf_bitmap_scatter<false>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S,
+                               bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
     }
     if (span) (void)hipEventRecord(span[1], st);
     return hipGetLastError();

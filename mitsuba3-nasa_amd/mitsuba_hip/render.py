@@ -238,8 +238,10 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
                     stats: Optional[A.Stats] = None, mode: str = "auto"):
     """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
     Returns a list of gradient tensors (one per key, same shape as the param).
-    mode: 'auto' (wavefront single-traversal kernels when every key is an rgb
-    constant, else the per-lane primal + adjoint replay), 'mega' (per-lane
+    mode: 'auto' (wavefront single-traversal kernels when the keys are rgb
+    constants and at most one bitmap -- a bitmap's vertices are logged and
+    scattered to its texels once the paths end -- else the per-lane primal +
+    adjoint replay), 'mega' (per-lane
     single traversal) or 'replay' (per-lane primal + adjoint replay, the
     reference's own two-pass structure)."""
     torch = _torch()

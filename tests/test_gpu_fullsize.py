@@ -119,21 +119,28 @@ def test_config3a_rgb_gradient_parity(mode):
     np.testing.assert_allclose(g, ref, rtol=1e-3)
 
 
+@pytest.mark.parametrize("mode", ["auto", "replay"])
 @pytest.mark.parametrize("lds", ["1", "0"])
-def test_config3b_bitmap_gradient_parity(lds, monkeypatch):
+def test_config3b_bitmap_gradient_parity(lds, mode, monkeypatch):
     """64x64x3 texels = 48 KiB: the per-workgroup LDS accumulator exactly at
-    its limit (lds=1), and the global-atomic path (MH_PRB_LDS_TEX=0)."""
+    its limit (lds=1), and the global-atomic path (MH_PRB_LDS_TEX=0); on the
+    fused wavefront (auto: vertex records + k_wf_bitmap_scatter, one 2^24-path
+    chunk) and on the replay megakernel (a persistent grid whose threads loop
+    over many samples)."""
     monkeypatch.setenv("MH_PRB_LDS_TEX", lds)
     mi = _mi()
     import torch
+    from mitsuba_hip import _abi as A
     scene = mi.load_dict(mi.cornell_box_bitmap(64, 512, 512, 64))
     integ = mi.load_dict({"type": "prb", "max_depth": 8})
     params = mi.traverse(scene)
     key = "white.reflectance.data"
     sg = mi.sample_tea_32(0, 1)[0]
     gi = np.random.default_rng(3).random((512, 512, 3)).astype(np.float32) / (512 * 512 * 3)
+    st = A.Stats()
     g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), [key], integ, seed=sg,
-                           spp=64)[0].cpu().numpy()
+                           spp=64, mode=mode, stats=st)[0].cpu().numpy()
+    assert st.mode == (1 if mode == "auto" else 0), st.mode
     ref = O.render_backward(scene, integ, sg, 64, gi, [params.texture_of(key)], [(64, 64, 3)])[0]
     assert g.shape == ref.shape == (64, 64, 3)
     assert (np.abs(ref) > 0).mean() > 0.9

@@ -395,12 +395,15 @@ def test_prbvolpath_grid_update_changes_majorant():
 
 
 # ---------------------------------------------------------------------------
-# PRB wrt a bitmap texture (config 3(b)): texel gradients, replay path
+# PRB wrt a bitmap texture (config 3(b)): texel gradients on the fused
+# wavefront (vertex records + scatter pass) and on the replay megakernel
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["auto", "replay"])
 @pytest.mark.parametrize("spp", [4, 16])
-def test_prb_backward_bitmap_parity(spp):
+def test_prb_backward_bitmap_parity(spp, mode):
     mi = _mi()
     import torch
+    from mitsuba_hip import _abi as A
     scene = mi.load_dict(mi.cornell_box_bitmap(tex_res=8, width=32, height=24, spp=spp))
     integ = mi.load_dict({"type": "prb", "max_depth": 6})
     params = mi.traverse(scene)
@@ -408,13 +411,46 @@ def test_prb_backward_bitmap_parity(spp):
     H, W = scene.height, scene.width
     rng = np.random.default_rng(2)
     gi = rng.random((H, W, 3)).astype(np.float32) / (H * W * 3)
-    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=13, spp=spp)
+    st = A.Stats()
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=13, spp=spp,
+                           mode=mode, stats=st)
+    assert st.mode == (1 if mode == "auto" else 0), st.mode
     ref = O.render_backward(scene, integ, 13, spp, gi, [params.texture_of(k) for k in keys],
                             [tuple(params[k].shape) for k in keys])
     for a, b in zip(g, ref):
         a = a.cpu().numpy()
         assert a.shape == b.shape
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max())
+
+
+@pytest.mark.parametrize("channels,max_depth", [(3, 3), (1, 6), (3, 12)])
+def test_prb_bitmap_wavefront_chunks(channels, max_depth, monkeypatch):
+    """Bitmap on the fused wavefront across several 4096-path chunks (the
+    vertex records and L_total are per chunk), with two rgb slots beside it
+    (the 4-slot kernel instance), a one-channel bitmap (adjoint summed over
+    r, g, b) and shallow / deep max_depth (record count max_depth - 1)."""
+    monkeypatch.setenv("MH_WF_CHUNK", "4096")
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box_bitmap(tex_res=8, width=40, height=32, spp=16)
+    if channels == 1:
+        d["white"]["reflectance"]["data"] = np.full((8, 8, 1), 0.7, np.float32)
+    scene = mi.load_dict(d)
+    integ = mi.load_dict({"type": "prb", "max_depth": max_depth})
+    params = mi.traverse(scene)
+    keys = ["red.reflectance.value", "white.reflectance.data", "green.reflectance.value"]
+    rng = np.random.default_rng(7)
+    gi = rng.random((32, 40, 3)).astype(np.float32) / (32 * 40 * 3)
+    st = A.Stats()
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=21, spp=16, stats=st)
+    assert st.mode == 1
+    ref = O.render_backward(scene, integ, 21, 16, gi, [params.texture_of(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    for k, a, b in zip(keys, g, ref):
+        a = a.cpu().numpy()
+        assert a.shape == b.shape and np.abs(b).max() > 0, k
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max(), err_msg=k)
 
 
 # ---------------------------------------------------------------------------

@@ -48,9 +48,11 @@ def main():
                           "Msamples_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 2)}), flush=True)
     sb = mi.load_dict(mi.cornell_box_bitmap(64, 512, 512, 64))
     pb = mi.traverse(sb)
-    dt = timeit(lambda: mi.render_backward(sb, pb, gi, ["white.reflectance.data"], prb, seed=sg, spp=64))
-    print(json.dumps({"config": "3(b): prb grad wrt white 64^2 bitmap, 512^2 @ 64",
-                      "Msamples_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 2)}), flush=True)
+    for mode in ("auto", "replay"):
+        dt = timeit(lambda: mi.render_backward(sb, pb, gi, ["white.reflectance.data"], prb, seed=sg, spp=64,
+                                               mode=mode))
+        print(json.dumps({"config": f"3(b): prb grad wrt white 64^2 bitmap, 512^2 @ 64 ({mode})",
+                          "Msamples_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 2)}), flush=True)
 
 
 if __name__ == "__main__":
