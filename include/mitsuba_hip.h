@@ -97,7 +97,9 @@ enum {
     MH_FLAG_NO_SYNC         = 1u << 2,  /* do not synchronise the stream before returning */
     MH_FLAG_MEGAKERNEL      = 1u << 3,  /* mh_render: force the per-lane megakernel */
     MH_FLAG_WAVEFRONT       = 1u << 4,  /* mh_render: force the wavefront (trace/shade/shadow) kernels */
-    MH_FLAG_PRB_REPLAY      = 1u << 5   /* mh_render_backward: primal + adjoint replay even for rgb params */
+    MH_FLAG_PRB_REPLAY      = 1u << 5,  /* mh_render_backward: primal + adjoint replay even for rgb params */
+    MH_FLAG_DETERMINISTIC   = 1u << 6   /* film / W-image splat as a fixed-order gather instead of float
+                                           atomics: bit-reproducible films (also env MH_DETERMINISTIC=1) */
 };
 
 /* ----------------------------------------------------------------------- */
@@ -223,7 +225,8 @@ typedef struct mh_stats {
     uint64_t n_trace_launches;  /* wavefront: number of those launches */
     uint32_t mode;              /* 0 megakernel, 1 wavefront (trace/shade/shadow), 2 wavefront fused bounce kernel,
                                    3 volpath wavefront (main / walk rounds) */
-    uint32_t pad0;
+    uint32_t invalid_samples;   /* samples with a non-finite or negative (< -1e-5) radiance channel: the
+                                   test of ImageBlock::put's warn_invalid / warn_negative (imageblock.cpp:180-204) */
 } mh_stats;
 
 typedef struct mh_scene mh_scene;   /* opaque; owns all device buffers */

@@ -16,9 +16,21 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "mh_device.hpp"
 #include "mh_internal.hpp"
 #include "mh_shading.hpp"
+
+// The reference's ProfilerPhase scopes (include/mitsuba/core/profiler.h:20-47,
+// ScopedPhase -> ITT / NVTX ranges at :81-110) as roctx ranges around the host
+// stages (rocprofv3 --marker-trace shows them beside the kernels).
+struct ScopedPhase {
+    explicit ScopedPhase(const char *name) { roctxRangePushA(name); }
+    ~ScopedPhase() { roctxRangePop(); }
+    ScopedPhase(const ScopedPhase &) = delete;
+    ScopedPhase &operator=(const ScopedPhase &) = delete;
+};
 
 using namespace mh;
 
@@ -127,6 +139,7 @@ static int require_device(int device) {
 
 
 int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scene **out) {
+    ScopedPhase phase_("InitScene");
     if (!desc || !out) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: NULL argument");
     if (desc->abi_version != MH_ABI_VERSION)
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: ABI version mismatch");
@@ -222,6 +235,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
         const char *el = getenv("MH_BVH_LEAF"), *ec = getenv("MH_BVH_CT");
         uint32_t max_leaf = el ? (uint32_t)std::max(2, std::min(31, atoi(el))) : (small ? 12u : 8u);
         float ct = ec ? (float)atof(ec) : (small ? 4.0f : 2.0f);
+        ScopedPhase accel_("InitAccel");
         build_bvh(bp, bvh, max_leaf, ct);
     }
     s->bvh_nodes = bvh.n_nodes;
@@ -606,6 +620,14 @@ static LaneMap lane_map(const Layout &L, uint32_t pixel_begin) {
     return m;
 }
 
+// counters[kCtrInvalid] of the scene's 32-word counter block: invalid samples
+constexpr int kCtrInvalid = 31;
+// MH_FLAG_DETERMINISTIC or MH_DETERMINISTIC=1: fixed-order splat (k_splat_gather)
+static bool deterministic(uint32_t flags) {
+    const char *e = getenv("MH_DETERMINISTIC");
+    return (flags & MH_FLAG_DETERMINISTIC) || (e && !strcmp(e, "1"));
+}
+
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
@@ -613,6 +635,7 @@ static double now_ms() {
 
 int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
               uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
+    ScopedPhase phase_("Render");
     if (!s || !in || !film_rgbw) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: NULL argument");
     if (in->type > MH_INTEGRATOR_PRBVOLPATH)
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: unknown integrator");
@@ -677,6 +700,8 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                             s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
     const int coalesce = L.spp_pp >= 4;
     const uint32_t seed_value = s->S.sampler_seed + seed;
+    const bool determ = deterministic(flags);
+    unsigned long long *invalid = s->counters.as<unsigned long long>() + kCtrInvalid;
     float kernel_ms = 0.f, trace_ms = 0.f;
     const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
     const uint32_t n_bounces = wavefront ? in->max_depth : 0;
@@ -706,6 +731,8 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         uint64_t n = (uint64_t)npx * S_;
         hipEvent_t *ev = &s->evpool[ev_per_chunk * chunk];
         MH_HIP(hipEventRecord(ev[0], st));
+        {
+        ScopedPhase sample_("SamplingIntegratorSample");
         if (wavefront) {
             MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
                                     s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
@@ -722,17 +749,19 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
             MH_HIP(launch_render(s->S, *in, lm, seed_value, L.n_passes, n, plane, s->work.as<float>(),
                                  s->counters.as<unsigned long long>(), st, alpha));
         }
+        }
         MH_HIP(hipEventRecord(ev[1], st));
+        ScopedPhase put_("ImageBlockPut");
         MH_HIP(launch_splat(s->S, lm, kSplatFilm, fast_splat, npx, L.n_passes, n, plane,
-                            s->work.as<float>(), film4, seed_value, coalesce, st));
+                            s->work.as<float>(), film4, seed_value, coalesce, st, invalid, determ));
         if (alpha)
             MH_HIP(launch_splat(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane,
-                                s->work.as<float>(), film_a, seed_value, coalesce, st));
+                                s->work.as<float>(), film_a, seed_value, coalesce, st, nullptr, determ));
     }
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
-    unsigned long long ctr[2] = {0, 0};
+    unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
     std::vector<uint32_t> wctr;
     if (wavefront) {
         wctr.resize(ctr_per_chunk * n_chunks);
@@ -740,6 +769,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     } else {
         MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     }
+    MH_HIP(hipMemcpyAsync(&n_invalid, invalid, sizeof(n_invalid), hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));  // the stats counters are read back
     for (size_t c = 0; c < n_chunks; ++c) {
         hipEvent_t *ev = &s->evpool[ev_per_chunk * c];
@@ -799,12 +829,14 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         stats->ms_trace = trace_ms;
         stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces * L.n_passes : 0;
         stats->mode = wavefront ? (wf_fused(s->S) ? 2u : 1u) : volwave ? 3u : 0u;
+        stats->invalid_samples = (uint32_t)std::min<unsigned long long>(n_invalid, 0xffffffffull);
     }
     return MH_OK;
 }
 
 int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                       uint32_t spp_begin, uint32_t spp_end, float *out, uint32_t flags) {
+    ScopedPhase phase_("Render");
     if (!s || !in || !out) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_samples: NULL argument");
     if (in->type > MH_INTEGRATOR_PRBVOLPATH)
         return set_error(MH_ERR_UNSUPPORTED, "mh_render_samples: unsupported integrator");
@@ -886,6 +918,7 @@ int mh_develop(mh_scene *s, const float *film_rgbw, float *image_rgb, uint32_t f
 // ---------------------------------------------------------------------------
 int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
                    float *weights, uint32_t flags) {
+    ScopedPhase phase_("ImageBlockPut");
     if (!s || !weights) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: NULL argument");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: spp must be > 0");
     Layout L;
@@ -905,7 +938,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     LaneMap lm = lane_map(L, 0);
     const uint32_t S_ = L.s_end - L.s_begin;
     MH_HIP(launch_splat(s->S, lm, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w,
-                        s->S.sampler_seed + seed, L.spp_pp >= 4, st));
+                        s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr, deterministic(flags)));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
@@ -916,6 +949,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                        uint32_t spp_begin, uint32_t spp_end, const float *grad_in,
                        const float *weights, uint32_t n_params, const uint32_t *param_tex,
                        float *const *grads, uint32_t flags, mh_stats *stats) {
+    ScopedPhase phase_("RenderBackward");
     if (!s || !in || !grad_in || (n_params && (!param_tex || !grads)))
         return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: NULL argument");
     if (in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_PRBVOLPATH)
@@ -1039,7 +1073,8 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         Lall.s_end = L.spp_pp;
         LaneMap lmw = lane_map(Lall, 0);
         MH_HIP(launch_splat(s->S, lmw, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
-                            s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st));
+                            s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr,
+                            deterministic(flags)));
         w = s->weights_tmp.as<float>();
     } else if (!dev) {
         MH_HIP(s->tmp_e.alloc(n_px * 4));
@@ -1189,6 +1224,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
 static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, float *t, float *u,
                       float *v, uint32_t *prim, uint32_t *shape, uint32_t *inst, uint32_t *occ, uint32_t flags,
                       mh_stats *stats) {
+    ScopedPhase phase_("RayIntersect");
     if (!s || (n && !rays)) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace: NULL argument");
     if (n == 0) return MH_OK;
     double t_start = now_ms();

@@ -63,10 +63,13 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
 // splat modes: RGBW film from (L, pos) planes; W image from the RNG jitter;
 // alpha channel from (alpha, pos) planes (plane 5)
 enum { kSplatFilm = 0, kSplatWeights = 1, kSplatAlpha = 2 };
+// invalid: counts samples with a non-finite or negative radiance channel
+// (mode 0; ImageBlock::put's warn_invalid / warn_negative test); deterministic:
+// the fast path as a fixed-order gather (k_splat_gather) instead of atomics
 hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
-                        hipStream_t st);
+                        hipStream_t st, unsigned long long *invalid = nullptr, bool deterministic = false);
 hipError_t launch_film_rgbaw(uint64_t n_px, const float *rgbw, const float *a, float *out, hipStream_t st);
 size_t wf_workspace_bytes(uint64_t cap);
 uint32_t wf_counter_words(uint32_t n_bounces);

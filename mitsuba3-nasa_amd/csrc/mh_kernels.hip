@@ -166,11 +166,21 @@ MH_DEV float row16_sum(float x) {
     return x;
 }
 
+// ImageBlock::put's sample check (imageblock.cpp:180-204: warn_negative
+// `v >= -1e-5`, warn_invalid `isfinite(v)`), counted instead of logged
+MH_DEV bool sample_invalid(const float *v) {
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) bad = bad || !(v[c] >= -1e-5f) || !isfinite(v[c]);
+    return bad;
+}
+
 template <int Mode>
 __global__ void __launch_bounds__(128)
 k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t n_passes,
            uint64_t n, uint64_t plane, const float *__restrict__ in, float *__restrict__ film,
-           uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin) {
+           uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin, unsigned long long *__restrict__ invalid) {
+    uint32_t n_bad = 0;
     const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t pl = gl / kSplatLanes, g = gl % kSplatLanes;
     if (pl >= n_pix) return;  // whole DPP rows leave together (n_pix granularity = 16 lanes)
@@ -207,6 +217,7 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
                 vals[3] = 1.f;
                 sx = nv[3];
                 sy = nv[4];
+                n_bad += sample_invalid(vals) ? 1u : 0u;
                 const uint32_t jn = j + kSplatLanes;
                 if (jn < Sn) {
 #pragma unroll
@@ -272,6 +283,7 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
                 }
         }
     }
+    if (Mode == 0 && invalid && n_bad) atomicAdd(invalid, (unsigned long long)n_bad);  // rare: no reduction
 #pragma unroll
     for (int ys = 0; ys < 5; ++ys)
 #pragma unroll
@@ -298,13 +310,97 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
     }
 }
 
+// sample check of a chunk's (L, pos) planes for the deterministic splat
+__global__ void k_count_invalid(uint64_t total, uint64_t n, uint64_t plane, const float *__restrict__ in,
+                                unsigned long long *__restrict__ invalid) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const float v[3] = {in[i], in[plane + i], in[2 * plane + i]};  // sample (k, pass) at pass * n + k
+    if (sample_invalid(v)) atomicAdd(invalid, 1ull);
+}
+
+// Deterministic splat (MH_FLAG_DETERMINISTIC / MH_DETERMINISTIC=1; the
+// ordered-reduction build of SURVEY.md §5): every film pixel of the rows a
+// chunk can reach gathers, in a fixed order (source row, source column,
+// pass, sample), the weighted values of the chunk's samples whose coalesced
+// footprint covers it, and adds the sum once.  A sample's footprint starts at
+// floor(pos) - 2 and floor(pos) is its pixel or, when the jitter rounds up,
+// the next one, so the sources of pixel o are the pixels o - 3 .. o + 2.
+// Each contribution is the scatter's own `value * (wx * wy)`; only the
+// summation order differs from k_splat_px, and it no longer depends on
+// scheduling, so the film is bit-reproducible from run to run.
+template <int Mode>
+__global__ void __launch_bounds__(256)
+k_splat_gather(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row0, uint32_t n_rows, uint32_t Sn,
+               uint32_t n_passes, uint64_t n, uint64_t plane, const float *__restrict__ in,
+               float *__restrict__ film, uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin) {
+    const uint32_t W = S.width, H = S.height;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n_rows * W) return;
+    const int32_t oy = (int32_t)(row0 + t / W), ox = (int32_t)(t % W);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int32_t qy = oy - 3; qy <= oy + 2; ++qy) {
+        if (qy < 0 || qy >= (int32_t)H) continue;
+        for (int32_t qx = ox - 3; qx <= ox + 2; ++qx) {
+            if (qx < 0 || qx >= (int32_t)W) continue;
+            const uint32_t q = (uint32_t)qy * W + (uint32_t)qx;
+            if (q < pixel_begin || q - pixel_begin >= n_pix) continue;
+            const uint32_t pl = q - pixel_begin;
+            for (uint32_t pass = 0; pass < n_passes; ++pass) {
+                const float *src = in + (uint64_t)pass * n + (uint64_t)pl * Sn;
+                for (uint32_t j = 0; j < Sn; ++j) {
+                    float sx, sy, vals[4];
+                    if (Mode == 1) {
+                        Pcg rng;
+                        rng.seed(seed_value, q * spp_pp + s_begin + j);
+                        sx = (float)qx + rng.next_float();
+                        sy = (float)qy + rng.next_float();
+                        vals[0] = vals[1] = vals[2] = 0.f;
+                        vals[3] = 1.f;
+                    } else {
+                        sx = src[3 * plane + j];
+                        sy = src[4 * plane + j];
+                        if (Mode == 0) {
+                            vals[0] = src[j]; vals[1] = src[plane + j]; vals[2] = src[2 * plane + j]; vals[3] = 1.f;
+                        } else {
+                            vals[0] = vals[1] = vals[2] = 0.f;
+                            vals[3] = src[5 * plane + j];
+                        }
+                    }
+                    const int32_t p0x = (int32_t)floorf(sx) - 2, p0y = (int32_t)floorf(sy) - 2;
+                    const int32_t dx = ox - p0x, dy = oy - p0y;
+                    if (dx < 0 || dx > 4 || dy < 0 || dy > 4) continue;
+                    const float relx = ((float)p0x + 0.5f) - sx, rely = ((float)p0y + 0.5f) - sy;
+                    const float w = gaussian_eval(S.filter_coeff, relx + (float)dx) *
+                                    gaussian_eval(S.filter_coeff, rely + (float)dy);
+                    if (Mode == 0) {
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) acc[c] += vals[c] * w;
+                    } else {
+                        acc[3] += vals[3] * w;
+                    }
+                }
+            }
+        }
+    }
+    const uint64_t o = (uint64_t)oy * W + (uint32_t)ox;
+    if (Mode == 0) {
+        float4 *f = reinterpret_cast<float4 *>(film) + o;
+        float4 v = *f;
+        v.x += acc[0]; v.y += acc[1]; v.z += acc[2]; v.w += acc[3];
+        *f = v;
+    } else {
+        film[o] += acc[3];
+    }
+}
+
 // Generic per-sample splat (box filter / non-coalesced spp < 4 / other radii)
 // — ImageBlock::put (imageblock.cpp:210-233, 264-409, 418-531)
 template <int Mode>
 __global__ void __launch_bounds__(256)
 k_splat_generic(DScene S, LaneMap lm, uint32_t n_passes, uint64_t n, uint64_t plane,
                 const float *__restrict__ in, float *__restrict__ film, uint32_t seed_value,
-                int coalesce) {
+                int coalesce, unsigned long long *__restrict__ invalid) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint32_t W = S.width, H = S.height;
@@ -319,6 +415,7 @@ k_splat_generic(DScene S, LaneMap lm, uint32_t n_passes, uint64_t n, uint64_t pl
             uint64_t o = (uint64_t)pass * n + k;
             vals[0] = in[o]; vals[1] = in[plane + o]; vals[2] = in[2 * plane + o]; vals[3] = 1.f;
             px = in[3 * plane + o]; py = in[4 * plane + o];
+            if (invalid && sample_invalid(vals)) atomicAdd(invalid, 1ull);
         } else if (Mode == 2) {
             uint64_t o = (uint64_t)pass * n + k;
             vals[0] = in[5 * plane + o];
@@ -598,15 +695,30 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
 hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
-                        hipStream_t st) {
+                        hipStream_t st, unsigned long long *invalid, bool deterministic) {
     if (n == 0) return hipSuccess;
 #define MH_SPLAT_PX(M)                                                                                          \
     hipLaunchKernelGGL(k_splat_px<M>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S, lm.pixel_begin, n_pix, \
-                       lm.S, n_passes, n, plane, in, film, seed_value, lm.spp_pp, lm.s_begin)
+                       lm.S, n_passes, n, plane, in, film, seed_value, lm.spp_pp, lm.s_begin, invalid)
 #define MH_SPLAT_GEN(M)                                                                                         \
     hipLaunchKernelGGL(k_splat_generic<M>, dim3(blocks_for(n, bs)), dim3(bs), 0, st, S, lm, n_passes, n, plane, \
-                       in, film, seed_value, coalesce)
-    if (fast) {
+                       in, film, seed_value, coalesce, invalid)
+#define MH_SPLAT_GATHER(M)                                                                                      \
+    hipLaunchKernelGGL(k_splat_gather<M>, dim3(blocks_for((uint64_t)n_rows * S.width, 256)), dim3(256), 0, st, S, \
+                       lm.pixel_begin, n_pix, row0, n_rows, lm.S, n_passes, n, plane, in, film, seed_value,      \
+                       lm.spp_pp, lm.s_begin)
+    if (fast && deterministic) {
+        // film rows the chunk's footprints reach: its first row - 2 .. its last row + 3
+        const uint32_t r_first = lm.pixel_begin / S.width, r_last = (lm.pixel_begin + n_pix - 1) / S.width;
+        const uint32_t row0 = r_first >= 2 ? r_first - 2 : 0, row1 = std::min<uint32_t>(S.height - 1, r_last + 3);
+        const uint32_t n_rows = row1 - row0 + 1;
+        if (mode == kSplatWeights) MH_SPLAT_GATHER(1);
+        else if (mode == kSplatAlpha) MH_SPLAT_GATHER(2);
+        else MH_SPLAT_GATHER(0);
+        if (mode == kSplatFilm && invalid)  // the sample check of the atomic path, counted by the generic kernel's rule
+            hipLaunchKernelGGL(k_count_invalid, dim3(blocks_for(n * n_passes, 256)), dim3(256), 0, st, n * n_passes,
+                               n, plane, in, invalid);
+    } else if (fast) {
         const uint32_t bs = 128;
         const uint64_t lanes = (uint64_t)n_pix * kSplatLanes;
         if (mode == kSplatWeights) MH_SPLAT_PX(1);
@@ -620,6 +732,7 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
     }
 #undef MH_SPLAT_PX
 #undef MH_SPLAT_GEN
+#undef MH_SPLAT_GATHER
     return hipGetLastError();
 }
 

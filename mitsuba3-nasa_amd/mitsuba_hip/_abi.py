@@ -57,6 +57,7 @@ FLAG_NO_SYNC = 1 << 2
 FLAG_MEGAKERNEL = 1 << 3
 FLAG_WAVEFRONT = 1 << 4
 FLAG_PRB_REPLAY = 1 << 5
+FLAG_DETERMINISTIC = 1 << 6
 
 u32, u64, f32, f64 = C.c_uint32, C.c_uint64, C.c_float, C.c_double
 PF = C.POINTER(C.c_float)
@@ -120,7 +121,7 @@ class Integrator(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("samples", u64), ("rays_closest", u64), ("rays_shadow", u64), ("bounces", u64),
                 ("ms_total", f64), ("ms_kernel", f64), ("ms_trace", f64), ("n_trace_launches", u64),
-                ("mode", u32), ("pad0", u32)]
+                ("mode", u32), ("invalid_samples", u32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -170,9 +170,12 @@ def traverse(scene: Scene, device=None) -> SceneParameters:
 # ---------------------------------------------------------------------------
 def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                 spp_begin: int = 0, spp_end: int = 0, device=None, film=None, accumulate=False,
-                stats: Optional[A.Stats] = None, mode: str = "auto"):
+                stats: Optional[A.Stats] = None, mode: str = "auto", deterministic: bool = False):
     """Integrator::render(develop=False): RGBW film (H, W, 4) on the device.
-    mode: 'auto' (wavefront for `path`), 'mega' (per-lane megakernel) or 'wavefront'."""
+    mode: 'auto' (wavefront for `path`), 'mega' (per-lane megakernel) or 'wavefront'.
+    deterministic: splat as a fixed-order gather (bit-reproducible film) instead
+    of float atomics.  stats.invalid_samples counts samples with a non-finite
+    or negative channel (ImageBlock::put's warn_invalid / warn_negative test)."""
     torch = _torch()
     dev = _device_index(device)
     integrator = integrator or scene.integrator()
@@ -183,6 +186,7 @@ def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int
                            dtype=torch.float32, device=f"cuda:{dev}")
     flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_ACCUMULATE if accumulate else 0)
     flags |= {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "wavefront": A.FLAG_WAVEFRONT}[mode]
+    flags |= A.FLAG_DETERMINISTIC if deterministic else 0
     ic = integrator.c()
     A.check(A.lib().mh_render(h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(film), flags,
                               C.byref(stats) if stats is not None else None))
@@ -199,12 +203,13 @@ def develop(scene: Scene, film, device=None):
     return out
 
 
-def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, device=None):
+def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, device=None, deterministic=False):
     torch = _torch()
     dev = _device_index(device)
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
     w = torch.empty((scene.height, scene.width), dtype=torch.float32, device=f"cuda:{dev}")
-    A.check(A.lib().mh_prb_weights(h, seed, spp, spp_begin, spp_end, _ptr(w), A.FLAG_DEVICE_POINTERS))
+    A.check(A.lib().mh_prb_weights(h, seed, spp, spp_begin, spp_end, _ptr(w),
+                                   A.FLAG_DEVICE_POINTERS | (A.FLAG_DETERMINISTIC if deterministic else 0)))
     return w
 
 
