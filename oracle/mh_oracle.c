@@ -998,8 +998,19 @@ static inline float emitter_hit_pdf(const mh_scene_desc *d, uint32_t em, const s
 /* PathIntegrator::sample, JIT semantics (src/integrators/path.cpp:95-287)  */
 /* counters: [0] closest rays, [1] shadow rays, [2] lane-bounces            */
 /* ------------------------------------------------------------------------ */
+/* scalar != 0: the scalar_rgb control flow (config 1): dr::none_or<false>
+   breaks the loop before the emitter / BSDF / RR draws when the path cannot
+   continue (path.cpp:179-180), and dr::any_or<true> skips the emitter draw
+   when emitter sampling is inactive (path.cpp:193-196); in JIT both are
+   taken (every lane active at the loop head draws 6 floats) */
+static v3 path_sample_mode(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
+                           int *valid_out, uint64_t *counters, int scalar);
 static v3 path_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
                       int *valid_out, uint64_t *counters) {
+    return path_sample_mode(sv, in, rng, ray, valid_out, counters, 0);
+}
+static v3 path_sample_mode(const scene_view *sv, const mh_integrator *in, pcg32 *rng, ray3 ray,
+                           int *valid_out, uint64_t *counters, int scalar) {
     const mh_scene_desc *d = sv->d;
     if (in->max_depth == 0) { *valid_out = 0; return V3(0, 0, 0); }
     v3 throughput = V3(1, 1, 1), result = V3(0, 0, 0);
@@ -1028,12 +1039,14 @@ static v3 path_sample(const scene_view *sv, const mh_integrator *in, pcg32 *rng,
         }
 
         int active_next = (depth + 1 < in->max_depth) && si.valid;
+        if (scalar && !active_next) break; /* path.cpp:179-180 (scalar early exit) */
         uint32_t b = si_bsdf(d, &si);
         int smooth = b != MH_INVALID && d->bsdfs[b].type == MH_BSDF_DIFFUSE;
         int active_em = active_next && smooth;
 
         /* ---- emitter sampling (path.cpp:187-208) ---- */
-        float e0 = pcg_float(rng), e1 = pcg_float(rng);
+        float e0 = 0.f, e1 = 0.f;
+        if (!scalar || active_em) { e0 = pcg_float(rng); e1 = pcg_float(rng); }
         dir_sample ds;
         memset(&ds, 0, sizeof(ds));
         v3 em_weight = V3(0, 0, 0), wo = V3(0, 0, 0);
@@ -2119,6 +2132,143 @@ int oracle_sample_range(const mh_scene_desc *desc, const mh_integrator *integ, u
     }
     scene_view_free(&sv);
     return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* scalar_rgb render (BASELINE config 1, the reference's CPU case):          */
+/* SamplingIntegrator::render's non-JIT branch (src/render/integrator.cpp:   */
+/* 189-275) and render_block (:1099-1124).  Blocks of block_size^2 pixels in */
+/* the order of Spiral::next_block (src/render/spiral.cpp:17-70); block b    */
+/* seeds pixel i (Morton order inside the block) with                       */
+/*   seed * W * H + b * block_size^2 + i                                     */
+/* through PCG32Sampler::seed's scalar branch (sampler.cpp:128-131: PCG32    */
+/* initstate = base_seed + seed, initseq = PCG32_DEFAULT_STREAM) and draws   */
+/* the pixel's spp samples from that one stream (advance() only resets the   */
+/* dimension).  The `path` loop takes the scalar control flow               */
+/* (path_sample_mode), and the block splats with the non-coalesced filter    */
+/* (coalesce = is_jit = false, hdrfilm.cpp:282-290).  The reference's        */
+/* block_size shrinks from 32 until there is a block per thread             */
+/* (integrator.cpp:200-211): pass the value its run used.                   */
+/* ------------------------------------------------------------------------ */
+#define PCG32_DEFAULT_STREAM 0xda3e39cb94b95bdbull
+
+static uint32_t morton_compact1(uint32_t v) { /* bits 0, 2, 4, ... -> 0, 1, 2, ... */
+    v &= 0x55555555u;
+    v = (v | (v >> 1)) & 0x33333333u;
+    v = (v | (v >> 2)) & 0x0f0f0f0fu;
+    v = (v | (v >> 4)) & 0x00ff00ffu;
+    v = (v | (v >> 8)) & 0x0000ffffu;
+    return v;
+}
+
+/* block positions (in blocks) of Spiral::next_block for one pass */
+static uint32_t spiral_order(uint32_t bw, uint32_t bh, uint32_t *bx, uint32_t *by) {
+    const uint32_t count = bw * bh;
+    int32_t px = (int32_t)(bw / 2), py = (int32_t)(bh / 2);
+    int dir = 0; /* Right, Down, Left, Up */
+    uint32_t steps_left = 1, spiral_size = 1;
+    for (uint32_t k = 0; k < count; ++k) {
+        bx[k] = (uint32_t)px;
+        by[k] = (uint32_t)py;
+        if (k + 1 == count) break;
+        do {
+            switch (dir) {
+                case 0: ++px; break;
+                case 1: ++py; break;
+                case 2: --px; break;
+                default: --py; break;
+            }
+            if (--steps_left == 0) {
+                dir = (dir + 1) % 4;
+                if (dir == 2 || dir == 0) ++spiral_size;
+                steps_left = spiral_size;
+            }
+        } while (px < 0 || py < 0 || px >= (int32_t)bw || py >= (int32_t)bh);
+    }
+    return count;
+}
+
+typedef struct {
+    const scene_view *sv;
+    const mh_integrator *in;
+    uint32_t seed, spp, block_size, n_blocks;
+    const uint32_t *bx, *by;
+    uint32_t *next;         /* shared block counter */
+    pthread_mutex_t *lock;
+    float *film;            /* this worker's full RGBW film */
+} scalar_job;
+
+static void *scalar_worker(void *arg) {
+    scalar_job *j = (scalar_job *)arg;
+    const mh_scene_desc *d = j->sv->d;
+    const mh_sensor *s = &d->sensor;
+    const uint32_t W = s->width, H = s->height, bs = j->block_size, pc = bs * bs;
+    film_band band = {j->film, W, H, 0, H, 4};
+    for (;;) {
+        pthread_mutex_lock(j->lock);
+        const uint32_t b = (*j->next)++;
+        pthread_mutex_unlock(j->lock);
+        if (b >= j->n_blocks) break;
+        const uint32_t ox = j->bx[b] * bs, oy = j->by[b] * bs;
+        const uint32_t sw = W - ox < bs ? W - ox : bs, sh = H - oy < bs ? H - oy : bs;
+        const uint32_t seed_b = j->seed * (W * H) + b * pc; /* integrator.cpp:230, :1103 */
+        for (uint32_t i = 0; i < pc; ++i) {
+            const uint32_t lx = morton_compact1(i), ly = morton_compact1(i >> 1);
+            if (lx >= sw || ly >= sh) continue;
+            pcg32 rng;
+            pcg_seed(&rng, (uint64_t)(uint32_t)(s->sampler_seed + seed_b + i), PCG32_DEFAULT_STREAM);
+            const uint32_t px = ox + lx, py = oy + ly;
+            for (uint32_t k = 0; k < j->spp; ++k) {
+                const float jx = pcg_float(&rng), jy = pcg_float(&rng);
+                const float sx = (float)px + jx, sy = (float)py + jy;
+                ray3 r = camera_ray(s, fmaf(sx, inv_size(W), -0.f), fmaf(sy, inv_size(H), -0.f));
+                int valid;
+                v3 l = path_sample_mode(j->sv, j->in, &rng, r, &valid, NULL, 1);
+                const float vals[4] = {l.x, l.y, l.z, 1.f};
+                splat(s, &band, sx, sy, vals, 0);
+            }
+        }
+    }
+    return NULL;
+}
+
+int oracle_render_scalar(const mh_scene_desc *desc, const mh_integrator *integ, uint32_t seed,
+                         uint32_t spp, uint32_t block_size, int n_threads, float *film_rgbw) {
+    if (integ->type != MH_INTEGRATOR_PATH) return fail("oracle_render_scalar: the 'path' integrator only");
+    if (fmt_alpha(desc->sensor.pixel_format)) return fail("oracle_render_scalar: rgb films only");
+    if (block_size == 0 || (block_size & (block_size - 1))) return fail("oracle_render_scalar: block_size must be a power of two");
+    scene_view sv;
+    if (scene_view_init(&sv, desc)) return 1;
+    if (spp == 0) spp = desc->sensor.sample_count;
+    const uint32_t W = desc->sensor.width, H = desc->sensor.height;
+    const uint32_t bw = (W + block_size - 1) / block_size, bh = (H + block_size - 1) / block_size;
+    uint32_t *bx = (uint32_t *)malloc(sizeof(uint32_t) * bw * bh), *by = (uint32_t *)malloc(sizeof(uint32_t) * bw * bh);
+    const uint32_t nb = spiral_order(bw, bh, bx, by);
+    if (n_threads < 1) n_threads = 1;
+    float *films = (float *)calloc((size_t)n_threads * W * H * 4, sizeof(float));
+    scalar_job *jobs = (scalar_job *)calloc((size_t)n_threads, sizeof(scalar_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
+    uint32_t next = 0;
+    for (int t = 0; t < n_threads; ++t) {
+        scalar_job *j = &jobs[t];
+        j->sv = &sv; j->in = integ; j->seed = seed; j->spp = spp; j->block_size = block_size;
+        j->n_blocks = nb; j->bx = bx; j->by = by; j->next = &next; j->lock = &lock;
+        j->film = films + (size_t)t * W * H * 4;
+        pthread_create(&th[t], NULL, scalar_worker, j);
+    }
+    for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
+    memset(film_rgbw, 0, sizeof(float) * (size_t)W * H * 4);
+    for (int t = 0; t < n_threads; ++t)
+        for (size_t i = 0; i < (size_t)W * H * 4; ++i) film_rgbw[i] += films[(size_t)t * W * H * 4 + i];
+    free(films); free(jobs); free(th); free(bx); free(by);
+    scene_view_free(&sv);
+    return 0;
+}
+
+/* the block order itself, for tests (block positions in units of blocks) */
+uint32_t oracle_spiral_order(uint32_t bw, uint32_t bh, uint32_t *bx, uint32_t *by) {
+    return spiral_order(bw, bh, bx, by);
 }
 
 /* ---- threaded film renderer (row bands, deterministic merge) ---- */

@@ -54,6 +54,10 @@ def lib():
     L.oracle_render_backward.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32,
                                          C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint32,
                                          vp, C.POINTER(C.c_void_p), C.c_int]
+    L.oracle_render_scalar.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32, C.c_uint32,
+                                       C.c_uint32, C.c_int, vp]
+    L.oracle_spiral_order.restype = C.c_uint32
+    L.oracle_spiral_order.argtypes = [C.c_uint32, C.c_uint32, vp, vp]
     L.oracle_last_error.restype = C.c_char_p
     _lib = L
     return L
@@ -88,6 +92,25 @@ def render(scene, integrator=None, seed=0, spp=0, spp_begin=0, spp_end=0, thread
     check(lib().oracle_render(C.byref(scene.desc), C.byref(ic), seed, spp or scene.sample_count(),
                               spp_begin, spp_end, threads or nthreads(), _p(film)))
     return film
+
+
+def render_scalar(scene, integrator=None, seed=0, spp=0, block_size=32, threads=None):
+    """scalar_rgb render (config 1): spiral blocks, per-pixel Morton-order
+    PCG32 seeding and the scalar `path` control flow
+    (integrator.cpp:189-275, 1099-1124; path.cpp:179-196)."""
+    integrator = integrator or scene.integrator()
+    film = np.zeros((scene.height, scene.width, 4), np.float32)
+    ic = integrator.c()
+    check(lib().oracle_render_scalar(C.byref(scene.desc), C.byref(ic), seed, spp or scene.sample_count(),
+                                     block_size, threads or nthreads(), _p(film)))
+    return film
+
+
+def spiral_order(bw, bh):
+    bx = np.zeros(bw * bh, np.uint32)
+    by = np.zeros(bw * bh, np.uint32)
+    n = lib().oracle_spiral_order(bw, bh, _p(bx), _p(by))
+    return list(zip(bx[:n].tolist(), by[:n].tolist()))
 
 
 def develop(film, pixel_format=0):
