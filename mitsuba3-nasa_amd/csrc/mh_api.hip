@@ -101,6 +101,7 @@ struct mh_scene {
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     DevBuf wf_ws_bmp;  // wavefront PRB with a bitmap parameter: vertex records (WfBmp)
+    DevBuf pvp_log;    // prbvolpath backward: per-thread NEE-walk step logs (NeeLog)
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     std::vector<mh_medium> h_media;
@@ -461,7 +462,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->pvp_log})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -622,6 +623,11 @@ static LaneMap lane_map(const Layout &L, uint32_t pixel_begin) {
 
 // counters[kCtrInvalid] of the scene's 32-word counter block: invalid samples
 constexpr int kCtrInvalid = 31;
+// counters[kCtrPvpHead]: work head of the persistent prbvolpath backward
+constexpr int kCtrPvpHead = 30;
+// prbvolpath backward grid (MH_VOL_WAVES = 4 waves / SIMD: 4 workgroups per CU)
+// and NEE-log entries per thread (16 B each; longer walks replay)
+constexpr uint32_t kPvpBlocksPerCu = 4, kPvpNeeCap = 256;
 // MH_FLAG_DETERMINISTIC or MH_DETERMINISTIC=1: fixed-order splat (k_splat_gather)
 static bool deterministic(uint32_t flags) {
     const char *e = getenv("MH_DETERMINISTIC");
@@ -1101,6 +1107,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     // scatter pass charges the texels (WfBmp, mh_wavefront.hip) -- packet-engine
     // scenes, max_depth <= 32 (MH_PRB_BMP_WF=0: the replay megakernel)
     const char *env_bwf = getenv("MH_PRB_BMP_WF");
+    const char *env_pvl = getenv("MH_PVP_NEE_LOG");  // 0: prbvolpath replays its NEE walks (no log)
     const bool bmp_wf = !vol && n_bmp == 1 && !replay && !mega && wf_fused(s->S) && in->max_depth >= 1 &&
                         in->max_depth <= 32 && !(env_bwf && !strcmp(env_bwf, "0"));
     const bool wavefront = ((fused && in->max_depth <= 64 && !mega) || bmp_wf);
@@ -1161,6 +1168,18 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
         wf_ctr_words = ctr_per_chunk;
         wf_chunks = n_chunks;
+    } else if (vol && !(env_pvl && !strcmp(env_pvl, "0"))) {
+        // prbvolpath: persistent grid, one NEE-walk log per thread (NeeLog)
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+        const char *ecap = getenv("MH_PVP_NEE_CAP");  // tests: small logs exercise the replay fallback
+        const uint32_t blocks = (uint32_t)cus * kPvpBlocksPerCu,
+                       cap = ecap ? (uint32_t)std::max(1, atoi(ecap)) : kPvpNeeCap;
+        MH_HIP(s->pvp_log.alloc((size_t)blocks * 256 * cap * 16));
+        MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
+                                   g_in, w, ga, fused, s->counters.as<unsigned long long>(), st,
+                                   s->pvp_log.as<float4>(), cap, blocks,
+                                   s->counters.as<unsigned long long>() + kCtrPvpHead));
     } else {
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));

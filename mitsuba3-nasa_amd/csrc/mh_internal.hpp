@@ -126,7 +126,11 @@ hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
                                const float *grad_in, const float *weights, const GradArgs &ga,
-                               bool fused, unsigned long long *counters, hipStream_t st);
+                               bool fused, unsigned long long *counters, hipStream_t st,
+                               // prbvolpath: NEE-walk logs ([cap][nee_blocks * 256] float4) on a
+                               // persistent grid of nee_blocks pulling work from *head (nullptr: none)
+                               float4 *nee_log = nullptr, uint32_t nee_cap = 0, uint32_t nee_blocks = 0,
+                               unsigned long long *head = nullptr);
 // wavefront volpath (mh_volwave.hip): k_vw_main / k_vw_walk rounds
 uint64_t vw_max_chunk();
 size_t vw_workspace_bytes(uint64_t cap);

@@ -614,28 +614,56 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
 
 // prbvolpath backward: dL gather + primal + adjoint replay per lane
 // (RBIntegrator.render_backward, common.py:900-983, with prbvolpath.sample)
+// PvpWork: a persistent grid (one NEE log region per thread) pulling
+// 64-sample batches per wave from an atomic head; log == nullptr: one thread
+// per sample, adjoint NEE walks replayed
+struct PvpWork {
+    float4 *log;                  // [cap][threads] NeeLog entries
+    uint32_t cap;
+    unsigned long long *head;     // work counter (zeroed by the launcher)
+};
+
 template <bool InLds>
 __global__ void __launch_bounds__(256, MH_VOL_WAVES)
 k_prbvol_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, int coalesce,
-                  const float *__restrict__ grad_in, GradArgs ga, unsigned long long *__restrict__ counters) {
+                  const float *__restrict__ grad_in, GradArgs ga, unsigned long long *__restrict__ counters,
+                  PvpWork wk) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
     GradCtx g = make_grad_ctx(ga);
     uint32_t n_closest = 0, n_shadow = 0;
+    NeeLog nl;
+    nl.buf = wk.log;
+    nl.stride = gridDim.x * blockDim.x;
+    nl.cap = wk.cap;
+    nl.t = blockIdx.x * blockDim.x + threadIdx.x;
+    nl.n = 0;
+    nl.med = 0;
+    nl.overflow = false;
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) {
-        uint32_t lane, px, py;
-        lane_of(lm, k, lane, px, py);
-        Pcg rng;
-        rng.seed(seed_value, lane);
-        float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
-        RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                            __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
-        V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
-        Pcg rng_primal = rng;  // sampler.clone()
-        V3 Lp = prbvol_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest,
-                                     n_shadow);
-        prbvol_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
+    for (;;) {
+        if (wk.log) {  // next batch of 64 samples for this wave
+            unsigned long long b = 0;
+            if ((threadIdx.x & 63u) == 0) b = atomicAdd(wk.head, 64ull);
+            b = __builtin_amdgcn_readfirstlane((uint32_t)b) | ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32);
+            if (b >= n) break;
+            k = b + (threadIdx.x & 63u);
+        }
+        if (k < n) {
+            uint32_t lane, px, py;
+            lane_of(lm, k, lane, px, py);
+            Pcg rng;
+            rng.seed(seed_value, lane);
+            float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+            RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
+                                __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+            V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
+            Pcg rng_primal = rng;  // sampler.clone()
+            V3 Lp = prbvol_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest,
+                                         n_shadow);
+            prbvol_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow, nullptr, wk.log ? &nl : nullptr);
+        }
+        if (!wk.log) break;
     }
     flush_small_slots(g, ga);
     if (counters) {
@@ -843,7 +871,9 @@ hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
                                const float *grad_in, const float *weights, const GradArgs &ga_in,
-                               bool fused, unsigned long long *counters, hipStream_t st) {
+                               bool fused, unsigned long long *counters, hipStream_t st,
+                               float4 *nee_log, uint32_t nee_cap, uint32_t nee_blocks,
+                               unsigned long long *head) {
     const uint32_t bs = 256;
     if (n == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
@@ -873,10 +903,17 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
         ga.lds_slot = -1;
     }
     if (in.type == MH_INTEGRATOR_PRBVOLPATH) {
+        PvpWork wk{nullptr, 0, nullptr};
+        if (nee_log && head && nee_cap && nee_blocks) {
+            wk = PvpWork{nee_log, nee_cap, head};
+            g = dim3(nee_blocks);
+            hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned long long), st);
+            if (e != hipSuccess) return e;
+        }
         if (S.lds_bytes_bvh)
-            hipLaunchKernelGGL((k_prbvol_backward<true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters);
+            hipLaunchKernelGGL((k_prbvol_backward<true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters, wk);
         else
-            hipLaunchKernelGGL((k_prbvol_backward<false>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters);
+            hipLaunchKernelGGL((k_prbvol_backward<false>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, ga, counters, wk);
     } else if (S.lds_bytes_bvh && fused)
         hipLaunchKernelGGL((k_prb_backward<true, true>), g, b, sh, st, S, in, lm, seed_value, n, coalesce, grad_in, weights, ga, counters);
     else if (S.lds_bytes_bvh)

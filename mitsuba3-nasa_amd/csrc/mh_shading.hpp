@@ -2420,6 +2420,9 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
     for (int c = 0; c < 8; ++c) {
         const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
         const float w = ((bz ? w1z : w0z) * (by ? w1y : w0y)) * (bx ? w1x : w0x);
+#ifdef MH_EXP_NO_SIGMA_ATOMIC  // diagnostic: cost of the grid-gradient scatter
+        if (as * w == 12345.f)
+#endif
         unsafeAtomicAdd(buf + (uint64_t)zs[bz] * sz + (uint64_t)ys[by] * sy + (uint64_t)xs[bx], as * w);
     }
 }
@@ -2430,13 +2433,36 @@ MH_DEV void albedo_backward(uint32_t med, V3 adj, GradCtx &g) {
     if (k >= 0) acc_add(g, k, adj);
 }
 
+// Per-thread log of the gradient steps of one NEE walk (the adjoint pass of
+// k_prbvol_backward).  The reference replays the walk with the cloned sampler
+// to back-propagate dL * adj_emitted through every tr_multiplier
+// (prbvolpath.py:412-414), because adj_emitted (the NEE contribution) is
+// known only once the walk has ended.  The transmittance multipliers of a
+// grey medium are grey, so a step's gradient is coef * (dL . adj_emitted),
+// coef = -1 / (majorant * tr) for a null collision, -hom_t for a homogeneous
+// segment: the walk logs (p, coef) and the caller scatters them once
+// adj_emitted is known -- one walk instead of two.  Steps beyond `cap`, or in
+// a second medium, fall back to the replay.
+struct NeeLog {
+    float4 *buf;         // [cap][stride]: (p, coef)
+    uint32_t stride;     // threads of the launch
+    uint32_t cap;        // entries per thread
+    uint32_t t;          // this thread
+    uint32_t n;          // entries of the current walk
+    uint32_t med;        // their medium
+    bool overflow;
+};
+
 // PRBVolpathIntegrator.sample_emitter (prbvolpath.py:336-431): emitter sample
-// + ratio-tracked transmittance; Adj: replay with the cloned sampler and
-// back-propagate dL * adj_emitted through every tr_multiplier (:412-414)
-template <bool Adj>
+// + ratio-tracked transmittance; Mode 1 (adjoint): replay with the cloned
+// sampler and back-propagate dL * adj_emitted through every tr_multiplier
+// (:412-414); Mode 2: the primal walk, logging the gradient steps (NeeLog)
+template <int Mode>
 MH_DEV V3 pvp_sample_emitter(const DScene &S, const LdsBvh &B, const MEI &mei_ref, const SI &si_ref,
                              bool active_medium, Pcg &rng, uint32_t medium, DirS &ds, V3 adj_emitted, V3 dL,
-                             GradCtx *g, uint32_t &n_shadow) {
+                             GradCtx *g, uint32_t &n_shadow, NeeLog *nl = nullptr) {
+    constexpr bool Adj = Mode == 1;
+    if (Mode == 2) { nl->n = 0; nl->overflow = false; }
     const V3 ref_p = active_medium ? mei_ref.p : si_ref.p;
     const V3 ref_n = active_medium ? v3(0.f, 0.f, 0.f) : si_ref.n;
     const float sx = rng.next_float(), sy = rng.next_float();
@@ -2503,6 +2529,17 @@ MH_DEV V3 pvp_sample_emitter(const DScene &S, const LdsBvh &B, const MEI &mei_re
             }
             sigma_t_backward(S, medium, mei.p, gs, *g);
         }
+        if (Mode == 2 && (act_med || hom) && (act_med || act_surf)) {
+            const float tc = trm.x;  // grey: scalar sigma_n / majorant, scalar homogeneous tr
+            const float coef = !(tc > 0.f) ? 0.f : act_med ? (1.f / tc) * (-1.f / mei.maj) : -hom_t;
+            if (nl->n < nl->cap && (nl->n == 0 || nl->med == medium)) {
+                nl->buf[(uint64_t)nl->n * nl->stride + nl->t] = make_float4(mei.p.x, mei.p.y, mei.p.z, coef);
+                nl->med = medium;
+                ++nl->n;
+            } else {
+                nl->overflow = true;
+            }
+        }
         transmittance = transmittance * trm;
         if (act_surf) ray = spawn_ray(si.p, si.n, ray.d);
         needs_intersection = act_surf;
@@ -2516,7 +2553,7 @@ MH_DEV V3 pvp_sample_emitter(const DScene &S, const LdsBvh &B, const MEI &mei_re
 template <bool Adj>
 MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, RayT ray,
                         V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow,
-                        bool *valid_out = nullptr) {
+                        bool *valid_out = nullptr, NeeLog *nl = nullptr) {
     const bool handle_null = S.vol_flags & kVolHandleNull;
     uint32_t depth = 0;
     if (!Adj) L = v3(0.f, 0.f, 0.f);
@@ -2626,8 +2663,11 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
         if (active_e_surface || active_e_medium) {
             const Pcg nee_rng = rng;   // sampler.clone()
             DirS ds;
-            const V3 emitted = pvp_sample_emitter<false>(S, B, mei, si, active_e_medium, rng, medium, ds,
-                                                         v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), nullptr, n_shadow);
+            const bool logged = Adj && nl;
+            const V3 emitted = logged ? pvp_sample_emitter<2>(S, B, mei, si, active_e_medium, rng, medium, ds,
+                                                              v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), nullptr, n_shadow, nl)
+                                      : pvp_sample_emitter<0>(S, B, mei, si, active_e_medium, rng, medium, ds,
+                                                              v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), nullptr, n_shadow);
             V3 nee_w, bv = v3(0.f, 0.f, 0.f);
             float nee_pdf, bp = 0.f;
             const V3 wo_s = to_local(si, ds.d);
@@ -2645,9 +2685,17 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
             const V3 contrib = ((throughput * nee_w) * mis) * emitted;
             L = Adj ? L + (-contrib) : L + contrib;
             if (Adj) {
-                Pcg r2 = nee_rng;
-                DirS ds2;
-                pvp_sample_emitter<true>(S, B, mei, si, active_e_medium, r2, medium, ds2, contrib, dL, g, n_shadow);
+                if (logged && !nl->overflow) {  // the logged walk's steps: coef * (dL . adj_emitted)
+                    const float K = (dL.x * contrib.x + dL.y * contrib.y) + dL.z * contrib.z;
+                    for (uint32_t j = 0; j < nl->n; ++j) {
+                        const float4 e = nl->buf[(uint64_t)j * nl->stride + nl->t];
+                        sigma_t_backward(S, nl->med, v3(e.x, e.y, e.z), e.w * K, *g);
+                    }
+                } else {
+                    Pcg r2 = nee_rng;
+                    DirS ds2;
+                    pvp_sample_emitter<1>(S, B, mei, si, active_e_medium, r2, medium, ds2, contrib, dL, g, n_shadow);
+                }
                 if (active_e_surface && si.wi.z > 0.f && wo_s.z > 0.f) {
                     // backward(dL * contrib) through bsdf_val = rho / pi * cos
                     const V3 adj = ((((dL * emitted) * mis) * throughput) * kInvPi) * wo_s.z;

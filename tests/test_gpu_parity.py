@@ -354,10 +354,18 @@ def test_prbvolpath_per_sample_parity(kw):
     assert close.mean() >= 0.999
 
 
+@pytest.mark.parametrize("nee", ["log", "replay", "cap2"])
 @pytest.mark.parametrize("kw", [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0}])
-def test_prbvolpath_backward_parity(kw):
+def test_prbvolpath_backward_parity(kw, nee, monkeypatch):
     """Gradients (sigma_t, albedo, floor reflectance) vs the oracle: same
-    samples, float vs double accumulation and atomic order -> 2e-3."""
+    samples, float vs double accumulation and atomic order -> 2e-3.  NEE
+    walks of the adjoint pass: logged once (NeeLog, the default), replayed
+    with the cloned sampler (MH_PVP_NEE_LOG=0, the reference's structure),
+    or logged with 2 entries per thread so most walks overflow into the replay."""
+    if nee == "replay":
+        monkeypatch.setenv("MH_PVP_NEE_LOG", "0")
+    elif nee == "cap2":
+        monkeypatch.setenv("MH_PVP_NEE_CAP", "2")
     mi = _mi()
     import torch
     scene = _pvp_scene(mi, 24, 20, 8, **kw)

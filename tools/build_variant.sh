@@ -12,5 +12,5 @@ FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-c
 for f in mh_api.hip mh_kernels.hip mh_wavefront.hip mh_volwave.hip; do /opt/rocm/bin/hipcc $FLAGS -c $f -o "$OBJ/${f%.hip}.o" & done
 /opt/rocm/bin/hipcc $FLAGS -x hip -c mh_bvh.cpp -o "$OBJ/mh_bvh.o" &
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/gpurun_exp/lib_$NAME.so" "$OBJ"/*.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/gpurun_exp/lib_$NAME.so" "$OBJ"/*.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 echo "built gpurun_exp/lib_$NAME.so"
