@@ -102,6 +102,7 @@ struct mh_scene {
     DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     DevBuf wf_ws_bmp;  // wavefront PRB with a bitmap parameter: vertex records (WfBmp)
     DevBuf pvp_log;    // prbvolpath backward: per-thread NEE-walk step logs (NeeLog)
+    DevBuf pvp_main;   // prbvolpath backward: per-thread path logs of the single pass (MainLog)
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     std::vector<mh_medium> h_media;
@@ -462,7 +463,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->pvp_log})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->pvp_log, &s->pvp_main})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -628,6 +629,9 @@ constexpr int kCtrPvpHead = 30;
 // prbvolpath backward grid (MH_VOL_WAVES = 4 waves / SIMD: 4 workgroups per CU)
 // and NEE-log entries per thread (16 B each; longer walks replay)
 constexpr uint32_t kPvpBlocksPerCu = 4, kPvpNeeCap = 256;
+// MainLog entries per thread (64 B each: 4 GiB over the 262,144 threads of a
+// 256-CU grid); a path with more logged vertices replays its adjoint
+constexpr uint32_t kPvpMainCap = 256;
 // MH_FLAG_DETERMINISTIC or MH_DETERMINISTIC=1: fixed-order splat (k_splat_gather)
 static bool deterministic(uint32_t flags) {
     const char *e = getenv("MH_DETERMINISTIC");
@@ -1176,10 +1180,16 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         const uint32_t blocks = (uint32_t)cus * kPvpBlocksPerCu,
                        cap = ecap ? (uint32_t)std::max(1, atoi(ecap)) : kPvpNeeCap;
         MH_HIP(s->pvp_log.alloc((size_t)blocks * 256 * cap * 16));
+        // single pass (MainLog) unless MH_PVP_SINGLE=0; MH_PVP_MAIN_CAP: entries per thread
+        const char *esp = getenv("MH_PVP_SINGLE"), *emc = getenv("MH_PVP_MAIN_CAP");
+        const uint32_t main_cap = (esp && !strcmp(esp, "0")) ? 0u
+                                  : emc ? (uint32_t)std::max(1, atoi(emc)) : kPvpMainCap;
+        if (main_cap) MH_HIP(s->pvp_main.alloc((size_t)blocks * 256 * main_cap * 64));
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st,
                                    s->pvp_log.as<float4>(), cap, blocks,
-                                   s->counters.as<unsigned long long>() + kCtrPvpHead));
+                                   s->counters.as<unsigned long long>() + kCtrPvpHead,
+                                   main_cap ? s->pvp_main.as<float4>() : nullptr, main_cap));
     } else {
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));

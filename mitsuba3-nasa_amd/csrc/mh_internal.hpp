@@ -130,7 +130,9 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
                                // prbvolpath: NEE-walk logs ([cap][nee_blocks * 256] float4) on a
                                // persistent grid of nee_blocks pulling work from *head (nullptr: none)
                                float4 *nee_log = nullptr, uint32_t nee_cap = 0, uint32_t nee_blocks = 0,
-                               unsigned long long *head = nullptr);
+                               unsigned long long *head = nullptr,
+                               // + single pass: per-thread MainLog ([4 main_cap][threads] float4)
+                               float4 *main_log = nullptr, uint32_t main_cap = 0);
 // wavefront volpath (mh_volwave.hip): k_vw_main / k_vw_walk rounds
 uint64_t vw_max_chunk();
 size_t vw_workspace_bytes(uint64_t cap);

@@ -105,7 +105,7 @@ k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_
             else if (Kind == MH_INTEGRATOR_VOLPATH)
                 L = volpath_sample(S, B, in, rng, r, n_closest, n_shadow, &valid);
             else if (Kind == MH_INTEGRATOR_PRBVOLPATH)
-                L = prbvol_sample<false>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow,
+                L = prbvol_sample<0>(S, B, in, rng, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest, n_shadow,
                                          &valid);
             else
                 L = path_sample(S, B, in, rng, r, n_closest, n_shadow, &valid);
@@ -621,6 +621,8 @@ struct PvpWork {
     float4 *log;                  // [cap][threads] NeeLog entries
     uint32_t cap;
     unsigned long long *head;     // work counter (zeroed by the launcher)
+    float4 *main;                 // [4 main_cap][threads] MainLog entries (nullptr: primal + adjoint replay)
+    uint32_t main_cap;
 };
 
 template <bool InLds>
@@ -659,9 +661,17 @@ k_prbvol_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value
                                 __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
             V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
             Pcg rng_primal = rng;  // sampler.clone()
-            V3 Lp = prbvol_sample<false>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest,
+            if (wk.main) {  // single pass: primal + logged adjoint terms, replay only on overflow
+                MainLog ml{wk.main, nl.stride, wk.main_cap, nl.t, 0u, false};
+                const V3 Lp = prbvol_sample<2>(S, B, in, rng_primal, r, dL, v3(0, 0, 0), &g, n_closest, n_shadow,
+                                               nullptr, &nl, &ml);
+                if (!ml.overflow) pvp_log_apply(S, ml, Lp, g);
+                else prbvol_sample<3>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow);
+            } else {
+                V3 Lp = prbvol_sample<0>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest,
                                          n_shadow);
-            prbvol_sample<true>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow, nullptr, wk.log ? &nl : nullptr);
+                prbvol_sample<1>(S, B, in, rng, r, dL, Lp, &g, n_closest, n_shadow, nullptr, wk.log ? &nl : nullptr);
+            }
         }
         if (!wk.log) break;
     }
@@ -873,7 +883,7 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
                                const float *grad_in, const float *weights, const GradArgs &ga_in,
                                bool fused, unsigned long long *counters, hipStream_t st,
                                float4 *nee_log, uint32_t nee_cap, uint32_t nee_blocks,
-                               unsigned long long *head) {
+                               unsigned long long *head, float4 *main_log, uint32_t main_cap) {
     const uint32_t bs = 256;
     if (n == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
@@ -903,9 +913,9 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
         ga.lds_slot = -1;
     }
     if (in.type == MH_INTEGRATOR_PRBVOLPATH) {
-        PvpWork wk{nullptr, 0, nullptr};
+        PvpWork wk{nullptr, 0, nullptr, nullptr, 0};
         if (nee_log && head && nee_cap && nee_blocks) {
-            wk = PvpWork{nee_log, nee_cap, head};
+            wk = PvpWork{nee_log, nee_cap, head, main_cap ? main_log : nullptr, main_cap};
             g = dim3(nee_blocks);
             hipError_t e = hipMemsetAsync(head, 0, sizeof(unsigned long long), st);
             if (e != hipSuccess) return e;

@@ -2550,13 +2550,48 @@ MH_DEV V3 pvp_sample_emitter(const DScene &S, const LdsBvh &B, const MEI &mei_re
     return emitter_val * transmittance;
 }
 
-template <bool Adj>
+// Per-thread log of the L-dependent adjoint terms of one path (single-pass
+// prbvolpath backward, Mode 2).  The adjoint replay back-propagates
+// dL * weight * (L / weight) at every medium interaction (prbvolpath.py:
+// 202-204) and dL * bsdf_eval * (L / bsdf_eval) at every surface vertex
+// (:305-312), with L the radiance still to come: L_total minus the
+// contributions P collected before that point.  The primal pass logs, per
+// such vertex, P and the factors that do not depend on L; once the path ends
+// (L_total known) pvp_log_apply charges them.  NEE terms do not depend on L
+// and are charged in the pass itself.  One traversal instead of primal +
+// adjoint; a path with more than `cap` vertices replays (Mode 3).
+// Entry: 4 float4 at ((4 j + q) * stride + t):
+//   q0 (p, bits: 1 surface | 2 scatter | index << 2)   q1 (P, uv.x)
+//   q2 (dL / max(1e-8, w), uv.y)                       q3 (dws, dwa) or (cos, 0, 0, 0)
+struct MainLog {
+    float4 *buf;
+    uint32_t stride, cap, t, n;
+    bool overflow;
+    MH_DEV void add(float4 a, float4 b, float4 c, float4 d) {
+        if (n >= cap) { overflow = true; return; }
+        const uint64_t o = (uint64_t)4 * n * stride + t;
+        buf[o] = a;
+        buf[o + stride] = b;
+        buf[o + 2 * (uint64_t)stride] = c;
+        buf[o + 3 * (uint64_t)stride] = d;
+        ++n;
+    }
+};
+
+// Mode 0: primal; 1: adjoint replay (L = primal radiance); 2: primal + MainLog
+// + NEE gradients (single pass); 3: adjoint replay without the NEE gradients
+// (the fallback of a Mode-2 path whose log overflowed)
+template <int Mode>
 MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, RayT ray,
                         V3 dL, V3 L, GradCtx *g, uint32_t &n_closest, uint32_t &n_shadow,
-                        bool *valid_out = nullptr, NeeLog *nl = nullptr) {
+                        bool *valid_out = nullptr, NeeLog *nl = nullptr, MainLog *ml = nullptr) {
+    constexpr bool Adj = Mode == 1 || Mode == 3;   // adjoint arithmetic, L-dependent terms in place
+    constexpr bool Log = Mode == 2;                 // primal arithmetic, L-dependent terms logged
+    constexpr bool NeeGrad = Mode == 1 || Mode == 2;
     const bool handle_null = S.vol_flags & kVolHandleNull;
     uint32_t depth = 0;
     if (!Adj) L = v3(0.f, 0.f, 0.f);
+    if (Log) { ml->n = 0; ml->overflow = false; }
     V3 throughput = v3(1.f, 1.f, 1.f);
     float eta = 1.f;
     bool active = true, needs_intersection = true;
@@ -2619,7 +2654,7 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
         if (act_scatter)
             weight = v3(weight.x * (mei.sigma_s.x / P), weight.y * (mei.sigma_s.y / P), weight.z * (mei.sigma_s.z / P));
         throughput = throughput * weight;
-        if (Adj && (active_medium || escaped)) {
+        if ((Adj || Log) && (active_medium || escaped)) {
             // backward(dL * weight * Lo), Lo = L / max(1e-8, weight) (:202-204)
             const DMedium &m = S.media[med];
             const bool homog = m.type == MH_MEDIUM_HOMOGENEOUS;
@@ -2627,11 +2662,10 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
             const float al[3] = {m.albedo[0], m.albedo[1], m.albedo[2]};
             const float ss[3] = {mei.sigma_s.x, mei.sigma_s.y, mei.sigma_s.z};
             const float dfw = homog ? -mt * fw : 0.f;   // d (tr / tr_pdf) / d sigma_t
-            float gs = 0.f, ga[3];
+            float gs = 0.f, ga[3], dwsc[3], dwa = 0.f;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const float up = dc[c] * (Lc[c] / fmaxf(1e-8f, wc[c]));
-                float dws, dwa = 0.f;
+                float dws;
                 if (act_scatter) {
                     dws = dfw * ss[c] / P + fw * al[c] / P;   // sigma_s = sigma_t * albedo
                     dwa = fw * mei.sigma_t / P;
@@ -2640,11 +2674,23 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
                 } else {
                     dws = dfw;
                 }
-                gs += up * dws;
-                ga[c] = up * dwa;
+                dwsc[c] = dws;
+                if (Adj) {
+                    const float up = dc[c] * (Lc[c] / fmaxf(1e-8f, wc[c]));
+                    gs += up * dws;
+                    ga[c] = up * dwa;
+                }
             }
-            sigma_t_backward(S, med, mei.p, gs, *g);
-            if (act_scatter) albedo_backward(med, v3(ga[0], ga[1], ga[2]), *g);
+            if (Adj) {
+                sigma_t_backward(S, med, mei.p, gs, *g);
+                if (act_scatter) albedo_backward(med, v3(ga[0], ga[1], ga[2]), *g);
+            }
+            if (Log)
+                ml->add(make_float4(mei.p.x, mei.p.y, mei.p.z, __uint_as_float((act_scatter ? 2u : 0u) | (med << 2))),
+                        make_float4(L.x, L.y, L.z, 0.f),
+                        make_float4(dc[0] / fmaxf(1e-8f, wc[0]), dc[1] / fmaxf(1e-8f, wc[1]),
+                                    dc[2] / fmaxf(1e-8f, wc[2]), 0.f),
+                        make_float4(dwsc[0], dwsc[1], dwsc[2], dwa));
         }
 
         // ---- surface interaction (:212-238)
@@ -2663,7 +2709,7 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
         if (active_e_surface || active_e_medium) {
             const Pcg nee_rng = rng;   // sampler.clone()
             DirS ds;
-            const bool logged = Adj && nl;
+            const bool logged = NeeGrad && nl;
             const V3 emitted = logged ? pvp_sample_emitter<2>(S, B, mei, si, active_e_medium, rng, medium, ds,
                                                               v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 0.f), nullptr, n_shadow, nl)
                                       : pvp_sample_emitter<0>(S, B, mei, si, active_e_medium, rng, medium, ds,
@@ -2684,7 +2730,7 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
             const float mis = mis_weight(ds.pdf, nee_pdf);
             const V3 contrib = ((throughput * nee_w) * mis) * emitted;
             L = Adj ? L + (-contrib) : L + contrib;
-            if (Adj) {
+            if (NeeGrad) {
                 if (logged && !nl->overflow) {  // the logged walk's steps: coef * (dL . adj_emitted)
                     const float K = (dL.x * contrib.x + dL.y * contrib.y) + dL.z * contrib.z;
                     for (uint32_t j = 0; j < nl->n; ++j) {
@@ -2733,13 +2779,21 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
             }
             active_surface = active_surface && bs_pdf > 0.f;
             if (active_surface) {
-                if (Adj && smooth && si.wi.z > 0.f && bs_wo.z > 0.f) {
+                if ((Adj || Log) && smooth && si.wi.z > 0.f && bs_wo.z > 0.f) {
                     // Lo = bsdf_eval * detach(L / max(1e-8, bsdf_eval)) (:305-312)
                     const V3 be = (rho * kInvPi) * bs_wo.z;
-                    V3 adj = v3(dL.x * (L.x / fmaxf(1e-8f, be.x)), dL.y * (L.y / fmaxf(1e-8f, be.y)),
-                                dL.z * (L.z / fmaxf(1e-8f, be.z)));
-                    adj = (adj * kInvPi) * bs_wo.z;
-                    tex_backward(S, S.bsdf_tex[b], si.uvx, si.uvy, adj, *g);
+                    if (Adj) {
+                        V3 adj = v3(dL.x * (L.x / fmaxf(1e-8f, be.x)), dL.y * (L.y / fmaxf(1e-8f, be.y)),
+                                    dL.z * (L.z / fmaxf(1e-8f, be.z)));
+                        adj = (adj * kInvPi) * bs_wo.z;
+                        tex_backward(S, S.bsdf_tex[b], si.uvx, si.uvy, adj, *g);
+                    }
+                    if (Log)
+                        ml->add(make_float4(0.f, 0.f, 0.f, __uint_as_float(1u | (S.bsdf_tex[b] << 2))),
+                                make_float4(L.x, L.y, L.z, si.uvx),
+                                make_float4(dL.x / fmaxf(1e-8f, be.x), dL.y / fmaxf(1e-8f, be.y),
+                                            dL.z / fmaxf(1e-8f, be.z), si.uvy),
+                                make_float4(bs_wo.z, 0.f, 0.f, 0.f));
                 }
                 throughput = throughput * bw;
                 ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
@@ -2752,6 +2806,26 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
     }
     if (valid_out) *valid_out = valid_ray;
     return L;
+}
+
+// the logged L-dependent terms of a path whose radiance is now L_total
+MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &g) {
+    for (uint32_t j = 0; j < ml.n; ++j) {
+        const uint64_t o = (uint64_t)4 * j * ml.stride + ml.t;
+        const float4 q0 = ml.buf[o], q1 = ml.buf[o + ml.stride], q2 = ml.buf[o + 2 * (uint64_t)ml.stride],
+                     q3 = ml.buf[o + 3 * (uint64_t)ml.stride];
+        const uint32_t bits = __float_as_uint(q0.w), idx = bits >> 2;
+        const V3 Lsuf = Ltot - v3(q1.x, q1.y, q1.z);  // prbvolpath.py: L - (contributions so far)
+        const V3 up = v3(q2.x * Lsuf.x, q2.y * Lsuf.y, q2.z * Lsuf.z);
+        if (bits & 1u) {
+            const V3 adj = (up * kInvPi) * q3.x;
+            tex_backward(S, idx, q1.w, q2.w, adj, g);
+        } else {
+            const float gs = (up.x * q3.x + up.y * q3.y) + up.z * q3.z;
+            sigma_t_backward(S, idx, v3(q0.x, q0.y, q0.z), gs, g);
+            if (bits & 2u) albedo_backward(idx, up * q3.w, g);
+        }
+    }
 }
 
 }  // namespace mh

@@ -354,18 +354,28 @@ def test_prbvolpath_per_sample_parity(kw):
     assert close.mean() >= 0.999
 
 
-@pytest.mark.parametrize("nee", ["log", "replay", "cap2"])
+@pytest.mark.parametrize("nee", ["single", "main4", "twopass", "cap2", "replay"])
 @pytest.mark.parametrize("kw", [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0}])
 def test_prbvolpath_backward_parity(kw, nee, monkeypatch):
     """Gradients (sigma_t, albedo, floor reflectance) vs the oracle: same
-    samples, float vs double accumulation and atomic order -> 2e-3.  NEE
-    walks of the adjoint pass: logged once (NeeLog, the default), replayed
-    with the cloned sampler (MH_PVP_NEE_LOG=0, the reference's structure),
-    or logged with 2 entries per thread so most walks overflow into the replay."""
+    samples, float vs double accumulation and atomic order -> 2e-3.
+      single   one traversal: the L-dependent terms logged per thread
+               (MainLog) and charged once L_total is known, NEE walks logged
+               (NeeLog) -- the default
+      main4    4 MainLog entries per thread: most paths overflow and replay
+               their adjoint (without the NEE terms already charged)
+      twopass  primal + adjoint replay, NEE walks logged (MH_PVP_SINGLE=0)
+      cap2     two-pass with 2 NeeLog entries: most walks replay
+      replay   the reference's structure: two passes, NEE walks replayed"""
     if nee == "replay":
         monkeypatch.setenv("MH_PVP_NEE_LOG", "0")
     elif nee == "cap2":
         monkeypatch.setenv("MH_PVP_NEE_CAP", "2")
+        monkeypatch.setenv("MH_PVP_SINGLE", "0")
+    elif nee == "twopass":
+        monkeypatch.setenv("MH_PVP_SINGLE", "0")
+    elif nee == "main4":
+        monkeypatch.setenv("MH_PVP_MAIN_CAP", "4")
     mi = _mi()
     import torch
     scene = _pvp_scene(mi, 24, 20, 8, **kw)
