@@ -7,10 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 #include "mh_device.hpp"
 #include "mh_internal.hpp"
@@ -40,37 +43,93 @@ constexpr int kBins = 16;
 // leaf limits: the per-lane stream engine packs the count in 3 bits (<= 7)
 constexpr uint32_t kMaxDepth = 48;
 
+// Large ranges (the top levels of a big mesh) run each O(n) pass over T
+// threads: chunk-local boxes and bins reduced in chunk order (min / max and
+// integer counts, so the result does not depend on T), and a stable
+// partition through a scratch array.  Below `task_min` primitives a subtree
+// is deferred and built by one worker (build_bvh: subtrees in parallel,
+// stitched in task order), so the BVH is the same for any thread count.
+struct Par {
+    uint32_t threads = 1;
+    uint32_t min_range = 1u << 16;   // ranges below this run their passes on one thread
+    template <class F>
+    void chunks(uint32_t b, uint32_t e, F &&f) const {   // f(chunk, cb, ce)
+        const uint32_t n = e - b;
+        const uint32_t T = (threads > 1 && n >= min_range) ? threads : 1u;
+        if (T == 1) { f(0u, b, e); return; }
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < T; ++t)
+            th.emplace_back([&, t] { f(t, b + (uint32_t)((uint64_t)n * t / T), b + (uint32_t)((uint64_t)n * (t + 1) / T)); });
+        for (auto &x : th) x.join();
+    }
+    uint32_t nchunks(uint32_t n) const { return (threads > 1 && n >= min_range) ? threads : 1u; }
+};
+
+struct Pending { uint32_t node, slot, b, e, depth; };
+
 struct Builder {
     const std::vector<BuildPrim> &p;
-    std::vector<uint32_t> idx;
+    std::vector<uint32_t> &idx;
     std::vector<Node> nodes;
     std::vector<uint32_t> order;  // final prim order
     uint32_t max_depth = 0;
     uint32_t kMaxLeaf = 4;
     float trav_cost = 1.0f;  // SAH traversal cost relative to one primitive test
+    Par par;
+    uint32_t task_min = 0;            // defer subtrees smaller than this (0: never)
+    std::vector<Pending> pending;
 
-    explicit Builder(const std::vector<BuildPrim> &prims) : p(prims) {
-        idx.resize(p.size());
-        for (size_t i = 0; i < p.size(); ++i) idx[i] = (uint32_t)i;
-    }
+    Builder(const std::vector<BuildPrim> &prims, std::vector<uint32_t> &ids) : p(prims), idx(ids) {}
 
     Box bounds(uint32_t b, uint32_t e) const {
+        std::vector<Box> part(par.nchunks(e - b));
+        par.chunks(b, e, [&](uint32_t t, uint32_t cb, uint32_t ce) {
+            Box bb;
+            for (uint32_t i = cb; i < ce; ++i) bb.grow(p[idx[i]].lo, p[idx[i]].hi);
+            part[t] = bb;
+        });
         Box bb;
-        for (uint32_t i = b; i < e; ++i) bb.grow(p[idx[i]].lo, p[idx[i]].hi);
+        for (const Box &x : part) bb.grow(x);
         return bb;
     }
     float centroid(uint32_t i, int a) const { return 0.5f * (p[idx[i]].lo[a] + p[idx[i]].hi[a]); }
 
     // split [b, e) -> returns mid (b < mid < e) or e for "make leaf"
-    uint32_t split(uint32_t b, uint32_t e, uint32_t depth) {
+    uint32_t split(uint32_t b, uint32_t e, uint32_t depth, const Box &node_box) {
         const uint32_t n = e - b;
         if (n <= 2) return e;
+        const uint32_t T = par.nchunks(n);
+        std::vector<Box> cparts(T);
+        par.chunks(b, e, [&](uint32_t t, uint32_t cb0, uint32_t ce) {
+            Box cb;
+            for (uint32_t i = cb0; i < ce; ++i) {
+                float c[3] = {centroid(i, 0), centroid(i, 1), centroid(i, 2)};
+                cb.grow(c, c);
+            }
+            cparts[t] = cb;
+        });
         Box cb;
-        for (uint32_t i = b; i < e; ++i) {
-            float c[3] = {centroid(i, 0), centroid(i, 1), centroid(i, 2)};
-            cb.grow(c, c);
-        }
-        Box node_box = bounds(b, e);
+        for (const Box &x : cparts) cb.grow(x);
+        // the three axes' bins in one pass
+        struct Bins { Box box[3][kBins]; uint32_t cnt[3][kBins]; };
+        std::vector<Bins> bparts(T);
+        par.chunks(b, e, [&](uint32_t t, uint32_t c0, uint32_t c1) {
+            Bins &B = bparts[t];
+            memset(B.cnt, 0, sizeof(B.cnt));
+            for (int a = 0; a < 3; ++a)
+                for (int k = 0; k < kBins; ++k) B.box[a][k] = Box();
+            for (uint32_t i = c0; i < c1; ++i) {
+                const BuildPrim &q = p[idx[i]];
+                for (int a = 0; a < 3; ++a) {
+                    const float ext = cb.hi[a] - cb.lo[a];
+                    if (!(ext > 0.f)) continue;
+                    int k = (int)((0.5f * (q.lo[a] + q.hi[a]) - cb.lo[a]) / ext * kBins);
+                    k = std::min(std::max(k, 0), kBins - 1);
+                    B.cnt[a][k]++;
+                    B.box[a][k].grow(q.lo, q.hi);
+                }
+            }
+        });
         float best_cost = FLT_MAX;
         int best_axis = -1, best_bin = -1;
         for (int a = 0; a < 3; ++a) {
@@ -78,12 +137,11 @@ struct Builder {
             if (!(ext > 0.f)) continue;
             Box bin_box[kBins];
             uint32_t cnt[kBins] = {0};
-            for (uint32_t i = b; i < e; ++i) {
-                int k = (int)((centroid(i, a) - cb.lo[a]) / ext * kBins);
-                k = std::min(std::max(k, 0), kBins - 1);
-                cnt[k]++;
-                bin_box[k].grow(p[idx[i]].lo, p[idx[i]].hi);
-            }
+            for (uint32_t t = 0; t < T; ++t)
+                for (int k = 0; k < kBins; ++k) {
+                    cnt[k] += bparts[t].cnt[a][k];
+                    bin_box[k].grow(bparts[t].box[a][k]);
+                }
             Box lb[kBins], rb[kBins];
             uint32_t lc[kBins], rc[kBins];
             Box acc;
@@ -122,13 +180,39 @@ struct Builder {
         if (!force && area > 0.f && trav_cost + best_cost / area >= (float)n) return e;
         const int a = best_axis;
         const float ext = cb.hi[a] - cb.lo[a];
-        auto mid_it = std::partition(idx.begin() + b, idx.begin() + e, [&](uint32_t q) {
+        auto left = [&](uint32_t q) {
             float c = 0.5f * (p[q].lo[a] + p[q].hi[a]);
             int k = (int)((c - cb.lo[a]) / ext * kBins);
             k = std::min(std::max(k, 0), kBins - 1);
             return k <= best_bin;
-        });
-        uint32_t mid = (uint32_t)(mid_it - idx.begin());
+        };
+        uint32_t mid;
+        if (T == 1) {
+            mid = (uint32_t)(std::stable_partition(idx.begin() + b, idx.begin() + e, left) - idx.begin());
+        } else {  // stable partition over T chunks: count, offsets, scatter, copy back
+            std::vector<uint32_t> nl(T, 0), tmp(n);
+            par.chunks(b, e, [&](uint32_t t, uint32_t c0, uint32_t c1) {
+                uint32_t c = 0;
+                for (uint32_t i = c0; i < c1; ++i) c += left(idx[i]) ? 1u : 0u;
+                nl[t] = c;
+            });
+            uint32_t total_l = 0;
+            std::vector<uint32_t> ol(T), orr(T);
+            for (uint32_t t = 0; t < T; ++t) { ol[t] = total_l; total_l += nl[t]; }
+            uint32_t acc_r = total_l;
+            for (uint32_t t = 0; t < T; ++t) {
+                orr[t] = acc_r;
+                acc_r += (uint32_t)((uint64_t)n * (t + 1) / T - (uint64_t)n * t / T) - nl[t];
+            }
+            par.chunks(b, e, [&](uint32_t t, uint32_t c0, uint32_t c1) {
+                uint32_t l = ol[t], r = orr[t];
+                for (uint32_t i = c0; i < c1; ++i) tmp[left(idx[i]) ? l++ : r++] = idx[i];
+            });
+            par.chunks(b, e, [&](uint32_t, uint32_t c0, uint32_t c1) {
+                std::copy(tmp.begin() + (c0 - b), tmp.begin() + (c1 - b), idx.begin() + c0);
+            });
+            mid = b + total_l;
+        }
         if (mid == b || mid == e) mid = b + n / 2;
         return mid;
     }
@@ -142,13 +226,19 @@ struct Builder {
         }
     }
 
-    // emit a child reference (leaf or inner) for range [b, e)
-    void child(uint32_t b, uint32_t e, uint32_t depth, float4 &lo, float4 &hi) {
+    // emit a child reference (leaf or inner) for range [b, e) into slot
+    // `slot` of node `node` (deferred as a Pending task below task_min)
+    void child(uint32_t b, uint32_t e, uint32_t depth, float4 &lo, float4 &hi, uint32_t node = 0, uint32_t slot = 0) {
         Box bb = bounds(b, e);
+        const Box raw = bb;
         pad(bb);
         lo = make_float4(bb.lo[0], bb.lo[1], bb.lo[2], 0.f);
         hi = make_float4(bb.hi[0], bb.hi[1], bb.hi[2], 0.f);
-        uint32_t mid = split(b, e, depth);
+        if (task_min && e - b < task_min) {  // built later by a worker (build_bvh stitches it in)
+            pending.push_back(Pending{node, slot, b, e, depth});
+            return;
+        }
+        uint32_t mid = split(b, e, depth, raw);
         if (mid == e) {  // leaf
             uint32_t first = (uint32_t)order.size();
             // primitives of one type together (scene order within a type): the
@@ -177,22 +267,36 @@ struct Builder {
         uint32_t ni = (uint32_t)nodes.size();
         nodes.push_back(Node{});
         Node n;
-        child(b, mid, depth + 1, n.lo0, n.hi0);
-        child(mid, e, depth + 1, n.lo1, n.hi1);
+        child(b, mid, depth + 1, n.lo0, n.hi0, ni, 0);
+        child(mid, e, depth + 1, n.lo1, n.hi1, ni, 1);
         nodes[ni] = n;
         return ni;
     }
 };
+
+// build threads: MH_BVH_THREADS, else the host's cores (at most 32)
+uint32_t bvh_threads() {
+    if (const char *e = getenv("MH_BVH_THREADS")) return (uint32_t)std::max(1, atoi(e));
+    const uint32_t hc = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(32u, hc ? hc : 1u));
+}
 
 }  // namespace
 
 void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf, float trav_cost) {
     out = BvhOut();
     if (in.empty()) return;
-    Builder bld(in);
+    const uint32_t n = (uint32_t)in.size();
+    std::vector<uint32_t> ids(n);
+    for (uint32_t i = 0; i < n; ++i) ids[i] = i;
+    Builder bld(in, ids);
     bld.kMaxLeaf = std::max<uint32_t>(2, max_leaf);
     bld.trav_cost = trav_cost;
-    const uint32_t n = (uint32_t)in.size();
+    const uint32_t T = bvh_threads();
+    bld.par.threads = T;
+    // subtrees below n / 64 primitives (and at least 4096) go to the workers;
+    // the cut does not depend on T, so neither does the node layout
+    if (n >= (1u << 15)) bld.task_min = std::max<uint32_t>(4096, n / 64);
     if (n == 1) {
         // root with two identical single-prim leaves (the traversal needs an inner root)
         Node r;
@@ -209,9 +313,54 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf,
         bld.nodes.push_back(r);
         bld.max_depth = 1;
     } else {
-        uint32_t mid = bld.split(0, n, 0);
+        uint32_t mid = bld.split(0, n, 0, bld.bounds(0, n));
         if (mid == n) mid = n / 2;  // the root is always an inner node
         bld.inner(0, mid, n, 0);
+    }
+    if (!bld.pending.empty()) {
+        // deferred subtrees: one sequential builder each, T workers, stitched in task order
+        const size_t np = bld.pending.size();
+        std::vector<Builder *> sub(np, nullptr);
+        std::vector<float4> sub_lo(np), sub_hi(np);   // each subtree's own reference (leaf or local node 0)
+        std::atomic<size_t> next{0};
+        std::vector<std::thread> th;
+        for (uint32_t t = 0; t < std::min<size_t>(T, np); ++t)
+            th.emplace_back([&] {
+                for (size_t k; (k = next.fetch_add(1)) < np;) {
+                    const Pending &pd = bld.pending[k];
+                    Builder *sb = new Builder(in, ids);
+                    sb->kMaxLeaf = bld.kMaxLeaf;
+                    sb->trav_cost = bld.trav_cost;
+                    sb->child(pd.b, pd.e, pd.depth, sub_lo[k], sub_hi[k]);
+                    sub[k] = sb;
+                }
+            });
+        for (auto &x : th) x.join();
+        for (size_t k = 0; k < np; ++k) {
+            const Pending &pd = bld.pending[k];
+            Builder *sb = sub[k];
+            const uint32_t nbase = (uint32_t)bld.nodes.size(), obase = (uint32_t)bld.order.size();
+            auto fix = [&](float4 &lo, const float4 &hi) {   // a subtree-local child reference -> global
+                uint32_t w, cnt;
+                memcpy(&w, &lo.w, 4);
+                memcpy(&cnt, &hi.w, 4);
+                w = (cnt & kLeafCountMask) ? w + obase : w + nbase;
+                memcpy(&lo.w, &w, 4);
+            };
+            float4 rlo = sub_lo[k];
+            fix(rlo, sub_hi[k]);
+            Node &parent = bld.nodes[pd.node];
+            (pd.slot ? parent.lo1 : parent.lo0).w = rlo.w;
+            (pd.slot ? parent.hi1 : parent.hi0).w = sub_hi[k].w;
+            for (Node q : sb->nodes) {
+                fix(q.lo0, q.hi0);
+                fix(q.lo1, q.hi1);
+                bld.nodes.push_back(q);
+            }
+            bld.order.insert(bld.order.end(), sb->order.begin(), sb->order.end());
+            bld.max_depth = std::max(bld.max_depth, sb->max_depth);
+            delete sb;
+        }
     }
     out.n_nodes = (uint32_t)bld.nodes.size();
     out.n_prims = (uint32_t)bld.order.size();
