@@ -1306,10 +1306,10 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 
 // Texel gradients of the logged bitmap vertices of one chunk (see WfBmp):
 // adj_k = D_k + dL (L_total - P_k) q_k / pi per record, spread over the
-// bilinear taps (tex_backward's weights).  Item t of each 4096-path block is
-// path (t & 63) * 64 + (t >> 6) of the block, so the 64 lanes of a wave take
-// paths 64 apart -- 64 different pixels at 64 spp -- instead of the samples
-// of one pixel, whose camera vertices all land on the same texels.  InLds: a
+// bilinear taps (tex_backward's weights).  Lane l of a wave takes path
+// 64 l + c of a 4096-path tile (column c), so the lanes hold paths 64 apart
+// -- 64 different pixels at 64 spp -- instead of the samples of one pixel,
+// whose camera vertices all land on the same texels.  InLds: a
 // persistent grid accumulating into a per-workgroup LDS copy of the texture
 // (grouped ds_add_f32), flushed once with one global atomic per non-zero
 // texel; otherwise global atomics.
@@ -1323,11 +1323,14 @@ k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restr
         __syncthreads();
     }
     const DTexture tx = S.textures[tex];
-    const uint32_t full = n & ~4095u;
-    const uint32_t n_pad = (n + 63u) & ~63u;  // whole waves iterate together (grouped adds)
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_pad; t += stride) {
-        const uint32_t pid = t < full ? (t & ~4095u) | ((t & 63u) << 6) | ((t >> 6) & 63u) : t;
+    // a workgroup owns whole 4096-path tiles (its waves take the tile's 64
+    // columns in turn), so the 64 lines a wave's transposed load touches are
+    // re-read by the same CU's next columns from its L1 / L2
+    const uint32_t n_tiles = (n + 4095u) / 4096u, waves = blockDim.x >> 6, wave = threadIdx.x >> 6,
+                   lane = threadIdx.x & 63u;
+    for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+      for (uint32_t col = wave; col < 64u; col += waves) {
+        const uint32_t pid = tile * 4096u + lane * 64u + col;
         uint32_t mask = 0;
         float4 f0 = make_float4(0.f, 0.f, 0.f, 0.f), f1 = f0;
         if (pid < n) {
@@ -1370,9 +1373,13 @@ k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restr
                 }
             }
         }
+      }
     }
     if (InLds) {
         __syncthreads();
+#ifdef MH_EXP_NO_FLUSH  // diagnostic: cost of the per-workgroup flush
+        if (blockIdx.x == 0)
+#endif
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x)
             if (acc[i] != 0.f) atomicAdd(grad + i, acc[i]);
     }
@@ -1497,12 +1504,12 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
 #undef MH_BOUNCE_PRB
     if (with_bmp) {
         const bool in_lds = (size_t)bmp->n_floats * 4 <= bmp->lds_max;
-        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->blocks, (uint32_t)((n + 255) / 256)));
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->blocks, (uint32_t)((n + 4095) / 4096)));
         if (in_lds)
             hipLaunchKernelGGL(k_wf_bitmap_scatter<true>, dim3(blocks), dim3(256), (size_t)bmp->n_floats * 4, st, S,
                                bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
         else
-            hipLaunchKernelGGL(k_wf_bitmap_scatter<false>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S,
+            hipLaunchKernelGGL(k_wf_bitmap_scatter<false>, dim3((uint32_t)((n + 4095) / 4096)), dim3(256), 0, st, S,
                                bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
     }
     if (span) (void)hipEventRecord(span[1], st);
