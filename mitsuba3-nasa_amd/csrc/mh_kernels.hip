@@ -589,7 +589,7 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
         float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
         RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
                             __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
-        V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
+        V3 dL = gather_dL_wave(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
         if (Fused) {
             prb_fused(S, B, in, rng, r, dL, ga.n_rgb, g, n_closest, n_shadow);
         } else {
@@ -659,7 +659,7 @@ k_prbvol_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value
             float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
             RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
                                 __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
-            V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
+            V3 dL = gather_dL_wave(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
             Pcg rng_primal = rng;  // sampler.clone()
             if (wk.main) {  // single pass: primal + logged adjoint terms, replay only on overflow
                 MainLog ml{wk.main, nl.stride, wk.main_cap, nl.t, 0u, false};

@@ -1756,6 +1756,63 @@ MH_DEV V3 gather_dL(const DScene &S, int coalesce, const float *__restrict__ gw,
     return v3(o0, o1, o2);
 }
 
+// gather_dL for a wave whose active lanes share one footprint -- the usual
+// case: the wavefront is pixel-major, so a wave holds 64 samples of one pixel
+// at >= 64 spp per slab.  The 25 grad / W texels are then wave-uniform and
+// are read once through the scalar cache (s_load into SGPRs, the operands of
+// the multiplies) instead of by 25 vector loads per lane, and the 10 filter
+// weights run on packed f32.  Per lane the operations and their order are
+// gather_dL's, so dL is bit-identical; any other wave (box filter, spp < 4,
+// lanes of several pixels) takes gather_dL.
+MH_DEV F2 gaussian_eval2(const float *k, F2 x) {
+    const F2 X = x * x;  // estrin10(x * x, k), two arguments per instruction
+    const F2 c0 = fma2(X, sp2(k[1]), sp2(k[0])), c1 = fma2(X, sp2(k[3]), sp2(k[2])),
+             c2 = fma2(X, sp2(k[5]), sp2(k[4])), c3 = fma2(X, sp2(k[7]), sp2(k[6])),
+             c4 = fma2(X, sp2(k[9]), sp2(k[8]));
+    const F2 X2 = X * X;
+    const F2 d0 = fma2(X2, c1, c0), d1 = fma2(X2, c3, c2);
+    const F2 X4 = X2 * X2;
+    const F2 e0 = fma2(X4, d1, d0);
+    const F2 X8 = X4 * X4;
+    const F2 r = fma2(X8, c4, e0);
+    return pair(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f));
+}
+
+MH_DEV V3 gather_dL_wave(const DScene &S, int coalesce, const float *__restrict__ gw, float px, float py) {
+    if (!(coalesce && S.rfilter == MH_RFILTER_GAUSSIAN && S.rfilter_radius > 1.5f && S.rfilter_radius <= 2.5f))
+        return gather_dL(S, coalesce, gw, px, py);
+    const int32_t fx = (int32_t)floorf(px), fy = (int32_t)floorf(py);
+    const int32_t ux = __builtin_amdgcn_readfirstlane(fx), uy = __builtin_amdgcn_readfirstlane(fy);
+    if (__builtin_amdgcn_ballot_w64(fx != ux || fy != uy) != 0) return gather_dL(S, coalesce, gw, px, py);
+    const int32_t pix = ux - 2, piy = uy - 2;  // nn = ceil(radius - 0.5) = 2, count = 5
+    const float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
+    const F2 wa = gaussian_eval2(S.filter_coeff, pair(relx + 0.f, relx + 1.f)),
+             wb = gaussian_eval2(S.filter_coeff, pair(relx + 2.f, relx + 3.f)),
+             wc = gaussian_eval2(S.filter_coeff, pair(relx + 4.f, rely + 0.f)),
+             wd = gaussian_eval2(S.filter_coeff, pair(rely + 1.f, rely + 2.f)),
+             we = gaussian_eval2(S.filter_coeff, pair(rely + 3.f, rely + 4.f));
+    const float wxs[5] = {wa.x, wa.y, wb.x, wb.y, wc.x}, wys[5] = {wc.y, wd.x, wd.y, we.x, we.y};
+    const uint32_t W = S.width, H = S.height;
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+#pragma unroll
+    for (int32_t ys = 0; ys < 5; ++ys) {
+        const uint32_t yy = (uint32_t)(piy + ys);
+        if (yy >= H) continue;  // wave-uniform
+        const float wy = wys[ys];
+#pragma unroll
+        for (int32_t xs = 0; xs < 5; ++xs) {
+            const uint32_t xx = (uint32_t)(pix + xs);
+            if (xx >= W) continue;
+            const CFloat *t = (CFloat *)gw + 4ull * ((uint64_t)yy * W + xx);
+            const float w = wy * wxs[xs];
+            o0 += t[0] * w;
+            o1 += t[1] * w;
+            o2 += t[2] * w;
+        }
+    }
+    return v3(o0, o1, o2);
+}
+
 // ---------------------------------------------------------------------------
 // Fused PRB gradient for constant (rgb) reflectance parameters: ONE traversal
 // of the path instead of the primal + adjoint replay of

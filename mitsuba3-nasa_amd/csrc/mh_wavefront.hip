@@ -1113,7 +1113,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                                  __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
                 gen_state = g.state;
                 gen_inc = g.inc;  // the TEA of this lane, reused below
-                dL = gather_dL(S0, gen.coalesce, gen.grad_in, sx, sy);
+#ifdef MH_EXP_NO_GATHER  // diagnostic: cost of the first bounce's dL gather
+                { const float4 g = reinterpret_cast<const float4 *>(gen.grad_in)[px + py * S0.width]; dL = v3(g.x, g.y, g.z); }
+#else
+                dL = gather_dL_wave(S0, gen.coalesce, gen.grad_in, sx, sy);
+#endif
             } else {
                 const uint32_t pd = w.pd[cur][j];
                 pid = pd & kPidMask;
