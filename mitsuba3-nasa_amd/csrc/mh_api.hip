@@ -375,7 +375,7 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
               upload(s->texels, desc->texels, desc->n_texels, st) == hipSuccess &&
               upload(s->media, meds.data(), meds.size(), st) == hipSuccess &&
               upload(s->grid, bricked.data(), bricked.size(), st) == hipSuccess &&
-              s->counters.alloc(256) == hipSuccess;
+              s->counters.alloc(256 + 1024) == hipSuccess;  // 32 counters + 8 work heads on own lines
     if (!ok) return fail(MH_ERR_OUT_OF_MEMORY, "mh_scene_create: device upload failed");
 
     DScene &S = s->S;
@@ -622,9 +622,11 @@ static LaneMap lane_map(const Layout &L, uint32_t pixel_begin) {
     return m;
 }
 
-// counters[kCtrInvalid] of the scene's 32-word counter block: invalid samples
-constexpr int kCtrInvalid = 31;
-// counters[kCtrPvpHead]: work head of the persistent prbvolpath backward
+// The scene's 32-word counter block (zeroed per call): [0] closest rays,
+// [1] shadow rays, [2..22] k_vol_sched phase statistics (MH_EXP_VSCNT
+// builds), [kCtrInvalid] invalid samples, [kCtrPvpHead] the prbvolpath
+// backward's work head; bytes 256.. hold k_vol_sched's 8 queue heads
+constexpr int kCtrInvalid = 28;
 constexpr int kCtrPvpHead = 30;
 // prbvolpath backward grid (MH_VOL_WAVES = 4 waves / SIMD: 4 workgroups per CU)
 // and NEE-log entries per thread (16 B each; longer walks replay)

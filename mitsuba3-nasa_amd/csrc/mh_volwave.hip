@@ -721,8 +721,34 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     WMei wm;
     Pcg rng;
     uint32_t pid = 0, ph = kPhFree;
-    uint64_t next = 0, end = 0;  // wave-uniform: the wave's current batch [next, end)
-    bool drained = false;        // wave-uniform: the device counter has passed n
+    // XCD-aware work queues.  Workgroups are dispatched round-robin over the
+    // 8 XCDs (b % 8), and each XCD has its own 4-MiB L2, while the grid of
+    // config 4 is 64 MiB.  Queue x holds the samples of the x-th column band
+    // of the chunk's rows (contiguous eighths when the chunk is not whole
+    // rows); an XCD serves its own queue first, then the others', so its
+    // paths -- and the NEE walks up toward a sun that stays in the band's
+    // x-slab -- touch about an eighth of the medium.
+    const uint32_t xcd = blockIdx.x & 7u;
+    const uint32_t Wd = lm.W;
+    const uint64_t S_ = lm.S, npx = n / S_;
+    const bool bands = Wd >= 8u && lm.pixel_begin % Wd == 0u && npx % Wd == 0u && npx * S_ == n;
+    const uint32_t rows = bands ? (uint32_t)(npx / Wd) : 0u;
+    const uint64_t part = (n + 7u) / 8u;
+    auto q_size = [&](uint32_t q) -> uint64_t {
+        if (bands) return (uint64_t)rows * ((q + 1u) * Wd / 8u - q * Wd / 8u) * S_;
+        const uint64_t lo = (uint64_t)q * part;
+        return lo >= n ? 0ull : std::min<uint64_t>(part, n - lo);
+    };
+    auto q_sample = [&](uint32_t q, uint64_t i) -> uint64_t {  // queue-local index -> chunk sample
+        if (!bands) return (uint64_t)q * part + i;
+        const uint32_t c0 = q * Wd / 8u, bw = (q + 1u) * Wd / 8u - c0;
+        const uint64_t j = i / S_, sidx = i - j * S_;
+        const uint64_t r = j / bw, c = c0 + (j - r * bw);
+        return (r * Wd + c) * S_ + sidx;
+    };
+    uint32_t cq = 0, tried = 0;  // wave-uniform: queue of the current batch, queues exhausted so far
+    uint64_t next = 0, end = 0;  // wave-uniform: the wave's current batch [next, end) of queue cq
+    bool drained = false;        // wave-uniform: every queue is exhausted
 #ifdef MH_EXP_VSCNT
     unsigned long long d_trips[kNGroups] = {}, d_lanes[kNGroups] = {}, d_ticks[kNGroups] = {};
 #endif
@@ -745,18 +771,26 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 #endif
         bool ended = false;
         if (sel == kGFree) {
-            if (next >= end) {  // take the next batch of 64 samples
+            while (next >= end && tried < 8u) {  // take the next batch of 64 samples: own queue first
+                const uint32_t q = (xcd + tried) & 7u;
                 uint64_t b = 0;
-                if (vw_lane() == 0) b = atomicAdd(work, 64ull);
+                if (vw_lane() == 0) b = atomicAdd(work + 16u * q, 64ull);
                 b = __builtin_amdgcn_readfirstlane((uint32_t)b) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32);
-                next = std::min<uint64_t>(b, n);
-                end = std::min<uint64_t>(b + 64u, n);
-                drained = b + 64u >= n;
+                const uint64_t qs = q_size(q);
+                if (b < qs) {
+                    cq = q;
+                    next = b;
+                    end = std::min<uint64_t>(b + 64u, qs);
+                } else {
+                    ++tried;
+                }
             }
+            drained = tried >= 8u;
             const unsigned long long m = __builtin_amdgcn_ballot_w64(ph == kPhFree);
             if (ph == kPhFree) {
-                const uint64_t k = next + (uint64_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
-                if (k < end) {
+                const uint64_t i = next + (uint64_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
+                if (i < end) {
+                    const uint64_t k = q_sample(cq, i);
                     pid = (uint32_t)k;
                     uint32_t lane, px, py;
                     lane_of(lm, k, lane, px, py);
@@ -849,8 +883,8 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
 #define MH_VS(L, P, T)                                                                                        \
     hipLaunchKernelGGL((k_vol_sched<L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), st, S, in, \
                        lm, seed_value, n, plane, out, counters, work, alpha)
-    unsigned long long *work = counters + 31;  // the batch counter of this launch
-    hipError_t e = hipMemsetAsync(work, 0, sizeof(*work), st);
+    unsigned long long *work = counters + 32;  // the 8 queue heads of this launch (128 B apart)
+    hipError_t e = hipMemsetAsync(work, 0, 8 * 128, st);
     if (e != hipSuccess) return e;
     if (pk && tab) MH_VS(false, true, true);
     else if (pk) MH_VS(false, true, false);

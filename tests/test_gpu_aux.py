@@ -65,6 +65,23 @@ def test_invalid_sample_counter(light, mode):
     assert (expect == 0) == (light is None)
 
 
+@pytest.mark.parametrize("sky", [0.2, -0.2])
+def test_invalid_sample_counter_volpath(sky):
+    """volpath (the phase-scheduled kernel, whose work head shares the
+    counter block): a negative sky gives negative samples."""
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = mi.load_dict(mi.volume_cube(24, 20, 8, grid=mi.fbm_grid(16), scale=4.0, sky=sky, max_depth=8))
+    integ = scene.integrator()
+    st = A.Stats()
+    mi.render_film(scene, integ, seed=2, spp=8, stats=st)
+    assert st.mode == 3
+    L = _samples(mi, scene, integ, 2, 8, A.FLAG_WAVEFRONT)
+    expect = int(np.sum(np.any(~(L >= -1e-5) | ~np.isfinite(L), axis=1)))
+    assert st.invalid_samples == expect
+    assert (expect == 0) == (sky > 0)
+
+
 @pytest.mark.parametrize("chunk", [None, "4096"])
 def test_deterministic_film_bit_reproducible(chunk, monkeypatch):
     if chunk:
