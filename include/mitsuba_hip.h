@@ -317,6 +317,24 @@ int mh_render_backward(mh_scene *scene, const mh_integrator *integrator, uint32_
                        mh_stats *stats);
 
 /*
+ * Forward-mode derivative of render(): RBIntegrator.render_forward
+ * (src/python/python/ad/integrators/common.py:696-826).  tangents[k] holds
+ * the input tangent of parameter param_textures[k] (same shape and ids as
+ * mh_render_backward's grads[k]; host or device per flags).  The sample's
+ * tangent radiance dL (prb.py:244-248, `δL += dr.forward_to(Lo)`) is splatted
+ * like a primal sample, value = dL, weight 1 and alpha = the ray validity
+ * (common.py:799-806), into the film storage of mh_render (RGBW, or R G B A W
+ * for alpha films); mh_develop then yields the gradient image, whose alpha
+ * channel is the developed coverage, as film.develop() returns it
+ * (common.py:808-824).  One AD wavefront of <= 2^32 samples per call
+ * (common.py:571-578).  integrator: MH_INTEGRATOR_PRB or MH_INTEGRATOR_PRBVOLPATH.
+ */
+int mh_render_forward(mh_scene *scene, const mh_integrator *integrator, uint32_t seed,
+                      uint32_t spp, uint32_t spp_begin, uint32_t spp_end, uint32_t n_params,
+                      const uint32_t *param_textures, const float *const *tangents,
+                      float *film_rgbw, uint32_t flags, mh_stats *stats);
+
+/*
  * Ray-query sub-boundary (the OptiX slot).  Rays are SoA: ray[0..6][n] =
  * o.x o.y o.z d.x d.y d.z maxt (mint = 0).  Output = the payload of
  * Scene::ray_intersect_preliminary_gpu (scene_optix.inl:592-657,

@@ -957,6 +957,112 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     return MH_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Differentiated parameters -> slots: small slots 0..n_rgb-1 (register
+// accumulators): rgb textures, medium albedo, homogeneous sigma_t; large
+// slots (global atomics / tangent arrays): bitmaps, grids
+// ---------------------------------------------------------------------------
+struct Slots {
+    std::vector<int32_t> slot_of_tex, sigma_slot, albedo_slot;
+    std::vector<uint32_t> is_rgb;
+    std::vector<size_t> counts;
+    std::vector<uint32_t> slot_of_param;
+    uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0, bmp_tex = 0;
+    std::vector<uint8_t> meta;  // host copy of the meta block (alive until the caller's stream sync)
+};
+
+static int build_slots(const mh_scene *s, uint32_t n_params, const uint32_t *param_tex, bool vol, const char *api,
+                       const char *method, Slots &P) {
+    const std::string a(api), m(method);
+    P.slot_of_tex.assign(std::max<uint32_t>(s->n_textures, 1), -1);
+    P.sigma_slot.assign(std::max<uint32_t>(s->n_media, 1), -1);
+    P.albedo_slot = P.sigma_slot;
+    P.is_rgb.assign(kMaxParams, 0);
+    P.counts.assign(kMaxParams, 0);
+    P.slot_of_param.assign(n_params, 0);
+    for (uint32_t k = 0; k < n_params; ++k) {
+        const uint32_t kind = param_tex[k] & MH_PARAM_KIND_MASK, idx = param_tex[k] & ~MH_PARAM_KIND_MASK;
+        int32_t *owner;
+        bool small;
+        size_t cnt;
+        if (kind == 0) {
+            if (idx >= s->n_textures) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": texture index out of bounds");
+            const DTexture &tx = s->h_textures[idx];
+            owner = &P.slot_of_tex[idx];
+            small = tx.type == MH_TEX_RGB;
+            cnt = small ? 3 : (size_t)tx.width * tx.height * tx.channels;
+        } else if (kind == MH_PARAM_MEDIUM_SIGMA_T || kind == MH_PARAM_MEDIUM_ALBEDO) {
+            if (!vol)
+                return set_error(MH_ERR_UNSUPPORTED, m + "(): medium parameters require the 'prbvolpath' integrator");
+            if (idx >= s->n_media) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": medium index out of bounds");
+            const mh_medium &md = s->h_media[idx];
+            ++P.n_medium_params;
+            if (kind == MH_PARAM_MEDIUM_ALBEDO) {
+                owner = &P.albedo_slot[idx]; small = true; cnt = 3;
+            } else {
+                owner = &P.sigma_slot[idx];
+                small = md.type == MH_MEDIUM_HOMOGENEOUS;
+                cnt = small ? 1 : (size_t)md.grid_res[0] * md.grid_res[1] * md.grid_res[2];
+            }
+        } else {
+            return set_error(MH_ERR_INVALID_ARGUMENT, a + ": unknown parameter kind");
+        }
+        if (*owner >= 0) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": duplicate parameter");
+        int slot;
+        if (small) {
+            if (P.n_rgb >= (uint32_t)kMaxRgbParams) return set_error(MH_ERR_UNSUPPORTED, a + ": too many rgb parameters");
+            slot = (int)P.n_rgb++;
+            P.is_rgb[slot] = 1;
+        } else {
+            if (P.n_bmp >= (uint32_t)kMaxBitmapParams) return set_error(MH_ERR_UNSUPPORTED, a + ": too many bitmap parameters");
+            slot = kMaxRgbParams + (int)P.n_bmp++;
+            if (kind == 0) P.bmp_tex = idx;
+        }
+        P.counts[slot] = cnt;
+        *owner = slot;
+        P.slot_of_param[k] = (uint32_t)slot;
+    }
+    return MH_OK;
+}
+
+// per-slot device buffers (s->tmp_c, zeroed) and the meta block (copied from
+// P.meta, which the caller keeps until its stream synchronises)
+// slot_of_tex | is_rgb | bufs | sigma_slot | albedo_slot (s->grad_meta)
+static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vector<float *> &bufs, GradArgs &ga) {
+    size_t total = 0;
+    std::vector<size_t> off(kMaxParams, 0);
+    for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += (P.counts[k] + 3) / 4 * 4; }
+    hipError_t e = s->tmp_c.alloc(std::max<size_t>(total, 1) * 4);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st);
+    if (e != hipSuccess) return e;
+    bufs.assign(kMaxParams, nullptr);
+    for (int k = 0; k < kMaxParams; ++k) bufs[k] = P.counts[k] ? s->tmp_c.as<float>() + off[k] : nullptr;
+    auto al16 = [](size_t x) { return (x + 15) / 16 * 16; };
+    const size_t o_slot = 0, o_isrgb = al16(P.slot_of_tex.size() * 4), o_bufs = al16(o_isrgb + kMaxParams * 4),
+                 o_sig = al16(o_bufs + kMaxParams * 8), o_alb = al16(o_sig + P.sigma_slot.size() * 4),
+                 meta_bytes = al16(o_alb + P.albedo_slot.size() * 4);
+    std::vector<uint8_t> &meta = P.meta;
+    meta.assign(meta_bytes, 0);
+    memcpy(meta.data() + o_slot, P.slot_of_tex.data(), P.slot_of_tex.size() * 4);
+    memcpy(meta.data() + o_isrgb, P.is_rgb.data(), kMaxParams * 4);
+    memcpy(meta.data() + o_bufs, bufs.data(), kMaxParams * 8);
+    memcpy(meta.data() + o_sig, P.sigma_slot.data(), P.sigma_slot.size() * 4);
+    memcpy(meta.data() + o_alb, P.albedo_slot.data(), P.albedo_slot.size() * 4);
+    e = s->grad_meta.alloc(meta_bytes);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(s->grad_meta.ptr, meta.data(), meta_bytes, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    const uint8_t *mb = s->grad_meta.as<uint8_t>();
+    ga.slot_of_tex = reinterpret_cast<const int32_t *>(mb + o_slot);
+    ga.is_rgb = reinterpret_cast<const uint32_t *>(mb + o_isrgb);
+    ga.bufs = reinterpret_cast<float *const *>(mb + o_bufs);
+    ga.n_rgb = P.n_rgb;
+    ga.sigma_slot = P.n_medium_params ? reinterpret_cast<const int32_t *>(mb + o_sig) : nullptr;
+    ga.albedo_slot = P.n_medium_params ? reinterpret_cast<const int32_t *>(mb + o_alb) : nullptr;
+    return hipSuccess;
+}
+
 int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                        uint32_t spp_begin, uint32_t spp_end, const float *grad_in,
                        const float *weights, uint32_t n_params, const uint32_t *param_tex,
@@ -980,84 +1086,15 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
 
     // ---- parameter slots ----
-    // small slots 0..n_small-1 (register accumulators): rgb textures, medium
-    // albedo, homogeneous sigma_t; large slots (global atomics): bitmaps, grids
-    std::vector<int32_t> slot_of_tex(std::max<uint32_t>(s->n_textures, 1), -1);
-    std::vector<int32_t> sigma_slot(std::max<uint32_t>(s->n_media, 1), -1), albedo_slot(sigma_slot);
-    std::vector<uint32_t> is_rgb(kMaxParams, 0);
-    std::vector<float *> bufs(kMaxParams, nullptr);
-    std::vector<size_t> counts(kMaxParams, 0);
-    std::vector<uint32_t> slot_of_param(n_params);
-    uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0, bmp_tex = 0;
-    for (uint32_t k = 0; k < n_params; ++k) {
-        const uint32_t kind = param_tex[k] & MH_PARAM_KIND_MASK, idx = param_tex[k] & ~MH_PARAM_KIND_MASK;
-        int32_t *owner;
-        bool small;
-        size_t cnt;
-        if (kind == 0) {
-            if (idx >= s->n_textures) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: texture index out of bounds");
-            const DTexture &tx = s->h_textures[idx];
-            owner = &slot_of_tex[idx];
-            small = tx.type == MH_TEX_RGB;
-            cnt = small ? 3 : (size_t)tx.width * tx.height * tx.channels;
-        } else if (kind == MH_PARAM_MEDIUM_SIGMA_T || kind == MH_PARAM_MEDIUM_ALBEDO) {
-            if (!vol)
-                return set_error(MH_ERR_UNSUPPORTED, "render_backward(): medium parameters require the 'prbvolpath' integrator");
-            if (idx >= s->n_media) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: medium index out of bounds");
-            const mh_medium &m = s->h_media[idx];
-            ++n_medium_params;
-            if (kind == MH_PARAM_MEDIUM_ALBEDO) {
-                owner = &albedo_slot[idx]; small = true; cnt = 3;
-            } else {
-                owner = &sigma_slot[idx];
-                small = m.type == MH_MEDIUM_HOMOGENEOUS;
-                cnt = small ? 1 : (size_t)m.grid_res[0] * m.grid_res[1] * m.grid_res[2];
-            }
-        } else {
-            return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: unknown parameter kind");
-        }
-        if (*owner >= 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: duplicate parameter");
-        int slot;
-        if (small) {
-            if (n_rgb >= (uint32_t)kMaxRgbParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many rgb parameters");
-            slot = (int)n_rgb++;
-            is_rgb[slot] = 1;
-        } else {
-            if (n_bmp >= (uint32_t)kMaxBitmapParams) return set_error(MH_ERR_UNSUPPORTED, "mh_render_backward: too many bitmap parameters");
-            slot = kMaxRgbParams + (int)n_bmp++;
-            if (kind == 0) bmp_tex = idx;
-        }
-        counts[slot] = cnt;
-        *owner = slot;
-        slot_of_param[k] = (uint32_t)slot;
-    }
-    // gradient buffers: device scratch, zeroed, accumulated into the caller's
-    size_t total = 0;
-    std::vector<size_t> off(kMaxParams, 0);
-    for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += (counts[k] + 3) / 4 * 4; }
-    MH_HIP(s->tmp_c.alloc(std::max<size_t>(total, 1) * 4));
-    MH_HIP(hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st));
-    for (int k = 0; k < kMaxParams; ++k) bufs[k] = counts[k] ? s->tmp_c.as<float>() + off[k] : nullptr;
-    // meta block: slot_of_tex | is_rgb | bufs | sigma_slot | albedo_slot
-    auto al16 = [](size_t x) { return (x + 15) / 16 * 16; };
-    const size_t o_slot = 0, o_isrgb = al16(slot_of_tex.size() * 4), o_bufs = al16(o_isrgb + kMaxParams * 4),
-                 o_sig = al16(o_bufs + kMaxParams * 8), o_alb = al16(o_sig + sigma_slot.size() * 4),
-                 meta_bytes = al16(o_alb + albedo_slot.size() * 4);
-    std::vector<uint8_t> meta(meta_bytes, 0);
-    memcpy(meta.data() + o_slot, slot_of_tex.data(), slot_of_tex.size() * 4);
-    memcpy(meta.data() + o_isrgb, is_rgb.data(), kMaxParams * 4);
-    memcpy(meta.data() + o_bufs, bufs.data(), kMaxParams * 8);
-    memcpy(meta.data() + o_sig, sigma_slot.data(), sigma_slot.size() * 4);
-    memcpy(meta.data() + o_alb, albedo_slot.data(), albedo_slot.size() * 4);
-    MH_HIP(s->grad_meta.alloc(meta_bytes));
-    MH_HIP(hipMemcpyAsync(s->grad_meta.ptr, meta.data(), meta_bytes, hipMemcpyHostToDevice, st));
+    Slots P;
+    int rc_slots = build_slots(s, n_params, param_tex, vol, "mh_render_backward", "render_backward", P);
+    if (rc_slots) return rc_slots;
+    std::vector<float *> bufs;
     GradArgs ga;
-    ga.slot_of_tex = reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_slot);
-    ga.is_rgb = reinterpret_cast<const uint32_t *>(s->grad_meta.as<uint8_t>() + o_isrgb);
-    ga.bufs = reinterpret_cast<float *const *>(s->grad_meta.as<uint8_t>() + o_bufs);
-    ga.n_rgb = n_rgb;
-    ga.sigma_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_sig) : nullptr;
-    ga.albedo_slot = n_medium_params ? reinterpret_cast<const int32_t *>(s->grad_meta.as<uint8_t>() + o_alb) : nullptr;
+    MH_HIP(upload_slots(s, P, st, bufs, ga));
+    const std::vector<size_t> &counts = P.counts;
+    const std::vector<uint32_t> &slot_of_param = P.slot_of_param;
+    const uint32_t n_rgb = P.n_rgb, n_bmp = P.n_bmp, bmp_tex = P.bmp_tex;
     // one bitmap parameter of <= 48 KiB: the replay kernel accumulates its
     // texel gradients per workgroup in LDS (k_prb_backward)
     // (MH_PRB_LDS_TEX=0: global atomics, the parity tests' cross-check)
@@ -1245,6 +1282,108 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         stats->bounces = ctr[0];
         stats->ms_total = now_ms() - t_start;
         stats->ms_kernel = ms;
+    }
+    return MH_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Forward-mode derivative: RBIntegrator.render_forward (common.py:696-826)
+// ---------------------------------------------------------------------------
+int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+                      uint32_t spp_end, uint32_t n_params, const uint32_t *param_tex, const float *const *tangents,
+                      float *film_rgbw, uint32_t flags, mh_stats *stats) {
+    ScopedPhase phase_("RenderForward");
+    if (!s || !in || !film_rgbw || (n_params && (!param_tex || !tangents)))
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_forward: NULL argument");
+    if (in->type != MH_INTEGRATOR_PRB && in->type != MH_INTEGRATOR_PRBVOLPATH)
+        return set_error(MH_ERR_UNSUPPORTED, "render_forward(): requires the 'prb' or 'prbvolpath' integrator");
+    if (in->rr_depth == 0)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
+    if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_forward: spp must be > 0");
+    const double t_start = now_ms();
+    Layout L;
+    int rc = make_layout(s, spp, spp_begin, spp_end, L, true);  // prepare(): one wavefront of <= 2^32
+    if (rc) return rc;
+    MH_HIP(hipSetDevice(s->device));
+    hipStream_t st = s->stream;
+    const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
+    Slots P;
+    rc = build_slots(s, n_params, param_tex, in->type == MH_INTEGRATOR_PRBVOLPATH, "mh_render_forward",
+                     "render_forward", P);
+    if (rc) return rc;
+    std::vector<float *> bufs;
+    GradArgs ga;
+    MH_HIP(upload_slots(s, P, st, bufs, ga));  // zeroed slot buffers, here the tangents
+    for (uint32_t k = 0; k < n_params; ++k) {
+        const uint32_t slot = P.slot_of_param[k];
+        if (!tangents[k]) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_forward: NULL tangent");
+        MH_HIP(hipMemcpyAsync(bufs[slot], tangents[k], P.counts[slot] * 4,
+                              dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    }
+    // the film: as mh_render (RGBW, or RGBW + an alpha plane gathered into R G B A W)
+    const uint64_t n_px = (uint64_t)L.W * L.H;
+    const bool alpha = has_alpha(s->pixel_format);
+    const size_t film_bytes = n_px * (alpha ? 20 : 16);
+    float *film = film_rgbw;
+    if (!dev) {
+        MH_HIP(s->film_tmp.alloc(film_bytes));
+        film = s->film_tmp.as<float>();
+    }
+    if (!(flags & MH_FLAG_ACCUMULATE)) MH_HIP(hipMemsetAsync(film, 0, film_bytes, st));
+    else if (!dev) MH_HIP(hipMemcpyAsync(film, film_rgbw, film_bytes, hipMemcpyHostToDevice, st));
+    float *film4 = film, *film_a = nullptr;
+    if (alpha) {
+        MH_HIP(s->film4.alloc(n_px * 16));
+        MH_HIP(s->alpha_px.alloc(n_px * 4));
+        film4 = s->film4.as<float>();
+        film_a = s->alpha_px.as<float>();
+        MH_HIP(hipMemsetAsync(film4, 0, n_px * 16, st));
+        MH_HIP(hipMemsetAsync(film_a, 0, n_px * 4, st));
+    }
+    MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 256, st));
+    const uint32_t S_ = L.s_end - L.s_begin;
+    const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, (1ull << 25) / S_));
+    const uint64_t plane = (uint64_t)chunk_px * S_;
+    MH_HIP(s->work.alloc(plane * (alpha ? 6 : 5) * sizeof(float)));
+    const bool fast_splat = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN && s->S.rfilter_radius > 1.5f &&
+                            s->S.rfilter_radius <= 2.5f;
+    const int coalesce = L.spp_pp >= 4;  // block.set_coalesce(... and spp >= 4) (common.py:795-796)
+    const uint32_t seed_value = s->S.sampler_seed + seed;
+    const bool determ = deterministic(flags);
+    unsigned long long *invalid = s->counters.as<unsigned long long>() + kCtrInvalid;
+    MH_HIP(hipEventRecord(s->ev0, st));
+    for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px) {
+        const uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
+        const LaneMap lm = lane_map(L, (uint32_t)p0);
+        const uint64_t n = (uint64_t)npx * S_;
+        MH_HIP(launch_render_forward(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), ga,
+                                     s->counters.as<unsigned long long>(), st, alpha));
+        MH_HIP(launch_splat(s->S, lm, kSplatFilm, fast_splat, npx, 1, n, plane, s->work.as<float>(), film4,
+                            seed_value, coalesce, st, invalid, determ));
+        if (alpha)
+            MH_HIP(launch_splat(s->S, lm, kSplatAlpha, fast_splat, npx, 1, n, plane, s->work.as<float>(), film_a,
+                                seed_value, coalesce, st, nullptr, determ));
+    }
+    if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
+    MH_HIP(hipEventRecord(s->ev1, st));
+    if (!dev) MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
+    unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
+    MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
+    MH_HIP(hipMemcpyAsync(&n_invalid, invalid, sizeof(n_invalid), hipMemcpyDeviceToHost, st));
+    MH_HIP(hipStreamSynchronize(st));
+    if (stats) {
+        float ms = 0.f;
+        MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        stats->samples = n_px * S_;
+        stats->rays_closest = ctr[0];
+        stats->rays_shadow = ctr[1];
+        stats->bounces = ctr[0];
+        stats->ms_total = now_ms() - t_start;
+        stats->ms_kernel = ms;
+        stats->ms_trace = 0.f;
+        stats->n_trace_launches = 0;
+        stats->mode = 0;
+        stats->invalid_samples = (uint32_t)std::min<unsigned long long>(n_invalid, 0xffffffffull);
     }
     return MH_OK;
 }

@@ -133,6 +133,10 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
                                unsigned long long *head = nullptr,
                                // + single pass: per-thread MainLog ([4 main_cap][threads] float4)
                                float4 *main_log = nullptr, uint32_t main_cap = 0);
+// render_forward: per-sample tangent radiance (L, pos[, alpha] planes of launch_render); ga.bufs = tangents
+hipError_t launch_render_forward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                 uint32_t seed_value, uint64_t n, uint64_t plane, float *out, const GradArgs &ga,
+                                 unsigned long long *counters, hipStream_t st, int alpha);
 // wavefront volpath (mh_volwave.hip): k_vw_main / k_vw_walk rounds
 uint64_t vw_max_chunk();
 size_t vw_workspace_bytes(uint64_t cap);

@@ -548,9 +548,70 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.lds_slot = -1;
     g.lds_acc = nullptr;
     g.lds_floats = 0;
+    g.fwd = false;
+    g.fsum = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
     return g;
+}
+
+// ---------------------------------------------------------------------------
+// render_forward (common.py:696-826): per sample the tangent radiance dL,
+// written to the (L, pos, alpha) planes of k_render for the film splat.
+// prb: prb_forward, one traversal.  prbvolpath: the reference's primal +
+// forward-mode replay, the replay run once per colour channel c with dL = e_c
+// through the adjoint sinks in forward mode (GradCtx::fwd), whose
+// <adj, tangent> sum is then dL_c (the medium's sigma_t adjoint mixes the
+// channels, so one replay cannot give all three)
+// ---------------------------------------------------------------------------
+template <bool Vol, bool InLds>
+__global__ void __launch_bounds__(256, Vol ? MH_VOL_WAVES : 1)
+k_render_forward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane,
+                 float *__restrict__ out, GradArgs ga, unsigned long long *__restrict__ counters, int alpha) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    GradCtx g = make_grad_ctx(ga);
+    g.fwd = true;
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t n_closest = 0, n_shadow = 0;
+    if (k < n) {
+        uint32_t lane, px, py;
+        lane_of(lm, k, lane, px, py);
+        Pcg rng;
+        rng.seed(seed_value, lane);
+        const float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
+        RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
+                            __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+        V3 dL;
+        bool valid = false;
+        if (Vol) {
+            Pcg rng_primal = rng;  // sampler.clone()
+            const V3 Lp = prbvol_sample<0>(S, B, in, rng_primal, r, v3(0, 0, 0), v3(0, 0, 0), nullptr, n_closest,
+                                           n_shadow, &valid);
+            float d[3];
+#pragma unroll 1
+            for (int c = 0; c < 3; ++c) {
+                Pcg rc = rng;
+                g.fsum = 0.f;
+                prbvol_sample<1>(S, B, in, rc, r, v3(c == 0 ? 1.f : 0.f, c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f), Lp,
+                                 &g, n_closest, n_shadow);
+                d[c] = g.fsum;
+            }
+            dL = v3(d[0], d[1], d[2]);
+        } else {
+            dL = prb_forward(S, B, in, rng, r, g, n_closest, n_shadow, &valid);
+        }
+        out[k] = dL.x;
+        out[plane + k] = dL.y;
+        out[2 * plane + k] = dL.z;
+        out[3 * plane + k] = sx;
+        out[4 * plane + k] = sy;
+        if (alpha) out[5 * plane + k] = valid ? 1.f : 0.f;  // common.py:803-804
+    }
+    if (counters) {
+        wave_count(&counters[0], n_closest);
+        wave_count(&counters[1], n_shadow);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -727,6 +788,21 @@ hipError_t launch_render(const DScene &S, const IntegratorParams &in, const Lane
     else if (in.type == MH_INTEGRATOR_PRBVOLPATH) MH_LAUNCH_RENDER(MH_INTEGRATOR_PRBVOLPATH);
     else MH_LAUNCH_RENDER(MH_INTEGRATOR_PATH);
 #undef MH_LAUNCH_RENDER
+    return hipGetLastError();
+}
+
+hipError_t launch_render_forward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                 uint32_t seed_value, uint64_t n, uint64_t plane, float *out, const GradArgs &ga,
+                                 unsigned long long *counters, hipStream_t st, int alpha) {
+    const uint32_t bs = 256;
+    if (n == 0) return hipSuccess;
+    const size_t sh = lds_bytes(S, bs);
+    const bool lds = S.lds_bytes_bvh != 0, vol = in.type == MH_INTEGRATOR_PRBVOLPATH;
+    const dim3 g(blocks_for(n, bs)), b(bs);
+    if (vol && lds) hipLaunchKernelGGL((k_render_forward<true, true>), g, b, sh, st, S, in, lm, seed_value, n, plane, out, ga, counters, alpha);
+    else if (vol) hipLaunchKernelGGL((k_render_forward<true, false>), g, b, sh, st, S, in, lm, seed_value, n, plane, out, ga, counters, alpha);
+    else if (lds) hipLaunchKernelGGL((k_render_forward<false, true>), g, b, sh, st, S, in, lm, seed_value, n, plane, out, ga, counters, alpha);
+    else hipLaunchKernelGGL((k_render_forward<false, false>), g, b, sh, st, S, in, lm, seed_value, n, plane, out, ga, counters, alpha);
     return hipGetLastError();
 }
 

@@ -1471,6 +1471,11 @@ struct GradCtx {
     int32_t lds_slot;             // bitmap slot whose texels accumulate in LDS (-1: none)
     float *lds_acc;               // that slot's workgroup accumulator
     uint32_t lds_floats;          // its size (floats; checked under MH_DEBUG)
+    // forward mode (render_forward, common.py:696-826): bufs hold the input
+    // tangents, and every adjoint sink adds <adj, tangent> to fsum instead of
+    // scattering -- with dL = e_c that is the channel-c tangent radiance
+    bool fwd;
+    float fsum;
 };
 
 // register accumulator of a small (rgb / scalar) parameter slot; the
@@ -1526,9 +1531,41 @@ MH_DEV void lds_add_grouped(LdsFloat *acc, uint32_t key, bool on, const float (&
     }
 }
 
+// tangent of a reflectance texture at uv: tex_eval's taps and operation order
+// over the tangent texels of its slot (the bitmap is linear in its data), or
+// the slot's rgb tangent; zero when the texture is not differentiated
+MH_DEV V3 tex_tangent(const DScene &S, uint32_t tex, float uvx, float uvy, const GradCtx &g) {
+    const int32_t k = g.slot_of_tex[tex];
+    if (k < 0) return v3(0.f, 0.f, 0.f);
+    const float *t = g.bufs[k];
+    if (g.is_rgb[k]) return v3(t[0], t[1], t[2]);
+    const DTexture &tx = S.textures[tex];
+    Taps tp;
+    bitmap_taps(tx, uvx, uvy, tp);
+    float out[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint64_t cc = tx.channels == 3 ? (uint64_t)c : 0u;
+        if (tp.n == 1) {
+            out[c] = t[tp.idx[0] - tx.data_offset + cc];
+        } else {
+            const float f00 = t[tp.idx[0] - tx.data_offset + cc], f10 = t[tp.idx[1] - tx.data_offset + cc],
+                        f01 = t[tp.idx[2] - tx.data_offset + cc], f11 = t[tp.idx[3] - tx.data_offset + cc];
+            out[c] = __builtin_fmaf(tp.w0y, __builtin_fmaf(tp.w0x, f00, tp.w1x * f10),
+                                    tp.w1y * __builtin_fmaf(tp.w0x, f01, tp.w1x * f11));
+        }
+    }
+    return v3(out[0], out[1], out[2]);
+}
+
 MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3 adj, GradCtx &g) {
     int32_t k = g.slot_of_tex[tex];
     if (k < 0) return;
+    if (g.fwd) {
+        const V3 t = tex_tangent(S, tex, uvx, uvy, g);
+        g.fsum += (adj.x * t.x + adj.y * t.y) + adj.z * t.z;
+        return;
+    }
     const DTexture &tx = S.textures[tex];
     if (g.is_rgb[k]) {
 #pragma unroll
@@ -1951,6 +1988,102 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         if (si.valid) depth += 1;
         active = active_next;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Forward-mode PRB (render_forward, common.py:696-826; prb.py:244-248
+// `δL += dr.forward_to(Lo)`) in the single-traversal form of prb_fused.  The
+// replay's tangent at vertex k is (D_k + (L_total - P_k) c_k / pi) * t_k with
+// t_k = d rho / d pi . delta pi at the vertex (tex_tangent) and D_k the direct
+// term's cos-weighted NEE factor; regrouped as in prb_fused, every radiance
+// contribution e_j is charged with T(<j) / pi, T = sum_{k<j} c_k t_k.  T is
+// one rgb vector whatever the number of parameters (each vertex brings its
+// own t_k, bitmap texels included), so a path carries 6 floats.  Returns the
+// sample's tangent radiance dL; valid = depth != 0 (prb.py:253-257).
+// ---------------------------------------------------------------------------
+MH_DEV V3 prb_forward(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, RayT ray,
+                      const GradCtx &g, uint32_t &n_closest, uint32_t &n_shadow, bool *valid_out) {
+    uint32_t depth = 0;
+    V3 beta = v3(1, 1, 1), T = v3(0, 0, 0), dL = v3(0, 0, 0);
+    float eta = 1.f;
+    bool active = true;
+    V3 prev_p = v3(0, 0, 0);
+    float prev_bsdf_pdf = 1.f;
+    bool prev_bsdf_delta = true;
+    while (active) {
+        bool active_next = active;
+        Hit h;
+        traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
+        ++n_closest;
+        SI si;
+        compute_si(S, ray, h, si);
+        uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
+        bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+        if (in.hide_emitters && depth == 0 && !si.valid) active_next = false;
+        uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+        if (em != MH_INVALID) {
+            float em_pdf = prev_bsdf_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
+            float mis = mis_weight(prev_bsdf_pdf, em_pdf);
+            V3 le = v3(0, 0, 0);
+            if (active_next)
+                le = emitter_eval(S, em, si);
+            dL = dL + ((beta * mis) * le) * (T * kInvPi);
+        }
+        active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
+        bool active_em = active_next && smooth;
+        float e0 = rng.next_float(), e1 = rng.next_float();
+        DirS ds;
+        ds.pdf = 0.f;
+        ds.d = v3(0, 0, 0);
+        ds.delta = false;
+        V3 em_weight = v3(0, 0, 0);
+        if (active_em) {
+            em_weight = sample_emitter_direction(S, B, si, e0, e1, ds, n_shadow);
+            active_em = ds.pdf != 0.f;
+        }
+        V3 rho = v3(0, 0, 0);
+        if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+        V3 wo_em = to_local(si, ds.d);
+        V3 bsdf_value_em;
+        float bsdf_pdf_em;
+        diffuse_eval_pdf(rho, si.wi, wo_em, active_em, bsdf_value_em, bsdf_pdf_em);
+        float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
+        V3 beta_mis_em = beta * mis_em;
+        if (active_em) dL = dL + ((beta_mis_em * bsdf_value_em) * em_weight) * (T * kInvPi);
+        (void)rng.next_float();
+        float s2x = rng.next_float(), s2y = rng.next_float();
+        V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
+        float bs_pdf = 0.f, bs_eta = 0.f;
+        if (smooth && active_next) {
+            bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+            bs_pdf = kInvPi * bs_wo.z;
+            bs_eta = 1.f;
+            bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+        }
+        ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+        eta *= bs_eta;
+        beta = beta * bsdf_weight;
+        prev_p = si.p;
+        prev_bsdf_pdf = bs_pdf;
+        prev_bsdf_delta = false;
+        float beta_max = hmax(beta);
+        active_next = active_next && beta_max != 0.f;
+        float rr_prob = fminf(beta_max * (eta * eta), 0.95f);
+        bool rr_active = depth >= in.rr_depth;
+        if (rr_active) beta = beta * rcp(rr_prob);
+        bool rr_continue = rng.next_float() < rr_prob;
+        active_next = active_next && (!rr_active || rr_continue);
+        if (smooth && g.slot_of_tex[S.bsdf_tex[b]] >= 0) {
+            const V3 t = tex_tangent(S, S.bsdf_tex[b], si.uvx, si.uvy, g);
+            if (active_em && si.wi.z > 0.f && wo_em.z > 0.f)
+                dL = dL + (((em_weight * beta_mis_em) * wo_em.z) * kInvPi) * t;
+            T = T + prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf) * t;
+        }
+        if (si.valid) depth += 1;
+        active = active_next;
+    }
+    if (valid_out) *valid_out = depth != 0;
+    return dL;
 }
 
 // ===========================================================================
@@ -2460,7 +2593,11 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
     if (k < 0) return;
     const DMedium &m = S.media[med];
     const float as = adj * m.scale;
-    if (m.type == MH_MEDIUM_HOMOGENEOUS) { acc_add(g, k, v3(as, 0.f, 0.f)); return; }
+    if (m.type == MH_MEDIUM_HOMOGENEOUS) {
+        if (g.fwd) g.fsum += as * g.bufs[k][0];
+        else acc_add(g, k, v3(as, 0.f, 0.f));
+        return;
+    }
     V3 q = xf_point(m.to_local, p);
     const int32_t rx = (int32_t)m.res[0], ry = (int32_t)m.res[1], rz = (int32_t)m.res[2];
     float px = __builtin_fmaf(q.x, (float)rx, -0.5f), py = __builtin_fmaf(q.y, (float)ry, -0.5f),
@@ -2477,17 +2614,24 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
     for (int c = 0; c < 8; ++c) {
         const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
         const float w = ((bz ? w1z : w0z) * (by ? w1y : w0y)) * (bx ? w1x : w0x);
+        const uint64_t idx = (uint64_t)zs[bz] * sz + (uint64_t)ys[by] * sy + (uint64_t)xs[bx];
+        if (g.fwd) {  // tangent of the grid at p: the same taps over the tangent voxels
+            g.fsum += (as * w) * buf[idx];
+            continue;
+        }
 #ifdef MH_EXP_NO_SIGMA_ATOMIC  // diagnostic: cost of the grid-gradient scatter
         if (as * w == 12345.f)
 #endif
-        unsafeAtomicAdd(buf + (uint64_t)zs[bz] * sz + (uint64_t)ys[by] * sy + (uint64_t)xs[bx], as * w);
+        unsafeAtomicAdd(buf + idx, as * w);
     }
 }
 
 MH_DEV void albedo_backward(uint32_t med, V3 adj, GradCtx &g) {
     if (!g.albedo_slot) return;
     const int32_t k = g.albedo_slot[med];
-    if (k >= 0) acc_add(g, k, adj);
+    if (k < 0) return;
+    if (g.fwd) g.fsum += (adj.x * g.bufs[k][0] + adj.y * g.bufs[k][1]) + adj.z * g.bufs[k][2];
+    else acc_add(g, k, adj);
 }
 
 // Per-thread log of the gradient steps of one NEE walk (the adjoint pass of

@@ -21,7 +21,7 @@ from __future__ import annotations
 from . import _abi
 from ._abi import MitsubaHipError
 from .render import (SceneParameters, develop, prb_weights, render, render_1, render_backward,
-                     render_film, sample_tea_32, traverse)
+                     render_film, render_forward, sample_tea_32, traverse)
 from .scene import Integrator, Scene, cornell_box, gaussian_coefficients, load_dict
 from .transform import ScalarTransform4f, Transform4f
 from .scenes import cornell_box_bitmap, volume_cube
@@ -68,7 +68,7 @@ def is_available() -> bool:
 
 
 __all__ = ["set_variant", "variant", "variants", "load_dict", "cornell_box", "render", "traverse",
-           "render_backward", "render_film", "develop", "prb_weights", "SceneParameters", "Scene",
+           "render_backward", "render_forward", "render_film", "develop", "prb_weights", "SceneParameters", "Scene",
            "Integrator", "Transform4f", "ScalarTransform4f", "sample_tea_32", "MitsubaHipError",
            "gaussian_coefficients", "is_available", "volume_cube", "cornell_box_bitmap", "VolumeGrid", "fbm_grid",
            "load_file", "load_string", "meshio", "imageio",

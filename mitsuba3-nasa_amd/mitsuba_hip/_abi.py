@@ -133,6 +133,7 @@ EXPORTS = [
     "mh_scene_set_stream", "mh_scene_update_rgb", "mh_scene_update_texture", "mh_render",
     "mh_develop", "mh_prb_weights", "mh_render_backward", "mh_trace_closest", "mh_trace_shadow",
     "mh_scene_bvh_info", "mh_render_samples", "mh_scene_update_medium", "mh_trace_preliminary",
+    "mh_render_forward",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -178,6 +179,8 @@ def lib():
     L.mh_prb_weights.argtypes = [vp, u32, u32, u32, u32, vp, u32]
     L.mh_render_backward.argtypes = [vp, C.POINTER(Integrator), u32, u32, u32, u32, vp, vp, u32,
                                      PU, C.POINTER(vp), u32, C.POINTER(Stats)]
+    L.mh_render_forward.argtypes = [vp, C.POINTER(Integrator), u32, u32, u32, u32, u32, PU, C.POINTER(vp), vp,
+                                    u32, C.POINTER(Stats)]
     L.mh_trace_closest.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, u32, C.POINTER(Stats)]
     L.mh_trace_shadow.argtypes = [vp, u64, vp, vp, u32, C.POINTER(Stats)]
     L.mh_trace_preliminary.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, C.POINTER(Stats)]

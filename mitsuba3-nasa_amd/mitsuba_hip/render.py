@@ -269,6 +269,49 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     return outs
 
 
+def render_forward(scene: Scene, params: SceneParameters, tangents: Dict[str, object],
+                   integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
+                   spp_begin: int = 0, spp_end: int = 0, stats: Optional[A.Stats] = None,
+                   develop_image: bool = True, deterministic: bool = False):
+    """RBIntegrator.render_forward (ad/integrators/common.py:696-826): the
+    forward-mode derivative of the rendered image -- the gradient image --
+    for the input tangents ``{key: tensor shaped like params[key]}`` (the
+    reference reads them from ``dr.set_grad`` on ``params``).  Returns the
+    developed (H, W, C) image, or the un-developed film with
+    ``develop_image=False`` (slab renders are summed before developing).  As
+    film.develop() in the reference, an alpha film's alpha channel holds
+    the coverage, not a derivative."""
+    torch = _torch()
+    integrator = integrator or scene.integrator()
+    if integrator.type not in ("prb", "prbvolpath"):
+        raise A.MitsubaHipError("render_forward(): requires the 'prb' or 'prbvolpath' integrator")
+    spp = spp or scene.sample_count()
+    keys = list(tangents.keys())
+    dev = _device_index(None)
+    for k in keys:
+        t = tangents[k]
+        if hasattr(t, "device") and t.device.type == "cuda":
+            dev = t.device.index or 0
+            break
+    h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
+    tans = []
+    for k in keys:
+        t = torch.as_tensor(tangents[k], dtype=torch.float32).to(f"cuda:{dev}").contiguous()
+        if tuple(t.shape) != tuple(params[k].shape):
+            raise A.MitsubaHipError(f"render_forward(): tangent of '{k}' has shape {tuple(t.shape)}, "
+                                    f"expected {tuple(params[k].shape)}")
+        tans.append(t)
+    ids = (C.c_uint32 * max(len(keys), 1))(*[params.param_id(k) for k in keys])
+    ptrs = (C.c_void_p * max(len(keys), 1))(*[t.data_ptr() for t in tans])
+    film = torch.empty((scene.height, scene.width, A.film_channels(scene.desc.sensor.pixel_format)),
+                       dtype=torch.float32, device=f"cuda:{dev}")
+    ic = integrator.c()
+    flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_DETERMINISTIC if deterministic else 0)
+    A.check(A.lib().mh_render_forward(h, C.byref(ic), seed, spp, spp_begin, spp_end, len(keys), ids, ptrs,
+                                      _ptr(film), flags, C.byref(stats) if stats is not None else None))
+    return develop(scene, film) if develop_image else film
+
+
 # ---------------------------------------------------------------------------
 # mi.render with torch autograd (util.py:356-408, 512-625)
 # ---------------------------------------------------------------------------
@@ -291,7 +334,20 @@ def _render_op():
             grads = [g.to(d) for g, d in zip(grads, ctx.value_devices)]
             return (None, None, None, None, None, None, *grads)
 
+        @staticmethod
+        def jvp(ctx, *tangents_in):
+            # _RenderOp.forward (util.py:386-395): render_forward at the
+            # differential seed / spp, driven by torch.autograd.forward_ad
+            tans = {k: t for k, t in zip(ctx.keys, tangents_in[6:]) if t is not None}
+            return render_forward(ctx.scene, ctx.params, tans, ctx.integrator, ctx.seeds[1], ctx.spps[1])
+
     return _RenderOp
+
+
+def _has_tangent(v) -> bool:
+    """a forward-mode dual tensor (torch.autograd.forward_ad.make_dual)"""
+    import torch.autograd.forward_ad as fwAD
+    return fwAD.unpack_dual(v).tangent is not None
 
 
 def render(scene: Scene, params: Optional[SceneParameters] = None, sensor: int = 0,
@@ -314,7 +370,7 @@ def render(scene: Scene, params: Optional[SceneParameters] = None, sensor: int =
     elif seed_grad == seed:
         raise A.MitsubaHipError("The primal and differential seed should be different to ensure "
                                 "unbiased gradient computation!")
-    keys = [k for k, v in params.items() if v.requires_grad] if params is not None else []
+    keys = [k for k, v in params.items() if v.requires_grad or _has_tangent(v)] if params is not None else []
     if not keys:
         film = render_film(scene, integrator, seed, spp)
         return develop(scene, film)

@@ -785,6 +785,12 @@ typedef struct {
     uint32_t n_params;
     const uint32_t *tex;
     double **acc;
+    /* forward mode (render_forward, common.py:696-826): tan[k] is the input
+       tangent of parameter k, and every sink adds <adj, tangent> to fsum
+       instead of scattering adj -- with dL = e_c that is the tangent of
+       L_c (prb.py:244-248 `δL += dr.forward_to(Lo)`) */
+    const float *const *tan;
+    double fsum;
 } grad_sink;
 
 /* adjoint of tex_eval: scatter adj (= d loss / d rho) into the texels */
@@ -793,6 +799,30 @@ static void tex_backward(const mh_scene_desc *d, uint32_t tex, float uvx, float 
     for (uint32_t k = 0; k < g->n_params; ++k) {
         if (g->tex[k] != tex) continue;
         const mh_texture *tx = &d->textures[tex];
+        if (g->tan) {  /* tangent of tex_eval at uv: the same taps over the tangent texels */
+            const float *t = g->tan[k];
+            if (tx->type == MH_TEX_RGB) {
+                g->fsum += (double)adj.x * t[0] + (double)adj.y * t[1] + (double)adj.z * t[2];
+                continue;
+            }
+            tex_taps tp;
+            bitmap_taps(tx, uvx, uvy, &tp);
+            float av[3] = {adj.x, adj.y, adj.z};
+            for (int c = 0; c < 3; ++c) {
+                uint32_t cc = tx->channels == 3 ? (uint32_t)c : 0u;
+                double tv;
+                if (tp.n == 1) {
+                    tv = t[tp.idx[0] - tx->data_offset + cc];
+                } else {
+                    double w[4] = {(double)tp.w0y * tp.w0x, (double)tp.w0y * tp.w1x, (double)tp.w1y * tp.w0x,
+                                   (double)tp.w1y * tp.w1x};
+                    tv = 0.0;
+                    for (int j = 0; j < 4; ++j) tv += w[j] * t[tp.idx[j] - tx->data_offset + cc];
+                }
+                g->fsum += (double)av[c] * tv;
+            }
+            continue;
+        }
         double *a = g->acc[k];
         if (tx->type == MH_TEX_RGB) {
             a[0] += adj.x; a[1] += adj.y; a[2] += adj.z;
@@ -1766,9 +1796,14 @@ static void sigma_t_backward(const mh_scene_desc *d, uint32_t med, v3 p, double 
     for (uint32_t k = 0; k < g->n_params; ++k) {
         if (g->tex[k] != (MH_PARAM_MEDIUM_SIGMA_T | med)) continue;
         const mh_medium *m = &d->media[med];
-        double *a = g->acc[k];
+        double *a = g->tan ? NULL : g->acc[k];
+        const float *t = g->tan ? g->tan[k] : NULL;
         const double as = adj * (double)m->scale;
-        if (m->type == MH_MEDIUM_HOMOGENEOUS) { a[0] += as; continue; }
+        if (m->type == MH_MEDIUM_HOMOGENEOUS) {
+            if (t) g->fsum += as * t[0];
+            else a[0] += as;
+            continue;
+        }
         /* grid_eval's taps and weights (Texture3f linear, clamp) */
         v3 q = xf_point(m->grid_to_local, p);
         const int32_t rx = (int32_t)m->grid_res[0], ry = (int32_t)m->grid_res[1], rz = (int32_t)m->grid_res[2];
@@ -1783,7 +1818,9 @@ static void sigma_t_backward(const mh_scene_desc *d, uint32_t med, v3 p, double 
         for (int c = 0; c < 8; ++c) {
             const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
             const double w = (bz ? w1[2] : w0[2]) * (by ? w1[1] : w0[1]) * (bx ? w1[0] : w0[0]);
-            a[((size_t)zs[bz] * (size_t)ry + (size_t)ys[by]) * (size_t)rx + (size_t)xs[bx]] += as * w;
+            const size_t vi = ((size_t)zs[bz] * (size_t)ry + (size_t)ys[by]) * (size_t)rx + (size_t)xs[bx];
+            if (t) g->fsum += as * w * t[vi];
+            else a[vi] += as * w;
         }
     }
 }
@@ -1792,6 +1829,10 @@ static void sigma_t_backward(const mh_scene_desc *d, uint32_t med, v3 p, double 
 static void albedo_backward(uint32_t med, v3 adj, grad_sink *g) {
     for (uint32_t k = 0; k < g->n_params; ++k) {
         if (g->tex[k] != (MH_PARAM_MEDIUM_ALBEDO | med)) continue;
+        if (g->tan) {
+            g->fsum += (double)adj.x * g->tan[k][0] + (double)adj.y * g->tan[k][1] + (double)adj.z * g->tan[k][2];
+            continue;
+        }
         g->acc[k][0] += adj.x; g->acc[k][1] += adj.y; g->acc[k][2] += adj.z;
     }
 }
@@ -2272,7 +2313,7 @@ uint32_t oracle_spiral_order(uint32_t bw, uint32_t bh, uint32_t *bx, uint32_t *b
 }
 
 /* ---- threaded film renderer (row bands, deterministic merge) ---- */
-typedef enum { JOB_RENDER = 0, JOB_WEIGHTS = 1, JOB_BACKWARD = 2 } job_kind;
+typedef enum { JOB_RENDER = 0, JOB_WEIGHTS = 1, JOB_BACKWARD = 2, JOB_FORWARD = 3 } job_kind;
 
 typedef struct {
     const scene_view *sv;
@@ -2371,7 +2412,33 @@ static void *band_worker(void *arg) {
                 for (uint32_t pass = 0; pass < L->n_passes; ++pass) {
                     float pos[2];
                     int valid;
-                    if (j->kind == JOB_RENDER) {
+                    if (j->kind == JOB_FORWARD) {
+                        /* render_forward (common.py:766-806): primal with the
+                           cloned sampler, then the forward-mode replay -- here
+                           once per colour channel c with dL = e_c through the
+                           sinks in forward mode -- splatted as (dL, weight 1,
+                           alpha = valid) */
+                        float jx = pcg_float(&rng), jy = pcg_float(&rng);
+                        float sx = (float)px + jx, sy = (float)py + jy;
+                        ray3 r = camera_ray(s, fmaf(sx, inv_size(L->W), -0.f), fmaf(sy, inv_size(L->H), -0.f));
+                        const int vol = j->in->type == MH_INTEGRATOR_PRBVOLPATH;
+                        pcg32 rng_primal = rng;
+                        v3 Lp = vol ? prbvol_sample(j->sv, j->in, &rng_primal, r, V3(0, 0, 0), V3(0, 0, 0), NULL, &valid, NULL)
+                                    : prb_sample(j->sv, j->in, &rng_primal, r, V3(0, 0, 0), V3(0, 0, 0), NULL, &valid);
+                        float dl[3];
+                        for (int c = 0; c < 3; ++c) {
+                            pcg32 rc = rng;
+                            int v2;
+                            v3 e = V3(c == 0 ? 1.f : 0.f, c == 1 ? 1.f : 0.f, c == 2 ? 1.f : 0.f);
+                            j->sink.fsum = 0.0;
+                            if (vol) prbvol_sample(j->sv, j->in, &rc, r, e, Lp, &j->sink, &v2, NULL);
+                            else prb_sample(j->sv, j->in, &rc, r, e, Lp, &j->sink, &v2);
+                            dl[c] = (float)j->sink.fsum;
+                        }
+                        float vals[5] = {dl[0], dl[1], dl[2], 1.f, 1.f};
+                        if (j->band.ch == 5) vals[3] = valid ? 1.f : 0.f;
+                        splat(s, &j->band, sx, sy, vals, coalesce);
+                    } else if (j->kind == JOB_RENDER) {
                         v3 l = lane_sample(j->sv, j->in, L, &rng, lane, pos, &valid, NULL);
                         /* aovs (integrator.cpp:1216-1233): alpha = valid ? 1 : 0 */
                         float vals[5] = {l.x, l.y, l.z, 1.f, 1.f};
@@ -2424,7 +2491,7 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
                      uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
                      int n_threads, float *film, const float *grad_in, const float *weights,
                      uint32_t n_params, const uint32_t *param_tex, float *const *grads,
-                     uint32_t row_lo, uint32_t row_hi) {
+                     uint32_t row_lo, uint32_t row_hi, const float *const *tangents) {
     scene_view sv;
     if (scene_view_init(&sv, desc)) return 1;
     const mh_sensor *s = &desc->sensor;
@@ -2461,8 +2528,13 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
             if (r1 > (int32_t)L.H) r1 = (int32_t)L.H;
             j->band.width = L.W; j->band.height = L.H; j->band.row0 = r0;
             j->band.rows = (uint32_t)(r1 - r0);
-            j->band.ch = kind == JOB_RENDER ? fch : 4;
+            j->band.ch = (kind == JOB_RENDER || kind == JOB_FORWARD) ? fch : 4;
             j->band.data = (float *)calloc((size_t)j->band.rows * L.W * j->band.ch, sizeof(float));
+            if (kind == JOB_FORWARD) {
+                j->sink.n_params = n_params;
+                j->sink.tex = param_tex;
+                j->sink.tan = tangents;
+            }
         } else {
             j->sink.n_params = n_params;
             j->sink.tex = param_tex;
@@ -2488,7 +2560,7 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
         }
     } else {
         size_t npx = (size_t)L.W * L.H;
-        if (kind == JOB_RENDER) memset(film, 0, npx * fch * sizeof(float));
+        if (kind == JOB_RENDER || kind == JOB_FORWARD) memset(film, 0, npx * fch * sizeof(float));
         else memset(film, 0, npx * sizeof(float));
         for (int t = 0; t < n_threads; ++t) {
             band_job *j = &jobs[t];
@@ -2497,7 +2569,7 @@ static int run_bands(const mh_scene_desc *desc, const mh_integrator *in, job_kin
                 size_t row = (size_t)(j->band.row0 + (int32_t)r);
                 for (uint32_t x = 0; x < L.W; ++x) {
                     const float *src = j->band.data + ((size_t)r * L.W + x) * bc;
-                    if (kind == JOB_RENDER) {
+                    if (kind == JOB_RENDER || kind == JOB_FORWARD) {
                         float *dst = film + (row * L.W + x) * bc;
                         for (uint32_t c = 0; c < bc; ++c) dst[c] += src[c];
                     } else {
@@ -2518,14 +2590,14 @@ int oracle_render(const mh_scene_desc *desc, const mh_integrator *integ, uint32_
                   uint32_t spp, uint32_t spp_begin, uint32_t spp_end, int n_threads,
                   float *film_rgbw) {
     return run_bands(desc, integ, JOB_RENDER, seed, spp, spp_begin, spp_end, n_threads,
-                     film_rgbw, NULL, NULL, 0, NULL, NULL, 0, 0);
+                     film_rgbw, NULL, NULL, 0, NULL, NULL, 0, 0, NULL);
 }
 
 int oracle_prb_weights(const mh_scene_desc *desc, uint32_t seed, uint32_t spp,
                        uint32_t spp_begin, uint32_t spp_end, int n_threads, float *weights) {
     mh_integrator dummy = {MH_INTEGRATOR_PRB, 1, 1, 0};
     return run_bands(desc, &dummy, JOB_WEIGHTS, seed, spp, spp_begin, spp_end, n_threads,
-                     weights, NULL, NULL, 0, NULL, NULL, 0, 0);
+                     weights, NULL, NULL, 0, NULL, NULL, 0, 0, NULL);
 }
 
 /* W image from the samples of pixel rows [row_lo, row_hi) only (test helper
@@ -2535,7 +2607,7 @@ int oracle_prb_weights_rows(const mh_scene_desc *desc, uint32_t seed, uint32_t s
                             uint32_t row_hi, int n_threads, float *weights) {
     mh_integrator dummy = {MH_INTEGRATOR_PRB, 1, 1, 0};
     return run_bands(desc, &dummy, JOB_WEIGHTS, seed, spp, 0, 0, n_threads, weights, NULL, NULL, 0, NULL,
-                     NULL, row_lo, row_hi);
+                     NULL, row_lo, row_hi, NULL);
 }
 
 int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ,
@@ -2560,7 +2632,25 @@ int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ
         weights = w_local;
     }
     int rc = run_bands(desc, integ, JOB_BACKWARD, seed, spp, spp_begin, spp_end, n_threads, NULL,
-                       grad_in, weights, n_params, param_textures, grads, 0, 0);
+                       grad_in, weights, n_params, param_textures, grads, 0, 0, NULL);
     free(w_local);
     return rc;
+}
+
+int oracle_render_forward(const mh_scene_desc *desc, const mh_integrator *integ, uint32_t seed,
+                          uint32_t spp, uint32_t spp_begin, uint32_t spp_end, uint32_t n_params,
+                          const uint32_t *param_ids, const float *const *tangents, int n_threads,
+                          float *film) {
+    if (integ->type != MH_INTEGRATOR_PRB && integ->type != MH_INTEGRATOR_PRBVOLPATH)
+        return fail("render_forward(): requires the 'prb' or 'prbvolpath' integrator");
+    for (uint32_t k = 0; k < n_params; ++k) {
+        const uint32_t kind = param_ids[k] & MH_PARAM_KIND_MASK, idx = param_ids[k] & ~MH_PARAM_KIND_MASK;
+        if (kind == 0 ? idx >= desc->n_textures
+                      : (kind != MH_PARAM_MEDIUM_SIGMA_T && kind != MH_PARAM_MEDIUM_ALBEDO) || idx >= desc->n_media)
+            return fail("render_forward: parameter index out of bounds");
+        if (kind != 0 && integ->type != MH_INTEGRATOR_PRBVOLPATH)
+            return fail("render_forward(): medium parameters require the 'prbvolpath' integrator");
+    }
+    return run_bands(desc, integ, JOB_FORWARD, seed, spp, spp_begin, spp_end, n_threads, film, NULL, NULL,
+                     n_params, param_ids, NULL, 0, 0, tangents);
 }

@@ -79,6 +79,13 @@ int oracle_render_backward(const mh_scene_desc *desc, const mh_integrator *integ
                            const float *grad_in, const float *weights, uint32_t n_params,
                            const uint32_t *param_textures, float *const *grads, int n_threads);
 
+/* PRB render_forward (common.py:696-826): the film (as oracle_render) of the
+   per-sample tangent radiance; tangents[k] has the shape of grads[k] above. */
+int oracle_render_forward(const mh_scene_desc *desc, const mh_integrator *integ, uint32_t seed,
+                          uint32_t spp, uint32_t spp_begin, uint32_t spp_end, uint32_t n_params,
+                          const uint32_t *param_ids, const float *const *tangents, int n_threads,
+                          float *film);
+
 const char *oracle_last_error(void);
 
 #ifdef __cplusplus

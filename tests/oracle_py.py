@@ -54,6 +54,9 @@ def lib():
     L.oracle_render_backward.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32,
                                          C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, C.c_uint32,
                                          vp, C.POINTER(C.c_void_p), C.c_int]
+    L.oracle_render_forward.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32,
+                                        C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp,
+                                        C.POINTER(C.c_void_p), C.c_int, vp]
     L.oracle_render_scalar.argtypes = [C.POINTER(A.SceneDesc), C.POINTER(A.Integrator), C.c_uint32, C.c_uint32,
                                        C.c_uint32, C.c_int, vp]
     L.oracle_spiral_order.restype = C.c_uint32
@@ -177,3 +180,17 @@ def render_backward(scene, integrator, seed, spp, grad_in, textures, shapes, wei
         _p(np.ascontiguousarray(weights, np.float32)) if weights is not None else None,
         len(grads), _p(tex), ptrs, threads or nthreads()))
     return grads
+
+
+def render_forward(scene, integrator, seed, spp, param_ids, tangents, spp_begin=0, spp_end=0, threads=None):
+    """RBIntegrator.render_forward (common.py:696-826): the film of the
+    per-sample tangent radiance (develop it with develop())."""
+    from mitsuba_hip import _abi as A
+    film = np.zeros((scene.height, scene.width, A.film_channels(scene.desc.sensor.pixel_format)), np.float32)
+    tans = [np.ascontiguousarray(t, np.float32) for t in tangents]
+    ptrs = (C.c_void_p * max(len(tans), 1))(*[t.ctypes.data for t in tans])
+    ids = np.asarray(param_ids, np.uint32)
+    ic = integrator.c()
+    check(lib().oracle_render_forward(C.byref(scene.desc), C.byref(ic), seed, spp, spp_begin, spp_end,
+                                      len(tans), _p(ids), ptrs, threads or nthreads(), _p(film)))
+    return film
