@@ -1850,6 +1850,62 @@ MH_DEV V3 gather_dL_wave(const DScene &S, int coalesce, const float *__restrict_
     return v3(o0, o1, o2);
 }
 
+// gather_dL_wave with the footprint staged in LDS: lanes 0..24 each load one
+// grad / W texel (a vector load) into the wave's LDS scratch, and every lane
+// reads the 25 taps back as broadcast ds_read_b128.  The scalar-cache form
+// holds the 25 float4 taps in 100 SGPRs, which the fused PRB bounce (already
+// at the SGPR limit) spills; here the taps pass through VGPRs one at a time.
+// Same taps, weights and summation order: bit-identical dL.
+MH_DEV V3 gather_dL_wave_lds(const DScene &S, int coalesce, const float *__restrict__ gw, float px, float py,
+                             uint8_t *scratch) {
+    if (!(coalesce && S.rfilter == MH_RFILTER_GAUSSIAN && S.rfilter_radius > 1.5f && S.rfilter_radius <= 2.5f))
+        return gather_dL(S, coalesce, gw, px, py);
+    const int32_t fx = (int32_t)floorf(px), fy = (int32_t)floorf(py);
+    const int32_t ux = __builtin_amdgcn_readfirstlane(fx), uy = __builtin_amdgcn_readfirstlane(fy);
+    if (__builtin_amdgcn_ballot_w64(fx != ux || fy != uy) != 0) return gather_dL(S, coalesce, gw, px, py);
+    const int32_t pix = ux - 2, piy = uy - 2;  // nn = ceil(radius - 0.5) = 2, count = 5
+    const uint32_t W = S.width, H = S.height;
+    LdsFloat *taps = (LdsFloat *)scratch;  // 25 x (r, g, b, -)
+    // the active lanes (a wave's tail may be partial) share the 25 loads
+    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+    const uint32_t n_act = (uint32_t)__popcll(act);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    for (uint32_t t = rank; t < 25u; t += n_act) {
+        const uint32_t yy = (uint32_t)(piy + (int32_t)(t / 5u)), xx = (uint32_t)(pix + (int32_t)(t % 5u));
+        if (yy < H && xx < W) {
+            const float4 g = reinterpret_cast<const float4 *>(gw)[(uint64_t)yy * W + xx];
+            taps[4 * t + 0] = g.x;
+            taps[4 * t + 1] = g.y;
+            taps[4 * t + 2] = g.z;
+        }
+    }
+    const float relx = ((float)pix + 0.5f) - px, rely = ((float)piy + 0.5f) - py;
+    const F2 wa = gaussian_eval2(S.filter_coeff, pair(relx + 0.f, relx + 1.f)),
+             wb = gaussian_eval2(S.filter_coeff, pair(relx + 2.f, relx + 3.f)),
+             wc = gaussian_eval2(S.filter_coeff, pair(relx + 4.f, rely + 0.f)),
+             wd = gaussian_eval2(S.filter_coeff, pair(rely + 1.f, rely + 2.f)),
+             we = gaussian_eval2(S.filter_coeff, pair(rely + 3.f, rely + 4.f));
+    const float wxs[5] = {wa.x, wa.y, wb.x, wb.y, wc.x}, wys[5] = {wc.y, wd.x, wd.y, we.x, we.y};
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+#pragma unroll
+    for (int32_t ys = 0; ys < 5; ++ys) {
+        const uint32_t yy = (uint32_t)(piy + ys);
+        if (yy >= H) continue;  // wave-uniform
+        const float wy = wys[ys];
+#pragma unroll
+        for (int32_t xs = 0; xs < 5; ++xs) {
+            const uint32_t xx = (uint32_t)(pix + xs);
+            if (xx >= W) continue;
+            const LdsFloat *t = taps + 4 * (ys * 5 + xs);
+            const float w = wy * wxs[xs];
+            o0 += t[0] * w;
+            o1 += t[1] * w;
+            o2 += t[2] * w;
+        }
+    }
+    return v3(o0, o1, o2);
+}
+
 // ---------------------------------------------------------------------------
 // Fused PRB gradient for constant (rgb) reflectance parameters: ONE traversal
 // of the path instead of the primal + adjoint replay of

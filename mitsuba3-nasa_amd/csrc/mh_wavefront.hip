@@ -1116,7 +1116,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 #ifdef MH_EXP_NO_GATHER  // diagnostic: cost of the first bounce's dL gather
                 { const float4 g = reinterpret_cast<const float4 *>(gen.grad_in)[px + py * S0.width]; dL = v3(g.x, g.y, g.z); }
 #else
+#ifdef MH_EXP_SGPR_GATHER  // the scalar-cache gather (taps in SGPRs)
                 dL = gather_dL_wave(S0, gen.coalesce, gen.grad_in, sx, sy);
+#else
+                dL = gather_dL_wave_lds(S0, gen.coalesce, gen.grad_in, sx, sy, dscr);
+#endif
 #endif
             } else {
                 const uint32_t pd = w.pd[cur][j];
