@@ -197,7 +197,7 @@ def main():
     if rank == 0:
         # ---- rooflines of the two bounce-kernel families, the dominant one as
         # `roofline`.  One launch = one bounce of every live path
-        # of a 2^24-path chunk (closest trace + shading + NEE visibility).
+        # of a 2^25-path chunk (closest trace + shading + NEE visibility).
         # mh_render / mh_render_backward time the bounce launches with HIP
         # events on the scene's stream (stats.ms_trace / n_trace_launches).
         # Algorithmic bytes: the path state streamed per path-bounce (the BVH,

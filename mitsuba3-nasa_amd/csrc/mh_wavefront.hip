@@ -58,7 +58,13 @@ constexpr uint32_t kSeg = 64;
 #define MH_BOUNCE_PRB_WAVES MH_BOUNCE_WAVES  // the fused PRB bounce kernel's
 #endif
 constexpr uint32_t kCtrStride = kSeg * 32;
-constexpr uint32_t kPidBits = 24, kPidMask = (1u << kPidBits) - 1u;
+// path id and depth share a word: 2^MH_PID_BITS paths per chunk, depth
+// < 2^(32 - MH_PID_BITS) (the wavefront runs max_depth <= 64: 7 bits)
+#ifndef MH_PID_BITS
+#define MH_PID_BITS 25
+#endif
+constexpr uint32_t kPidBits = MH_PID_BITS, kPidMask = (1u << kPidBits) - 1u;
+constexpr uint32_t kMaxWfBounces = (1u << (32 - kPidBits)) - 1u;
 
 // Traversal engine of the stream kernels: wave-coherent packets for small
 // BVHs (every wave visits about the whole tree anyway; no divergence, no
@@ -662,7 +668,7 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             hipEvent_t *trace_ev, hipStream_t st, uint32_t n_passes, uint64_t *carry,
                             int alpha) {
     if (n == 0) return hipSuccess;
-    if (n > (1ull << kPidBits) || n_bounces > 255 || n_passes == 0) return hipErrorInvalidValue;
+    if (n > (1ull << kPidBits) || n_bounces > kMaxWfBounces || n_passes == 0) return hipErrorInvalidValue;
     if (n_passes == 1)
         return launch_wavefront_pass(S, in, lm, seed_value, n, plane, out, ws, cap, ctr, n_bounces, grid, trace_ev,
                                      st, nullptr, 0, alpha);
@@ -1450,7 +1456,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 uint32_t grid, float *partial, hipStream_t st, hipEvent_t *span,
                                 const WfBitmapArgs *bmp) {
     if (n == 0) return hipSuccess;
-    if (n > (1ull << kPidBits) || n_bounces > 255 || n_rgb > (uint32_t)kMaxRgbParams) return hipErrorInvalidValue;
+    if (n > (1ull << kPidBits) || n_bounces > kMaxWfBounces || n_rgb > (uint32_t)kMaxRgbParams) return hipErrorInvalidValue;
     WfState w = carve(ws, cap);
     WfPrb q = carve_prb(ws_prb, cap, partial, slot_of_tex, n_rgb);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);

@@ -2,9 +2,9 @@
 
 The small-film tests of test_gpu_parity.py never reach the production
 layouts these configurations run on:
-  config 2     512^2 @ 256 = 2^26 paths: four 2^24-path wavefront chunks, the
-               24-bit path id at its maximum (mh_wavefront.hip kPidBits)
-  config 3(a)  512^2 @ 64 = 2^24 paths: one full chunk of the fused PRB bounce
+  config 2     512^2 @ 256 = 2^26 paths: two 2^25-path wavefront chunks, the
+               25-bit path id at its maximum (mh_wavefront.hip kPidBits)
+  config 3(a)  512^2 @ 64 = 2^24 paths: one chunk of the fused PRB bounce
   config 3(b)  a 64x64x3 bitmap: the 48 KiB per-workgroup LDS texel
                accumulator exactly full, on a persistent grid whose threads
                loop over many samples (mh_kernels.hip k_prb_backward)
@@ -69,7 +69,7 @@ def test_config2_film_parity():
     integ = mi.load_dict({"type": "path", "max_depth": 8})
     st = A.Stats()
     film = mi.render_film(scene, integ, seed=0, spp=256, stats=st).cpu().numpy()
-    assert st.mode == 2 and st.n_trace_launches == 4 * 8, (st.mode, st.n_trace_launches)  # 4 chunks x 8 bounces
+    assert st.mode == 2 and st.n_trace_launches == 2 * 8, (st.mode, st.n_trace_launches)  # 2 chunks x 8 bounces
     ref = O.render(scene, integ, seed=0, spp=256)
     assert ref[..., 3].min() > 0
     film_parity(film, ref)
@@ -78,21 +78,21 @@ def test_config2_film_parity():
 
 
 def test_config2_samples_at_the_chunk_limit():
-    """Slab [192, 256) of every pixel: exactly 2^24 paths in one wavefront
-    chunk (path ids up to 2^24 - 1); samples of pixels spread over the film,
-    the last one included, vs the oracle's lanes pixel * 256 + [192, 256)."""
+    """Slab [128, 256) of every pixel: exactly 2^25 paths in one wavefront
+    chunk (path ids up to 2^25 - 1); samples of pixels spread over the film,
+    the last one included, vs the oracle's lanes pixel * 256 + [128, 256)."""
     mi = _mi()
     from mitsuba_hip import _abi as A
     scene = cbox(mi, 512, 256)
     integ = mi.load_dict({"type": "path", "max_depth": 8})
-    L, pos = gpu_samples(mi, scene, integ, 0, 256, 192, 256, A.FLAG_WAVEFRONT)
-    assert L.shape[0] == 1 << 24
+    L, pos = gpu_samples(mi, scene, integ, 0, 256, 128, 256, A.FLAG_WAVEFRONT)
+    assert L.shape[0] == 1 << 25
     pixels = np.unique(np.concatenate([np.linspace(0, 512 * 512 - 1, 200).astype(np.int64),
                                        [512 * 512 - 1, 512 * 256, 1]]))
     exact = []
     for p in pixels:
-        rL, rpos, _ = O.sample_range(scene, integ, 0, 256, p * 256 + 192, p * 256 + 256)
-        g = slice(p * 64, p * 64 + 64)
+        rL, rpos, _ = O.sample_range(scene, integ, 0, 256, p * 256 + 128, p * 256 + 256)
+        g = slice(p * 128, p * 128 + 128)
         np.testing.assert_array_equal(pos[g], rpos)
         exact.append(np.all(L[g] == rL, axis=1))
     exact = np.concatenate(exact)
