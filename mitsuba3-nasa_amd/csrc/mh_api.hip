@@ -98,6 +98,7 @@ struct mh_scene {
     DevBuf nodes, nodes4, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, film4, alpha_px, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
+    std::vector<uint8_t> meta_host;  // the bytes last uploaded to grad_meta (upload_slots)
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     DevBuf wf_ws_bmp;  // wavefront PRB with a bitmap parameter: vertex records (WfBmp)
@@ -645,6 +646,12 @@ static double now_ms() {
         .count();
 }
 
+// MH_FLAG_DEVICE_POINTERS | MH_FLAG_NO_SYNC without stats: nothing is read
+// back to the host, so the call returns with its work enqueued on the stream
+static bool async_call(uint32_t flags, const mh_stats *stats) {
+    return (flags & MH_FLAG_DEVICE_POINTERS) && (flags & MH_FLAG_NO_SYNC) && !stats;
+}
+
 int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
               uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
     ScopedPhase phase_("Render");
@@ -773,6 +780,9 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
+    // asynchronous call (device film, no stats): return once the work is
+    // enqueued on the scene's stream, as a stream-ordered library op does
+    if (async_call(flags, stats)) return MH_OK;
     unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
     std::vector<uint32_t> wctr;
     if (wavefront) {
@@ -953,7 +963,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
                         s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr, deterministic(flags)));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
+    if (!async_call(flags, nullptr)) MH_HIP(hipStreamSynchronize(st));
     return MH_OK;
 }
 
@@ -1049,10 +1059,18 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     memcpy(meta.data() + o_bufs, bufs.data(), kMaxParams * 8);
     memcpy(meta.data() + o_sig, P.sigma_slot.data(), P.sigma_slot.size() * 4);
     memcpy(meta.data() + o_alb, P.albedo_slot.data(), P.albedo_slot.size() * 4);
-    e = s->grad_meta.alloc(meta_bytes);
-    if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(s->grad_meta.ptr, meta.data(), meta_bytes, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return e;
+    // uploaded only when it changes (a new parameter set or reallocated slot
+    // buffers), then with a stream sync; repeated calls with the same
+    // parameters stay asynchronous
+    if (!(s->grad_meta.ptr && s->meta_host == meta)) {
+        e = s->grad_meta.alloc(meta_bytes);
+        if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(s->grad_meta.ptr, meta.data(), meta_bytes, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return e;
+        e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        s->meta_host = meta;
+    }
     const uint8_t *mb = s->grad_meta.as<uint8_t>();
     ga.slot_of_tex = reinterpret_cast<const int32_t *>(mb + o_slot);
     ga.is_rgb = reinterpret_cast<const uint32_t *>(mb + o_isrgb);
@@ -1248,6 +1266,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             for (size_t i = 0; i < c; ++i) grads[k][i] += host_tmp[i];
         }
     }
+    if (async_call(flags, stats)) return MH_OK;  // gradients stay stream-ordered on the device
     unsigned long long ctr[2] = {0, 0};
     std::vector<uint32_t> wctr(wf_ctr_words * wf_chunks);
     if (wavefront)
@@ -1367,6 +1386,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     MH_HIP(hipEventRecord(s->ev1, st));
     if (!dev) MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
+    if (async_call(flags, stats)) return MH_OK;
     unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
     MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     MH_HIP(hipMemcpyAsync(&n_invalid, invalid, sizeof(n_invalid), hipMemcpyDeviceToHost, st));

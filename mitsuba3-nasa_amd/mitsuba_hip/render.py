@@ -10,6 +10,7 @@ tensors (torch is plumbing here: device memory + streams).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -43,6 +44,14 @@ def _device_index(device) -> int:
             raise A.MitsubaHipError("mitsuba_hip: no HIP device available (hip_ad_rgb has no CPU fallback)")
         return torch.cuda.current_device()
     return torch.device(device).index or 0
+
+
+# MH_ASYNC_CALLS=1: the wrappers return once their kernels are enqueued on
+# the current stream (torch-op semantics, MH_FLAG_NO_SYNC).  Off by default:
+# the bench step measured 36.7 ms with a sync per call and 38.1-40.2 ms
+# without, its PRB bounce launches running ~9 % slower back to back
+# 
+_NO_SYNC = A.FLAG_NO_SYNC if os.environ.get("MH_ASYNC_CALLS") == "1" else 0
 
 
 def _ptr(t) -> C.c_void_p:
@@ -184,7 +193,9 @@ def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int
     if film is None:
         film = torch.empty((scene.height, scene.width, A.film_channels(scene.desc.sensor.pixel_format)),
                            dtype=torch.float32, device=f"cuda:{dev}")
-    flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_ACCUMULATE if accumulate else 0)
+    # stream-ordered like a torch op: the call returns once its kernels are
+    # enqueued (a stats request reads counters back, which synchronises)
+    flags = A.FLAG_DEVICE_POINTERS | _NO_SYNC | (A.FLAG_ACCUMULATE if accumulate else 0)
     flags |= {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "wavefront": A.FLAG_WAVEFRONT}[mode]
     flags |= A.FLAG_DETERMINISTIC if deterministic else 0
     ic = integrator.c()
@@ -199,7 +210,7 @@ def develop(scene: Scene, film, device=None):
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
     ch = A.image_channels(scene.desc.sensor.pixel_format)
     out = torch.empty((scene.height, scene.width, ch), dtype=torch.float32, device=film.device)
-    A.check(A.lib().mh_develop(h, _ptr(film.contiguous()), _ptr(out), A.FLAG_DEVICE_POINTERS))
+    A.check(A.lib().mh_develop(h, _ptr(film.contiguous()), _ptr(out), A.FLAG_DEVICE_POINTERS | _NO_SYNC))
     return out
 
 
@@ -209,7 +220,8 @@ def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, devic
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
     w = torch.empty((scene.height, scene.width), dtype=torch.float32, device=f"cuda:{dev}")
     A.check(A.lib().mh_prb_weights(h, seed, spp, spp_begin, spp_end, _ptr(w),
-                                   A.FLAG_DEVICE_POINTERS | (A.FLAG_DETERMINISTIC if deterministic else 0)))
+                                   A.FLAG_DEVICE_POINTERS | _NO_SYNC |
+                                   (A.FLAG_DETERMINISTIC if deterministic else 0)))
     return w
 
 
@@ -264,7 +276,7 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     A.check(A.lib().mh_render_backward(
         h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(grad_in),
         _ptr(weights) if weights is not None else None, len(keys), tex, ptrs,
-        A.FLAG_DEVICE_POINTERS | {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "replay": A.FLAG_PRB_REPLAY}[mode],
+        A.FLAG_DEVICE_POINTERS | _NO_SYNC | {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "replay": A.FLAG_PRB_REPLAY}[mode],
         C.byref(stats) if stats is not None else None))
     return outs
 
@@ -306,7 +318,7 @@ def render_forward(scene: Scene, params: SceneParameters, tangents: Dict[str, ob
     film = torch.empty((scene.height, scene.width, A.film_channels(scene.desc.sensor.pixel_format)),
                        dtype=torch.float32, device=f"cuda:{dev}")
     ic = integrator.c()
-    flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_DETERMINISTIC if deterministic else 0)
+    flags = A.FLAG_DEVICE_POINTERS | _NO_SYNC | (A.FLAG_DETERMINISTIC if deterministic else 0)
     A.check(A.lib().mh_render_forward(h, C.byref(ic), seed, spp, spp_begin, spp_end, len(keys), ids, ptrs,
                                       _ptr(film), flags, C.byref(stats) if stats is not None else None))
     return develop(scene, film) if develop_image else film
