@@ -26,6 +26,9 @@
  *   mh_render_backward
  *       RBIntegrator.render_backward                   src/python/python/ad/integrators/common.py:828-983
  *       (+ PRBIntegrator.sample adjoint mode           src/python/python/ad/integrators/prb.py:59-257)
+ *   mh_render_forward
+ *       RBIntegrator.render_forward                    src/python/python/ad/integrators/common.py:696-826
+ *       (+ PRBIntegrator.sample forward mode           src/python/python/ad/integrators/prb.py:244-248)
  *   mh_trace_closest / mh_trace_shadow
  *       Scene::ray_intersect_preliminary_gpu / ray_test_gpu (the OptiX slot)
  *       src/render/scene_optix.inl:592-721, include/mitsuba/render/optix/common.h:43-58
@@ -94,7 +97,10 @@ enum { MH_INTEGRATOR_PATH = 0, MH_INTEGRATOR_VOLPATH = 1, MH_INTEGRATOR_PRB = 2,
 enum {
     MH_FLAG_DEVICE_POINTERS = 1u << 0,  /* in/out buffers are device pointers on the scene's device */
     MH_FLAG_ACCUMULATE      = 1u << 1,  /* mh_render: add into `film_rgbw` instead of overwriting */
-    MH_FLAG_NO_SYNC         = 1u << 2,  /* do not synchronise the stream before returning */
+    MH_FLAG_NO_SYNC         = 1u << 2,  /* do not synchronise the stream before returning: with
+                                           MH_FLAG_DEVICE_POINTERS and stats == NULL, mh_render /
+                                           mh_prb_weights / mh_render_backward / mh_render_forward /
+                                           mh_develop return once their work is enqueued */
     MH_FLAG_MEGAKERNEL      = 1u << 3,  /* mh_render: force the per-lane megakernel */
     MH_FLAG_WAVEFRONT       = 1u << 4,  /* mh_render: force the wavefront (trace/shade/shadow) kernels */
     MH_FLAG_PRB_REPLAY      = 1u << 5,  /* mh_render_backward: primal + adjoint replay even for rgb params */

@@ -53,6 +53,15 @@ def main():
                                                mode=mode))
         print(json.dumps({"config": f"3(b): prb grad wrt white 64^2 bitmap, 512^2 @ 64 ({mode})",
                           "Msamples_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 2)}), flush=True)
+    # render_forward (common.py:696-826): forward-mode gradient images
+    tw = {"white.reflectance.value": torch.tensor([1.0, 0.5, 0.25], device="cuda")}
+    dt = timeit(lambda: mi.render_forward(scene, params, tw, prb, seed=sg, spp=64))
+    print(json.dumps({"config": "render_forward: prb wrt white rgb, 512^2 @ 64",
+                      "Msamples_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 2)}), flush=True)
+    tb = {"white.reflectance.data": torch.ones(tuple(pb["white.reflectance.data"].shape), device="cuda")}
+    dt = timeit(lambda: mi.render_forward(sb, pb, tb, prb, seed=sg, spp=64))
+    print(json.dumps({"config": "render_forward: prb wrt white 64^2 bitmap, 512^2 @ 64",
+                      "Msamples_s": round(n / dt / 1e6, 1), "ms": round(dt * 1e3, 2)}), flush=True)
 
 
 if __name__ == "__main__":
