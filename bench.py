@@ -262,7 +262,7 @@ def main():
         roofline = roofs[0][1] if roofs else None
         roofline_other = roofs[1][1] if len(roofs) > 1 else None
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N = 1 only
             cpu = cpu_baseline(scene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)
         line = {
             "metric": "Msamples/s (pixels×spp/s) fwd + PRB grad, cornell_box 512²; 1/2/4/8 GPU",
