@@ -144,6 +144,40 @@ def test_render_forward_adjoint_identity_config3():
     assert abs(lhs - rhs) <= 2e-3 * abs(rhs), (lhs, rhs)
 
 
+def test_render_forward_adjoint_identity_config3b():
+    """Config 3(b)'s size (64^2 x 3 bitmap, 512^2 @ 64): the tangent texels are
+    gathered by tex_eval's bilinear taps, the backward scatters through the
+    same taps -- the two are adjoint."""
+    mi = _mi()
+    import torch
+    scene = mi.load_dict(mi.cornell_box_bitmap(64, 512, 512, 64))
+    integ = mi.load_dict({"type": "prb", "max_depth": 8})
+    params = mi.traverse(scene)
+    key = "white.reflectance.data"
+    t = np.random.default_rng(5).standard_normal(tuple(params[key].shape)).astype(np.float32)
+    img = _gpu_forward(mi, scene, params, {key: t}, integ, 4, 64)
+    gi = np.random.default_rng(6).random((512, 512, 3)).astype(np.float32) / (512 * 512 * 3)
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), [key], integ, seed=4, spp=64)[0]
+    lhs = float((gi.astype(np.float64) * img).sum())
+    rhs = float((g.cpu().numpy().astype(np.float64) * t).sum())
+    assert abs(lhs - rhs) <= 2e-3 * max(abs(rhs), 1e-12), (lhs, rhs)
+
+
+def test_render_forward_sample_slabs_add_up():
+    """Sample-slab sharding of the forward-mode film: the
+    films of slabs [0, 8) and [8, 16) sum to the one-call film."""
+    mi = _mi()
+    import torch
+    scene = _cbox(mi, 48, 40, 16)
+    integ = mi.load_dict({"type": "prb", "max_depth": 8})
+    params = mi.traverse(scene)
+    t = {"white.reflectance.value": torch.tensor([1.0, 2.0, 0.5], device="cuda")}
+    full = mi.render_forward(scene, params, t, integ, seed=9, spp=16, develop_image=False).cpu().numpy()
+    parts = [mi.render_forward(scene, params, t, integ, seed=9, spp=16, spp_begin=b, spp_end=e,
+                               develop_image=False).cpu().numpy() for b, e in ((0, 8), (8, 16))]
+    np.testing.assert_allclose(parts[0] + parts[1], full, rtol=1e-5, atol=1e-6)
+
+
 def test_render_forward_torch_forward_ad():
     """mi.render under torch.autograd.forward_ad: _RenderOp.jvp runs
     render_forward at (seed_grad, spp_grad), as _RenderOp.forward does
