@@ -1361,9 +1361,22 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     }
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 256, st));
     const uint32_t S_ = L.s_end - L.s_begin;
-    const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, (1ull << 25) / S_));
+    const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, wf_max_chunk() / S_));
     const uint64_t plane = (uint64_t)chunk_px * S_;
     MH_HIP(s->work.alloc(plane * (alpha ? 6 : 5) * sizeof(float)));
+    // prb on packet-engine scenes: the fused forward-mode wavefront
+    // (k_wf_bounce_fwd); prbvolpath, larger scenes or MH_FLAG_MEGAKERNEL /
+    // MH_MODE=mega: the per-sample kernel (k_render_forward)
+    const char *env_mode = getenv("MH_MODE");
+    const bool wavefront = in->type == MH_INTEGRATOR_PRB && wf_fused(s->S) && in->max_depth >= 1 &&
+                           in->max_depth <= 64 && !(flags & MH_FLAG_MEGAKERNEL) && !(env_mode && !strcmp(env_mode, "mega"));
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
+    if (wavefront) {
+        MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(plane)));
+        MH_HIP(s->wf_ws_prb.alloc(wf_prb_workspace_bytes(plane)));
+        MH_HIP(s->wf_ctr.alloc((size_t)wf_counter_words(in->max_depth) * 4));
+    }
     const bool fast_splat = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN && s->S.rfilter_radius > 1.5f &&
                             s->S.rfilter_radius <= 2.5f;
     const int coalesce = L.spp_pp >= 4;  // block.set_coalesce(... and spp >= 4) (common.py:795-796)
@@ -1375,8 +1388,13 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         const uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
         const LaneMap lm = lane_map(L, (uint32_t)p0);
         const uint64_t n = (uint64_t)npx * S_;
-        MH_HIP(launch_render_forward(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), ga,
-                                     s->counters.as<unsigned long long>(), st, alpha));
+        if (wavefront)
+            MH_HIP(launch_wavefront_fwd(s->S, *in, lm, seed_value, n, ga.slot_of_tex, ga.bufs, ga.is_rgb,
+                                        s->work.as<float>(), plane, alpha, s->wf_ws.ptr, s->wf_ws_prb.ptr, plane,
+                                        s->wf_ctr.as<uint32_t>(), in->max_depth, wf_grid(wf_blocks(cus)), st));
+        else
+            MH_HIP(launch_render_forward(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), ga,
+                                         s->counters.as<unsigned long long>(), st, alpha));
         MH_HIP(launch_splat(s->S, lm, kSplatFilm, fast_splat, npx, 1, n, plane, s->work.as<float>(), film4,
                             seed_value, coalesce, st, invalid, determ));
         if (alpha)
@@ -1402,7 +1420,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         stats->ms_kernel = ms;
         stats->ms_trace = 0.f;
         stats->n_trace_launches = 0;
-        stats->mode = 0;
+        stats->mode = wavefront ? 2u : 0u;  // fused wavefront / per-sample kernel
         stats->invalid_samples = (uint32_t)std::min<unsigned long long>(n_invalid, 0xffffffffull);
     }
     return MH_OK;

@@ -106,6 +106,13 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 uint32_t grid, float *partial, hipStream_t st,
                                 hipEvent_t *span = nullptr,               // span: 2 events around the bounce launches
                                 const WfBitmapArgs *bmp = nullptr);      // one bitmap parameter (or none)
+// render_forward of `prb` on the fused wavefront (packet-engine scenes): the
+// tangent radiance of every path written to the sample planes of launch_render
+hipError_t launch_wavefront_fwd(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                                uint64_t n, const int32_t *slot_of_tex, float *const *tangents,
+                                const uint32_t *is_rgb, float *out, uint64_t plane, int alpha, void *ws,
+                                void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
+                                hipStream_t st);
 hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n_rgb, float *const *bufs,
                                  hipStream_t st);
 // max of a float array (gridvolume max for the majorant), as an order-preserving

@@ -1318,6 +1318,230 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
     flush_partial(acc, q);
 }
 
+// ---------------------------------------------------------------------------
+// Forward-mode PRB on the fused wavefront (render_forward, common.py:696-826):
+// prb_forward (mh_shading.hpp) as bounce kernels.  Per path the dL planes of
+// WfPrb carry the tangent radiance and the first three A planes the tangent
+// sum T = sum c_k t_k; a contribution e_j adds e_j T / pi, an unoccluded NEE
+// sample also its direct term (em_weight beta mis cos / pi) t_k, and a path
+// that ends writes dL to the sample planes of the film splat (L, pos, alpha:
+// the layout of k_wf_bounce), which the generating bounce fills with pos.
+// Tangents: the slot table and tangent arrays of a GradArgs (GradCtx::fwd).
+// ---------------------------------------------------------------------------
+struct WfFwdOut {
+    float *out;          // sample planes: L.r L.g L.b pos.x pos.y [alpha]
+    uint64_t plane;      // floats between planes
+    int alpha;
+    const int32_t *slot_of_tex;
+    float *const *tan;   // per slot: tangent values (rgb: 3, bitmap: the texels)
+    const uint32_t *is_rgb;
+};
+
+template <bool Gen>
+__global__ void __launch_bounds__(256, MH_BOUNCE_PRB_WAVES)
+k_wf_bounce_fwd(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q, int cur,
+                uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, uint64_t n_total, WfFwdOut fo) {
+    extern __shared__ uint4 lds[];
+    const SegIter it = seg_iter();
+    uint32_t n;
+    if (Gen) {
+        const uint64_t b0 = (uint64_t)it.seg * seg_cap;
+        n = b0 >= n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, n_total - b0);
+        if (blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
+    } else {
+        n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!block_has_stride_work(it, n)) return;
+    float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
+    stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
+    const DScene S = stage_tables(S0, lds);
+    uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
+                   (threadIdx.x >> 6) * S0.stack_size;
+    uint8_t *dscr = reinterpret_cast<uint8_t *>(lds) + fused_scratch_offset(S0) + (threadIdx.x >> 6) * kDeferScratch;
+    GradCtx tg;  // tangent lookups only (tex_tangent)
+    tg.slot_of_tex = fo.slot_of_tex;
+    tg.bufs = fo.tan;
+    tg.is_rgb = fo.is_rgb;
+    uint32_t n_shadow = 0;
+    const uint32_t sbase = it.seg * seg_cap;
+    const int nxt = cur ^ 1;
+    const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
+    for (uint32_t itr = 0; itr < n_iter; ++itr) {
+        const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
+        bool alive = false, shadow = false;
+        uint32_t pid = 0, depth = 0;
+        RayT ray{v3(0, 0, 0), v3(0, 0, 1), -1.f}, sray{v3(0, 0, 0), v3(0, 0, 1), -1.f};
+        V3 beta, prev_p, dL = v3(0, 0, 0), T = v3(0, 0, 0), G = v3(0, 0, 0);
+        float prev_pdf = 1.f;
+        Pcg rng;
+        const uint32_t j = sbase + i;
+        uint64_t gen_state = 0, gen_inc = 0;
+        if (i < n) {
+            if (Gen) {  // camera ray and PCG32 state (integrator.cpp:1139-1176)
+                pid = j;
+                uint32_t lane, px, py;
+                lane_of(lm, pid, lane, px, py);
+                Pcg g;
+                g.seed(seed_value, lane);
+                const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
+                ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
+                                 __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
+                gen_state = g.state;
+                gen_inc = g.inc;
+                fo.out[3 * fo.plane + pid] = sx;
+                fo.out[4 * fo.plane + pid] = sy;
+            } else {
+                const uint32_t pd = w.pd[cur][j];
+                pid = pd & kPidMask;
+                depth = pd >> kPidBits;
+                ray.o = v3(w.ox[cur][j], w.oy[cur][j], w.oz[cur][j]);
+                ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
+                ray.maxt = w.mt[cur][j];
+            }
+        }
+        const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n, recs, dscr);
+        if (i < n) {
+            if (Gen) {
+                beta = v3(1.f, 1.f, 1.f);
+                prev_p = v3(0.f, 0.f, 0.f);
+                prev_pdf = 1.f;
+                rng.state = gen_state;
+            } else {
+                beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
+                prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
+                prev_pdf = w.ppdf[cur][j];
+                dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
+                T = v3(q.A(cur, 0)[j], q.A(cur, 1)[j], q.A(cur, 2)[j]);
+                rng.state = w.rng[cur][j];
+            }
+            const bool prev_delta = depth == 0;
+            const float eta = 1.f;
+            uint32_t lane, px, py;
+            lane_of(lm, pid, lane, px, py);
+            rng.inc = Gen ? gen_inc : pcg_inc(seed_value, lane);
+            SI si;
+            compute_si(S, ray, h, si);
+            const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
+            const bool smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+            bool active_next = !(in.hide_emitters && depth == 0 && !si.valid);
+            const uint32_t em = si.valid ? S.shapes[si.shape].emitter : S.environment;
+            if (em != MH_INVALID) {
+                float em_pdf = prev_delta ? 0.f : emitter_pdf_direction(S, em, si, prev_p);
+                float mis = mis_weight(prev_pdf, em_pdf);
+                V3 le = v3(0, 0, 0);
+                if (active_next)
+                    le = emitter_eval(S, em, si);
+                dL = dL + ((beta * mis) * le) * (T * kInvPi);
+            }
+            active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
+            const bool active_em0 = active_next && smooth;
+            float e0 = rng.next_float(), e1 = rng.next_float();
+            DirS ds;
+            ds.pdf = 0.f;
+            ds.d = v3(0, 0, 0);
+            ds.delta = false;
+            V3 em_weight = v3(0, 0, 0);
+            if (active_em0) {
+                em_weight = scene_sample_emitter_direction(S, si.p, e0, e1, ds);
+                if (ds.pdf != 0.f && nonzero(em_weight)) {
+                    shadow = true;
+                    sray = spawn_ray_to(si.p, si.n, ds.p);
+                }
+            }
+            V3 rho = v3(0, 0, 0);
+            if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
+            const bool tvtx = smooth && tg.slot_of_tex[S.bsdf_tex[b]] >= 0;
+            const V3 t = tvtx ? tex_tangent(S, S.bsdf_tex[b], si.uvx, si.uvy, tg) : v3(0, 0, 0);
+            if (shadow) {  // as if unoccluded; applied after the visibility test
+                V3 wo_em = to_local(si, ds.d);
+                V3 bsdf_value_em;
+                float bsdf_pdf_em;
+                diffuse_eval_pdf(rho, si.wi, wo_em, true, bsdf_value_em, bsdf_pdf_em);
+                float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
+                V3 beta_mis_em = beta * mis_em;
+                G = ((beta_mis_em * bsdf_value_em) * em_weight) * (T * kInvPi);
+                if (tvtx && si.wi.z > 0.f && wo_em.z > 0.f)
+                    G = G + (((em_weight * beta_mis_em) * wo_em.z) * kInvPi) * t;
+            }
+            (void)rng.next_float();
+            float s2x = rng.next_float(), s2y = rng.next_float();
+            V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
+            float bs_pdf = 0.f;
+            if (smooth && active_next) {
+                bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+                bs_pdf = kInvPi * bs_wo.z;
+                bsdf_weight = (si.wi.z > 0.f && bs_pdf > 0.f) ? rho : v3(0, 0, 0);
+            }
+            ray = spawn_ray(si.p, si.n, to_world(si, bs_wo));
+            beta = beta * bsdf_weight;
+            prev_p = si.p;
+            prev_pdf = bs_pdf;
+            float beta_max = hmax(beta);
+            active_next = active_next && beta_max != 0.f;
+            float rr_prob = fminf(beta_max * (eta * eta), 0.95f);
+            bool rr_active = depth >= in.rr_depth;
+            if (rr_active) beta = beta * rcp(rr_prob);
+            bool rr_continue = rng.next_float() < rr_prob;
+            active_next = active_next && (!rr_active || rr_continue);
+            if (tvtx) T = T + prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf) * t;
+            if (si.valid) depth += 1;
+            alive = active_next;
+        }
+        const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        if (alive) {
+            w.pd[nxt][slot_n] = pid | (depth << kPidBits);
+            w.ox[nxt][slot_n] = ray.o.x; w.oy[nxt][slot_n] = ray.o.y; w.oz[nxt][slot_n] = ray.o.z;
+            w.dx[nxt][slot_n] = ray.d.x; w.dy[nxt][slot_n] = ray.d.y; w.dz[nxt][slot_n] = ray.d.z;
+            w.mt[nxt][slot_n] = ray.maxt;
+            w.bx[nxt][slot_n] = beta.x; w.by[nxt][slot_n] = beta.y; w.bz[nxt][slot_n] = beta.z;
+            w.ppx[nxt][slot_n] = prev_p.x; w.ppy[nxt][slot_n] = prev_p.y; w.ppz[nxt][slot_n] = prev_p.z;
+            w.ppdf[nxt][slot_n] = prev_pdf;
+            w.rng[nxt][slot_n] = rng.state;
+            q.A(nxt, 0)[slot_n] = T.x; q.A(nxt, 1)[slot_n] = T.y; q.A(nxt, 2)[slot_n] = T.z;
+        }
+        // ---- visibility of the NEE sample; its tangent is charged if unoccluded
+        const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
+        if (shadow && sh.shape == MH_INVALID) dL = dL + G;
+        if (alive) {
+            q.dl(nxt, 0)[slot_n] = dL.x; q.dl(nxt, 1)[slot_n] = dL.y; q.dl(nxt, 2)[slot_n] = dL.z;
+        } else if (i < n) {  // the path ends: its tangent radiance and validity (prb.py:253-257)
+            fo.out[pid] = dL.x;
+            fo.out[fo.plane + pid] = dL.y;
+            fo.out[2 * fo.plane + pid] = dL.z;
+            if (fo.alpha) fo.out[5 * fo.plane + pid] = depth != 0 ? 1.f : 0.f;
+        }
+        n_shadow += (uint32_t)__popcll(__ballot(shadow));
+    }
+    if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
+}
+
+hipError_t launch_wavefront_fwd(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                                uint64_t n, const int32_t *slot_of_tex, float *const *tangents,
+                                const uint32_t *is_rgb, float *out, uint64_t plane, int alpha, void *ws,
+                                void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces, uint32_t grid,
+                                hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (n > (1ull << kPidBits) || n_bounces > kMaxWfBounces || !wf_fused(S)) return hipErrorInvalidValue;
+    WfState w = carve(ws, cap);
+    WfPrb q = carve_prb(ws_prb, cap, nullptr, slot_of_tex, 1);
+    hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
+    if (e != hipSuccess) return e;
+    const uint32_t seg_cap = seg_len(n);
+    const size_t sh_fused = fused_lds_bytes(S);
+    const WfFwdOut fo{out, plane, alpha, slot_of_tex, tangents, is_rgb};
+    for (uint32_t b = 0; b < n_bounces; ++b) {
+        uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
+        const int cur = (int)(b & 1);
+        if (b == 0)
+            hipLaunchKernelGGL(k_wf_bounce_fwd<true>, dim3(grid), dim3(256), sh_fused, st, S, in, lm, seed_value, w, q,
+                               cur, seg_cap, c, cn, n, fo);
+        else
+            hipLaunchKernelGGL(k_wf_bounce_fwd<false>, dim3(grid), dim3(256), sh_fused, st, S, in, lm, seed_value, w,
+                               q, cur, seg_cap, c, cn, n, fo);
+    }
+    return hipGetLastError();
+}
+
 // Texel gradients of the logged bitmap vertices of one chunk (see WfBmp):
 // adj_k = D_k + dL (L_total - P_k) q_k / pi per record, spread over the
 // bilinear taps (tex_backward's weights).  Lane l of a wave takes path

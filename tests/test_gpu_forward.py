@@ -59,15 +59,23 @@ def _oracle_forward(scene, params, tans, integ, seed, spp):
     return O.develop(film, scene.desc.sensor.pixel_format)
 
 
+@pytest.mark.parametrize("mode", ["auto", "mega"])
 @pytest.mark.parametrize("fmt", [None, "rgba", "luminance"])
-def test_render_forward_rgb_parity(fmt):
+def test_render_forward_rgb_parity(fmt, mode, monkeypatch):
+    """auto: the fused forward-mode wavefront (k_wf_bounce_fwd); mega: the
+    per-sample kernel (k_render_forward, prb_forward)."""
+    if mode == "mega":
+        monkeypatch.setenv("MH_MODE", "mega")
     mi = _mi()
+    from mitsuba_hip import _abi as A
     scene = _cbox(mi, 40, 32, 16, fmt)
     integ = mi.load_dict({"type": "prb", "max_depth": 8})
     params = mi.traverse(scene)
     tans = {"white.reflectance.value": np.array([1.0, -0.5, 0.25], np.float32),
             "red.reflectance.value": np.array([0.3, 0.2, 0.1], np.float32)}
-    img = _gpu_forward(mi, scene, params, tans, integ, 11, 16)
+    st = A.Stats()
+    img = _gpu_forward(mi, scene, params, tans, integ, 11, 16, stats=st)
+    assert st.mode == (2 if mode == "auto" else 0)
     ref = _oracle_forward(scene, params, tans, integ, 11, 16)
     assert img.shape == ref.shape
     _close(img, ref)
@@ -75,8 +83,11 @@ def test_render_forward_rgb_parity(fmt):
         assert np.allclose(img[..., 3], ref[..., 3], atol=1e-5)
 
 
+@pytest.mark.parametrize("mode", ["auto", "mega"])
 @pytest.mark.parametrize("channels", [3, 1])
-def test_render_forward_bitmap_parity(channels):
+def test_render_forward_bitmap_parity(channels, mode, monkeypatch):
+    if mode == "mega":
+        monkeypatch.setenv("MH_MODE", "mega")
     mi = _mi()
     d = mi.cornell_box_bitmap(tex_res=8, width=32, height=24, spp=16)
     if channels == 1:
