@@ -978,7 +978,7 @@ struct Slots {
     std::vector<size_t> counts;
     std::vector<uint32_t> slot_of_param;
     uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0, bmp_tex = 0;
-    std::vector<uint8_t> meta;  // host copy of the meta block (alive until the caller's stream sync)
+    std::vector<uint8_t> meta;  // host image of the meta block (uploaded by upload_slots when it changed)
 };
 
 static int build_slots(const mh_scene *s, uint32_t n_params, const uint32_t *param_tex, bool vol, const char *api,
@@ -1035,8 +1035,7 @@ static int build_slots(const mh_scene *s, uint32_t n_params, const uint32_t *par
     return MH_OK;
 }
 
-// per-slot device buffers (s->tmp_c, zeroed) and the meta block (copied from
-// P.meta, which the caller keeps until its stream synchronises)
+// per-slot device buffers (s->tmp_c, zeroed) and the meta block
 // slot_of_tex | is_rgb | bufs | sigma_slot | albedo_slot (s->grad_meta)
 static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vector<float *> &bufs, GradArgs &ga) {
     size_t total = 0;
