@@ -783,6 +783,10 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     // asynchronous call (device film, no stats): return once the work is
     // enqueued on the scene's stream, as a stream-ordered library op does
     if (async_call(flags, stats)) return MH_OK;
+    if (!stats && !getenv("MH_VW_DEBUG")) {  // nothing to read back: only the call's own sync
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    }
     unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
     std::vector<uint32_t> wctr;
     if (wavefront) {
@@ -1266,6 +1270,10 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         }
     }
     if (async_call(flags, stats)) return MH_OK;  // gradients stay stream-ordered on the device
+    if (!stats) {
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    }
     unsigned long long ctr[2] = {0, 0};
     std::vector<uint32_t> wctr(wf_ctr_words * wf_chunks);
     if (wavefront)
@@ -1404,6 +1412,10 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     MH_HIP(hipEventRecord(s->ev1, st));
     if (!dev) MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
     if (async_call(flags, stats)) return MH_OK;
+    if (!stats) {
+        MH_HIP(hipStreamSynchronize(st));
+        return MH_OK;
+    }
     unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
     MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     MH_HIP(hipMemcpyAsync(&n_invalid, invalid, sizeof(n_invalid), hipMemcpyDeviceToHost, st));
