@@ -12,7 +12,9 @@
   (gradients are not covered: the wavefront queues are compacted by
   wave-ballot atomics, so the order in which a thread's registers
   accumulate paths varies from run to run);
-* roctx ranges: the library links the roctx API (the ScopedPhase ranges).
+* roctx ranges: the library links the roctx API (the ScopedPhase ranges);
+* asynchronous entry points (MH_FLAG_NO_SYNC): same results once the stream
+  drains.
 """
 import ctypes as C
 
@@ -114,3 +116,41 @@ def test_deterministic_weights_and_alpha():
     assert np.array_equal(w1, w2)
     np.testing.assert_allclose(w1, mi.prb_weights(scene, 9, 8).cpu().numpy(), rtol=1e-5)
     np.testing.assert_allclose(w1, a[..., 4], rtol=1e-5)  # the film's W channel is the same sum
+
+
+def test_async_entry_points_match_synchronous():
+    """MH_FLAG_DEVICE_POINTERS | MH_FLAG_NO_SYNC without stats: mh_render,
+    mh_prb_weights and mh_render_backward return with their work enqueued on
+    the scene's stream; once the stream drains, the film, W image and
+    gradient equal the synchronous calls' (deterministic splat: bitwise)."""
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    scene = mi.load_dict(_cbox(mi, 64, 48, 16))
+    path = mi.load_dict({"type": "path", "max_depth": 8})
+    prb = mi.load_dict({"type": "prb", "max_depth": 8})
+    params = mi.traverse(scene)
+    key = "white.reflectance.value"
+    st = torch.cuda.current_stream()
+    h = scene.handle(0, st.cuda_stream)
+    lib = A.lib()
+    P = lambda t: C.c_void_p(t.data_ptr())
+    results = []
+    for flags in (A.FLAG_DEVICE_POINTERS | A.FLAG_DETERMINISTIC,
+                  A.FLAG_DEVICE_POINTERS | A.FLAG_DETERMINISTIC | A.FLAG_NO_SYNC):
+        film = torch.full((48, 64, 4), -1.0, device="cuda")
+        w = torch.full((48, 64), -1.0, device="cuda")
+        gi = torch.full((48, 64, 3), 1.0 / (48 * 64 * 3), device="cuda")
+        g = torch.zeros(3, device="cuda")
+        ic_f, ic_b = path.c(), prb.c()
+        A.check(lib.mh_render(h, C.byref(ic_f), 3, 16, 0, 0, P(film), flags, None))
+        A.check(lib.mh_prb_weights(h, 5, 16, 0, 0, P(w), flags))
+        ids = (C.c_uint32 * 1)(params.param_id(key))
+        ptrs = (C.c_void_p * 1)(g.data_ptr())
+        A.check(lib.mh_render_backward(h, C.byref(ic_b), 5, 16, 0, 0, P(gi), P(w), 1, ids, ptrs, flags, None))
+        torch.cuda.synchronize()
+        results.append((film.cpu().numpy(), w.cpu().numpy(), g.cpu().numpy()))
+    (f0, w0, g0), (f1, w1, g1) = results
+    assert np.array_equal(f0, f1) and np.array_equal(w0, w1)
+    assert f0.min() >= 0.0 and w0.min() > 0.0
+    np.testing.assert_allclose(g1, g0, rtol=1e-5)
