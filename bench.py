@@ -202,12 +202,12 @@ def main():
         # events on the scene's stream (stats.ms_trace / n_trace_launches).
         # Algorithmic bytes: the path state streamed per path-bounce (the BVH,
         # pair records and shading tables are LDS / scalar-cache resident):
-        #   k_wf_bounce      80 B state (pd 4, ray 28, throughput 12, prev_p 12,
-        #                    prev_pdf 4, PCG32 8, L 12) read by every non-first
+        #   k_wf_bounce      84 B state (pd 4, ray 28, throughput 12, prev_p 12,
+        #                    prev_pdf 4, PCG32 state 8 + TEA word 4, L 12) read by every non-first
         #                    bounce and written by every survivor; a finished
         #                    path writes L (12 B); the first bounce writes the
         #                    film position (8 B) of every sample
-        #   k_wf_bounce_prb  104 B (the same without L, + dL 12 + A_s 12) read and
+        #   k_wf_bounce_prb  108 B (the same without L, + dL 12 + A_s 12) read and
         #                    written alike; the first bounce reads the sample's
         #                    grad / W texel (16 B)
         # with R = rays (sum of queue lengths), N = samples: survivors R - N.
@@ -255,9 +255,9 @@ def main():
 
         roofs = []
         if st_f.mode == 2:
-            roofs.append((st_f.ms_trace, roof("k_wf_bounce", st_f, 80.0, 12.0, 8.0)))
+            roofs.append((st_f.ms_trace, roof("k_wf_bounce", st_f, 84.0, 12.0, 8.0)))
         if not args.fwd_only and st_b.mode == 1 and st_b.n_trace_launches:
-            roofs.append((st_b.ms_trace, roof("k_wf_bounce_prb", st_b, 104.0, 0.0, 16.0)))
+            roofs.append((st_b.ms_trace, roof("k_wf_bounce_prb", st_b, 108.0, 0.0, 16.0)))
         roofs.sort(key=lambda x: -x[0])
         roofline = roofs[0][1] if roofs else None
         roofline_other = roofs[1][1] if len(roofs) > 1 else None

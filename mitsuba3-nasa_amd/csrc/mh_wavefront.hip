@@ -148,8 +148,11 @@ constexpr uint32_t kPkPlanes = 5, kPkExt = 3;
 struct WfPacked {
     float4 *base, *ext;
     uint64_t stride;  // float4 per plane
+    uint32_t *tea_base;  // ping-pong: the TEA word of the path's PCG32 increment (WfPrb::tea)
+    uint64_t tstride;    // uint32 per tea plane
     MH_DEV float4 *pl(int b, uint32_t k) const { return base + (uint64_t)(b * (int)kPkPlanes + (int)k) * stride; }
     MH_DEV float4 *ex(int b, uint32_t k) const { return ext + (uint64_t)(b * (int)kPkExt + (int)k) * stride; }
+    MH_DEV uint32_t *tea(int b) const { return tea_base + (uint64_t)b * tstride; }
 };
 static WfPacked carve_packed(void *ws, void *ws_ext, uint64_t cap) {
     cap = (cap + kSeg - 1) / kSeg * kSeg;
@@ -157,6 +160,9 @@ static WfPacked carve_packed(void *ws, void *ws_ext, uint64_t cap) {
     p.stride = align_up(cap * 16) / 16;
     p.base = reinterpret_cast<float4 *>(ws);
     p.ext = reinterpret_cast<float4 *>(ws_ext);
+    // two 4-B planes after the 2 x kPkPlanes records (inside wf_workspace_bytes)
+    p.tea_base = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws) + 2 * kPkPlanes * align_up(cap * 16));
+    p.tstride = align_up(cap * 4) / 4;
     return p;
 }
 
@@ -518,9 +524,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             }
             eta = 1.f;  // diffuse / null BSDFs: eta stays 1, only the camera vertex is delta
             const bool prev_delta = depth == 0;
-            uint32_t lane, px, py;
-            lane_of(lm, pid, lane, px, py);
-            rng.inc = Gen ? gen_inc : pcg_inc(seed_value, lane);
+            rng.inc = Gen ? gen_inc : (((uint64_t)w.tea(cur)[j] << 1) | 1u);
             SI si;
             compute_si(S, ray, h, si);
 
@@ -599,6 +603,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             w.pl(nxt, 1)[slot] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(pid | (depth << kPidBits)));
             w.pl(nxt, 2)[slot] = make_float4(tp.x, tp.y, tp.z, prev_pdf);
             w.pl(nxt, 3)[slot] = make_float4(prev_p.x, prev_p.y, prev_p.z, __uint_as_float((uint32_t)rng.state));
+            w.tea(nxt)[slot] = (uint32_t)(rng.inc >> 1);
         } else if (has && carry) {
             carry[pid] = rng.state;  // multi-pass: the next pass continues the stream
         }
@@ -764,11 +769,17 @@ struct WfPrb {
     MH_DEV float *dl(int k, int c) const { return base + (uint64_t)(k * (3 + kG) + c) * stride; }
     MH_DEV float *A(int k, int c) const { return base + (uint64_t)(k * (3 + kG) + 3 + c) * stride; }
     MH_DEV float *G(int c) const { return base + (uint64_t)(2 * (3 + kG) + c) * stride; }
+    // ping-pong k: the TEA word behind the path's PCG32 increment
+    // (inc = (v1 << 1) | 1, sampler.cpp:128-132): one 4-B load instead of
+    // re-running TEA (64 integer ops) and the lane map every bounce
+    MH_DEV uint32_t *tea(int k) const {
+        return reinterpret_cast<uint32_t *>(base + (uint64_t)(2 * (3 + kG) + kG + k) * stride);
+    }
 };
 
 size_t wf_prb_workspace_bytes(uint64_t cap) {
     cap = (cap + kSeg - 1) / kSeg * kSeg;
-    return (size_t)(6 + 2 * kG + kG) * align_up(cap * 4);
+    return (size_t)(6 + 2 * kG + kG + 2) * align_up(cap * 4);
 }
 
 static WfPrb carve_prb(void *ws, uint64_t cap, float *partial, const int32_t *slot_of_tex, uint32_t n_rgb) {
@@ -1163,9 +1174,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             }
             const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
             const float eta = 1.f;
-            uint32_t lane, px, py;
-            lane_of(lm, pid, lane, px, py);
-            rng.inc = Gen ? gen_inc : pcg_inc(seed_value, lane);
+            rng.inc = Gen ? gen_inc : (((uint64_t)q.tea(cur)[j] << 1) | 1u);
             SI si;
             compute_si(S, ray, h, si);
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
@@ -1273,6 +1282,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             w.ppx[nxt][slot_n] = prev_p.x; w.ppy[nxt][slot_n] = prev_p.y; w.ppz[nxt][slot_n] = prev_p.z;
             w.ppdf[nxt][slot_n] = prev_pdf;
             w.rng[nxt][slot_n] = rng.state;
+            q.tea(nxt)[slot_n] = (uint32_t)(rng.inc >> 1);
             q.dl(nxt, 0)[slot_n] = dL.x; q.dl(nxt, 1)[slot_n] = dL.y; q.dl(nxt, 2)[slot_n] = dL.z;
 #pragma unroll
             for (int kk = 0; kk < NR; ++kk)
@@ -1416,9 +1426,7 @@ k_wf_bounce_fwd(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             }
             const bool prev_delta = depth == 0;
             const float eta = 1.f;
-            uint32_t lane, px, py;
-            lane_of(lm, pid, lane, px, py);
-            rng.inc = Gen ? gen_inc : pcg_inc(seed_value, lane);
+            rng.inc = Gen ? gen_inc : (((uint64_t)q.tea(cur)[j] << 1) | 1u);
             SI si;
             compute_si(S, ray, h, si);
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
@@ -1497,6 +1505,7 @@ k_wf_bounce_fwd(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             w.ppx[nxt][slot_n] = prev_p.x; w.ppy[nxt][slot_n] = prev_p.y; w.ppz[nxt][slot_n] = prev_p.z;
             w.ppdf[nxt][slot_n] = prev_pdf;
             w.rng[nxt][slot_n] = rng.state;
+            q.tea(nxt)[slot_n] = (uint32_t)(rng.inc >> 1);
             q.A(nxt, 0)[slot_n] = T.x; q.A(nxt, 1)[slot_n] = T.y; q.A(nxt, 2)[slot_n] = T.z;
         }
         // ---- visibility of the NEE sample; its tangent is charged if unoccluded
