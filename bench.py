@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--res", type=int, default=512)
     p.add_argument("--spp", type=int, default=256, help="samples per pixel per GPU")
     p.add_argument("--max-depth", type=int, default=8)
-    p.add_argument("--cpu-seconds", type=float, default=24.0, help="budget of the CPU baseline (3 timed runs)")
+    p.add_argument("--cpu-seconds", type=float, default=24.0, help="budget of the CPU baseline (thread curve: 1, 4, all threads)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     p.add_argument("--fwd-only", action="store_true")
     p.add_argument("--backend", default="nccl",
@@ -77,8 +77,11 @@ def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
     """CPU baseline: the oracle -- the
     CPU restatement of llvm_ad_rgb (scalar C, no SIMD), kind 'port' -- on the
     host's cores, on a bounded sample of the same workload: the same scene and
-    integrators at a reduced spp sized so one run takes ~budget_s / 4.  One
-    warm-up run (the spp calibration), then the min of 3 timed runs."""
+    integrators at a reduced spp.  A thread curve (1, 4 and all the threads
+    this job may use): per point one warm-up run (the spp calibration), then
+    the min of 2 timed runs sized to ~budget_s / 8 each.  `value` is the
+    all-threads point; `per_core` and the linear extrapolation to every core
+    of the host are derived from it and labelled as such."""
     import numpy as np
     import oracle_py as O
     threads = cpu_threads()
@@ -87,22 +90,31 @@ def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
     gi = np.full((H, W, 3), 1.0 / (H * W * 3), np.float32)
     tex = [scene.params[key][1]]
 
-    def run(spp):
+    def run(spp, t):
         t0 = time.perf_counter()
-        O.render(scene, fwd, seed=0, spp=spp, threads=threads)
+        O.render(scene, fwd, seed=0, spp=spp, threads=t)
         if not fwd_only:
-            O.render_backward(scene, prb, 1, spp, gi, tex, [(3,)], threads=threads)
+            O.render_backward(scene, prb, 1, spp, gi, tex, [(3,)], threads=t)
         return time.perf_counter() - t0
 
-    t1 = run(1)  # warm-up + calibration
-    spp = int(max(1, min(spp_gpu, budget_s / 4 / max(t1, 1e-3))))
-    spp = 1 << max(0, spp.bit_length() - 1)
-    best = min(run(spp) for _ in range(3))
-    rate = H * W * spp / best / 1e6
-    return {"value": round(rate, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"cornell_box {W}x{H} @ {spp} spp, path fwd" + ("" if fwd_only else " + prb grad")
-                      + f"; min of 3 runs after 1 warm-up, {best:.2f} s each",
+    curve = []
+    for t in sorted({1, min(4, threads), threads}):
+        t1 = run(1, t)  # warm-up + calibration
+        spp = int(max(1, min(spp_gpu, budget_s / 8 / max(t1, 1e-3))))
+        spp = 1 << max(0, spp.bit_length() - 1)
+        best = min(run(spp, t) for _ in range(2)) if spp > 1 or t1 < budget_s / 8 else t1
+        curve.append({"threads": t, "spp": spp, "seconds": round(best, 3),
+                      "value": round(H * W * spp / best / 1e6, 4),
+                      "per_core": round(H * W * spp / best / 1e6 / t, 4)})
+    top = curve[-1]
+    return {"value": top["value"], "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"cornell_box {W}x{H} @ {top['spp']} spp, path fwd" + ("" if fwd_only else " + prb grad")
+                      + f" on {threads} threads; min of 2 runs after 1 warm-up, {top['seconds']:.2f} s each",
             "label": "CPU restatement of llvm_ad_rgb (oracle/libmh_oracle.so: scalar C, no SIMD)",
+            "thread_curve": curve, "per_core": top["per_core"],
+            "extrapolated_all_cores": {"value": round(top["per_core"] * nproc, 2), "cores": nproc,
+                                       "label": "linear extrapolation of per_core to every host core "
+                                                "(not measured: this job's CPU share is `cores`)"},
             "cpu_model": model, "nproc": nproc, "affinity": aff, "threads": threads}
 
 
@@ -244,7 +256,11 @@ def main():
             traffic, valu, clk = family(kname)
             r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                 "kernel_avg_us": round(us, 1), "algorithmic_bytes_per_launch": round(bytes_launch)}
+                 "kernel_avg_us": round(us, 1), "algorithmic_bytes_per_launch": round(bytes_launch),
+                 # everything the bytes come from, so the line alone reproduces them:
+                 # bytes = (2 S (R - N) + b_end N + b_first N) / launches
+                 "launches_per_step": launches, "rays_closest": int(R), "samples": int(N),
+                 "state_bytes": state_b, "end_bytes": per_death, "first_bytes": per_sample}
             if valu and clk:
                 r["valu_issue_frac"] = round(valu * 2.0 / (1024 * us * 1e-6 * clk * 1e9), 4)
                 r["valu_insts_per_launch"] = round(valu)
@@ -277,6 +293,10 @@ def main():
             "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
             "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
             "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),
+            "rays_closest_per_sample_prb": (round(st_b.rays_closest / max(1, n_local), 4)
+                                            if not args.fwd_only else None),
+            "rays_shadow_per_sample_prb": (round(st_b.rays_shadow / max(1, n_local), 4)
+                                           if not args.fwd_only else None),
             "roofline": roofline, "roofline_other": roofline_other, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

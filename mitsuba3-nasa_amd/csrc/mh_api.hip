@@ -629,6 +629,23 @@ static LaneMap lane_map(const Layout &L, uint32_t pixel_begin) {
 // backward's work head; bytes 256.. hold k_vol_sched's 8 queue heads
 constexpr int kCtrInvalid = 28;
 constexpr int kCtrPvpHead = 30;
+// [kCtrBounds]: rows of the splat kernels that would have read past their
+// input planes (skipped; the call then fails; none in a correct build)
+constexpr int kCtrBounds = 29;
+
+// launch_splat with its bounds contract: hipErrorInvalidValue from the host
+// check becomes a named error instead of a bare HIP code
+#define MH_SPLAT(...)                                                                                   \
+    do {                                                                                                \
+        hipError_t _e = launch_splat(__VA_ARGS__);                                                      \
+        if (_e == hipErrorInvalidValue)                                                                 \
+            return set_error(MH_ERR_INVALID_ARGUMENT, "splat: sample planes / film smaller than the "   \
+                                                      "chunk's layout (bounds contract of launch_splat)"); \
+        if (_e != hipSuccess) return set_error(MH_ERR_HIP, std::string("launch_splat: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// the device half of the contract: a non-zero bounds counter fails the call
+static int check_bounds_counter(mh_scene *s, const char *api);
 // prbvolpath backward grid (MH_VOL_WAVES = 4 waves / SIMD: 4 workgroups per CU)
 // and NEE-log entries per thread (16 B each; longer walks replay)
 constexpr uint32_t kPvpBlocksPerCu = 4, kPvpNeeCap = 256;
@@ -644,6 +661,15 @@ static bool deterministic(uint32_t flags) {
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
+}
+
+static int check_bounds_counter(mh_scene *s, const char *api) {
+    unsigned long long v = 0;
+    MH_HIP(hipMemcpy(&v, s->counters.as<unsigned long long>() + kCtrBounds, sizeof(v), hipMemcpyDeviceToHost));
+    if (v)
+        return set_error(MH_ERR_HIP, std::string(api) + ": " + std::to_string(v) +
+                                         " splat rows would have read past the sample planes (skipped)");
+    return MH_OK;
 }
 
 // MH_FLAG_DEVICE_POINTERS | MH_FLAG_NO_SYNC without stats: nothing is read
@@ -721,6 +747,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     const uint32_t seed_value = s->S.sampler_seed + seed;
     const bool determ = deterministic(flags);
     unsigned long long *invalid = s->counters.as<unsigned long long>() + kCtrInvalid;
+    unsigned long long *bounds = s->counters.as<unsigned long long>() + kCtrBounds;
     float kernel_ms = 0.f, trace_ms = 0.f;
     const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
     const uint32_t n_bounces = wavefront ? in->max_depth : 0;
@@ -771,11 +798,11 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
         }
         MH_HIP(hipEventRecord(ev[1], st));
         ScopedPhase put_("ImageBlockPut");
-        MH_HIP(launch_splat(s->S, lm, kSplatFilm, fast_splat, npx, L.n_passes, n, plane,
-                            s->work.as<float>(), film4, seed_value, coalesce, st, invalid, determ));
+        MH_SPLAT(s->S, lm, kSplatFilm, fast_splat, npx, L.n_passes, n, plane, s->work.as<float>(), film4,
+                 seed_value, coalesce, st, invalid, determ, s->work.bytes / 4, n_px * 4, bounds);
         if (alpha)
-            MH_HIP(launch_splat(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane,
-                                s->work.as<float>(), film_a, seed_value, coalesce, st, nullptr, determ));
+            MH_SPLAT(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane, s->work.as<float>(), film_a,
+                     seed_value, coalesce, st, nullptr, determ, s->work.bytes / 4, n_px, bounds);
     }
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
@@ -783,9 +810,9 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     // asynchronous call (device film, no stats): return once the work is
     // enqueued on the scene's stream, as a stream-ordered library op does
     if (async_call(flags, stats)) return MH_OK;
-    if (!stats && !getenv("MH_VW_DEBUG")) {  // nothing to read back: only the call's own sync
+    if (!stats && !getenv("MH_VW_DEBUG")) {  // nothing to read back: the call's own sync + the bounds word
         MH_HIP(hipStreamSynchronize(st));
-        return MH_OK;
+        return check_bounds_counter(s, "mh_render");
     }
     unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
     std::vector<uint32_t> wctr;
@@ -795,8 +822,14 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     } else {
         MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     }
-    MH_HIP(hipMemcpyAsync(&n_invalid, invalid, sizeof(n_invalid), hipMemcpyDeviceToHost, st));
+    unsigned long long iv[2] = {0, 0};  // [kCtrInvalid], [kCtrBounds]
+    static_assert(kCtrBounds == kCtrInvalid + 1, "one read-back of both words");
+    MH_HIP(hipMemcpyAsync(iv, invalid, sizeof(iv), hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));  // the stats counters are read back
+    n_invalid = iv[0];
+    if (iv[1])
+        return set_error(MH_ERR_HIP, "mh_render: " + std::to_string(iv[1]) +
+                                         " splat rows would have read past the sample planes (skipped)");
     for (size_t c = 0; c < n_chunks; ++c) {
         hipEvent_t *ev = &s->evpool[ev_per_chunk * c];
         float ms = 0.f;
@@ -963,8 +996,8 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
                       s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
     LaneMap lm = lane_map(L, 0);
     const uint32_t S_ = L.s_end - L.s_begin;
-    MH_HIP(launch_splat(s->S, lm, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w,
-                        s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr, deterministic(flags)));
+    MH_SPLAT(s->S, lm, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w, s->S.sampler_seed + seed,
+             L.spp_pp >= 4, st, nullptr, deterministic(flags), 0, n_px, nullptr);
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
     if (!async_call(flags, nullptr)) MH_HIP(hipStreamSynchronize(st));
@@ -1142,9 +1175,9 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         Lall.s_begin = 0;
         Lall.s_end = L.spp_pp;
         LaneMap lmw = lane_map(Lall, 0);
-        MH_HIP(launch_splat(s->S, lmw, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
-                            s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr,
-                            deterministic(flags)));
+        MH_SPLAT(s->S, lmw, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
+                 s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr,
+                 deterministic(flags), 0, n_px, nullptr);
         w = s->weights_tmp.as<float>();
     } else if (!dev) {
         MH_HIP(s->tmp_e.alloc(n_px * 4));
@@ -1389,7 +1422,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     const int coalesce = L.spp_pp >= 4;  // block.set_coalesce(... and spp >= 4) (common.py:795-796)
     const uint32_t seed_value = s->S.sampler_seed + seed;
     const bool determ = deterministic(flags);
-    unsigned long long *invalid = s->counters.as<unsigned long long>() + kCtrInvalid;
+    unsigned long long *bounds = s->counters.as<unsigned long long>() + kCtrBounds;
     MH_HIP(hipEventRecord(s->ev0, st));
     for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px) {
         const uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
@@ -1402,11 +1435,12 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         else
             MH_HIP(launch_render_forward(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), ga,
                                          s->counters.as<unsigned long long>(), st, alpha));
-        MH_HIP(launch_splat(s->S, lm, kSplatFilm, fast_splat, npx, 1, n, plane, s->work.as<float>(), film4,
-                            seed_value, coalesce, st, invalid, determ));
+        // no sample check here: tangent radiance is legitimately negative
+        MH_SPLAT(s->S, lm, kSplatFilm, fast_splat, npx, 1, n, plane, s->work.as<float>(), film4, seed_value,
+                 coalesce, st, nullptr, determ, s->work.bytes / 4, n_px * 4, bounds);
         if (alpha)
-            MH_HIP(launch_splat(s->S, lm, kSplatAlpha, fast_splat, npx, 1, n, plane, s->work.as<float>(), film_a,
-                                seed_value, coalesce, st, nullptr, determ));
+            MH_SPLAT(s->S, lm, kSplatAlpha, fast_splat, npx, 1, n, plane, s->work.as<float>(), film_a, seed_value,
+                     coalesce, st, nullptr, determ, s->work.bytes / 4, n_px, bounds);
     }
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     MH_HIP(hipEventRecord(s->ev1, st));
@@ -1414,12 +1448,12 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     if (async_call(flags, stats)) return MH_OK;
     if (!stats) {
         MH_HIP(hipStreamSynchronize(st));
-        return MH_OK;
+        return check_bounds_counter(s, "mh_render_forward");
     }
-    unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
+    unsigned long long ctr[2] = {0, 0};
     MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
-    MH_HIP(hipMemcpyAsync(&n_invalid, invalid, sizeof(n_invalid), hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
+    if (int rc = check_bounds_counter(s, "mh_render_forward")) return rc;
     if (stats) {
         float ms = 0.f;
         MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -1432,7 +1466,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
         stats->ms_trace = 0.f;
         stats->n_trace_launches = 0;
         stats->mode = wavefront ? 2u : 0u;  // fused wavefront / per-sample kernel
-        stats->invalid_samples = (uint32_t)std::min<unsigned long long>(n_invalid, 0xffffffffull);
+        stats->invalid_samples = 0;  // not counted: a tangent's radiance may be negative
     }
     return MH_OK;
 }

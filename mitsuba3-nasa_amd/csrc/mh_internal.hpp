@@ -69,7 +69,8 @@ enum { kSplatFilm = 0, kSplatWeights = 1, kSplatAlpha = 2 };
 hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
-                        hipStream_t st, unsigned long long *invalid = nullptr, bool deterministic = false);
+                        hipStream_t st, unsigned long long *invalid, bool deterministic, uint64_t in_floats,
+                        uint64_t film_floats, unsigned long long *viol);
 hipError_t launch_film_rgbaw(uint64_t n_px, const float *rgbw, const float *a, float *out, hipStream_t st);
 size_t wf_workspace_bytes(uint64_t cap);
 uint32_t wf_counter_words(uint32_t n_bounces);

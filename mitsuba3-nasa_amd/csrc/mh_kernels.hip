@@ -179,11 +179,22 @@ template <int Mode>
 __global__ void __launch_bounds__(128)
 k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t n_passes,
            uint64_t n, uint64_t plane, const float *__restrict__ in, float *__restrict__ film,
-           uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin, unsigned long long *__restrict__ invalid) {
+           uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin, unsigned long long *__restrict__ invalid,
+           uint64_t in_lim, unsigned long long *__restrict__ viol) {
     uint32_t n_bad = 0;
     const uint32_t gl = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t pl = gl / kSplatLanes, g = gl % kSplatLanes;
     if (pl >= n_pix) return;  // whole DPP rows leave together (n_pix granularity = 16 lanes)
+    // bounds guard (the host checks the same contract per launch): the last
+    // float this pixel's row reads must lie inside the in planes; a row that
+    // would read past them counts a violation and leaves whole
+    if (Mode != 1) {
+        const uint64_t last = (uint64_t)(n_passes - 1) * n + (uint64_t)(pl + 1) * Sn - 1 + (Mode == 2 ? 5 : 4) * plane;
+        if (last >= in_lim) {
+            if (g == 0) atomicAdd(viol, 1ull);
+            return;
+        }
+    }
     const uint32_t W = S.width, H = S.height;
     const uint32_t pixel = pixel_begin + pl;
     const uint32_t py = pixel / W, px = pixel - py * W;
@@ -809,11 +820,22 @@ hipError_t launch_render_forward(const DScene &S, const IntegratorParams &in, co
 hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
                         uint32_t n_pix, uint32_t n_passes, uint64_t n, uint64_t plane,
                         const float *in, float *film, uint32_t seed_value, int coalesce,
-                        hipStream_t st, unsigned long long *invalid, bool deterministic) {
+                        hipStream_t st, unsigned long long *invalid, bool deterministic, uint64_t in_floats,
+                        uint64_t film_floats, unsigned long long *viol) {
     if (n == 0) return hipSuccess;
+    // the splat's bounds contract, checked before every launch: sample (k, pass)
+    // of pixel pl sits at pass * n + pl * S + k of each plane (k < S), the
+    // planes are `plane` floats apart (5 in planes, 6 with alpha), and the
+    // film holds W * H pixels of 4 (mode 0) or 1 (W image / alpha) floats
+    const uint64_t film_need = (uint64_t)S.width * S.height * (mode == kSplatFilm ? 4 : 1);
+    if (film_floats < film_need || (uint64_t)n_pix * lm.S > n || (uint64_t)lm.pixel_begin + n_pix > (uint64_t)S.width * S.height)
+        return hipErrorInvalidValue;
+    if (mode != kSplatWeights &&
+        (plane < (uint64_t)n_passes * n || in_floats < (uint64_t)(mode == kSplatAlpha ? 6 : 5) * plane || !in))
+        return hipErrorInvalidValue;
 #define MH_SPLAT_PX(M)                                                                                          \
     hipLaunchKernelGGL(k_splat_px<M>, dim3(blocks_for(lanes, bs)), dim3(bs), 0, st, S, lm.pixel_begin, n_pix, \
-                       lm.S, n_passes, n, plane, in, film, seed_value, lm.spp_pp, lm.s_begin, invalid)
+                       lm.S, n_passes, n, plane, in, film, seed_value, lm.spp_pp, lm.s_begin, invalid, in_floats, viol)
 #define MH_SPLAT_GEN(M)                                                                                         \
     hipLaunchKernelGGL(k_splat_generic<M>, dim3(blocks_for(n, bs)), dim3(bs), 0, st, S, lm, n_passes, n, plane, \
                        in, film, seed_value, coalesce, invalid)

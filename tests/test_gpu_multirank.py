@@ -31,14 +31,25 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     from mitsuba_hip import distributed as D
     res, spp = 48, 8
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    logs = tmp_path / "logs"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", f"--log-dir={logs}", "--redirects=3",
            os.path.join(ROOT, "tests", "dist_hip_worker.py"), str(tmp_path), str(res), str(spp)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, timeout=100, capture_output=True, text=True)
-    if r.returncode != 0:  # the ranks' own error lines first (the launcher's trailer is long)
-        err = [ln for ln in (r.stdout + r.stderr).splitlines()
-               if ln.startswith("[rank") or "Error" in ln or "error" in ln or "HSA" in ln or "Queue" in ln]
-        pytest.fail("\n".join(err[:60]) + "\n--- stdout tail ---\n" + r.stdout[-1500:])
+    if r.returncode != 0:
+        # every rank's full stdout / stderr (torchrun --redirects 3), kept under
+        # gpurun_out/ on the GPU box so a failure's whole log survives the run
+        text = []
+        for f in sorted(logs.rglob("*.log")):
+            text.append(f"=== {f.relative_to(logs)} ===\n" + f.read_text(errors="replace"))
+        text.append("=== launcher ===\n" + r.stdout + r.stderr)
+        full = "\n".join(text)
+        keep = os.environ.get("GRAFT_REPO_ROOT")
+        if keep:
+            os.makedirs(os.path.join(keep, "gpurun_out"), exist_ok=True)
+            with open(os.path.join(keep, "gpurun_out", "multirank_failure.log"), "w") as fh:
+                fh.write(full)
+        pytest.fail(full[-6000:])
     r0, r1 = (np.load(tmp_path / f"r{i}.npz") for i in range(2))
     assert (int(r0["begin"]), int(r0["end"]), int(r1["begin"]), int(r1["end"])) == (0, 8, 8, 16)
     assert float(r0["t"]) == float(r1["t"]) == 1.25  # max over ranks

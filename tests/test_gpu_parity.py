@@ -476,13 +476,23 @@ def test_prb_bitmap_wavefront_chunks(channels, max_depth, monkeypatch):
 # continuing across passes (integrator.cpp:281-295, 353-357)
 # ---------------------------------------------------------------------------
 @pytest.mark.slow
-def test_multipass_config5_slab_parity():
+@pytest.mark.parametrize("b,e", [(0, 2), (510, 512)])
+def test_multipass_config5_slab_parity(b, e):
+    """Config 5's forward as measured (tools/bench_config5.py: max_depth 8):
+    2048^2 * 1024 = 2^32 > 2^32 - 1 samples, so two passes of 512 spp
+    (integrator.cpp:281-295).  Lanes [b, e) of every pass-pixel run both
+    passes; pass 2 seeds from each lane's carried PCG32 state, continuing
+    pass 1's stream (integrator.cpp:353-357), at bounces 1..8.  [510, 512)
+    holds the last lanes of every pass-pixel (lane 2^32 - 2 .. 2^32 - 1 of
+    the last pixel sits at the pass's end)."""
     mi = _mi()
     scene = cbox(mi, 2048, 2048, 1024)
-    integ = mi.load_dict({"type": "path", "max_depth": 4})
-    # 2048^2 * 1024 = 2^32 > 2^32 - 1: two passes of 512; lanes [0, 2) of every pixel
-    film = mi.render_film(scene, integ, seed=2, spp=1024, spp_begin=0, spp_end=2).cpu().numpy()
-    ref = O.render(scene, integ, seed=2, spp=1024, spp_begin=0, spp_end=2)
+    integ = mi.load_dict({"type": "path", "max_depth": 8})
+    from mitsuba_hip import _abi as A
+    st = A.Stats()
+    film = mi.render_film(scene, integ, seed=2, spp=1024, spp_begin=b, spp_end=e, stats=st).cpu().numpy()
+    assert st.mode == 2 and st.n_trace_launches == 2 * 8  # one chunk x 2 passes x 8 bounces
+    ref = O.render(scene, integ, seed=2, spp=1024, spp_begin=b, spp_end=e)
     assert ref[..., 3].sum() > 0
     ok, frac = _film_close(film, ref)
     assert ok, f"film parity {frac}"
@@ -498,7 +508,7 @@ def test_config5_prb_gradient_slab_parity():
     mi = _mi()
     import torch
     scene = cbox(mi, 2048, 2048, 1024)
-    integ = mi.load_dict({"type": "prb", "max_depth": 4})
+    integ = mi.load_dict({"type": "prb", "max_depth": 8})  # as tools/bench_config5.py measures it
     params = mi.traverse(scene)
     key = "white.reflectance.value"
     seed = mi.sample_tea_32(2, 1)[0]
