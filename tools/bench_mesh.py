@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
     a = ap.parse_args()
     import torch
     import mitsuba_hip as mi
@@ -65,13 +66,15 @@ def main():
         A.lib().mh_scene_bvh_info(h, C.byref(nn), C.byref(npr), C.byref(dep))
         st = A.Stats()
         film = torch.empty((a.res, a.res, 4), device="cuda")
-        mi.render_film(scene, seed=100, spp=a.spp, film=film, stats=st)
+        for i in range(a.warmup):
+            mi.render_film(scene, seed=100 + i, spp=a.spp, film=film, stats=st)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ks = []
+        ks, ts = [], []
         for i in range(a.steps):
             mi.render_film(scene, seed=i, spp=a.spp, film=film, stats=st)
             ks.append(st.ms_kernel)
+            ts.append(st.ms_trace)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
         ns = a.res * a.res * a.spp
@@ -83,6 +86,12 @@ def main():
             "kernel_ms": round(sum(ks) / len(ks), 2), "mode": st.mode,
             "grays_s_closest": round(st.rays_closest / (dt * 1e9), 2),
             "grays_s_shadow": round(st.rays_shadow / (dt * 1e9), 2),
+            # k_wf_trace (closest hits) timed by HIP events on the scene's stream:
+            # algorithmic bytes 48 per closest ray (28-B ray in, 20-B hit out)
+            "rays_closest": int(st.rays_closest), "rays_shadow": int(st.rays_shadow),
+            "trace_ms": round(sum(ts) / len(ts), 3), "trace_launches": int(st.n_trace_launches),
+            "trace_grays_s": round(st.rays_closest / (sum(ts) / len(ts) * 1e6), 2) if sum(ts) else None,
+            "trace_alg_gbs": round(48 * st.rays_closest / (sum(ts) / len(ts) * 1e6), 1) if sum(ts) else None,
             "config": f"cornell box + {len(F)}-triangle PLY blob, {a.res}^2 @ {a.spp} spp, path max_depth 8"}),
             flush=True)
         scene.release()

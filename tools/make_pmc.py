@@ -54,6 +54,7 @@ def main():
     wr, wr_calls, _ = load(d, "write")
     cf, cf_calls, _ = load(d, "calib_fetch")
     cw, cw_calls, _ = load(d, "calib_write")
+    tc, tc_calls, _ = load(d, "tcc")  # optional pass: TCC_HIT_sum / TCC_MISS_sum
     known = 20 * (1 << 24) * 4  # tools/calib_fetch bytes per launch
     calib = {}
     for w in (4, 16):
@@ -88,6 +89,9 @@ def main():
             rec["write_bytes_raw"] = wb
             rec["access_width"] = w
             rec["hbm_bytes_per_call"] = rb * calib[w]["fetch"] + wb * calib[w]["write"]
+        if tc_calls.get(k):
+            h, m = tc[k].get("TCC_HIT_sum", 0.0), tc[k].get("TCC_MISS_sum", 0.0)
+            rec["l2_hit"] = h / (h + m) if h + m else None
         out["kernels"][k] = rec
         hb = rec.get("hbm_bytes_per_call")
         print(f"{k:44s} {n:5d} {avg * 1e6:8.1f} {rec.get('clock_ghz', 0):5.2f} {rec.get('valu_issue_frac') or 0:8.3f} "

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""profiles/pmc_traffic.json from a tools/profile_gpu.sh run (summary.json):
+"""profiles/pmc_traffic.json from a tools/profile_r2.sh run (summary.json):
 per-kernel PMC HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 corrections per MI355X_MICROARCH.md) and rocprof average duration.
 usage: make_traffic.py <profile dir> <label>"""
