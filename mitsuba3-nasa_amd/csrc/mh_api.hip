@@ -725,7 +725,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     // one pass to the next) unless forced
     bool wavefront = in->type == MH_INTEGRATOR_PATH && in->max_depth <= 64 && (L.n_passes == 1 || wf_fused(s->S));
     // volpath: main / walk rounds (mh_volwave.hip), single pass
-    bool volwave = vw_supported(s->S, *in) && L.n_passes == 1;
+    bool volwave = (vol_sched_mode() ? vs_supported(s->S, *in) : vw_supported(s->S, *in)) && L.n_passes == 1;
     const char *env_mode = getenv("MH_MODE");
     if (env_mode && !strcmp(env_mode, "mega")) wavefront = volwave = false;
     if (flags & MH_FLAG_MEGAKERNEL) wavefront = volwave = false;
@@ -917,7 +917,7 @@ int mh_render_samples(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     }
     MH_HIP(hipMemsetAsync(s->counters.ptr, 0, 256, st));
     LaneMap lm = lane_map(L, 0);
-    if ((flags & MH_FLAG_WAVEFRONT) && vw_supported(s->S, *in) && vol_sched_mode()) {
+    if ((flags & MH_FLAG_WAVEFRONT) && vs_supported(s->S, *in) && vol_sched_mode()) {
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
         MH_HIP(launch_vol_sched(s->S, *in, lm, s->S.sampler_seed + seed, n, n, dst, vs_blocks(cus),

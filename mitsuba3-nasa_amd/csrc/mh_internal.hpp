@@ -151,6 +151,7 @@ size_t vw_workspace_bytes(uint64_t cap);
 uint32_t vw_counter_words(uint32_t rounds);
 uint32_t vw_rounds(const IntegratorParams &in);
 bool vw_supported(const DScene &S, const IntegratorParams &in);
+bool vs_supported(const DScene &S, const IntegratorParams &in);
 uint32_t vw_blocks(int cus);
 bool vol_sched_mode();
 uint32_t vs_blocks(int cus);

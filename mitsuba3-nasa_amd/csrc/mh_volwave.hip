@@ -679,6 +679,359 @@ MH_DEV uint32_t vs_trace(const DScene &S, const LdsBvh &B, const IntegratorParam
     return kPhSurf;
 }
 
+// ===========================================================================
+// prbvolpath's primal (PRBVolpathIntegrator.sample, prbvolpath.py:91-431, mode
+// primal) as the same phase machine: prbvol_sample<0>'s loop trip cut at its
+// closest-hit queries and at every step of the ratio-tracked NEE walk
+// (sample_emitter, :336-431).  The fork's own choices stay as the megakernel
+// has them: emitter hits are not added (:216-234 commented out), the NEE ray
+// is spawn_ray(ds.d) walked over ds.dist * (1 - ShadowEpsilon) (:357-371),
+// the sensor medium is ignored (:123-124), homogeneous media get direct
+// transmittance in the walk (:390-394).  Per lane the operations and random
+// draws are those of prbvol_sample<0> in its order (bit-identical samples).
+//   HEAD     RR, sample_interaction of the current medium
+//   TRACE    the closest hit of the loop trip (TraceM: after the medium sample,
+//            TraceS: the surface query) or of a walk segment (TraceWS)
+//   SCATTER  a real scatter: the emitter sample that starts its walk
+//   SURF     a surface hit: albedo, emitter sample
+//   WALK     one trip of the transmittance loop up to its intersection
+//   POST     the NEE contribution, phase / BSDF sampling
+// A null collision (no scatter, no surface) returns to HEAD inside its trip.
+// ===========================================================================
+struct PvState {
+    RayT ray;
+    V3 throughput, L;
+    SI si;
+    float si_t, eta;
+    uint32_t medium, depth;
+    bool needs_intersection, valid_ray;
+    // inside a loop trip
+    bool active, active_medium, active_surface, act_scatter, smooth, e_surface, nee;
+    uint32_t med;
+    MEI mei;
+    V3 rho, emitter_val, transmittance;
+    DirS ds;
+    // the walk (sample_emitter's loop)
+    RayT wray;
+    SI wsi;
+    float wsi_t, total_dist;
+    uint32_t wmedium;
+    bool w_needs;
+};
+
+MH_DEV void pv_init(const DScene &S, const IntegratorParams &, Pcg &rng, RayT ray, PvState &v) {
+    v.ray = ray;
+    v.throughput = v3(1.f, 1.f, 1.f);
+    v.L = v3(0.f, 0.f, 0.f);
+    v.eta = 1.f;
+    v.depth = 0;
+    v.si.valid = false;
+    v.si_t = 0.f;
+    v.medium = MH_INVALID;   // "TODO: support sensors inside media" (prbvolpath.py:123-124)
+    v.needs_intersection = true;
+    v.valid_ray = false;
+    (void)fminf(3.f * rng.next_float(), 2.f);   // RGB channel (scalar majorants: all channels alike)
+}
+
+// SURF / SCATTER: the surface block and the emitter sample (:212-270); the
+// walk starts here, or the trip goes on to POST without one
+MH_DEV uint32_t pv_shade(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+    v.active_surface = v.active_surface && v.si.valid;
+    const uint32_t b = v.active_surface ? S.shapes[v.si.shape].bsdf : MH_INVALID;
+    v.smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
+    v.rho = v3(0.f, 0.f, 0.f);
+    if (v.smooth) v.rho = tex_eval(S, S.bsdf_tex[b], v.si.uvx, v.si.uvy);
+    v.e_surface = v.active_surface && v.smooth && v.depth + 1 < in.max_depth;
+    const bool sample_emitters = v.med != MH_INVALID && !(S.media[v.med].flags & MH_MEDIUM_NO_EMITTER_SAMPLING);
+    const bool e_medium = v.act_scatter && sample_emitters;
+    v.nee = v.e_surface || e_medium;
+    if (!v.nee) return kPhPost;
+    // sample_emitter's head (pvp_sample_emitter: active_medium = e_medium)
+    const V3 ref_p = e_medium ? v.mei.p : v.si.p;
+    const V3 ref_n = e_medium ? v3(0.f, 0.f, 0.f) : v.si.n;
+    const float sx = rng.next_float(), sy = rng.next_float();
+    v.emitter_val = scene_sample_emitter_direction(S, ref_p, sx, sy, v.ds);
+    v.transmittance = v3(1.f, 1.f, 1.f);
+    if (v.ds.pdf == 0.f) {  // emitted = 0
+        v.emitter_val = v3(0.f, 0.f, 0.f);
+        return kPhPost;
+    }
+    v.wmedium = v.medium;
+    if (!e_medium && is_medium_transition(S, v.si)) v.wmedium = target_medium(S, v.si, v.ds.d);
+    v.wray = spawn_ray(ref_p, ref_n, v.ds.d);
+    v.total_dist = 0.f;
+    v.wsi_t = 0.f;
+    v.wsi.valid = false;
+    v.w_needs = true;
+    return kPhWalk;
+}
+
+// the loop trip after its medium block (:206-212), up to the surface query
+MH_DEV uint32_t pv_mid(const DScene &S, const IntegratorParams &in, PvState &v, bool act_null, bool escaped,
+                       V3 weight, float P) {
+    v.active = v.active && v.depth < in.max_depth;
+    v.act_scatter = v.act_scatter && v.active;
+    if ((S.vol_flags & kVolHandleNull) && act_null) { v.ray.o = v.mei.p; v.si_t = v.si_t - v.mei.t; }
+    if (v.act_scatter)
+        weight = v3(weight.x * (v.mei.sigma_s.x / P), weight.y * (v.mei.sigma_s.y / P),
+                    weight.z * (v.mei.sigma_s.z / P));
+    v.throughput = v.throughput * weight;
+    v.active_surface = v.active_surface || escaped;
+    if (v.act_scatter) return kPhScatter;
+    if (v.active_surface) return v.needs_intersection ? kPhTraceS : kPhSurf;
+    // a null collision (or a scatter cut by max_depth): no surface, no NEE,
+    // no sampling -- the loop's tail test (:331)
+    v.valid_ray = v.valid_ray || v.act_scatter;
+    return (v.active && v.active_medium) ? kPhHead : kPhFree;
+}
+
+// the medium block after its (optional) intersection (:165-204)
+MH_DEV uint32_t pv_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+    MEI &mei = v.mei;
+    v.needs_intersection = false;
+    if (v.si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+    const float mt = fminf(mei.t, v.si_t) - mei.mint;
+    const float tr = exp_dr((-mt) * mei.maj);
+    const float tr_pdf = v.si_t < mei.t ? tr : tr * mei.maj;
+    const float fw = tr_pdf > 0.f ? tr / tr_pdf : 0.f;
+    V3 weight = v3(fw, fw, fw);
+    const bool escaped = !mei.valid;
+    v.active_medium = mei.valid;
+    bool act_null = false;
+    float P = 1.f;
+    if (S.vol_flags & kVolHandleNull) {
+        P = mei.sigma_t / mei.maj;
+        if (v.active_medium) act_null = rng.next_float() >= P;
+        v.act_scatter = !act_null && v.active_medium;
+        if (act_null) weight = weight * (mei.sigma_n / (1.f - P));
+    } else {
+        v.act_scatter = v.active_medium;
+    }
+    if (v.act_scatter) v.depth += 1;
+    return pv_mid(S, in, v, act_null, escaped, weight, P);
+}
+
+// HEAD: Russian roulette (:142-149) and the medium sample (:157-163)
+MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+    bool active = nonzero(v.throughput);
+    const float q = fminf(hmax(v.throughput) * (v.eta * v.eta), 0.99f);
+    const bool perform_rr = v.depth > in.rr_depth;
+    if (active) active = rng.next_float() < q || !perform_rr;
+    if (perform_rr) v.throughput = v.throughput * rcp(q);
+    if (!active) return kPhFree;
+    v.active = true;
+    v.active_medium = v.medium != MH_INVALID;
+    v.active_surface = !v.active_medium;
+    v.act_scatter = false;
+    v.nee = false;
+    v.med = v.medium;
+    MEI &mei = v.mei;
+    mei.valid = false;
+    mei.t = 0.f;
+    mei.maj = 1.f;
+    mei.sigma_t = 0.f;
+    mei.p = v3(0.f, 0.f, 0.f);
+    mei.sigma_s = v3(0.f, 0.f, 0.f);
+    if (v.active_medium) {
+        const DMedium &m = S.media[v.med];
+        sample_interaction(S, v.med, v.ray, rng.next_float(), mei);
+        if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) v.ray.maxt = mei.t;
+        if (v.needs_intersection) return kPhTraceM;
+        return pv_med_rest(S, in, rng, v);
+    }
+    return pv_mid(S, in, v, false, false, v3(1.f, 1.f, 1.f), 1.f);
+}
+
+// the walk step after its (optional) intersection (pvp_sample_emitter's loop)
+MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, PvState &v, float remaining_dist) {
+    v.w_needs = false;
+    bool act_med = v.wmedium != MH_INVALID, act_surf = !act_med, escaped = false;
+    MEI mei;
+    mei.valid = false;
+    mei.t = 0.f;
+    mei.maj = 1.f;
+    mei.p = v3(0.f, 0.f, 0.f);
+    V3 trm = v3(1.f, 1.f, 1.f);
+    if (act_med) {
+        const DMedium &m = S.media[v.wmedium];
+        sample_interaction(S, v.wmedium, v.wray, rng.next_float(), mei);
+        if (v.wsi_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
+        if ((S.vol_flags & kVolNeeHomogeneous) && m.type == MH_MEDIUM_HOMOGENEOUS) {
+            mei.t = fminf(remaining_dist, v.wsi_t);
+            const float hom_t = fminf(mei.t, v.wsi_t) - mei.mint;
+            const float tr = exp_dr((-hom_t) * mei.maj);
+            trm = v3(tr, tr, tr);
+            mei.t = __builtin_huge_valf();
+            mei.valid = false;
+        }
+        escaped = !mei.valid;
+        act_med = mei.valid;
+        if (act_med) {
+            v.wray.o = mei.p;
+            v.wsi_t = v.wsi_t - mei.t;
+            trm = trm * (mei.sigma_n / mei.maj);
+        }
+    }
+    act_surf = (act_surf || escaped) && v.wsi.valid && !act_med;
+    if (act_surf) {
+        const uint32_t b = S.shapes[v.wsi.shape].bsdf;
+        trm = trm * ((b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f);
+    }
+    v.transmittance = v.transmittance * trm;
+    if (act_surf) v.wray = spawn_ray(v.wsi.p, v.wsi.n, v.wray.d);
+    v.w_needs = act_surf;
+    const bool active = (act_med || act_surf) && nonzero(v.transmittance);
+    if (active) v.total_dist += act_med ? mei.t : v.wsi_t;
+    if (act_surf && is_medium_transition(S, v.wsi)) v.wmedium = target_medium(S, v.wsi, v.wray.d);
+    return active ? kPhWalk : kPhPost;
+}
+
+MH_DEV float pv_remaining(const PvState &v) { return v.ds.dist * (1.f - kShadowEps) - v.total_dist; }
+
+// WALK: the head of one transmittance-loop trip
+MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, PvState &v) {
+    const float remaining_dist = pv_remaining(v);
+    v.wray.maxt = remaining_dist;
+    if (!(remaining_dist > 0.f)) return kPhPost;
+    if (v.w_needs) return kPhTraceWS;
+    return pv_walk_rest(S, rng, v, remaining_dist);
+}
+
+// POST: the emitter sample's contribution (:256-270), phase sampling
+// (:274-294), BSDF sampling (:298-331) and the loop's tail test
+MH_DEV uint32_t pv_post(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+    if (v.nee) {
+        const V3 emitted = v.emitter_val * v.transmittance;
+        V3 nee_w, bv = v3(0.f, 0.f, 0.f);
+        float nee_pdf, bp = 0.f;
+        const V3 wo_s = to_local(v.si, v.ds.d);
+        if (v.e_surface) {
+            diffuse_eval_pdf(v.rho, v.si.wi, wo_s, true, bv, bp);
+            nee_w = bv;
+            nee_pdf = bp;
+        } else {
+            const float ph = phase_eval(S.media[v.med], mei_to_local(v.mei, v.ds.d));
+            nee_w = v3(ph, ph, ph);
+            nee_pdf = ph;
+        }
+        if (v.ds.delta) nee_pdf = 0.f;
+        const float mis = mis_weight(v.ds.pdf, nee_pdf);
+        const V3 contrib = ((v.throughput * nee_w) * mis) * emitted;
+        v.L = v.L + contrib;
+    }
+    v.valid_ray = v.valid_ray || v.act_scatter;
+    bool act_scatter = v.act_scatter;
+    if (act_scatter) {
+        (void)rng.next_float();
+        const float s2x = rng.next_float(), s2y = rng.next_float();
+        float ph_pdf;
+        const V3 wo = phase_sample(S.media[v.med], s2x, s2y, ph_pdf);
+        act_scatter = act_scatter && ph_pdf > 0.f;
+        if (act_scatter) {
+            v.ray = spawn_ray(v.mei.p, v3(0.f, 0.f, 0.f), mei_to_world(v.mei, wo));
+            v.needs_intersection = true;
+        }
+    }
+    if (v.active_surface) {
+        (void)rng.next_float();
+        const float s2x = rng.next_float(), s2y = rng.next_float();
+        V3 bs_wo, bw;
+        float bs_pdf;
+        if (!v.smooth) {
+            bs_wo = -v.si.wi; bs_pdf = 1.f; bw = v3(1.f, 1.f, 1.f);
+        } else {
+            bs_wo = square_to_cosine_hemisphere(s2x, s2y);
+            bs_pdf = kInvPi * bs_wo.z;
+            bw = (v.si.wi.z > 0.f && bs_pdf > 0.f) ? v.rho : v3(0.f, 0.f, 0.f);
+        }
+        v.active_surface = v.active_surface && bs_pdf > 0.f;
+        if (v.active_surface) {
+            v.throughput = v.throughput * bw;
+            v.ray = spawn_ray(v.si.p, v.si.n, to_world(v.si, bs_wo));
+            v.needs_intersection = true;
+            if (v.smooth) { v.depth += 1; v.valid_ray = true; }
+            if (is_medium_transition(S, v.si)) v.medium = target_medium(S, v.si, v.ray.d);
+        }
+    }
+    return (v.active && (v.active_surface || v.active_medium)) ? kPhHead : kPhFree;
+}
+
+template <bool Pk>
+MH_DEV uint32_t pv_trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, uint32_t ph,
+                         PvState &v, uint32_t &n_closest, uint32_t &n_shadow) {
+    if (ph == kPhTraceWS) {
+        trace_si<Pk>(S, B, v.wray, v.wsi, v.wsi_t);
+        ++n_shadow;
+        return pv_walk_rest(S, rng, v, pv_remaining(v));
+    }
+    trace_si<Pk>(S, B, v.ray, v.si, v.si_t);
+    ++n_closest;
+    if (ph == kPhTraceM) return pv_med_rest(S, in, rng, v);
+    return kPhSurf;
+}
+
+// The two integrators the phase scheduler runs: their state and phase steps
+struct VolMachine {
+    using State = VolState;
+    static constexpr bool kPrb = false;
+    MH_DEV static void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v) {
+        volpath_init(S, in, rng, r, v);
+    }
+    MH_DEV static uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return vs_head(S, in, rng, v);
+    }
+    template <bool Pk>
+    MH_DEV static uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
+                                 uint32_t ph, State &v, WMei &wm, uint32_t &nc, uint32_t &ns) {
+        return vs_trace<Pk>(S, B, in, rng, ph, v, wm, nc, ns);
+    }
+    MH_DEV static uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return vs_scatter(S, in, rng, v);
+    }
+    MH_DEV static uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return vs_surf(S, in, rng, v);
+    }
+    MH_DEV static uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &wm) { return vs_walk(S, rng, v.ds, v.ns, wm); }
+    MH_DEV static uint32_t post(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
+    }
+    MH_DEV static void write(float *out, uint64_t plane, uint32_t pid, const State &v, int alpha) {
+        vw_write_sample(out, plane, pid, v, alpha);
+    }
+};
+
+struct PvMachine {
+    using State = PvState;
+    static constexpr bool kPrb = true;
+    MH_DEV static void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v) {
+        pv_init(S, in, rng, r, v);
+    }
+    MH_DEV static uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_head(S, in, rng, v);
+    }
+    template <bool Pk>
+    MH_DEV static uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
+                                 uint32_t ph, State &v, WMei &, uint32_t &nc, uint32_t &ns) {
+        return pv_trace<Pk>(S, B, in, rng, ph, v, nc, ns);
+    }
+    MH_DEV static uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_shade(S, in, rng, v);
+    }
+    MH_DEV static uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_shade(S, in, rng, v);
+    }
+    MH_DEV static uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v); }
+    MH_DEV static uint32_t post(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_post(S, in, rng, v);
+    }
+    MH_DEV static void write(float *out, uint64_t plane, uint32_t pid, const State &v, int alpha) {
+        out[pid] = v.L.x;
+        out[plane + pid] = v.L.y;
+        out[2 * plane + pid] = v.L.z;
+        if (alpha) out[5 * plane + pid] = v.valid_ray ? 1.f : 0.f;  // aovs[3] (integrator.cpp:1229-1231)
+    }
+};
+
 #ifndef MH_VS_WAVES
 #define MH_VS_WAVES 2
 #endif
@@ -695,7 +1048,7 @@ MH_DEV uint32_t vs_trace(const DScene &S, const LdsBvh &B, const IntegratorParam
 __host__ __device__ inline uint32_t vs_media_bytes(const DScene &S) { return (S.n_media * (uint32_t)sizeof(DMedium) + 15u) & ~15u; }
 __host__ __device__ inline uint32_t vs_tab_bytes(const DScene &S) { return ((S.tab_bytes + 15u) & ~15u) + vs_media_bytes(S); }
 
-template <bool InLds, bool Pk, bool Tab>
+template <class M, bool InLds, bool Pk, bool Tab>
 __global__ void __launch_bounds__(256, MH_VS_WAVES)
 k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane,
             float *__restrict__ out, unsigned long long *__restrict__ counters, unsigned long long *__restrict__ work,
@@ -717,7 +1070,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     constexpr uint32_t W[kNGroups] = {MH_VS_W};
     const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
     uint32_t n_closest = 0, n_shadow = 0;
-    VolState v;
+    typename M::State v;
     WMei wm;
     Pcg rng;
     uint32_t pid = 0, ph = kPhFree;
@@ -799,28 +1152,28 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                     const RayT r = camera_ray(S, __builtin_fmaf(sx, sw, -0.f), __builtin_fmaf(sy, sh, -0.f));
                     out[3 * plane + k] = sx;
                     out[4 * plane + k] = sy;
-                    volpath_init(S, in, rng, r, v);
+                    M::init(S, in, rng, r, v);
                     ph = kPhHead;
                 }
             }
             next = std::min<uint64_t>(end, next + (uint64_t)__popcll(m));
         } else if (sel == kGHead) {
-            if (ph == kPhHead) { ph = vs_head(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhHead) { ph = M::head(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGTrace) {
             if (g == kGTrace) {
-                ph = vs_trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
+                ph = M::template trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
                 ended = ph == kPhFree;
             }
         } else if (sel == kGScatter) {
-            if (ph == kPhScatter) { ph = vs_scatter(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhScatter) { ph = M::scatter(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGSurf) {
-            if (ph == kPhSurf) { ph = vs_surf(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhSurf) { ph = M::surf(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGWalk) {
-            if (ph == kPhWalk) ph = vs_walk(S, rng, v.ds, v.ns, wm);
+            if (ph == kPhWalk) ph = M::walk(S, rng, v, wm);
         } else {
-            if (ph == kPhPost) { ph = volpath_post(S, in, rng, v) ? kPhHead : kPhFree; ended = ph == kPhFree; }
+            if (ph == kPhPost) { ph = M::post(S, in, rng, v); ended = ph == kPhFree; }
         }
-        if (ended) vw_write_sample(out, plane, pid, v, alpha);
+        if (ended) M::write(out, plane, pid, v, alpha);
 #ifdef MH_EXP_VSCNT
         {
             const uint64_t dt = __builtin_amdgcn_s_memtime() - t_phase;
@@ -865,6 +1218,12 @@ uint32_t vw_rounds(const IntegratorParams &in) { return in.max_depth + 1; }
 bool vw_supported(const DScene &S, const IntegratorParams &in) {
     return in.type == MH_INTEGRATOR_VOLPATH && in.max_depth <= 1024 && S.n_media < 255;
 }
+// the phase scheduler runs volpath and prbvolpath's primal (the rounds mode
+// only volpath)
+bool vs_supported(const DScene &S, const IntegratorParams &in) {
+    return (in.type == MH_INTEGRATOR_VOLPATH || in.type == MH_INTEGRATOR_PRBVOLPATH) && in.max_depth <= 1024 &&
+           S.n_media < 255;
+}
 uint32_t vw_blocks(int cus) {
     uint32_t bpc = 8;
     if (const char *e = getenv("MH_VW_BPC")) bpc = std::max(1, atoi(e));
@@ -880,9 +1239,14 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     const char *te = getenv("MH_TRAVERSAL");
     const bool pk = S.n_prims > 0 && S.n_prims <= wf_packet_max_prims() && !(te && !strcmp(te, "lane"));
     const bool tab = S.tab_bytes != 0 && !getenv("MH_VS_NOTAB");
-#define MH_VS(L, P, T)                                                                                        \
-    hipLaunchKernelGGL((k_vol_sched<L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), st, S, in, \
-                       lm, seed_value, n, plane, out, counters, work, alpha)
+#define MH_VS1(Mc, L, P, T)                                                                                   \
+    hipLaunchKernelGGL((k_vol_sched<Mc, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), st, S, \
+                       in, lm, seed_value, n, plane, out, counters, work, alpha)
+#define MH_VS(L, P, T)                                                  \
+    do {                                                                \
+        if (in.type == MH_INTEGRATOR_PRBVOLPATH) MH_VS1(PvMachine, L, P, T); \
+        else MH_VS1(VolMachine, L, P, T);                               \
+    } while (0)
     unsigned long long *work = counters + 32;  // the 8 queue heads of this launch (128 B apart)
     hipError_t e = hipMemsetAsync(work, 0, 8 * 128, st);
     if (e != hipSuccess) return e;
@@ -891,6 +1255,7 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     else if (lds) MH_VS(true, false, false);
     else MH_VS(false, false, false);
 #undef MH_VS
+#undef MH_VS1
     return hipGetLastError();
 }
 

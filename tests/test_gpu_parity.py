@@ -324,10 +324,12 @@ def test_volpath_white_furnace_gpu():
 # prbvolpath (prbvolpath.py): primal per sample and
 # the adjoint wrt the sigma_t grid, the albedo and a surface reflectance
 # ---------------------------------------------------------------------------
-def _pvp_scene(mi, w=24, h=20, spp=8, floor=True, **kw):
+def _pvp_scene(mi, w=24, h=20, spp=8, floor=True, pixel_format=None, **kw):
     kw.setdefault("grid", mi.fbm_grid(16))
     kw.setdefault("scale", 4.0)
     d = mi.volume_cube(w, h, spp, **kw)
+    if pixel_format:
+        d["sensor"]["film"]["pixel_format"] = pixel_format
     d["integrator"] = {"type": "prbvolpath", "max_depth": kw.get("max_depth", 6), "rr_depth": 5}
     if floor:
         T = mi.Transform4f
@@ -337,17 +339,29 @@ def _pvp_scene(mi, w=24, h=20, spp=8, floor=True, **kw):
     return mi.load_dict(d)
 
 
-@pytest.mark.parametrize("kw", [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0},
-                                {"max_depth": 8, "g": -0.3, "albedo": [0.9, 0.5, 0.2], "floor": False}])
-def test_prbvolpath_per_sample_parity(kw):
+PVP_CASES = [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0},
+             {"max_depth": 8, "g": -0.3, "albedo": [0.9, 0.5, 0.2], "floor": False},
+             {"max_depth": 3}, {"max_depth": 1}, {"max_depth": 0}, {"scale": 12.0, "max_depth": 12}]
+
+
+@pytest.mark.parametrize("mode", ["mega", "wavefront"])
+@pytest.mark.parametrize("kw", PVP_CASES)
+def test_prbvolpath_per_sample_parity(kw, mode):
+    """The primal per sample (prbvolpath.py:91-431, mode primal).  mega:
+    k_render<PRBVOLPATH>; wavefront: the phase-scheduled persistent kernel
+    (k_vol_sched<PvMachine>: the loop trip cut at its closest-hit queries
+    and at every step of the NEE walk).  Bit-identical per sample."""
     mi = _mi()
+    from mitsuba_hip import _abi as A
     scene = _pvp_scene(mi, **kw)
     integ = scene.integrator()
     assert integ.type == "prbvolpath"
-    L, pos = _gpu_samples(mi, scene, integ, 3, 8)
+    L, pos = _gpu_samples(mi, scene, integ, 3, 8, A.FLAG_WAVEFRONT if mode == "wavefront" else 0)
     rL, rpos, _ = O.sample_range(scene, integ, 3, 8, 0, L.shape[0])
     np.testing.assert_array_equal(pos, rpos)
-    assert np.abs(rL).max() > 0
+    # max_depth <= 1: nothing is added (emitter hits are not counted in the
+    # fork, prbvolpath.py:216-234, and NEE needs depth + 1 < max_depth)
+    assert (np.abs(rL).max() > 0) == (kw.get("max_depth", 6) > 1)
     exact = np.all(L == rL, axis=1)
     assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
     close = np.all(np.abs(L - rL) <= 1e-4 * np.maximum(1, np.abs(rL)), axis=1)
@@ -393,6 +407,26 @@ def test_prbvolpath_backward_parity(kw, nee, monkeypatch):
         assert a.shape == b.shape, k
         assert np.abs(b).max() > 0, k
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-7 + 2e-4 * np.abs(b).max(), err_msg=k)
+
+
+@pytest.mark.parametrize("alpha", [False, True])
+def test_prbvolpath_film_modes_agree(alpha):
+    """mh_render of prbvolpath: the phase scheduler (default) against the
+    megakernel and the oracle, films with and without the alpha channel
+    (valid_ray, prbvolpath.py:128, 274, 327), and the same ray counts."""
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    scene = _pvp_scene(mi, 40, 32, 16, **({"pixel_format": "rgba"} if alpha else {}))
+    integ = scene.integrator()
+    sw, sm = A.Stats(), A.Stats()
+    fw = mi.render_film(scene, integ, seed=5, spp=16, stats=sw).cpu().numpy()
+    fm = mi.render_film(scene, integ, seed=5, spp=16, mode="mega", stats=sm).cpu().numpy()
+    assert sw.mode == 3 and sm.mode == 0
+    assert (sw.rays_closest, sw.rays_shadow) == (sm.rays_closest, sm.rays_shadow)
+    ref = O.render(scene, integ, seed=5, spp=16)
+    for f in (fw, fm):
+        ok, frac = _film_close(f, ref)
+        assert ok, f"film parity {frac}"
 
 
 def test_prbvolpath_grid_update_changes_majorant():
