@@ -3,7 +3,7 @@
 cornell_box 512x512 @ 256 spp per GPU (BASELINE.json configs[1] + [2]).
 
 One step = one forward `path` render (max_depth 8) of the rank's 256-spp
-sample slab + the RCCL all-reduce of its RGBW film + develop, then one PRB
+sample slab + the RCCL reduce of its RGBW film onto rank 0 + develop, then one PRB
 render_backward (max_depth 8) w.r.t. 'white.reflectance.value' with
 grad_in = d mean(image) = 1/(H*W*3): the rank's W-image slab is all-reduced,
 its gradient slab computed and all-reduced.
@@ -42,6 +42,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=24.0, help="budget of the CPU baseline (thread curve: 1, 4, all threads)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     p.add_argument("--fwd-only", action="store_true")
+    p.add_argument("--local-weights", action="store_true",
+                   help="every rank computes the whole W image (no W all-reduce; N x the W splat work)")
+    p.add_argument("--film-all-reduce", action="store_true",
+                   help="all-reduce the film to every rank instead of reducing it onto rank 0")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' to rehearse "
                         "several ranks on one GPU)")
@@ -182,7 +186,8 @@ def main():
     spp_total = args.spp * world
 
     def step(i):
-        return D.fwd_grad_step(ops, slab, i, with_grad=not args.fwd_only)
+        return D.fwd_grad_step(ops, slab, i, with_grad=not args.fwd_only, local_weights=args.local_weights,
+                               film_to_root=not args.film_all_reduce)
 
     for i in range(args.warmup):
         step(1000 + i)
@@ -289,7 +294,10 @@ def main():
                                    + ("" if args.fwd_only else f" + prb backward wrt '{key}'"),
                        "film": f"{W}x{H}", "spp_per_gpu": args.spp, "spp_total": spp_total,
                        "parallelism": f"sample-slab x{world} + " +
-                                      ("RCCL all-reduce" if args.backend == "nccl" else f"{args.backend} all-reduce")},
+                                      ("RCCL" if args.backend == "nccl" else args.backend) +
+                                      (" all-reduce (film)" if args.film_all_reduce else " reduce to rank 0 (film)") +
+                                      (", local W" if args.local_weights else ", all-reduce (W)") +
+                                      ", all-reduce (gradient)"},
             "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
             "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
             "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),

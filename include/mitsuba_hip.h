@@ -32,6 +32,11 @@
  *   mh_trace_closest / mh_trace_shadow
  *       Scene::ray_intersect_preliminary_gpu / ray_test_gpu (the OptiX slot)
  *       src/render/scene_optix.inl:592-721, include/mitsuba/render/optix/common.h:43-58
+ *   mh_comm_* / mh_scene_set_comm / mh_render_sharded / mh_render_backward_sharded
+ *       no reference counterpart (the reference renders on one device); they
+ *       split the sample loop of SamplingIntegrator::render
+ *       (src/render/integrator.cpp:276-390) and of render_backward
+ *       (common.py:828-983) into per-device slabs, SURVEY.md §8(e)
  *
  * Units / conventions: all matrices are row-major float[16] (4x4) or
  * float[12] (3x4 affine, last row implicitly 0 0 0 1) and equal the
@@ -104,8 +109,19 @@ enum {
     MH_FLAG_MEGAKERNEL      = 1u << 3,  /* mh_render: force the per-lane megakernel */
     MH_FLAG_WAVEFRONT       = 1u << 4,  /* mh_render: force the wavefront (trace/shade/shadow) kernels */
     MH_FLAG_PRB_REPLAY      = 1u << 5,  /* mh_render_backward: primal + adjoint replay even for rgb params */
-    MH_FLAG_DETERMINISTIC   = 1u << 6   /* film / W-image splat as a fixed-order gather instead of float
+    MH_FLAG_DETERMINISTIC   = 1u << 6,  /* film / W-image splat as a fixed-order gather instead of float
                                            atomics: bit-reproducible films (also env MH_DETERMINISTIC=1) */
+    /* multi-GPU (the scene has a communicator, mh_scene_set_comm; one host
+       thread per rank): the call sums its result over the ranks in-call, on
+       the scene's stream -- mh_render / mh_render_forward the film,
+       mh_prb_weights the W image, mh_render_backward the W image it computes
+       (weights == NULL) and the gradients */
+    MH_FLAG_REDUCE          = 1u << 7,  /* all ranks receive the sum */
+    MH_FLAG_REDUCE_ROOT     = 1u << 8,  /* films: only rank 0 receives the sum (a reduce, not an all-reduce);
+                                           the other ranks' film is left undefined */
+    MH_FLAG_LOCAL_WEIGHTS   = 1u << 9   /* mh_render_backward with weights == NULL and MH_FLAG_REDUCE: every rank
+                                           computes the whole W image itself (all spp of every pixel) instead
+                                           of its slab's W + an all-reduce */
 };
 
 /* ----------------------------------------------------------------------- */
@@ -365,6 +381,75 @@ int mh_trace_shadow(mh_scene *scene, uint64_t n, const float *rays, uint32_t *oc
 
 /* BVH introspection (host): #nodes, #primitives, max depth. */
 int mh_scene_bvh_info(mh_scene *scene, uint32_t *n_nodes, uint32_t *n_prims, uint32_t *depth);
+
+/* ----------------------------------------------------------------------- */
+/* Multi-GPU: sample-slab sharding + RCCL over xGMI        */
+/* ----------------------------------------------------------------------- */
+/*
+ * The reference renders one device per process and has no collective: its
+ * splice point is SamplingIntegrator::render (src/render/integrator.cpp:276-390),
+ * whose sample loop this layer cuts into per-device slabs [spp*r/N, spp*(r+1)/N)
+ * of every pixel.  The global lane index (hence every lane's TEA seed,
+ * integrator.cpp:323-340) is the single-device one, so the slabs' union is
+ * sample-identical to one render and the only exchanges are sums: the film,
+ * the W image of render_backward (common.py:936-947) and the gradients.
+ *
+ * An mh_comm is one rank of an RCCL communicator, bound to one device.  RCCL
+ * (librccl.so.1) is loaded on first use; without it these calls return
+ * MH_ERR_UNSUPPORTED and the rest of the library is unaffected.
+ *   mh_comm_unique_id   : rank 0 creates the id and ships it to the others
+ *                         (any out-of-band channel: MPI, a file, a socket)
+ *   mh_comm_create      : one rank per host thread / process (ncclCommInitRank)
+ *   mh_comm_create_all  : one host thread drives `ndev` devices (ncclCommInitAll);
+ *                         out[i] is the rank on devices[i]
+ */
+#define MH_COMM_ID_BYTES 128
+typedef struct mh_comm mh_comm;
+int mh_comm_unique_id(uint8_t id[MH_COMM_ID_BYTES]);
+int mh_comm_create(const uint8_t id[MH_COMM_ID_BYTES], int nranks, int rank, int device, mh_comm **out);
+int mh_comm_create_all(int ndev, const int *devices, mh_comm **out);
+int mh_comm_destroy(mh_comm *comm);
+int mh_comm_info(const mh_comm *comm, int *nranks, int *rank, int *device);
+/*
+ * Sum `count` floats over the ranks, in place, for `n` ranks driven by the
+ * calling thread (n == 1 for one thread per rank; all of them in one RCCL
+ * group otherwise).  bufs[i] / streams[i] live on comms[i]'s device (a NULL
+ * stream is that device's null stream).  root < 0: all-reduce; root = r:
+ * reduce to rank r.  Stream-ordered: returns once enqueued.
+ */
+int mh_comm_reduce(mh_comm *const *comms, int n, float *const *bufs, uint64_t count, void *const *streams,
+                   int root);
+/* The scene's communicator for MH_FLAG_REDUCE / MH_FLAG_REDUCE_ROOT (NULL
+ * detaches); its device must be the scene's. */
+int mh_scene_set_comm(mh_scene *scene, mh_comm *comm);
+/* Wait for the scene's stream (after MH_FLAG_NO_SYNC calls). */
+int mh_scene_synchronize(mh_scene *scene);
+
+/*
+ * One host thread drives `n` scenes (one per device, or several on one device):
+ * scene i renders the sample slab [spp*i/n, spp*(i+1)/n) of every pixel, the
+ * slabs run concurrently on the scenes' streams, and the films are summed
+ * into films[0] (root) or into every films[i] (MH_FLAG_REDUCE).  The sum goes
+ * over the scenes' communicators when every scene has one (one RCCL group),
+ * else through device copies onto scene 0's device (peer copies between
+ * devices; scenes sharing a device need no peer access).  films[i]: device
+ * pointers on scene i's device (MH_FLAG_DEVICE_POINTERS is implied).  stats
+ * (optional): n entries.  Returns after every stream has drained.
+ */
+int mh_render_sharded(mh_scene *const *scenes, uint32_t n, const mh_integrator *integrator, uint32_t seed,
+                      uint32_t spp, float *const *films, uint32_t flags, mh_stats *stats);
+/*
+ * render_backward over the same slabs: every scene computes its slab's W
+ * image, the W images are summed to every scene, each scene differentiates
+ * its slab with the total W, and the gradients are summed into every
+ * grads[i * n_params + k] (device pointers on scene i's device; accumulated
+ * into like mh_render_backward).  grad_in[i]: d loss / d image on scene i's
+ * device (the same image on every scene).
+ */
+int mh_render_backward_sharded(mh_scene *const *scenes, uint32_t n, const mh_integrator *integrator,
+                               uint32_t seed, uint32_t spp, const float *const *grad_in, uint32_t n_params,
+                               const uint32_t *param_textures, float *const *grads, uint32_t flags,
+                               mh_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -89,6 +90,8 @@ hipError_t upload(DevBuf &b, const T *src, size_t count, hipStream_t st) {
 
 }  // namespace
 
+int mh_report_error(int code, const std::string &msg) { return set_error(code, msg); }
+
 struct mh_scene {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -104,6 +107,11 @@ struct mh_scene {
     DevBuf wf_ws_bmp;  // wavefront PRB with a bitmap parameter: vertex records (WfBmp)
     DevBuf pvp_log;    // prbvolpath backward: per-thread NEE-walk step logs (NeeLog)
     DevBuf pvp_main;   // prbvolpath backward: per-thread path logs of the single pass (MainLog)
+    // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
+    // buffers of the sharded entry points (slab W image, staged peer sums,
+    // slab gradients)
+    mh_comm *comm = nullptr;
+    DevBuf shard_w, shard_tmp, shard_g;
     // host mirrors (parameter updates)
     std::vector<DTexture> h_textures;
     std::vector<mh_medium> h_media;
@@ -464,7 +472,8 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->pvp_log, &s->pvp_main})
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->pvp_log, &s->pvp_main,
+                      &s->shard_w, &s->shard_tmp, &s->shard_g})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -650,7 +659,8 @@ static int check_bounds_counter(mh_scene *s, const char *api);
 // and NEE-log entries per thread (16 B each; longer walks replay)
 constexpr uint32_t kPvpBlocksPerCu = 4, kPvpNeeCap = 256;
 // MainLog entries per thread (64 B each: 4 GiB over the 262,144 threads of a
-// 256-CU grid); a path with more logged vertices replays its adjoint
+// 256-CU grid, less when the render has fewer samples than threads); a path
+// with more logged vertices replays its adjoint
 constexpr uint32_t kPvpMainCap = 256;
 // MH_FLAG_DETERMINISTIC or MH_DETERMINISTIC=1: fixed-order splat (k_splat_gather)
 static bool deterministic(uint32_t flags) {
@@ -672,6 +682,30 @@ static int check_bounds_counter(mh_scene *s, const char *api) {
     return MH_OK;
 }
 
+// MH_FLAG_REDUCE / MH_FLAG_REDUCE_ROOT: the call's result summed over the
+// scene's communicator (mh_comm.cpp), stream-ordered behind the kernels that
+// produced it.  A film honours MH_FLAG_REDUCE_ROOT (a reduce to rank 0); W
+// images and gradients are needed on every rank and are always all-reduced.
+static bool wants_reduce(uint32_t flags) { return flags & (MH_FLAG_REDUCE | MH_FLAG_REDUCE_ROOT); }
+
+static int check_reduce_flags(const mh_scene *s, uint32_t flags, const char *api, bool accumulating_output) {
+    if (!wants_reduce(flags)) return MH_OK;
+    if (!s->comm)
+        return set_error(MH_ERR_INVALID_ARGUMENT,
+                         std::string(api) + ": MH_FLAG_REDUCE needs a communicator (mh_scene_set_comm)");
+    if (accumulating_output && (flags & MH_FLAG_ACCUMULATE))
+        return set_error(MH_ERR_INVALID_ARGUMENT,
+                         std::string(api) + ": MH_FLAG_REDUCE cannot be combined with MH_FLAG_ACCUMULATE "
+                                            "(the sum would count the accumulated content once per rank)");
+    return MH_OK;
+}
+
+static int reduce_result(mh_scene *s, uint32_t flags, float *buf, uint64_t count, hipStream_t st, bool film) {
+    if (!wants_reduce(flags)) return MH_OK;
+    const int root = (film && (flags & MH_FLAG_REDUCE_ROOT) && !(flags & MH_FLAG_REDUCE)) ? 0 : -1;
+    return comm_reduce_one(s->comm, s->device, buf, count, st, root);
+}
+
 // MH_FLAG_DEVICE_POINTERS | MH_FLAG_NO_SYNC without stats: nothing is read
 // back to the host, so the call returns with its work enqueued on the stream
 static bool async_call(uint32_t flags, const mh_stats *stats) {
@@ -687,6 +721,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     if (in->rr_depth == 0)
         return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: spp must be > 0");
+    if (int rc = check_reduce_flags(s, flags, "mh_render", true)) return rc;
     double t_start = now_ms();
     Layout L;
     const bool ad = in->type == MH_INTEGRATOR_PRB || in->type == MH_INTEGRATOR_PRBVOLPATH;
@@ -805,6 +840,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                      seed_value, coalesce, st, nullptr, determ, s->work.bytes / 4, n_px, bounds);
     }
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
+    if (int rc = reduce_result(s, flags, film, film_bytes / 4, st, true)) return rc;
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
     // asynchronous call (device film, no stats): return once the work is
@@ -980,6 +1016,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     ScopedPhase phase_("ImageBlockPut");
     if (!s || !weights) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: NULL argument");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: spp must be > 0");
+    if (int rc = check_reduce_flags(s, flags, "mh_prb_weights", true)) return rc;
     Layout L;
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
     if (rc) return rc;
@@ -998,6 +1035,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     const uint32_t S_ = L.s_end - L.s_begin;
     MH_SPLAT(s->S, lm, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * S_, 0, nullptr, w, s->S.sampler_seed + seed,
              L.spp_pp >= 4, st, nullptr, deterministic(flags), 0, n_px, nullptr);
+    if (int rc = reduce_result(s, flags, w, n_px, st, false)) return rc;
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
     if (!async_call(flags, nullptr)) MH_HIP(hipStreamSynchronize(st));
@@ -1130,6 +1168,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (in->rr_depth == 0)
         return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: spp must be > 0");
+    if (int rc = check_reduce_flags(s, flags, "mh_render_backward", false)) return rc;
     double t_start = now_ms();
     Layout L;
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
@@ -1171,13 +1210,21 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(hipMemsetAsync(s->weights_tmp.ptr, 0, n_px * 4, st));
         const bool fast = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN &&
                           s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
+        // W of every sample of every pixel (common.py:936-947); with
+        // MH_FLAG_REDUCE the slab's own samples + an all-reduce, unless each
+        // rank is to compute the whole image itself (MH_FLAG_LOCAL_WEIGHTS)
+        const bool slab_w = wants_reduce(flags) && !(flags & MH_FLAG_LOCAL_WEIGHTS);
         Layout Lall = L;
-        Lall.s_begin = 0;
-        Lall.s_end = L.spp_pp;
+        if (!slab_w) {
+            Lall.s_begin = 0;
+            Lall.s_end = L.spp_pp;
+        }
         LaneMap lmw = lane_map(Lall, 0);
-        MH_SPLAT(s->S, lmw, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * L.spp_pp, 0, nullptr,
+        MH_SPLAT(s->S, lmw, kSplatWeights, fast, (uint32_t)n_px, 1, n_px * (Lall.s_end - Lall.s_begin), 0, nullptr,
                  s->weights_tmp.as<float>(), s->S.sampler_seed + seed, L.spp_pp >= 4, st, nullptr,
                  deterministic(flags), 0, n_px, nullptr);
+        if (slab_w)
+            if (int rc = reduce_result(s, flags, s->weights_tmp.as<float>(), n_px, st, false)) return rc;
         w = s->weights_tmp.as<float>();
     } else if (!dev) {
         MH_HIP(s->tmp_e.alloc(n_px * 4));
@@ -1270,17 +1317,28 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
         const char *ecap = getenv("MH_PVP_NEE_CAP");  // tests: small logs exercise the replay fallback
-        const uint32_t blocks = (uint32_t)cus * kPvpBlocksPerCu,
+        // the persistent grid (and with it both per-thread logs) shrinks to the
+        // work: a wave takes 64 samples per batch, so more threads than samples
+        // would only hold log space
+        const uint32_t blocks = (uint32_t)std::max<uint64_t>(
+                               1, std::min<uint64_t>((uint64_t)cus * kPvpBlocksPerCu, (n + 255) / 256)),
                        cap = ecap ? (uint32_t)std::max(1, atoi(ecap)) : kPvpNeeCap;
-        MH_HIP(s->pvp_log.alloc((size_t)blocks * 256 * cap * 16));
         // single pass (MainLog) unless MH_PVP_SINGLE=0; MH_PVP_MAIN_CAP: entries per thread
         const char *esp = getenv("MH_PVP_SINGLE"), *emc = getenv("MH_PVP_MAIN_CAP");
-        const uint32_t main_cap = (esp && !strcmp(esp, "0")) ? 0u
-                                  : emc ? (uint32_t)std::max(1, atoi(emc)) : kPvpMainCap;
-        if (main_cap) MH_HIP(s->pvp_main.alloc((size_t)blocks * 256 * main_cap * 64));
+        uint32_t main_cap = (esp && !strcmp(esp, "0")) ? 0u : emc ? (uint32_t)std::max(1, atoi(emc)) : kPvpMainCap;
+        // a log that cannot be allocated degrades the kernel instead of failing
+        // the call: no MainLog -> primal + adjoint replay per sample; no NeeLog
+        // either -> one thread per sample with the NEE walks replayed
+        bool nee_ok = s->pvp_log.alloc((size_t)blocks * 256 * cap * 16) == hipSuccess;
+        if (!nee_ok) { (void)hipGetLastError(); s->pvp_log.release(); }
+        if (main_cap && (!nee_ok || s->pvp_main.alloc((size_t)blocks * 256 * main_cap * 64) != hipSuccess)) {
+            (void)hipGetLastError();
+            s->pvp_main.release();
+            main_cap = 0;
+        }
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st,
-                                   s->pvp_log.as<float4>(), cap, blocks,
+                                   nee_ok ? s->pvp_log.as<float4>() : nullptr, cap, blocks,
                                    s->counters.as<unsigned long long>() + kCtrPvpHead,
                                    main_cap ? s->pvp_main.as<float4>() : nullptr, main_cap));
     } else {
@@ -1288,6 +1346,11 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
     }
     MH_HIP(hipEventRecord(s->ev1, st));
+    if (wants_reduce(flags)) {  // the slot buffers are one block of s->tmp_c (upload_slots)
+        size_t total = 0;
+        for (int k = 0; k < kMaxParams; ++k) total += (counts[k] + 3) / 4 * 4;
+        if (int rc = reduce_result(s, flags, s->tmp_c.as<float>(), total, st, false)) return rc;
+    }
     // accumulate into the caller's gradient buffers
     std::vector<float> host_tmp;
     for (uint32_t k = 0; k < n_params; ++k) {
@@ -1359,6 +1422,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     if (in->rr_depth == 0)
         return set_error(MH_ERR_INVALID_ARGUMENT, "\"rr_depth\" must be set to a value greater than zero!");
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_forward: spp must be > 0");
+    if (int rc = check_reduce_flags(s, flags, "mh_render_forward", true)) return rc;
     const double t_start = now_ms();
     Layout L;
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);  // prepare(): one wavefront of <= 2^32
@@ -1444,6 +1508,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     }
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     MH_HIP(hipEventRecord(s->ev1, st));
+    if (int rc2 = reduce_result(s, flags, film, film_bytes / 4, st, true)) return rc2;
     if (!dev) MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
     if (async_call(flags, stats)) return MH_OK;
     if (!stats) {
@@ -1550,6 +1615,200 @@ int mh_trace_shadow(mh_scene *s, uint64_t n, const float *rays, uint32_t *occlud
     if (n && !occluded) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace_shadow: NULL output");
     return trace_impl(s, true, n, rays, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, occluded, flags,
                       stats);
+}
+
+// ===========================================================================
+// Multi-GPU (include/mitsuba_hip.h, "Multi-GPU").  The
+// reference's splice point is SamplingIntegrator::render
+// (src/render/integrator.cpp:276-390): its sample loop is cut into per-device
+// slabs of every pixel, whose union is sample-identical to one render.
+// ===========================================================================
+int mh_scene_set_comm(mh_scene *s, mh_comm *comm) {
+    if (!s) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_set_comm: NULL scene");
+    if (comm) {
+        int dev = -1;
+        if (int rc = mh_comm_info(comm, nullptr, nullptr, &dev)) return rc;
+        if (dev != s->device)
+            return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_set_comm: the communicator's device is not the scene's");
+    }
+    s->comm = comm;
+    return MH_OK;
+}
+
+int mh_scene_synchronize(mh_scene *s) {
+    if (!s) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_synchronize: NULL scene");
+    MH_HIP(hipSetDevice(s->device));
+    MH_HIP(hipStreamSynchronize(s->stream));
+    return check_bounds_counter(s, "mh_scene_synchronize");
+}
+
+}  // extern "C"
+
+namespace {
+
+// slab i of n: samples [spp*i/n, spp*(i+1)/n) of every pixel
+uint32_t slab_edge(uint32_t spp, uint32_t i, uint32_t n) { return (uint32_t)((uint64_t)spp * i / n); }
+
+// fn(i) for every scene, each on a host thread of its own: the devices (and
+// streams) then run concurrently although every call synchronises, and an
+// in-call collective finds all of its ranks issued.  The first failure wins.
+template <class F>
+int for_each_scene(uint32_t n, F fn) {
+    std::vector<int> rc(n, MH_OK);
+    std::vector<std::string> msg(n);
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (uint32_t i = 0; i < n; ++i)
+        th.emplace_back([&, i] {
+            rc[i] = fn(i);
+            if (rc[i]) msg[i] = g_error;  // the worker thread's own message
+        });
+    for (auto &t : th) t.join();
+    for (uint32_t i = 0; i < n; ++i)
+        if (rc[i]) return set_error(rc[i], "scene " + std::to_string(i) + ": " + msg[i]);
+    return MH_OK;
+}
+
+// argument checks shared by the sharded entry points; *comm = every scene
+// has a communicator whose ranks are the scenes' order (else none may have one)
+int check_shards(mh_scene *const *sc, uint32_t n, uint32_t spp, const char *api, bool *comm) {
+    const std::string a(api);
+    if (!sc || n == 0) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": no scenes");
+    if (spp < n) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": spp must be >= the number of scenes (one slab each)");
+    uint32_t with = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!sc[i]) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": NULL scene");
+        for (uint32_t j = 0; j < i; ++j)
+            if (sc[j] == sc[i]) return set_error(MH_ERR_INVALID_ARGUMENT, a + ": a scene appears twice (one per slab)");
+        if (sc[i]->S.width != sc[0]->S.width || sc[i]->S.height != sc[0]->S.height ||
+            sc[i]->pixel_format != sc[0]->pixel_format)
+            return set_error(MH_ERR_INVALID_ARGUMENT, a + ": the scenes' films differ");
+        with += sc[i]->comm ? 1u : 0u;
+    }
+    if (with != 0 && with != n)
+        return set_error(MH_ERR_INVALID_ARGUMENT, a + ": either every scene has a communicator or none has");
+    for (uint32_t i = 0; i < with; ++i) {
+        int nr = 0, r = 0;
+        mh_comm_info(sc[i]->comm, &nr, &r, nullptr);
+        if (nr != (int)n || r != (int)i)
+            return set_error(MH_ERR_INVALID_ARGUMENT, a + ": scene i's communicator must be rank i of n");
+    }
+    *comm = with == n;
+    return MH_OK;
+}
+
+// the sum without a communicator: bufs[i] (count floats on scene i's device)
+// are copied onto scene 0's device (peer copies; a plain device copy when the
+// scenes share it) and added into bufs[0] in scene order; `all` copies the
+// sum back to every bufs[i].  Every stream has drained before and after.
+int peer_sum(mh_scene *const *sc, uint32_t n, float *const *bufs, uint64_t count, bool all) {
+    mh_scene *s0 = sc[0];
+    MH_HIP(hipSetDevice(s0->device));
+    MH_HIP(s0->shard_tmp.alloc(count * 4));
+    for (uint32_t i = 1; i < n; ++i) {
+        MH_HIP(hipMemcpyPeerAsync(s0->shard_tmp.ptr, s0->device, bufs[i], sc[i]->device, count * 4, s0->stream));
+        MH_HIP(launch_accumulate(bufs[0], s0->shard_tmp.as<float>(), count, s0->stream));
+    }
+    if (all)
+        for (uint32_t i = 1; i < n; ++i)
+            MH_HIP(hipMemcpyPeerAsync(bufs[i], sc[i]->device, bufs[0], s0->device, count * 4, s0->stream));
+    MH_HIP(hipStreamSynchronize(s0->stream));
+    return MH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mh_render_sharded(mh_scene *const *scenes, uint32_t n, const mh_integrator *in, uint32_t seed, uint32_t spp,
+                      float *const *films, uint32_t flags, mh_stats *stats) {
+    ScopedPhase phase_("Render");
+    bool comm = false;
+    if (int rc = check_shards(scenes, n, spp, "mh_render_sharded", &comm)) return rc;
+    if (!in || !films) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_sharded: NULL argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (!films[i]) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_sharded: NULL film");
+    if (flags & MH_FLAG_ACCUMULATE)
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_sharded: MH_FLAG_ACCUMULATE is not supported (the sum "
+                                                  "would count the accumulated film once per scene)");
+    const uint32_t pass = (flags & (MH_FLAG_DETERMINISTIC | MH_FLAG_MEGAKERNEL | MH_FLAG_WAVEFRONT)) |
+                          MH_FLAG_DEVICE_POINTERS;
+    const uint32_t red = comm ? ((flags & MH_FLAG_REDUCE) ? MH_FLAG_REDUCE : MH_FLAG_REDUCE_ROOT) : 0u;
+    int rc = for_each_scene(n, [&](uint32_t i) {
+        return mh_render(scenes[i], in, seed, spp, slab_edge(spp, i, n), slab_edge(spp, i + 1, n), films[i],
+                         pass | red, stats ? &stats[i] : nullptr);
+    });
+    if (rc || comm) return rc;
+    const uint64_t count = (uint64_t)scenes[0]->S.width * scenes[0]->S.height * (has_alpha(scenes[0]->pixel_format) ? 5 : 4);
+    return peer_sum(scenes, n, films, count, flags & MH_FLAG_REDUCE);
+}
+
+int mh_render_backward_sharded(mh_scene *const *scenes, uint32_t n, const mh_integrator *in, uint32_t seed,
+                               uint32_t spp, const float *const *grad_in, uint32_t n_params,
+                               const uint32_t *param_tex, float *const *grads, uint32_t flags, mh_stats *stats) {
+    ScopedPhase phase_("RenderBackward");
+    bool comm = false;
+    if (int rc = check_shards(scenes, n, spp, "mh_render_backward_sharded", &comm)) return rc;
+    if (!in || !grad_in || (n_params && (!param_tex || !grads)))
+        return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward_sharded: NULL argument");
+    const uint32_t pass = (flags & (MH_FLAG_DETERMINISTIC | MH_FLAG_MEGAKERNEL | MH_FLAG_PRB_REPLAY)) |
+                          MH_FLAG_DEVICE_POINTERS;
+    if (comm)  // every rank: slab W + all-reduce, its slab's gradient, all-reduce (mh_render_backward in-call)
+        return for_each_scene(n, [&](uint32_t i) {
+            return mh_render_backward(scenes[i], in, seed, spp, slab_edge(spp, i, n), slab_edge(spp, i + 1, n),
+                                      grad_in[i], nullptr, n_params, param_tex, grads + (size_t)i * n_params,
+                                      pass | MH_FLAG_REDUCE | (flags & MH_FLAG_LOCAL_WEIGHTS),
+                                      stats ? &stats[i] : nullptr);
+        });
+    // without communicators: the slab W images summed onto every scene ...
+    const uint64_t n_px = (uint64_t)scenes[0]->S.width * scenes[0]->S.height;
+    std::vector<float *> wb(n), gb(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        MH_HIP(hipSetDevice(scenes[i]->device));
+        MH_HIP(scenes[i]->shard_w.alloc(n_px * 4));
+        wb[i] = scenes[i]->shard_w.as<float>();
+    }
+    int rc = for_each_scene(n, [&](uint32_t i) {
+        return mh_prb_weights(scenes[i], seed, spp, slab_edge(spp, i, n), slab_edge(spp, i + 1, n), wb[i],
+                              pass & (MH_FLAG_DEVICE_POINTERS | MH_FLAG_DETERMINISTIC));
+    });
+    if (rc) return rc;
+    if ((rc = peer_sum(scenes, n, wb.data(), n_px, true))) return rc;
+    // ... each slab's gradient into zeroed per-scene buffers, summed, then
+    // accumulated into the caller's buffers as mh_render_backward does
+    Slots P;
+    if ((rc = build_slots(scenes[0], n_params, param_tex, in->type == MH_INTEGRATOR_PRBVOLPATH,
+                          "mh_render_backward_sharded", "render_backward", P)))
+        return rc;
+    std::vector<uint64_t> off(n_params + 1, 0);
+    for (uint32_t k = 0; k < n_params; ++k) off[k + 1] = off[k] + P.counts[P.slot_of_param[k]];
+    const uint64_t total = std::max<uint64_t>(off[n_params], 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        MH_HIP(hipSetDevice(scenes[i]->device));
+        MH_HIP(scenes[i]->shard_g.alloc(total * 4));
+        gb[i] = scenes[i]->shard_g.as<float>();
+        MH_HIP(hipMemsetAsync(gb[i], 0, total * 4, scenes[i]->stream));
+        MH_HIP(hipStreamSynchronize(scenes[i]->stream));
+    }
+    rc = for_each_scene(n, [&](uint32_t i) {
+        std::vector<float *> gp(std::max<uint32_t>(n_params, 1));
+        for (uint32_t k = 0; k < n_params; ++k) gp[k] = gb[i] + off[k];
+        return mh_render_backward(scenes[i], in, seed, spp, slab_edge(spp, i, n), slab_edge(spp, i + 1, n),
+                                  grad_in[i], wb[i], n_params, param_tex, gp.data(), pass, stats ? &stats[i] : nullptr);
+    });
+    if (rc) return rc;
+    if ((rc = peer_sum(scenes, n, gb.data(), total, true))) return rc;
+    for (uint32_t i = 0; i < n; ++i) {
+        MH_HIP(hipSetDevice(scenes[i]->device));
+        for (uint32_t k = 0; k < n_params; ++k) {
+            if (!grads[(size_t)i * n_params + k])
+                return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward_sharded: NULL gradient buffer");
+            MH_HIP(launch_accumulate(grads[(size_t)i * n_params + k], gb[i] + off[k], off[k + 1] - off[k],
+                                     scenes[i]->stream));
+        }
+        MH_HIP(hipStreamSynchronize(scenes[i]->stream));
+    }
+    return MH_OK;
 }
 
 }  // extern "C"

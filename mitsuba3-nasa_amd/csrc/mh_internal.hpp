@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
 #include <vector>
 
 #include "../../include/mitsuba_hip.h"
@@ -163,3 +164,9 @@ hipError_t launch_volwave(const DScene &S, const IntegratorParams &in, const Lan
                           uint32_t grid, unsigned long long *counters, hipStream_t st, int alpha);
 
 }  // namespace mh
+
+// ---- shared by mh_api.hip and mh_comm.cpp (global namespace, C-ABI side) ----
+// sets mh_last_error() of the calling thread and returns `code`
+int mh_report_error(int code, const std::string &msg);
+// one rank's in-call sum over its communicator (root < 0: all-reduce), stream-ordered on st
+int comm_reduce_one(mh_comm *c, int device, float *buf, uint64_t count, hipStream_t st, int root);

@@ -14,6 +14,7 @@ INVALID = 0xFFFFFFFF
 
 # status codes
 MH_OK = 0
+MH_ERR_INVALID_ARGUMENT, MH_ERR_HIP, MH_ERR_OUT_OF_MEMORY, MH_ERR_UNSUPPORTED, MH_ERR_NO_DEVICE = 1, 2, 3, 4, 5
 ERRORS = {1: "invalid argument", 2: "HIP error", 3: "out of memory", 4: "unsupported", 5: "no device"}
 
 SHAPE_RECTANGLE, SHAPE_MESH = 0, 1
@@ -58,6 +59,10 @@ FLAG_MEGAKERNEL = 1 << 3
 FLAG_WAVEFRONT = 1 << 4
 FLAG_PRB_REPLAY = 1 << 5
 FLAG_DETERMINISTIC = 1 << 6
+FLAG_REDUCE = 1 << 7
+FLAG_REDUCE_ROOT = 1 << 8
+FLAG_LOCAL_WEIGHTS = 1 << 9
+COMM_ID_BYTES = 128
 
 u32, u64, f32, f64 = C.c_uint32, C.c_uint64, C.c_float, C.c_double
 PF = C.POINTER(C.c_float)
@@ -133,7 +138,9 @@ EXPORTS = [
     "mh_scene_set_stream", "mh_scene_update_rgb", "mh_scene_update_texture", "mh_render",
     "mh_develop", "mh_prb_weights", "mh_render_backward", "mh_trace_closest", "mh_trace_shadow",
     "mh_scene_bvh_info", "mh_render_samples", "mh_scene_update_medium", "mh_trace_preliminary",
-    "mh_render_forward",
+    "mh_render_forward", "mh_comm_unique_id", "mh_comm_create", "mh_comm_create_all", "mh_comm_destroy",
+    "mh_comm_info", "mh_comm_reduce", "mh_scene_set_comm", "mh_scene_synchronize", "mh_render_sharded",
+    "mh_render_backward_sharded",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -185,6 +192,19 @@ def lib():
     L.mh_trace_shadow.argtypes = [vp, u64, vp, vp, u32, C.POINTER(Stats)]
     L.mh_trace_preliminary.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, C.POINTER(Stats)]
     L.mh_scene_bvh_info.argtypes = [vp, PU, PU, PU]
+    pi = C.POINTER(C.c_int)
+    L.mh_comm_unique_id.argtypes = [C.c_char_p]
+    L.mh_comm_create.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]
+    L.mh_comm_create_all.argtypes = [C.c_int, pi, C.POINTER(vp)]
+    L.mh_comm_destroy.argtypes = [vp]
+    L.mh_comm_info.argtypes = [vp, pi, pi, pi]
+    L.mh_comm_reduce.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), u64, C.POINTER(vp), C.c_int]
+    L.mh_scene_set_comm.argtypes = [vp, vp]
+    L.mh_scene_synchronize.argtypes = [vp]
+    L.mh_render_sharded.argtypes = [C.POINTER(vp), u32, C.POINTER(Integrator), u32, u32, C.POINTER(vp), u32,
+                                    C.POINTER(Stats)]
+    L.mh_render_backward_sharded.argtypes = [C.POINTER(vp), u32, C.POINTER(Integrator), u32, u32, C.POINTER(vp),
+                                             u32, PU, C.POINTER(vp), u32, C.POINTER(Stats)]
     for name in EXPORTS:
         if name not in ("mh_last_error", "mh_abi_version"):
             getattr(L, name).restype = C.c_int

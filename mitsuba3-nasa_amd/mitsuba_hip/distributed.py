@@ -7,7 +7,7 @@ the TEA seed of every lane, integrator.cpp:323-340) is the one the single-GPU
 render uses, hence the union of the slabs is sample-identical to it.  The
 only coupling is additive:
 
-  forward   film (H, W, 4) RGBW                 -> all-reduce(sum), develop
+  forward   film (H, W, 4) RGBW                 -> all-reduce(sum) (or reduce to rank 0), develop
   PRB       W image (H, W) of render_backward   -> all-reduce(sum) before the
             dL gather (common.py:936-947), then each rank's gradient slab
             -> all-reduce(sum)
@@ -48,6 +48,18 @@ def all_reduce_(t):
     return t
 
 
+def reduce_to_root_(t):
+    """In-place sum onto rank 0 (no-op on one rank); the other ranks' tensor
+    is left undefined, as a reduce leaves it."""
+    d = _dist()
+    if d is not None:
+        if t.is_cuda and d.get_backend() == "gloo":
+            d.all_reduce(t)  # gloo reduces device tensors only by all-reduce; rank 0 gets the same sum
+        else:
+            d.reduce(t, dst=0)
+    return t
+
+
 @dataclass
 class StepOps:
     """The hot-path entry points one step calls (the C-ABI wrappers of
@@ -55,20 +67,29 @@ class StepOps:
     render_film: Callable      # (seed, spp_total, begin, end) -> film tensor (H, W, 4)
     develop: Callable          # (film) -> image (H, W, 3)
     prb_weights: Callable      # (seed, spp_total, begin, end) -> W (H, W)
-    render_backward: Callable  # (seed, spp_total, begin, end, weights) -> [grad tensors]
+    render_backward: Callable  # (seed, spp_total, begin, end, weights) -> [grad tensors]; weights None:
+                               # the W image of every sample computed in-call (local W)
     seed_grad: Callable        # (seed) -> seed of the differential pass (TEA(seed, 1).v0)
 
 
-def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True):
+def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, local_weights: bool = False,
+                  film_to_root: bool = False):
     """One benchmark step: forward render of the rank's slab + film
     all-reduce + develop; then (with_grad) PRB render_backward of the slab
-    with the globally all-reduced W image and an all-reduced gradient."""
-    film = all_reduce_(ops.render_film(seed, slab.spp_total, slab.begin, slab.end))
+    with the globally all-reduced W image and an all-reduced gradient.
+
+    local_weights: every rank computes the whole W image itself (all
+    spp_total samples of every pixel) instead of its slab's W + an
+    all-reduce -- one collective fewer for N times the W splat work.
+    film_to_root: the film is summed onto rank 0 only (a reduce, not an
+    all-reduce); only rank 0's image is then defined."""
+    film = ops.render_film(seed, slab.spp_total, slab.begin, slab.end)
+    film = reduce_to_root_(film) if film_to_root else all_reduce_(film)
     img = ops.develop(film)
     if not with_grad:
         return img, None
     sg = ops.seed_grad(seed)
-    w = all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end))
+    w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end))
     grads: List = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
     for g in grads:
         all_reduce_(g)

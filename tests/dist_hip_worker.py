@@ -26,10 +26,14 @@ def main():
     # reused, each call stream-ordered behind the previous step's develop
     D.fwd_grad_step(w["ops"], w["slab"], seed=3)
     img, grads = D.fwd_grad_step(w["ops"], w["slab"], seed=11)
+    # the same step with every rank computing the whole W image itself (no W
+    # all-reduce; mh_render_backward's in-call W) and the film summed onto
+    # rank 0 only
+    img2, grads2 = D.fwd_grad_step(w["ops"], w["slab"], seed=11, local_weights=True, film_to_root=True)
     torch.cuda.synchronize()
     t = D.max_over_ranks(float(rank) + 0.25, torch.device("cuda:0"))
     np.savez(os.path.join(out, f"r{rank}.npz"), img=img.cpu().numpy(), g=grads[0].cpu().numpy(), t=t,
-             begin=w["slab"].begin, end=w["slab"].end)
+             begin=w["slab"].begin, end=w["slab"].end, img2=img2.cpu().numpy(), g2=grads2[0].cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
 

@@ -87,7 +87,8 @@ def test_struct_layouts_match_header():
 def test_flags_match_header():
     from mitsuba_hip import _abi as A
     src = open(HEADER).read()
-    for name in ("DEVICE_POINTERS", "ACCUMULATE", "NO_SYNC", "MEGAKERNEL", "WAVEFRONT", "PRB_REPLAY", "DETERMINISTIC"):
+    for name in ("DEVICE_POINTERS", "ACCUMULATE", "NO_SYNC", "MEGAKERNEL", "WAVEFRONT", "PRB_REPLAY", "DETERMINISTIC", "REDUCE",
+                 "REDUCE_ROOT", "LOCAL_WEIGHTS"):
         m = re.search(rf"MH_FLAG_{name}\s*=\s*1u << (\d+)", src)
         assert m, name
         assert getattr(A, "FLAG_" + name) == 1 << int(m.group(1))
@@ -107,3 +108,27 @@ def test_product_path_has_no_cpu_fallback():
         scene = mi.load_dict({"type": "scene", "r": {"type": "rectangle"}})
         with pytest.raises(Exception):
             mi.render_film(scene, spp=1)
+
+
+def test_comm_entry_points_without_a_device(lib):
+    """The multi-GPU C ABI loads RCCL lazily: a unique id can be made on any
+    host (RCCL's bootstrap handle), and creating a rank without a device
+    fails with MH_ERR_NO_DEVICE and a message -- no CPU fallback."""
+    from mitsuba_hip import _abi as A
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present (covered by tests/test_gpu_comm.py)")
+    uid = C.create_string_buffer(A.COMM_ID_BYTES)
+    rc = lib.mh_comm_unique_id(uid)
+    if rc == A.MH_ERR_UNSUPPORTED:  # RCCL not installed on this host
+        assert b"RCCL" in lib.mh_last_error()
+        return
+    assert rc == A.MH_OK and any(uid.raw)
+    h = C.c_void_p()
+    assert lib.mh_comm_create(uid, 1, 0, 0, C.byref(h)) == A.MH_ERR_NO_DEVICE
+    assert b"no HIP device" in lib.mh_last_error()
+    assert lib.mh_comm_create(uid, 2, 2, 0, C.byref(h)) == A.MH_ERR_INVALID_ARGUMENT
+    assert lib.mh_scene_set_comm(None, None) == A.MH_ERR_INVALID_ARGUMENT
+    assert lib.mh_comm_reduce(None, 0, None, 0, None, -1) == A.MH_ERR_INVALID_ARGUMENT
+    assert lib.mh_render_sharded(None, 0, None, 0, 1, None, 0, None) == A.MH_ERR_INVALID_ARGUMENT
+    assert lib.mh_comm_destroy(None) == A.MH_OK

@@ -38,7 +38,7 @@ def _ops(mi, O, scene, torch):
         develop=lambda f: torch.from_numpy(O.develop(f.numpy())),
         prb_weights=lambda seed, spp, b, e: torch.from_numpy(O.prb_weights(scene, seed, spp, b, e, threads=2)),
         render_backward=lambda seed, spp, b, e, w: [torch.from_numpy(
-            O.render_backward(scene, prb, seed, spp, gi, [tex], [(3,)], weights=w.numpy(),
+            O.render_backward(scene, prb, seed, spp, gi, [tex], [(3,)], weights=None if w is None else w.numpy(),
                               spp_begin=b, spp_end=e, threads=2)[0])],
         seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0])
 
@@ -55,9 +55,12 @@ def _worker(rank, world, port, out_dir):
     scene = _scene(mi)
     slab = D.sample_slab(rank, world, 4)
     img, grads = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7)
+    # the same step with the W image computed locally on every rank (no W
+    # all-reduce) and the film summed onto rank 0 only
+    img2, grads2 = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7, local_weights=True, film_to_root=True)
     t = D.max_over_ranks(float(rank) + 0.5)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), img=img.numpy(), g=grads[0].numpy(), t=t,
-             begin=slab.begin, end=slab.end)
+             begin=slab.begin, end=slab.end, img2=img2.numpy(), g2=grads2[0].numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -88,3 +91,8 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     img, grads = D.fwd_grad_step(_ops(mi, O, scene, torch), D.sample_slab(0, 1, 8), seed=7)
     np.testing.assert_allclose(r0["img"], img.numpy(), rtol=2e-6, atol=1e-7)
     np.testing.assert_allclose(r0["g"], grads[0].numpy(), rtol=1e-5, atol=1e-9)
+    # local W (no W all-reduce) + the film reduced onto rank 0 only: rank 0's
+    # image and both ranks' gradients equal the single-process step
+    np.testing.assert_allclose(r0["img2"], img.numpy(), rtol=2e-6, atol=1e-7)
+    assert np.array_equal(r0["g2"], r1["g2"])
+    np.testing.assert_allclose(r0["g2"], grads[0].numpy(), rtol=1e-5, atol=1e-9)

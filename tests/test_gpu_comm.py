@@ -1,0 +1,185 @@
+"""Multi-GPU through the C ABI (include/mitsuba_hip.h "Multi-GPU", SURVEY.md
+§8(e); the splice point is SamplingIntegrator::render,
+src/render/integrator.cpp:276-390).
+
+The 1-GPU box can run an RCCL communicator of one rank only (RCCL refuses
+two ranks on one device), so:
+  * world-1 communicators (mh_comm_create from a unique id, and
+    mh_comm_create_all) check that the in-call reductions (MH_FLAG_REDUCE /
+    MH_FLAG_REDUCE_ROOT) sit in the right place: results equal the plain
+    calls bit for bit (deterministic films) or to float order (gradients);
+  * the sharded entry points without communicators (2 and 3 scenes on
+    cuda:0, summed by device copies) check the slab split itself: the
+    union of the slabs equals one render of all samples to the float order
+    of the sum, and the sharded gradient equals one render_backward.
+The N-rank RCCL run is the driver's (bench.py over torch.distributed; its
+rehearsal with gloo ranks is tests/test_gpu_multirank.py).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mi():
+    import mitsuba_hip as mi
+    if not mi.is_available():
+        pytest.fail("no HIP device / native library: the GPU tests need an MI355X")
+    return mi
+
+
+def _scene(mi, res=48, spp=16):
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"] = d["sensor"]["film"]["height"] = res
+    d["sensor"]["sampler"]["sample_count"] = spp
+    return mi.load_dict(d)
+
+
+def _film(scene, torch):
+    return torch.zeros((scene.height, scene.width, 4), dtype=torch.float32, device="cuda:0")
+
+
+def _render(A, scene, integ, seed, spp, film, flags):
+    ic = integ.c()
+    A.check(A.lib().mh_render(scene.handle(0), C.byref(ic), seed, spp, 0, 0, C.c_void_p(film.data_ptr()),
+                              A.FLAG_DEVICE_POINTERS | flags, None))
+
+
+def test_comm_world1_reduce_is_identity():
+    mi = _mi()
+    import torch
+    from mitsuba_hip.comm import Comm
+    uid = Comm.unique_id()
+    assert len(uid) == 128
+    c = Comm(uid, 1, 0, 0)
+    assert c.info() == (1, 0, 0)
+    x = torch.randn(1 << 16, device="cuda:0")
+    ref = x.clone()
+    c.reduce_(x)
+    c.reduce_(x, root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    (c1,) = Comm.create_all([0])
+    assert c1.info() == (1, 0, 0)
+    c1.reduce_(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    c.close()
+    c1.close()
+    del mi
+
+
+def test_render_reduce_flags_world1_match_plain_calls():
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip.comm import Comm, scene_set_comm
+    scene = _scene(mi)
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    ref, red, root = _film(scene, torch), _film(scene, torch), _film(scene, torch)
+    _render(A, scene, integ, 5, 16, ref, A.FLAG_DETERMINISTIC)
+    with pytest.raises(A.MitsubaHipError, match="needs a communicator"):
+        _render(A, scene, integ, 5, 16, red, A.FLAG_DETERMINISTIC | A.FLAG_REDUCE)
+    scene_set_comm(scene, comm)
+    _render(A, scene, integ, 5, 16, red, A.FLAG_DETERMINISTIC | A.FLAG_REDUCE)
+    _render(A, scene, integ, 5, 16, root, A.FLAG_DETERMINISTIC | A.FLAG_REDUCE_ROOT)
+    with pytest.raises(A.MitsubaHipError, match="ACCUMULATE"):
+        _render(A, scene, integ, 5, 16, red, A.FLAG_REDUCE | A.FLAG_ACCUMULATE)
+    torch.cuda.synchronize()
+    assert torch.equal(red, ref) and torch.equal(root, ref)
+
+    # render_backward: the slab W + all-reduce (1 rank: every sample) and the
+    # all-reduced gradient equal the plain call; MH_FLAG_LOCAL_WEIGHTS too
+    prb = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    key = "white.reflectance.value"
+    gi = torch.full((scene.height, scene.width, 3), 1.0 / (scene.height * scene.width * 3), device="cuda:0")
+    tex = (C.c_uint32 * 1)(params.param_id(key))
+
+    def bwd(flags):
+        g = torch.zeros(3, device="cuda:0")
+        ptr = (C.c_void_p * 1)(g.data_ptr())
+        ic = prb.c()
+        A.check(A.lib().mh_render_backward(scene.handle(0), C.byref(ic), 9, 16, 0, 0, C.c_void_p(gi.data_ptr()),
+                                           None, 1, tex, ptr, A.FLAG_DEVICE_POINTERS | flags, None))
+        torch.cuda.synchronize()
+        return g.cpu().numpy()
+
+    g0 = bwd(0)
+    np.testing.assert_allclose(bwd(A.FLAG_REDUCE), g0, rtol=1e-5)
+    np.testing.assert_allclose(bwd(A.FLAG_REDUCE | A.FLAG_LOCAL_WEIGHTS), g0, rtol=1e-5)
+    scene_set_comm(scene, None)
+    comm.close()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_render_sharded_slabs_sum_to_one_render(n):
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip.comm import render_sharded
+    spp = 16
+    scenes = [_scene(mi, spp=spp) for _ in range(n)]
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+    ref = _film(scenes[0], torch)
+    _render(A, scenes[0], integ, 7, spp, ref, 0)
+    films = [_film(s, torch) for s in scenes]
+    stats = [None] * n
+    render_sharded(scenes, integ, 7, spp, films, stats=stats)
+    torch.cuda.synchronize()
+    for f in films[1:]:
+        assert torch.equal(f, films[0])  # the sum is copied to every scene
+    assert sum(s.samples for s in stats) == scenes[0].width * scenes[0].height * spp
+    tol = 1e-5 * float(ref.abs().max())
+    assert float((films[0] - ref).abs().max()) <= tol
+    # root-only: films[0] holds the sum
+    films2 = [_film(s, torch) for s in scenes]
+    render_sharded(scenes, integ, 7, spp, films2, reduce_all=False)
+    torch.cuda.synchronize()
+    assert float((films2[0] - ref).abs().max()) <= tol
+
+
+def test_render_backward_sharded_matches_one_call():
+    mi = _mi()
+    import torch
+    from mitsuba_hip.comm import render_backward_sharded
+    spp = 16
+    scenes = [_scene(mi, spp=spp) for _ in range(2)]
+    prb = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scenes[0])
+    key = "white.reflectance.value"
+    gi = torch.full((scenes[0].height, scenes[0].width, 3), 1.0 / (48 * 48 * 3), device="cuda:0")
+    (ref,) = mi.render_backward(scenes[0], params, gi, [key], prb, seed=3, spp=spp)
+    outs = render_backward_sharded(scenes, params, gi, [key], prb, 3, spp)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    np.testing.assert_allclose(outs[0][0].cpu().numpy(), ref.cpu().numpy(), rtol=1e-4)
+
+
+def test_render_sharded_with_world1_comm_and_argument_checks():
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip.comm import Comm, render_sharded, scene_set_comm
+    scene = _scene(mi)
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+    ref = _film(scene, torch)
+    _render(A, scene, integ, 2, 16, ref, A.FLAG_DETERMINISTIC)
+    (c,) = Comm.create_all([0])
+    scene_set_comm(scene, c)
+    f = _film(scene, torch)
+    render_sharded([scene], integ, 2, 16, [f], deterministic=True)
+    torch.cuda.synchronize()
+    assert torch.equal(f, ref)
+    with pytest.raises(A.MitsubaHipError, match="appears twice"):
+        render_sharded([scene, scene], integ, 2, 16, [f, f])
+    other = _scene(mi)
+    with pytest.raises(A.MitsubaHipError, match="every scene has a communicator or none"):
+        render_sharded([scene, other], integ, 2, 16, [f, _film(other, torch)])
+    scene_set_comm(scene, None)
+    with pytest.raises(A.MitsubaHipError, match="spp must be >="):
+        render_sharded([scene, other], integ, 2, 1, [f, _film(other, torch)])
+    c.close()

@@ -61,3 +61,7 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     assert img.mean() > 0 and np.abs(g).min() > 0
     np.testing.assert_allclose(r0["img"], img, rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(r0["g"], g, rtol=1e-4)
+    # local W + film to rank 0 (tests/dist_hip_worker.py's second step)
+    np.testing.assert_allclose(r0["img2"], img, rtol=1e-5, atol=1e-7)
+    np.testing.assert_array_equal(r0["g2"], r1["g2"])
+    np.testing.assert_allclose(r0["g2"], g, rtol=1e-4)
