@@ -11,6 +11,7 @@ cd "$ROOT/mitsuba3-nasa_amd/csrc"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-fast-math -Wno-unused-function $*"
 for f in mh_api.hip mh_kernels.hip mh_wavefront.hip mh_volwave.hip; do /opt/rocm/bin/hipcc $FLAGS -c $f -o "$OBJ/${f%.hip}.o" & done
 /opt/rocm/bin/hipcc $FLAGS -x hip -c mh_bvh.cpp -o "$OBJ/mh_bvh.o" &
+/opt/rocm/bin/hipcc $FLAGS -x hip -c mh_comm.cpp -o "$OBJ/mh_comm.o" &
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/gpurun_exp/lib_$NAME.so" "$OBJ"/*.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/gpurun_exp/lib_$NAME.so" "$OBJ"/*.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx -ldl -Wl,-rpath,/opt/rocm/lib
 echo "built gpurun_exp/lib_$NAME.so"
