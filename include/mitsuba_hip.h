@@ -110,7 +110,10 @@ enum {
     MH_FLAG_WAVEFRONT       = 1u << 4,  /* mh_render: force the wavefront (trace/shade/shadow) kernels */
     MH_FLAG_PRB_REPLAY      = 1u << 5,  /* mh_render_backward: primal + adjoint replay even for rgb params */
     MH_FLAG_DETERMINISTIC   = 1u << 6,  /* film / W-image splat as a fixed-order gather instead of float
-                                           atomics: bit-reproducible films (also env MH_DETERMINISTIC=1) */
+                                           atomics: bit-reproducible films; mh_render_backward on the fused
+                                           wavefront: rgb gradients summed per path and reduced in path-id
+                                           order, bit-reproducible (bitmap texels and prbvolpath grids stay
+                                           float atomics) (also env MH_DETERMINISTIC=1) */
     /* multi-GPU (the scene has a communicator, mh_scene_set_comm; one host
        thread per rank): the call sums its result over the ranks in-call, on
        the scene's stream -- mh_render / mh_render_forward the film,

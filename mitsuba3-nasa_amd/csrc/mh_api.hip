@@ -105,6 +105,7 @@ struct mh_scene {
     DevBuf wf_ws, wf_ctr;  // wavefront state (SoA) and per-chunk/bounce queue counters
     DevBuf wf_ws_prb, wf_partial, gw, wf_carry;  // wavefront PRB: dL / adjoint-factor planes, per-block gradient partials
     DevBuf wf_ws_bmp;  // wavefront PRB with a bitmap parameter: vertex records (WfBmp)
+    DevBuf wf_ws_det;  // wavefront PRB, MH_FLAG_DETERMINISTIC: per-path gradient sums (WfDet)
     DevBuf pvp_log;    // prbvolpath backward: per-thread NEE-walk step logs (NeeLog)
     DevBuf pvp_main;   // prbvolpath backward: per-thread path logs of the single pass (MainLog)
     // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
@@ -472,7 +473,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->pvp_log, &s->pvp_main,
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main,
                       &s->shard_w, &s->shard_tmp, &s->shard_g})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -1291,6 +1292,10 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (size_t)per_cu_lds / per_wg));
             bmp.blocks = (uint32_t)cus * per_cu;
         }
+        // MH_FLAG_DETERMINISTIC: rgb slots summed per path and reduced in a
+        // fixed order (WfDet); a bitmap's texel scatter stays atomic
+        const bool det_grad = deterministic(flags) && !bmp_wf && n_rgb > 0;
+        if (det_grad) MH_HIP(s->wf_ws_det.alloc(wf_det_workspace_bytes(cap)));
         MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
         MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));
         MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, (size_t)grid * kMaxRgbParams * 3 * 4, st));
@@ -1307,7 +1312,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                                         s->wf_ws.ptr, s->wf_ws_prb.ptr, cap,
                                         s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
                                         s->wf_partial.as<float>(), st, &s->evpool[2 * chunk],
-                                        bmp_wf ? &bmp : nullptr));
+                                        bmp_wf ? &bmp : nullptr, det_grad ? s->wf_ws_det.ptr : nullptr));
         }
         MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
         wf_ctr_words = ctr_per_chunk;

@@ -107,7 +107,9 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
                                 uint32_t grid, float *partial, hipStream_t st,
                                 hipEvent_t *span = nullptr,               // span: 2 events around the bounce launches
-                                const WfBitmapArgs *bmp = nullptr);      // one bitmap parameter (or none)
+                                const WfBitmapArgs *bmp = nullptr,       // one bitmap parameter (or none)
+                                void *ws_det = nullptr);                 // deterministic rgb gradients (or none)
+size_t wf_det_workspace_bytes(uint64_t cap);
 // render_forward of `prb` on the fused wavefront (packet-engine scenes): the
 // tangent radiance of every path written to the sample planes of launch_render
 hipError_t launch_wavefront_fwd(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,

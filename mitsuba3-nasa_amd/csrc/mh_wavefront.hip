@@ -793,6 +793,67 @@ static WfPrb carve_prb(void *ws, uint64_t cap, float *partial, const int32_t *sl
     return q;
 }
 
+// MH_FLAG_DETERMINISTIC (the ordered-reduction build of SURVEY.md §5) for
+// the rgb gradient slots: a thread's register accumulator sums whichever
+// paths the queue compaction handed it, so its float sum depends on the
+// wave-ballot order of the appends.  Instead each path carries its own sum
+// (P, ping-pong planes by slot), writes it under its path id when it ends
+// (fin), and k_wf_det_sum adds the fin planes in a fixed order: the gradient
+// is then bit-reproducible from run to run.  Cost: 12 B per rgb slot more
+// path state per bounce, and the fin planes.
+struct WfDet {
+    float *base = nullptr;
+    uint64_t stride = 0;  // floats between planes
+    MH_DEV float *P(int k, int c) const { return base + (uint64_t)(k * kG + c) * stride; }
+    MH_DEV float *fin(int c) const { return base + (uint64_t)(2 * kG + c) * stride; }
+    float *fin_host(int c) const { return base + (uint64_t)(2 * kG + c) * stride; }
+    __host__ __device__ float *blocks() const { return base + (uint64_t)(3 * kG) * stride; }  // [kDetBlocks][kG]
+};
+constexpr uint32_t kDetBlocks = 1024;
+
+size_t wf_det_workspace_bytes(uint64_t cap) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    return (size_t)3 * kG * align_up(cap * 4) + (size_t)kDetBlocks * kG * 4;
+}
+
+static WfDet carve_det(void *ws, uint64_t cap) {
+    cap = (cap + kSeg - 1) / kSeg * kSeg;
+    WfDet d;
+    d.base = reinterpret_cast<float *>(ws);
+    d.stride = align_up(cap * 4) / 4;
+    return d;
+}
+
+// block b sums the path ids [b * per, (b + 1) * per) of every fin plane: its
+// threads in a fixed strided order, then a fixed tree
+__global__ void __launch_bounds__(256) k_wf_det_sum(WfDet d, uint32_t m, uint32_t n_c) {
+    __shared__ float red[256];
+    const uint32_t per = (m + kDetBlocks - 1) / kDetBlocks;
+    const uint32_t b0 = blockIdx.x * per, b1 = std::min<uint32_t>(m, b0 + per);
+    for (uint32_t c = 0; c < n_c; ++c) {
+        float s = 0.f;
+        for (uint32_t i = b0 + threadIdx.x; i < b1; i += 256u) s += d.fin(c)[i];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (uint32_t o = 128; o > 0; o >>= 1) {
+            if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) d.blocks()[(size_t)blockIdx.x * kG + c] = red[0];
+        __syncthreads();
+    }
+}
+
+// the block sums in block order, added into the first block partial (which
+// k_wf_grad_reduce sums in a fixed order with the others)
+__global__ void k_wf_det_fold(WfDet d, uint32_t n_c, float *partial) {
+    const uint32_t c = threadIdx.x;
+    if (c >= n_c) return;
+    float s = 0.f;
+    for (uint32_t b = 0; b < kDetBlocks; ++b) s += d.blocks()[(size_t)b * kG + c];
+    partial[c] += s;
+}
+
 // block-reduce the per-thread accumulators into partial[blockIdx]
 template <int NR>
 MH_DEV void flush_partial(float (&acc)[NR][3], const WfPrb &q) {
@@ -1073,10 +1134,11 @@ static WfBmp carve_bmp(void *ws, uint64_t cap, uint32_t n_depth, int32_t slot) {
 #ifndef MH_BOUNCE_BMP_WAVES
 #define MH_BOUNCE_BMP_WAVES 4  // the Bm instance carries ~20 more live values across the shadow trace
 #endif
-template <int NR, bool Gen, bool Bm>
+template <int NR, bool Gen, bool Bm, bool Det>
 __global__ void __launch_bounds__(256, Bm ? MH_BOUNCE_BMP_WAVES : MH_BOUNCE_PRB_WAVES)
 k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
-                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen, WfBmp bm) {
+                int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen, WfBmp bm, WfDet det) {
+    static_assert(!(Det && Bm), "deterministic gradients: rgb slots only");
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
     uint32_t n;
@@ -1110,6 +1172,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         V3 beta, prev_p, dL;
         float prev_pdf = 1.f;
         float A[NR][3], G[NR][3];
+        float Pp[NR][3];  // Det: this path's own gradient sum
+#pragma unroll
+        for (int kk = 0; kk < NR; ++kk) Pp[kk][0] = Pp[kk][1] = Pp[kk][2] = 0.f;
         Pcg rng;
         const uint32_t j = sbase + i;
         uint64_t gen_state = 0, gen_inc = 0;
@@ -1167,6 +1232,12 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 #pragma unroll
                     for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
                 rng.state = w.rng[cur][j];
+                if (Det) {
+#pragma unroll
+                    for (int kk = 0; kk < NR; ++kk)
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) Pp[kk][c] = (uint32_t)kk < n_rgb ? det.P(cur, kk * 3 + c)[j] : 0.f;
+                }
                 if (Bm) {
                     Lrun = v3(w.lx[cur][j], w.ly[cur][j], w.lz[cur][j]);
                     vmask = bm.mask[cur][j];
@@ -1190,7 +1261,8 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 if (active_next)
                     le = emitter_eval(S, em, si);
                 const V3 Le = (beta * mis) * le;
-                charge(acc, A, n_rgb, dL * Le);
+                if (Det) charge(Pp, A, n_rgb, dL * Le);
+                else charge(acc, A, n_rgb, dL * Le);
                 if (Bm) Le_b = Le;
             }
             active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
@@ -1296,13 +1368,24 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
         const bool unocc = shadow && sh.shape == MH_INVALID;
         if (unocc) {
+            float (&ga)[NR][3] = Det ? Pp : acc;
 #pragma unroll
             for (int kk = 0; kk < NR; ++kk)
                 if ((uint32_t)kk < n_rgb) {
-                    acc[kk][0] += G[kk][0];
-                    acc[kk][1] += G[kk][1];
-                    acc[kk][2] += G[kk][2];
+                    ga[kk][0] += G[kk][0];
+                    ga[kk][1] += G[kk][1];
+                    ga[kk][2] += G[kk][2];
                 }
+        }
+        if (Det && i < n) {  // the path's sum travels with it, or lands under its id when it ends
+#pragma unroll
+            for (int kk = 0; kk < NR; ++kk)
+                if ((uint32_t)kk < n_rgb)
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        if (alive) det.P(nxt, kk * 3 + c)[slot_n] = Pp[kk][c];
+                        else det.fin(kk * 3 + c)[pid] = Pp[kk][c];
+                    }
         }
         if (Bm && i < n) {
             // primal state update L = (L + Le) + Lr_dir (prb.py:174-199), then the vertex record
@@ -1687,7 +1770,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 const float *weights, const int32_t *slot_of_tex, uint32_t n_rgb,
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
                                 uint32_t grid, float *partial, hipStream_t st, hipEvent_t *span,
-                                const WfBitmapArgs *bmp) {
+                                const WfBitmapArgs *bmp, void *ws_det) {
     if (n == 0) return hipSuccess;
     if (n > (1ull << kPidBits) || n_bounces > kMaxWfBounces || n_rgb > (uint32_t)kMaxRgbParams) return hipErrorInvalidValue;
     WfState w = carve(ws, cap);
@@ -1702,29 +1785,39 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     const bool with_bmp = bmp != nullptr;
     if (with_bmp && (!fused || bmp->n_depth > 31 || bmp->n_depth + 1 < n_bounces || !bmp->ws)) return hipErrorInvalidValue;
     const WfBmp bm = with_bmp ? carve_bmp(bmp->ws, cap, bmp->n_depth, bmp->slot) : WfBmp{};
+    const bool det_on = ws_det != nullptr;
+    if (det_on && (with_bmp || !fused)) return hipErrorInvalidValue;
+    const WfDet det = det_on ? carve_det(ws_det, cap) : WfDet{};
+    if (det_on) {  // paths whose id is never written (segment gaps) add zeros
+        e = hipMemsetAsync(det.fin_host(0), 0, (size_t)n_rgb * 3 * det.stride * 4, st);
+        if (e != hipSuccess) return e;
+    }
     if (!fused)  // the fused first bounce generates its camera rays itself
         hipLaunchKernelGGL(k_wf_raygen_prb, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                            seed_value, n, coalesce, grad_in, weights, w, q, ctr);
     const PrbGen gen{n, grad_in, coalesce};
     if (span) (void)hipEventRecord(span[0], st);
-#define MH_BOUNCE_PRB(NR, GEN, BM)                                                                             \
-    hipLaunchKernelGGL((k_wf_bounce_prb<NR, GEN, BM>), dim3(grid), dim3(256), sh_fused, st, S, in, lm, seed_value, \
-                       w, q, cur, seg_cap, c, cn, gen, bm)
-#define MH_BOUNCE_PRB_NR(GEN, BM)                                                                              \
+#define MH_BOUNCE_PRB(NR, GEN, BM, DET)                                                                        \
+    hipLaunchKernelGGL((k_wf_bounce_prb<NR, GEN, BM, DET>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,       \
+                       seed_value, w, q, cur, seg_cap, c, cn, gen, bm, det)
+#define MH_BOUNCE_PRB_NR(GEN, BM, DET)                                                                         \
     do {                                                                                                       \
-        if (n_rgb <= 1) MH_BOUNCE_PRB(1, GEN, BM);                                                             \
-        else MH_BOUNCE_PRB(kMaxRgbParams, GEN, BM);                                                            \
+        if (n_rgb <= 1) MH_BOUNCE_PRB(1, GEN, BM, DET);                                                        \
+        else MH_BOUNCE_PRB(kMaxRgbParams, GEN, BM, DET);                                                       \
     } while (0)
     for (uint32_t b = 0; b < n_bounces; ++b) {
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
             if (with_bmp) {
-                if (b == 0) MH_BOUNCE_PRB_NR(true, true);
-                else MH_BOUNCE_PRB_NR(false, true);
+                if (b == 0) MH_BOUNCE_PRB_NR(true, true, false);
+                else MH_BOUNCE_PRB_NR(false, true, false);
+            } else if (det_on) {
+                if (b == 0) MH_BOUNCE_PRB_NR(true, false, true);
+                else MH_BOUNCE_PRB_NR(false, false, true);
             } else {
-                if (b == 0) MH_BOUNCE_PRB_NR(true, false);
-                else MH_BOUNCE_PRB_NR(false, false);
+                if (b == 0) MH_BOUNCE_PRB_NR(true, false, false);
+                else MH_BOUNCE_PRB_NR(false, false, false);
             }
             continue;
         }
@@ -1760,6 +1853,10 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
     }
     if (span) (void)hipEventRecord(span[1], st);
+    if (det_on) {
+        hipLaunchKernelGGL(k_wf_det_sum, dim3(kDetBlocks), dim3(256), 0, st, det, (uint32_t)(seg_cap * kSeg), n_rgb * 3);
+        hipLaunchKernelGGL(k_wf_det_fold, dim3(1), dim3(64), 0, st, det, n_rgb * 3, partial);
+    }
     return hipGetLastError();
 }
 

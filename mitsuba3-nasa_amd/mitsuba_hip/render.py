@@ -252,7 +252,7 @@ def _grad_to_rgb(scene: Scene, grad_in):
 def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],
                     integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                     spp_begin: int = 0, spp_end: int = 0, weights=None,
-                    stats: Optional[A.Stats] = None, mode: str = "auto"):
+                    stats: Optional[A.Stats] = None, mode: str = "auto", deterministic: bool = False):
     """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
     Returns a list of gradient tensors (one per key, same shape as the param).
     mode: 'auto' (wavefront single-traversal kernels when the keys are rgb
@@ -260,7 +260,9 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     scattered to its texels once the paths end -- else the per-lane primal +
     adjoint replay), 'mega' (per-lane
     single traversal) or 'replay' (per-lane primal + adjoint replay, the
-    reference's own two-pass structure)."""
+    reference's own two-pass structure).
+    deterministic: bit-reproducible rgb gradients on the fused wavefront (each
+    path's sum reduced in a fixed order) and a fixed-order W splat."""
     torch = _torch()
     integrator = integrator or scene.integrator()
     if integrator.type not in ("prb", "prbvolpath"):
@@ -276,7 +278,8 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     A.check(A.lib().mh_render_backward(
         h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(grad_in),
         _ptr(weights) if weights is not None else None, len(keys), tex, ptrs,
-        A.FLAG_DEVICE_POINTERS | _NO_SYNC | {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "replay": A.FLAG_PRB_REPLAY}[mode],
+        A.FLAG_DEVICE_POINTERS | _NO_SYNC | {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "replay": A.FLAG_PRB_REPLAY}[mode]
+        | (A.FLAG_DETERMINISTIC if deterministic else 0),
         C.byref(stats) if stats is not None else None))
     return outs
 

@@ -118,6 +118,38 @@ def test_deterministic_weights_and_alpha():
     np.testing.assert_allclose(w1, a[..., 4], rtol=1e-5)  # the film's W channel is the same sum
 
 
+@pytest.mark.parametrize("chunk,keys", [(None, ["white.reflectance.value"]),
+                                        ("65536", ["white.reflectance.value", "red.reflectance.value"])])
+def test_deterministic_prb_gradient_bit_reproducible(chunk, keys, monkeypatch):
+    """MH_FLAG_DETERMINISTIC on the fused PRB wavefront: every path carries
+    its own gradient sum and the sums are reduced in path-id order, so
+    repeated runs give the same bits (also over several wavefront chunks and
+    with two rgb slots); equal to the atomic-order build and to the oracle
+    within the float-order tolerance (prb.py:245-246 scatter)."""
+    if chunk:
+        monkeypatch.setenv("MH_WF_CHUNK", chunk)
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    scene = mi.load_dict(_cbox(mi, 64, 48, 32))
+    prb = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    gi = torch.full((48, 64, 3), 1.0 / (48 * 64 * 3), device="cuda:0")
+    st = A.Stats()
+    runs = [mi.render_backward(scene, params, gi, keys, prb, seed=5, spp=32, deterministic=True, stats=st)
+            for _ in range(3)]
+    assert st.mode == 1  # the fused wavefront
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    atomic = mi.render_backward(scene, params, gi, keys, prb, seed=5, spp=32)
+    ref = O.render_backward(scene, prb, 5, 32, gi.cpu().numpy(), [params.texture_of(k) for k in keys],
+                            [(3,)] * len(keys))
+    for a, b, r in zip(runs[0], atomic, ref):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-5)
+        np.testing.assert_allclose(a.cpu().numpy(), r, rtol=1e-3)
+
+
 def test_async_entry_points_match_synchronous():
     """MH_FLAG_DEVICE_POINTERS | MH_FLAG_NO_SYNC without stats: mh_render,
     mh_prb_weights and mh_render_backward return with their work enqueued on
