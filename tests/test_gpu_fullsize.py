@@ -166,15 +166,18 @@ def test_config4_film_parity(config4):
     film_parity(film, ref)
 
 
-def test_config4_samples_parity(config4):
-    """Per sample over the first 16 rows (262,144 samples, lanes 0 .. 2^18-1)."""
+@pytest.mark.parametrize("row0", [0, 240])
+def test_config4_samples_parity(config4, row0):
+    """Per sample over 16 rows (262,144 samples): the top rows (lanes 0 ..
+    2^18-1) and the bottom rows, where the deepest walks through the fBm
+    medium sit and k_vol_sched's last column-band queues drain."""
     mi, scene = config4
     integ = scene.integrator()
     L, pos = gpu_samples(mi, scene, integ, 3, 64, 0, 64, 0)
-    n = 16 * 256 * 64
-    rL, rpos, _ = O.sample_range(scene, integ, 3, 64, 0, n)
-    np.testing.assert_array_equal(pos[:n], rpos)
-    exact = np.all(L[:n] == rL, axis=1)
+    n, k0 = 16 * 256 * 64, row0 * 256 * 64
+    rL, rpos, _ = O.sample_range(scene, integ, 3, 64, k0, k0 + n)
+    np.testing.assert_array_equal(pos[k0:k0 + n], rpos)
+    exact = np.all(L[k0:k0 + n] == rL, axis=1)
     assert exact.mean() >= 0.999, f"bit-exact fraction {exact.mean()}"
     assert np.abs(rL).max() > 0
 
