@@ -250,9 +250,16 @@ MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1
     r1 = min(n, r0 + per);
 }
 
+// occupancy target of the unfused trace kernels (experiments: -DMH_STREAM_WAVES=n)
+#ifdef MH_STREAM_WAVES
+#define MH_STREAM_LB __launch_bounds__(256, MH_STREAM_WAVES)
+#else
+#define MH_STREAM_LB __launch_bounds__(256)
+#endif
+
 // Packet: wave-coherent engine (small BVHs) instead of the per-lane stream engine
 template <bool InLds, bool Packet>
-__global__ void __launch_bounds__(256)
+__global__ void MH_STREAM_LB
 k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
@@ -630,7 +637,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 }
 
 template <bool InLds, bool Packet>
-__global__ void __launch_bounds__(256)
+__global__ void MH_STREAM_LB
 k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
