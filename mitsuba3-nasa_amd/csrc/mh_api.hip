@@ -108,6 +108,7 @@ struct mh_scene {
     DevBuf wf_ws_det;  // wavefront PRB, MH_FLAG_DETERMINISTIC: per-path gradient sums (WfDet)
     DevBuf pvp_log;    // prbvolpath backward: per-thread NEE-walk step logs (NeeLog)
     DevBuf pvp_main;   // prbvolpath backward: per-thread path logs of the single pass (MainLog)
+    DevBuf pvp_ovf;    // prbvolpath backward on the scheduler: overflow lists + their counters
     // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
     // buffers of the sharded entry points (slab W image, staged peer sums,
     // slab gradients)
@@ -473,7 +474,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main,
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf,
                       &s->shard_w, &s->shard_tmp, &s->shard_g})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -683,6 +684,19 @@ static int check_bounds_counter(mh_scene *s, const char *api) {
     return MH_OK;
 }
 
+// k_vol_sched's per-phase statistics of the last launch (MH_EXP_VSCNT
+// diagnostic builds, MH_VW_DEBUG=1): wave trips, lanes and shader cycles
+static int print_vs_phases(mh_scene *s) {
+    unsigned long long c[32];
+    MH_HIP(hipMemcpy(c, s->counters.ptr, sizeof(c), hipMemcpyDeviceToHost));
+    const char *nm[8] = {"free", "head", "trace", "scatter", "surf", "walk", "post", "end"};
+    for (int g = 0; g < 8; ++g)  // groups of k_vol_sched (kNGroups = 8): trips, lanes, cycles
+        fprintf(stderr, "vs phase %-8s wave trips %llu, lanes %llu (%.1f per trip), cycles %.3e (%.0f per trip)\n",
+                nm[g], c[2 + g], c[10 + g], c[2 + g] ? (double)c[10 + g] / c[2 + g] : 0.0, (double)c[18 + g],
+                c[2 + g] ? (double)c[18 + g] / c[2 + g] : 0.0);
+    return MH_OK;
+}
+
 // MH_FLAG_REDUCE / MH_FLAG_REDUCE_ROOT: the call's result summed over the
 // scene's communicator (mh_comm.cpp), stream-ordered behind the kernels that
 // produced it.  A film honours MH_FLAG_REDUCE_ROOT (a reduce to rank 0); W
@@ -888,15 +902,8 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                         ctr[1] += wctr[o + 1];
                     }
     }
-    if (volwave && vol_sched_mode() && getenv("MH_VW_DEBUG")) {  // MH_EXP_VSCNT builds: wave trips per phase
-        unsigned long long c[32];
-        MH_HIP(hipMemcpy(c, s->counters.ptr, sizeof(c), hipMemcpyDeviceToHost));
-        const char *nm[7] = {"free", "head", "trace", "scatter", "surf", "walk", "post"};
-        for (int g = 0; g < 7; ++g)
-            fprintf(stderr, "vs phase %-8s wave trips %llu, lanes %llu (%.1f per trip), cycles %.3e (%.0f per trip)\n",
-                    nm[g], c[2 + g], c[9 + g], c[2 + g] ? (double)c[9 + g] / c[2 + g] : 0.0, (double)c[16 + g],
-                    c[2 + g] ? (double)c[16 + g] / c[2 + g] : 0.0);
-    }
+    if (volwave && vol_sched_mode() && getenv("MH_VW_DEBUG"))  // MH_EXP_VSCNT builds: wave trips per phase
+        if (int rc2 = print_vs_phases(s)) return rc2;
     if (volwave && !vol_sched_mode() && getenv("MH_VW_DEBUG")) {  // per-round queue sizes (+ MH_EXP_VWCNT builds: trips / steps)
         const uint32_t R = vw_rounds(*in), W = vw_counter_words(R) / (R + 1);
         std::vector<uint32_t> c((size_t)W * (R + 1));
@@ -1257,6 +1264,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                         in->max_depth <= 32 && !(env_bwf && !strcmp(env_bwf, "0"));
     const bool wavefront = ((fused && in->max_depth <= 64 && !mega) || bmp_wf);
     size_t wf_ctr_words = 0, wf_chunks = 0;
+    uint32_t *pvb_lost = nullptr;  // prbvolpath on the scheduler: overflow entries that found their list full
     MH_HIP(hipEventRecord(s->ev0, st));
     if (wavefront) {
         int cus = 256;
@@ -1322,15 +1330,20 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
         const char *ecap = getenv("MH_PVP_NEE_CAP");  // tests: small logs exercise the replay fallback
-        // the persistent grid (and with it both per-thread logs) shrinks to the
-        // work: a wave takes 64 samples per batch, so more threads than samples
-        // would only hold log space
-        const uint32_t blocks = (uint32_t)std::max<uint64_t>(
-                               1, std::min<uint64_t>((uint64_t)cus * kPvpBlocksPerCu, (n + 255) / 256)),
-                       cap = ecap ? (uint32_t)std::max(1, atoi(ecap)) : kPvpNeeCap;
         // single pass (MainLog) unless MH_PVP_SINGLE=0; MH_PVP_MAIN_CAP: entries per thread
         const char *esp = getenv("MH_PVP_SINGLE"), *emc = getenv("MH_PVP_MAIN_CAP");
         uint32_t main_cap = (esp && !strcmp(esp, "0")) ? 0u : emc ? (uint32_t)std::max(1, atoi(emc)) : kPvpMainCap;
+        const uint32_t cap = ecap ? (uint32_t)std::max(1, atoi(ecap)) : kPvpNeeCap;
+        // the single pass runs on the phase scheduler (k_vol_sched<PvBwdMachine>)
+        // unless MH_PVP_SCHED=0 (the per-sample kernel k_prbvol_backward)
+        const char *esc = getenv("MH_PVP_SCHED");
+        bool sched = main_cap && vs_supported(s->S, *in) && !(esc && !strcmp(esc, "0"));
+        // the persistent grid (and with it both per-thread logs): the
+        // scheduler's, or k_prbvol_backward's shrunk to the work (a wave takes
+        // 64 samples per batch, so more threads than samples would only hold log space)
+        const uint32_t blocks = sched ? vs_blocks(cus)
+                                      : (uint32_t)std::max<uint64_t>(
+                                            1, std::min<uint64_t>((uint64_t)cus * kPvpBlocksPerCu, (n + 255) / 256));
         // a log that cannot be allocated degrades the kernel instead of failing
         // the call: no MainLog -> primal + adjoint replay per sample; no NeeLog
         // either -> one thread per sample with the NEE walks replayed
@@ -1341,11 +1354,44 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             s->pvp_main.release();
             main_cap = 0;
         }
-        MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
-                                   g_in, w, ga, fused, s->counters.as<unsigned long long>(), st,
-                                   nee_ok ? s->pvp_log.as<float4>() : nullptr, cap, blocks,
-                                   s->counters.as<unsigned long long>() + kCtrPvpHead,
-                                   main_cap ? s->pvp_main.as<float4>() : nullptr, main_cap));
+        // overflow lists of the scheduler (2 + kPvbWalkRec float4 per entry)
+        const uint32_t ovf_cap = (uint32_t)std::min<uint64_t>(n, 1ull << 26);
+        sched = sched && main_cap && nee_ok &&
+                s->pvp_ovf.alloc((size_t)ovf_cap * (2 + kPvbWalkRec) * 16 + 256) == hipSuccess;
+        if (sched) {
+            VsBwdArgs bw;
+            bw.grad_in = g_in;
+            bw.coalesce = L.spp_pp >= 4;
+            bw.ga = ga;
+            bw.main_log = s->pvp_main.as<float4>();
+            bw.nee_log = s->pvp_log.as<float4>();
+            bw.main_cap = main_cap;
+            bw.nee_cap = cap;
+            bw.ovf_paths = s->pvp_ovf.as<float4>();
+            bw.ovf_walks = bw.ovf_paths + (size_t)2 * ovf_cap;
+            bw.ovf_count = reinterpret_cast<uint32_t *>(bw.ovf_walks + (size_t)kPvbWalkRec * ovf_cap);
+            bw.ovf_cap = ovf_cap;
+            MH_HIP(hipMemsetAsync(bw.ovf_count, 0, 16, st));
+            pvb_lost = bw.ovf_count + 2;
+            const LaneMap lm0 = lane_map(L, 0);
+            MH_HIP(launch_vol_sched_bwd(s->S, *in, lm0, s->S.sampler_seed + seed, n, bw, blocks,
+                                        s->counters.as<unsigned long long>(), st));
+            MH_HIP(launch_vol_sched_bwd_replays(s->S, *in, lm0, s->S.sampler_seed + seed, n, bw,
+                                                s->counters.as<unsigned long long>(), st));
+            if (getenv("MH_VW_DEBUG")) {
+                MH_HIP(hipStreamSynchronize(st));
+                if (int rc2 = print_vs_phases(s)) return rc2;
+                uint32_t oc[3];
+                MH_HIP(hipMemcpy(oc, bw.ovf_count, sizeof(oc), hipMemcpyDeviceToHost));
+                fprintf(stderr, "pvb overflow replays: %u paths, %u walks, %u lost\n", oc[0], oc[1], oc[2]);
+            }
+        } else {
+            MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
+                                       g_in, w, ga, fused, s->counters.as<unsigned long long>(), st,
+                                       nee_ok ? s->pvp_log.as<float4>() : nullptr, cap, blocks,
+                                       s->counters.as<unsigned long long>() + kCtrPvpHead,
+                                       main_cap ? s->pvp_main.as<float4>() : nullptr, main_cap));
+        }
     } else {
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
@@ -1371,9 +1417,18 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         }
     }
     if (async_call(flags, stats)) return MH_OK;  // gradients stay stream-ordered on the device
+    auto check_lost = [&]() -> int {  // (after a stream sync) an overflow replay that did not run fails the call
+        uint32_t lost = 0;
+        if (pvb_lost) MH_HIP(hipMemcpy(&lost, pvb_lost, 4, hipMemcpyDeviceToHost));
+        if (lost)
+            return set_error(MH_ERR_OUT_OF_MEMORY, "render_backward(): " + std::to_string(lost) +
+                                                       " prbvolpath overflow replays did not fit their list "
+                                                       "(MH_PVP_SCHED=0 runs the per-sample kernel)");
+        return MH_OK;
+    };
     if (!stats) {
         MH_HIP(hipStreamSynchronize(st));
-        return MH_OK;
+        return check_lost();
     }
     unsigned long long ctr[2] = {0, 0};
     std::vector<uint32_t> wctr(wf_ctr_words * wf_chunks);
@@ -1382,6 +1437,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     else
         MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     MH_HIP(hipStreamSynchronize(st));
+    if (int rc_lost = check_lost()) return rc_lost;
     if (wavefront) {
         const size_t per_bounce = wf_ctr_words / (in->max_depth + 1), nseg = per_bounce / 32;
         for (size_t c = 0; c < wf_chunks; ++c)

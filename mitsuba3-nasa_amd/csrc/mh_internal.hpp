@@ -161,6 +161,32 @@ uint32_t vs_blocks(int cus);
 hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
                             uint64_t n, uint64_t plane, float *out, uint32_t grid, unsigned long long *counters,
                             hipStream_t st, int alpha);
+// prbvolpath's single-pass backward on the phase scheduler (mh_volwave.hip
+// PvBwdMachine): the kernel-wide inputs
+struct VsBwdArgs {
+    const float *grad_in = nullptr;  // grad_in / W, one float4 per pixel (k_grad_over_w)
+    int coalesce = 0;
+    GradArgs ga{};
+    float4 *main_log = nullptr;      // MainLog: [grid threads][main_cap][4] (contiguous per lane)
+    float4 *nee_log = nullptr;       // NeeLog: [grid threads][nee_cap]
+    uint32_t main_cap = 0, nee_cap = 0;
+    // overflow lists, replayed after the scheduler launch: paths whose MainLog
+    // overflowed (2 float4: L + pid, dL) and NEE walks whose NeeLog overflowed
+    // (kPvbWalkRec float4), at most ovf_cap entries each; ovf_count: [0]
+    // paths, [1] walks, [2] entries that found their list full (fails the call)
+    float4 *ovf_paths = nullptr;
+    float4 *ovf_walks = nullptr;
+    uint32_t *ovf_count = nullptr;
+    uint32_t ovf_cap = 0;
+};
+constexpr uint32_t kPvbWalkRec = 5;
+hipError_t launch_vol_sched_bwd(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                                uint64_t n, const VsBwdArgs &bw, uint32_t grid, unsigned long long *counters,
+                                hipStream_t st);
+// the replays of bw's overflow lists (after launch_vol_sched_bwd on the same stream)
+hipError_t launch_vol_sched_bwd_replays(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                        uint32_t seed_value, uint64_t n, const VsBwdArgs &bw,
+                                        unsigned long long *counters, hipStream_t st);
 hipError_t launch_volwave(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
                           uint64_t n, uint64_t plane, float *out, void *ws, uint64_t cap, uint32_t *ctr,
                           uint32_t grid, unsigned long long *counters, hipStream_t st, int alpha);

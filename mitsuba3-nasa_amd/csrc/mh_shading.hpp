@@ -3085,4 +3085,39 @@ MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &
     }
 }
 
+// small (register-accumulated) gradient slots: wave butterfly, then one
+// atomic per wave and component
+MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
+    for (uint32_t p = 0; p < ga.n_rgb; ++p) {
+        const int slot = (int)p;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < kMaxRgbParams; ++kk)
+                if (kk == slot) v = g.acc[kk][c];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(ga.bufs[slot] + c, v);
+        }
+    }
+}
+
+MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
+    GradCtx g;
+    g.slot_of_tex = ga.slot_of_tex;
+    g.bufs = ga.bufs;
+    g.is_rgb = ga.is_rgb;
+    g.sigma_slot = ga.sigma_slot;
+    g.albedo_slot = ga.albedo_slot;
+    g.lds_slot = -1;
+    g.lds_acc = nullptr;
+    g.lds_floats = 0;
+    g.fwd = false;
+    g.fsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
+    return g;
+}
+
 }  // namespace mh

@@ -449,12 +449,14 @@ k_vw_walk(DScene S, VwPlanes P, uint32_t seg_cap, const uint32_t *__restrict__ c
 // volpath_post / nee_step in their order (bit-identical samples).
 // ===========================================================================
 enum : uint32_t {
-    kPhFree = 0, kPhHead, kPhTraceM, kPhTraceS, kPhTraceWM, kPhTraceWS, kPhScatter, kPhSurf, kPhWalk, kPhPost
+    kPhFree = 0, kPhHead, kPhTraceM, kPhTraceS, kPhTraceWM, kPhTraceWS, kPhScatter, kPhSurf, kPhWalk, kPhPost, kPhEnd
 };
-enum : uint32_t { kGFree = 0, kGHead, kGTrace, kGScatter, kGSurf, kGWalk, kGPost, kNGroups };
+// kGEnd: a finished path's own end-of-path work (machines with kDeferEnd:
+// the backward's log application), scheduled like the other heavy phases
+enum : uint32_t { kGFree = 0, kGHead, kGTrace, kGScatter, kGSurf, kGWalk, kGPost, kGEnd, kNGroups };
 MH_DEV uint32_t ph_group(uint32_t ph) {
     return ph == kPhFree ? kGFree : ph == kPhHead ? kGHead : ph <= kPhTraceWS ? kGTrace : ph == kPhScatter ? kGScatter
-         : ph == kPhSurf ? kGSurf : ph == kPhWalk ? kGWalk : kGPost;
+         : ph == kPhSurf ? kGSurf : ph == kPhWalk ? kGWalk : ph == kPhPost ? kGPost : kGEnd;
 }
 
 // the walk's own medium interaction across its trace (nee_step's local mei)
@@ -719,6 +721,17 @@ struct PvState {
     bool w_needs;
 };
 
+// The primal's hook points into the trip: no-ops.  The single-pass backward
+// (PvBwdMachine below) logs and charges its adjoint terms at the same points.
+struct PvNoHook {
+    template <class V> MH_DEV void nee_begin(V &, const Pcg &) {}
+    template <class V> MH_DEV void medium_log(const DScene &, V &, V3, bool, float, float, float) {}
+    template <class V> MH_DEV void walk_step(V &, V3, float) {}
+    template <class V>
+    MH_DEV void nee_charge(const DScene &, const LdsBvh &, V &, const Pcg &, V3, V3, float, V3, uint32_t &) {}
+    template <class V> MH_DEV void surface_log(const DScene &, V &, V3) {}
+};
+
 MH_DEV void pv_init(const DScene &S, const IntegratorParams &, Pcg &rng, RayT ray, PvState &v) {
     v.ray = ray;
     v.throughput = v3(1.f, 1.f, 1.f);
@@ -735,7 +748,8 @@ MH_DEV void pv_init(const DScene &S, const IntegratorParams &, Pcg &rng, RayT ra
 
 // SURF / SCATTER: the surface block and the emitter sample (:212-270); the
 // walk starts here, or the trip goes on to POST without one
-MH_DEV uint32_t pv_shade(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_shade(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk) {
     v.active_surface = v.active_surface && v.si.valid;
     const uint32_t b = v.active_surface ? S.shapes[v.si.shape].bsdf : MH_INVALID;
     v.smooth = b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_DIFFUSE;
@@ -749,6 +763,7 @@ MH_DEV uint32_t pv_shade(const DScene &S, const IntegratorParams &in, Pcg &rng, 
     // sample_emitter's head (pvp_sample_emitter: active_medium = e_medium)
     const V3 ref_p = e_medium ? v.mei.p : v.si.p;
     const V3 ref_n = e_medium ? v3(0.f, 0.f, 0.f) : v.si.n;
+    hk.nee_begin(v, rng);  // sampler.clone() (prbvolpath.py: the NEE walk's replay)
     const float sx = rng.next_float(), sy = rng.next_float();
     v.emitter_val = scene_sample_emitter_direction(S, ref_p, sx, sy, v.ds);
     v.transmittance = v3(1.f, 1.f, 1.f);
@@ -767,8 +782,9 @@ MH_DEV uint32_t pv_shade(const DScene &S, const IntegratorParams &in, Pcg &rng, 
 }
 
 // the loop trip after its medium block (:206-212), up to the surface query
-MH_DEV uint32_t pv_mid(const DScene &S, const IntegratorParams &in, PvState &v, bool act_null, bool escaped,
-                       V3 weight, float P) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_mid(const DScene &S, const IntegratorParams &in, V &v, bool act_null, bool escaped,
+                       V3 weight, float P, float fw, float mt, Hk &hk) {
     v.active = v.active && v.depth < in.max_depth;
     v.act_scatter = v.act_scatter && v.active;
     if ((S.vol_flags & kVolHandleNull) && act_null) { v.ray.o = v.mei.p; v.si_t = v.si_t - v.mei.t; }
@@ -776,6 +792,7 @@ MH_DEV uint32_t pv_mid(const DScene &S, const IntegratorParams &in, PvState &v, 
         weight = v3(weight.x * (v.mei.sigma_s.x / P), weight.y * (v.mei.sigma_s.y / P),
                     weight.z * (v.mei.sigma_s.z / P));
     v.throughput = v.throughput * weight;
+    if (v.active_medium || escaped) hk.medium_log(S, v, weight, act_null, fw, mt, P);  // (:202-204)
     v.active_surface = v.active_surface || escaped;
     if (v.act_scatter) return kPhScatter;
     if (v.active_surface) return v.needs_intersection ? kPhTraceS : kPhSurf;
@@ -786,7 +803,8 @@ MH_DEV uint32_t pv_mid(const DScene &S, const IntegratorParams &in, PvState &v, 
 }
 
 // the medium block after its (optional) intersection (:165-204)
-MH_DEV uint32_t pv_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk) {
     MEI &mei = v.mei;
     v.needs_intersection = false;
     if (v.si_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
@@ -808,11 +826,12 @@ MH_DEV uint32_t pv_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rn
         v.act_scatter = v.active_medium;
     }
     if (v.act_scatter) v.depth += 1;
-    return pv_mid(S, in, v, act_null, escaped, weight, P);
+    return pv_mid(S, in, v, act_null, escaped, weight, P, fw, mt, hk);
 }
 
 // HEAD: Russian roulette (:142-149) and the medium sample (:157-163)
-MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk) {
     bool active = nonzero(v.throughput);
     const float q = fminf(hmax(v.throughput) * (v.eta * v.eta), 0.99f);
     const bool perform_rr = v.depth > in.rr_depth;
@@ -837,15 +856,17 @@ MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, P
         sample_interaction(S, v.med, v.ray, rng.next_float(), mei);
         if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) v.ray.maxt = mei.t;
         if (v.needs_intersection) return kPhTraceM;
-        return pv_med_rest(S, in, rng, v);
+        return pv_med_rest(S, in, rng, v, hk);
     }
-    return pv_mid(S, in, v, false, false, v3(1.f, 1.f, 1.f), 1.f);
+    return pv_mid(S, in, v, false, false, v3(1.f, 1.f, 1.f), 1.f, 1.f, 0.f, hk);
 }
 
 // the walk step after its (optional) intersection (pvp_sample_emitter's loop)
-MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, PvState &v, float remaining_dist) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, V &v, float remaining_dist, Hk &hk) {
     v.w_needs = false;
-    bool act_med = v.wmedium != MH_INVALID, act_surf = !act_med, escaped = false;
+    bool act_med = v.wmedium != MH_INVALID, act_surf = !act_med, escaped = false, hom = false;
+    float hom_t = 0.f;
     MEI mei;
     mei.valid = false;
     mei.t = 0.f;
@@ -858,9 +879,10 @@ MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, PvState &v, float remain
         if (v.wsi_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
         if ((S.vol_flags & kVolNeeHomogeneous) && m.type == MH_MEDIUM_HOMOGENEOUS) {
             mei.t = fminf(remaining_dist, v.wsi_t);
-            const float hom_t = fminf(mei.t, v.wsi_t) - mei.mint;
+            hom_t = fminf(mei.t, v.wsi_t) - mei.mint;
             const float tr = exp_dr((-hom_t) * mei.maj);
             trm = v3(tr, tr, tr);
+            hom = true;
             mei.t = __builtin_huge_valf();
             mei.valid = false;
         }
@@ -877,6 +899,10 @@ MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, PvState &v, float remain
         const uint32_t b = S.shapes[v.wsi.shape].bsdf;
         trm = trm * ((b != MH_INVALID && S.bsdf_type[b] == MH_BSDF_NULL) ? 1.f : 0.f);
     }
+    if ((act_med || hom) && (act_med || act_surf)) {  // a gradient step of the walk (:412-414)
+        const float tc = trm.x;  // grey: scalar sigma_n / majorant, scalar homogeneous tr
+        hk.walk_step(v, mei.p, !(tc > 0.f) ? 0.f : act_med ? (1.f / tc) * (-1.f / mei.maj) : -hom_t);
+    }
     v.transmittance = v.transmittance * trm;
     if (act_surf) v.wray = spawn_ray(v.wsi.p, v.wsi.n, v.wray.d);
     v.w_needs = act_surf;
@@ -889,17 +915,20 @@ MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, PvState &v, float remain
 MH_DEV float pv_remaining(const PvState &v) { return v.ds.dist * (1.f - kShadowEps) - v.total_dist; }
 
 // WALK: the head of one transmittance-loop trip
-MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, PvState &v) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, V &v, Hk &hk) {
     const float remaining_dist = pv_remaining(v);
     v.wray.maxt = remaining_dist;
     if (!(remaining_dist > 0.f)) return kPhPost;
     if (v.w_needs) return kPhTraceWS;
-    return pv_walk_rest(S, rng, v, remaining_dist);
+    return pv_walk_rest(S, rng, v, remaining_dist, hk);
 }
 
 // POST: the emitter sample's contribution (:256-270), phase sampling
 // (:274-294), BSDF sampling (:298-331) and the loop's tail test
-MH_DEV uint32_t pv_post(const DScene &S, const IntegratorParams &in, Pcg &rng, PvState &v) {
+template <class V, class Hk>
+MH_DEV uint32_t pv_post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk,
+                        uint32_t &n_shadow) {
     if (v.nee) {
         const V3 emitted = v.emitter_val * v.transmittance;
         V3 nee_w, bv = v3(0.f, 0.f, 0.f);
@@ -918,6 +947,7 @@ MH_DEV uint32_t pv_post(const DScene &S, const IntegratorParams &in, Pcg &rng, P
         const float mis = mis_weight(v.ds.pdf, nee_pdf);
         const V3 contrib = ((v.throughput * nee_w) * mis) * emitted;
         v.L = v.L + contrib;
+        hk.nee_charge(S, B, v, rng, contrib, emitted, mis, wo_s, n_shadow);
     }
     v.valid_ray = v.valid_ray || v.act_scatter;
     bool act_scatter = v.act_scatter;
@@ -946,6 +976,7 @@ MH_DEV uint32_t pv_post(const DScene &S, const IntegratorParams &in, Pcg &rng, P
         }
         v.active_surface = v.active_surface && bs_pdf > 0.f;
         if (v.active_surface) {
+            if (v.smooth && v.si.wi.z > 0.f && bs_wo.z > 0.f) hk.surface_log(S, v, bs_wo);  // (:305-312)
             v.throughput = v.throughput * bw;
             v.ray = spawn_ray(v.si.p, v.si.n, to_world(v.si, bs_wo));
             v.needs_intersection = true;
@@ -956,80 +987,267 @@ MH_DEV uint32_t pv_post(const DScene &S, const IntegratorParams &in, Pcg &rng, P
     return (v.active && (v.active_surface || v.active_medium)) ? kPhHead : kPhFree;
 }
 
-template <bool Pk>
+template <bool Pk, class V, class Hk>
 MH_DEV uint32_t pv_trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, uint32_t ph,
-                         PvState &v, uint32_t &n_closest, uint32_t &n_shadow) {
+                         V &v, uint32_t &n_closest, uint32_t &n_shadow, Hk &hk) {
     if (ph == kPhTraceWS) {
         trace_si<Pk>(S, B, v.wray, v.wsi, v.wsi_t);
         ++n_shadow;
-        return pv_walk_rest(S, rng, v, pv_remaining(v));
+        return pv_walk_rest(S, rng, v, pv_remaining(v), hk);
     }
     trace_si<Pk>(S, B, v.ray, v.si, v.si_t);
     ++n_closest;
-    if (ph == kPhTraceM) return pv_med_rest(S, in, rng, v);
+    if (ph == kPhTraceM) return pv_med_rest(S, in, rng, v, hk);
     return kPhSurf;
 }
 
-// The two integrators the phase scheduler runs: their state and phase steps
+// The integrators the phase scheduler runs: their state and phase steps.
+// Every machine is constructed once per thread from the kernel's backward
+// arguments (ignored by the primal machines) and offers the same calls.
 struct VolMachine {
     using State = VolState;
-    static constexpr bool kPrb = false;
-    MH_DEV static void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v) {
+    static constexpr bool kPrb = false, kWritesPos = true, kDeferEnd = false;
+    MH_DEV VolMachine(const VsBwdArgs &, const LaneMap &, uint32_t) {}
+    MH_DEV void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v, float, float) {
         volpath_init(S, in, rng, r, v);
     }
-    MH_DEV static uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+    MH_DEV uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
         return vs_head(S, in, rng, v);
     }
     template <bool Pk>
-    MH_DEV static uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                                 uint32_t ph, State &v, WMei &wm, uint32_t &nc, uint32_t &ns) {
+    MH_DEV uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
+                          uint32_t ph, State &v, WMei &wm, uint32_t &nc, uint32_t &ns) {
         return vs_trace<Pk>(S, B, in, rng, ph, v, wm, nc, ns);
     }
-    MH_DEV static uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+    MH_DEV uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
         return vs_scatter(S, in, rng, v);
     }
-    MH_DEV static uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+    MH_DEV uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
         return vs_surf(S, in, rng, v);
     }
-    MH_DEV static uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &wm) { return vs_walk(S, rng, v.ds, v.ns, wm); }
-    MH_DEV static uint32_t post(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+    MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &wm) { return vs_walk(S, rng, v.ds, v.ns, wm); }
+    MH_DEV uint32_t post(const DScene &S, const LdsBvh &, const IntegratorParams &in, Pcg &rng, State &v, uint32_t &) {
         return volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
     }
-    MH_DEV static void write(float *out, uint64_t plane, uint32_t pid, const State &v, int alpha) {
+    MH_DEV void end(const DScene &, const LdsBvh &, const IntegratorParams &, float *out, uint64_t plane,
+                    uint32_t pid, const State &v, int alpha, uint32_t &, uint32_t &) {
         vw_write_sample(out, plane, pid, v, alpha);
     }
+    MH_DEV void finish() {}
 };
 
 struct PvMachine {
     using State = PvState;
-    static constexpr bool kPrb = true;
-    MH_DEV static void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v) {
+    static constexpr bool kPrb = true, kWritesPos = true, kDeferEnd = false;
+    PvNoHook h;
+    MH_DEV PvMachine(const VsBwdArgs &, const LaneMap &, uint32_t) {}
+    MH_DEV void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v, float, float) {
         pv_init(S, in, rng, r, v);
     }
-    MH_DEV static uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
-        return pv_head(S, in, rng, v);
+    MH_DEV uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_head(S, in, rng, v, h);
     }
     template <bool Pk>
-    MH_DEV static uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                                 uint32_t ph, State &v, WMei &, uint32_t &nc, uint32_t &ns) {
-        return pv_trace<Pk>(S, B, in, rng, ph, v, nc, ns);
+    MH_DEV uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
+                          uint32_t ph, State &v, WMei &, uint32_t &nc, uint32_t &ns) {
+        return pv_trace<Pk>(S, B, in, rng, ph, v, nc, ns, h);
     }
-    MH_DEV static uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
-        return pv_shade(S, in, rng, v);
+    MH_DEV uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_shade(S, in, rng, v, h);
     }
-    MH_DEV static uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
-        return pv_shade(S, in, rng, v);
+    MH_DEV uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_shade(S, in, rng, v, h);
     }
-    MH_DEV static uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v); }
-    MH_DEV static uint32_t post(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
-        return pv_post(S, in, rng, v);
+    MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, h); }
+    MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
+                         uint32_t &ns) {
+        return pv_post(S, B, in, rng, v, h, ns);
     }
-    MH_DEV static void write(float *out, uint64_t plane, uint32_t pid, const State &v, int alpha) {
+    MH_DEV void end(const DScene &, const LdsBvh &, const IntegratorParams &, float *out, uint64_t plane,
+                    uint32_t pid, const State &v, int alpha, uint32_t &, uint32_t &) {
         out[pid] = v.L.x;
         out[plane + pid] = v.L.y;
         out[2 * plane + pid] = v.L.z;
         if (alpha) out[5 * plane + pid] = v.valid_ray ? 1.f : 0.f;  // aovs[3] (integrator.cpp:1229-1231)
     }
+    MH_DEV void finish() {}
+};
+
+// ===========================================================================
+// prbvolpath's single-pass backward (k_prbvol_backward's Mode 2: primal
+// arithmetic, the L-dependent adjoint terms logged per vertex in MainLog and
+// charged when the path ends, the NEE walks' gradient steps logged in NeeLog
+// and charged once the NEE contribution is known; prbvolpath.py:91-431 with
+// common.py:900-983) on the phase scheduler: the primal machine above with
+// its hooks filled in.  A path whose MainLog overflows replays its adjoint
+// when it ends (Mode 3, the NEE terms already charged); a walk whose NeeLog
+// overflows (more than nee_cap steps, or a second medium) is replayed with
+// the sampler cloned at its emitter sample (prbvolpath.py:412-414).  Both
+// replays run after the scheduler launch from overflow lists (inlined, their
+// register demand -- a whole adjoint sample -- would set the scheduler loop's
+// allocation: 256 VGPRs with spills instead of 222 without).  Per lane the
+// operations and draws are those of the per-sample kernel.
+// ===========================================================================
+struct PvBwdState : PvState {
+    V3 dL;                     // grad_in / W gathered over the sample's footprint (common.py:936-965)
+    uint64_t nee_state;        // the PCG32 state at the current emitter sample (sampler.clone())
+    uint32_t ml_n, nl_n, nl_med;
+    bool ml_over, nl_over;
+};
+
+struct PvBwdMachine {
+    using State = PvBwdState;
+    // the end-of-path log application is a phase of its own (kPhEnd): run
+    // when a path ends, it would hold the wave for the few lanes that ended
+    static constexpr bool kPrb = true, kWritesPos = false, kDeferEnd = true;
+    VsBwdArgs a;
+    GradCtx g;
+    LaneMap lm;
+    // The logs of a lane are contiguous (entry j of thread t: MainLog at
+    // float4 (t * main_cap + j) * 4, NeeLog at t * nee_cap + j): the lanes of a
+    // scheduler trip sit at different entries, so the per-sample kernel's
+    // entry-major layout (lanes writing their j-th entry as one 1-KiB run)
+    // would scatter every 64-B entry over four lines here.
+    uint32_t seed_value, t;
+    MH_DEV PvBwdMachine(const VsBwdArgs &a_, const LaneMap &lm_, uint32_t sv)
+        : a(a_), g(make_grad_ctx(a_.ga)), lm(lm_), seed_value(sv) {
+        t = blockIdx.x * blockDim.x + threadIdx.x;
+    }
+    MH_DEV uint64_t main_base() const { return (uint64_t)t * a.main_cap * 4; }
+    MH_DEV uint64_t nee_base() const { return (uint64_t)t * a.nee_cap; }
+    MH_DEV void log_main(State &v, float4 q0, float4 q1, float4 q2, float4 q3) {
+        if (v.ml_n >= a.main_cap) { v.ml_over = true; return; }
+        float4 *e = a.main_log + main_base() + (uint64_t)4 * v.ml_n;
+        e[0] = q0;
+        e[1] = q1;
+        e[2] = q2;
+        e[3] = q3;
+        ++v.ml_n;
+    }
+    // ---- hooks (PvNoHook's points)
+    MH_DEV void nee_begin(State &v, const Pcg &rng) {
+        v.nee_state = rng.state;
+        v.nl_n = 0;
+        v.nl_over = false;
+    }
+    // backward(dL * weight * Lo), Lo = L / max(1e-8, weight) (prbvolpath.py:202-204), logged
+    MH_DEV void medium_log(const DScene &S, State &v, V3 weight, bool act_null, float fw, float mt, float P) {
+        const DMedium &m = S.media[v.med];
+        const bool homog = m.type == MH_MEDIUM_HOMOGENEOUS;
+        const float wc[3] = {weight.x, weight.y, weight.z}, dc[3] = {v.dL.x, v.dL.y, v.dL.z};
+        const float al[3] = {m.albedo[0], m.albedo[1], m.albedo[2]};
+        const float ss[3] = {v.mei.sigma_s.x, v.mei.sigma_s.y, v.mei.sigma_s.z};
+        const float dfw = homog ? -mt * fw : 0.f;  // d (tr / tr_pdf) / d sigma_t
+        float dwsc[3], dwa = 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float dws;
+            if (v.act_scatter) {
+                dws = dfw * ss[c] / P + fw * al[c] / P;  // sigma_s = sigma_t * albedo
+                dwa = fw * v.mei.sigma_t / P;
+            } else if (act_null) {
+                dws = -fw / (1.f - P);
+            } else {
+                dws = dfw;
+            }
+            dwsc[c] = dws;
+        }
+        log_main(v, make_float4(v.mei.p.x, v.mei.p.y, v.mei.p.z, __uint_as_float((v.act_scatter ? 2u : 0u) | (v.med << 2))),
+                 make_float4(v.L.x, v.L.y, v.L.z, 0.f),
+                 make_float4(dc[0] / fmaxf(1e-8f, wc[0]), dc[1] / fmaxf(1e-8f, wc[1]), dc[2] / fmaxf(1e-8f, wc[2]), 0.f),
+                 make_float4(dwsc[0], dwsc[1], dwsc[2], dwa));
+    }
+    MH_DEV void walk_step(State &v, V3 p, float coef) {
+        if (v.nl_n < a.nee_cap && (v.nl_n == 0 || v.nl_med == v.wmedium)) {
+            a.nee_log[nee_base() + v.nl_n] = make_float4(p.x, p.y, p.z, coef);
+            v.nl_med = v.wmedium;
+            ++v.nl_n;
+        } else {
+            v.nl_over = true;
+        }
+    }
+    MH_DEV void nee_charge(const DScene &S, const LdsBvh &B, State &v, const Pcg &rng, V3 contrib, V3 emitted,
+                           float mis, V3 wo_s, uint32_t &n_shadow) {
+        if (!v.nl_over) {  // the logged walk's steps: coef * (dL . adj_emitted)
+            const float K = (v.dL.x * contrib.x + v.dL.y * contrib.y) + v.dL.z * contrib.z;
+            for (uint32_t j = 0; j < v.nl_n; ++j) {
+                const float4 e = a.nee_log[nee_base() + j];
+                sigma_t_backward(S, v.nl_med, v3(e.x, e.y, e.z), e.w * K, g);
+            }
+        } else {  // the walk is replayed with the cloned sampler after the launch (k_pvb_replay_walks)
+            const bool am = !v.e_surface;
+            const V3 rp = am ? v.mei.p : v.si.p, rn = am ? v3(0.f, 0.f, 0.f) : v.si.n;
+            const uint32_t k = atomicAdd(a.ovf_count + 1, 1u);
+            if (k < a.ovf_cap) {
+                float4 *r = a.ovf_walks + (uint64_t)kPvbWalkRec * k;
+                r[0] = make_float4(rp.x, rp.y, rp.z, __uint_as_float(v.si.shape));
+                r[1] = make_float4(rn.x, rn.y, rn.z, __uint_as_float((am ? 1u : 0u) | (v.si.valid ? 2u : 0u)));
+                r[2] = make_float4(contrib.x, contrib.y, contrib.z, __uint_as_float(v.medium));
+                r[3] = make_float4(v.dL.x, v.dL.y, v.dL.z, 0.f);
+                r[4] = make_float4(__uint_as_float((uint32_t)v.nee_state), __uint_as_float((uint32_t)(v.nee_state >> 32)),
+                                   __uint_as_float((uint32_t)rng.inc), __uint_as_float((uint32_t)(rng.inc >> 32)));
+            } else {
+                atomicAdd(a.ovf_count + 2, 1u);
+            }
+        }
+        if (v.e_surface && v.si.wi.z > 0.f && wo_s.z > 0.f) {
+            // backward(dL * contrib) through bsdf_val = rho / pi * cos
+            const V3 adj = ((((v.dL * emitted) * mis) * v.throughput) * kInvPi) * wo_s.z;
+            tex_backward(S, S.bsdf_tex[S.shapes[v.si.shape].bsdf], v.si.uvx, v.si.uvy, adj, g);
+        }
+    }
+    // Lo = bsdf_eval * detach(L / max(1e-8, bsdf_eval)) (prbvolpath.py:305-312), logged
+    MH_DEV void surface_log(const DScene &S, State &v, V3 bs_wo) {
+        const V3 be = (v.rho * kInvPi) * bs_wo.z;
+        log_main(v, make_float4(0.f, 0.f, 0.f, __uint_as_float(1u | (S.bsdf_tex[S.shapes[v.si.shape].bsdf] << 2))),
+                 make_float4(v.L.x, v.L.y, v.L.z, v.si.uvx),
+                 make_float4(v.dL.x / fmaxf(1e-8f, be.x), v.dL.y / fmaxf(1e-8f, be.y), v.dL.z / fmaxf(1e-8f, be.z), v.si.uvy),
+                 make_float4(bs_wo.z, 0.f, 0.f, 0.f));
+    }
+    // ---- the machine
+    MH_DEV void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v, float sx, float sy) {
+        v.dL = gather_dL_wave(S, a.coalesce, a.grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
+        pv_init(S, in, rng, r, v);
+        v.ml_n = v.nl_n = v.nl_med = 0;
+        v.ml_over = v.nl_over = false;
+    }
+    MH_DEV uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_head(S, in, rng, v, *this);
+    }
+    template <bool Pk>
+    MH_DEV uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
+                          uint32_t ph, State &v, WMei &, uint32_t &nc, uint32_t &ns) {
+        return pv_trace<Pk>(S, B, in, rng, ph, v, nc, ns, *this);
+    }
+    MH_DEV uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_shade(S, in, rng, v, *this);
+    }
+    MH_DEV uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v) {
+        return pv_shade(S, in, rng, v, *this);
+    }
+    MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, *this); }
+    MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
+                         uint32_t &ns) {
+        return pv_post(S, B, in, rng, v, *this, ns);
+    }
+    // the path ended with radiance v.L: charge its logged terms, or replay
+    MH_DEV void end(const DScene &S, const LdsBvh &B, const IntegratorParams &in, float *, uint64_t, uint32_t pid,
+                    State &v, int, uint32_t &nc, uint32_t &ns) {
+        if (!v.ml_over) {
+            // MainLog's entry-major addressing with stride 1 and the lane's base: entry j at base + 4 j
+            pvp_log_apply(S, MainLog{a.main_log + main_base(), 1u, a.main_cap, 0u, v.ml_n, false}, v.L, g);
+            return;
+        }
+        // the adjoint replayed after the launch (k_pvb_replay_paths)
+        const uint32_t k = atomicAdd(a.ovf_count, 1u);
+        if (k < a.ovf_cap) {
+            a.ovf_paths[2 * (uint64_t)k] = make_float4(v.L.x, v.L.y, v.L.z, __uint_as_float(pid));
+            a.ovf_paths[2 * (uint64_t)k + 1] = make_float4(v.dL.x, v.dL.y, v.dL.z, 0.f);
+        } else {
+            atomicAdd(a.ovf_count + 2, 1u);
+        }
+    }
+    MH_DEV void finish() { flush_small_slots(g, a.ga); }
 };
 
 #ifndef MH_VS_WAVES
@@ -1038,7 +1256,7 @@ struct PvMachine {
 // phase weights (x16): a phase runs when its pending lanes x weight is the
 // largest; heavy phases wait for more lanes
 #ifndef MH_VS_W
-#define MH_VS_W 8, 16, 12, 8, 8, 6, 12   // free, head, trace, scatter, surf, walk, post (swept on config 4: 194 -> 214 Msamples/s)
+#define MH_VS_W 8, 16, 12, 8, 8, 6, 12, 16   // free, head, trace, scatter, surf, walk, post (swept on config 4: 194 -> 214 Msamples/s), end
 #endif
 // Tab: the shading tables (stage_tables) and the media records staged into
 // LDS: every trip reads the medium record (transform, bbox, majorant,
@@ -1052,7 +1270,7 @@ template <class M, bool InLds, bool Pk, bool Tab>
 __global__ void __launch_bounds__(256, MH_VS_WAVES)
 k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane,
             float *__restrict__ out, unsigned long long *__restrict__ counters, unsigned long long *__restrict__ work,
-            int alpha) {
+            int alpha, VsBwdArgs bw) {
     // samples are handed out in batches of 64 from one device counter (work)
     extern __shared__ uint4 lds[];
     DScene S = S0;
@@ -1068,8 +1286,10 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     }
     LdsBvh B = stage_bvh<InLds>(S0, lds + tab);
     constexpr uint32_t W[kNGroups] = {MH_VS_W};
+    constexpr uint32_t NG = M::kDeferEnd ? kNGroups : kGEnd;  // groups this machine uses
     const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
     uint32_t n_closest = 0, n_shadow = 0;
+    M mc(bw, lm, seed_value);
     typename M::State v;
     WMei wm;
     Pcg rng;
@@ -1109,11 +1329,11 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         uint32_t cnt[kNGroups];
         const uint32_t g = ph_group(ph);
 #pragma unroll
-        for (uint32_t k = 0; k < kNGroups; ++k) cnt[k] = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(g == k));
+        for (uint32_t k = 0; k < NG; ++k) cnt[k] = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(g == k));
         if (drained && next >= end) cnt[kGFree] = 0;
         uint32_t sel = kNGroups, best = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < kNGroups; ++k)
+        for (uint32_t k = 0; k < NG; ++k)
             if (cnt[k] * W[k] > best) { best = cnt[k] * W[k]; sel = k; }
         if (sel == kNGroups) break;  // no lane holds a path and the range is done
 #ifdef MH_EXP_VSCNT  // diagnostic build: wave trips, lanes and shader cycles per phase (in registers)
@@ -1150,30 +1370,40 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                     rng.seed(seed_value, lane);
                     const float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
                     const RayT r = camera_ray(S, __builtin_fmaf(sx, sw, -0.f), __builtin_fmaf(sy, sh, -0.f));
-                    out[3 * plane + k] = sx;
-                    out[4 * plane + k] = sy;
-                    M::init(S, in, rng, r, v);
+                    if (M::kWritesPos) {
+                        out[3 * plane + k] = sx;
+                        out[4 * plane + k] = sy;
+                    }
+                    mc.init(S, in, rng, r, v, sx, sy);
                     ph = kPhHead;
                 }
             }
             next = std::min<uint64_t>(end, next + (uint64_t)__popcll(m));
         } else if (sel == kGHead) {
-            if (ph == kPhHead) { ph = M::head(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhHead) { ph = mc.head(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGTrace) {
             if (g == kGTrace) {
-                ph = M::template trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
+                ph = mc.template trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
                 ended = ph == kPhFree;
             }
         } else if (sel == kGScatter) {
-            if (ph == kPhScatter) { ph = M::scatter(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhScatter) { ph = mc.scatter(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGSurf) {
-            if (ph == kPhSurf) { ph = M::surf(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhSurf) { ph = mc.surf(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGWalk) {
-            if (ph == kPhWalk) ph = M::walk(S, rng, v, wm);
-        } else {
-            if (ph == kPhPost) { ph = M::post(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhWalk) ph = mc.walk(S, rng, v, wm);
+        } else if (sel == kGPost) {
+            if (ph == kPhPost) { ph = mc.post(S, B, in, rng, v, n_shadow); ended = ph == kPhFree; }
+        } else if (M::kDeferEnd) {
+            if (ph == kPhEnd) {
+                mc.end(S, B, in, out, plane, pid, v, alpha, n_closest, n_shadow);
+                ph = kPhFree;
+            }
         }
-        if (ended) M::write(out, plane, pid, v, alpha);
+        if (ended) {
+            if (M::kDeferEnd) ph = kPhEnd;
+            else mc.end(S, B, in, out, plane, pid, v, alpha, n_closest, n_shadow);
+        }
 #ifdef MH_EXP_VSCNT
         {
             const uint64_t dt = __builtin_amdgcn_s_memtime() - t_phase;
@@ -1183,6 +1413,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         }
 #endif
     }
+    mc.finish();
     if (counters) {
         wave_count(&counters[0], n_closest);
         wave_count(&counters[1], n_shadow);
@@ -1191,8 +1422,8 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     if (vw_lane() == 0 && counters)
         for (uint32_t k = 0; k < kNGroups; ++k) {
             atomicAdd(&counters[2 + k], d_trips[k]);
-            atomicAdd(&counters[9 + k], d_lanes[k]);
-            atomicAdd(&counters[16 + k], d_ticks[k]);
+            atomicAdd(&counters[2 + kNGroups + k], d_lanes[k]);
+            atomicAdd(&counters[2 + 2 * kNGroups + k], d_ticks[k]);
         }
 #endif
 }
@@ -1241,7 +1472,7 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     const bool tab = S.tab_bytes != 0 && !getenv("MH_VS_NOTAB");
 #define MH_VS1(Mc, L, P, T)                                                                                   \
     hipLaunchKernelGGL((k_vol_sched<Mc, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), st, S, \
-                       in, lm, seed_value, n, plane, out, counters, work, alpha)
+                       in, lm, seed_value, n, plane, out, counters, work, alpha, VsBwdArgs{})
 #define MH_VS(L, P, T)                                                  \
     do {                                                                \
         if (in.type == MH_INTEGRATOR_PRBVOLPATH) MH_VS1(PvMachine, L, P, T); \
@@ -1256,6 +1487,114 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     else MH_VS(false, false, false);
 #undef MH_VS
 #undef MH_VS1
+    return hipGetLastError();
+}
+
+// prbvolpath's single-pass backward on the phase scheduler: n samples of the
+// lane map, gradients into bw.ga's slot buffers (k_prbvol_backward's Mode 2)
+hipError_t launch_vol_sched_bwd(const DScene &S, const IntegratorParams &in, const LaneMap &lm, uint32_t seed_value,
+                                uint64_t n, const VsBwdArgs &bw, uint32_t grid, unsigned long long *counters,
+                                hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (in.type != MH_INTEGRATOR_PRBVOLPATH || !bw.main_log || !bw.nee_log || !bw.main_cap || !bw.nee_cap)
+        return hipErrorInvalidValue;
+    const size_t sh = lds_bytes(S, 256);
+    const bool lds = S.lds_bytes_bvh != 0;
+    const char *te = getenv("MH_TRAVERSAL");
+    const bool pk = S.n_prims > 0 && S.n_prims <= wf_packet_max_prims() && !(te && !strcmp(te, "lane"));
+    const bool tab = S.tab_bytes != 0 && !getenv("MH_VS_NOTAB");
+    unsigned long long *work = counters + 32;  // the 8 queue heads of this launch (128 B apart)
+    hipError_t e = hipMemsetAsync(work, 0, 8 * 128, st);
+    if (e != hipSuccess) return e;
+#define MH_VSB(L, P, T)                                                                                        \
+    hipLaunchKernelGGL((k_vol_sched<PvBwdMachine, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), \
+                       st, S, in, lm, seed_value, n, (uint64_t)0, (float *)nullptr, counters, work, 0, bw)
+    if (pk && tab) MH_VSB(false, true, true);
+    else if (pk) MH_VSB(false, true, false);
+    else if (lds) MH_VSB(true, false, false);
+    else MH_VSB(false, false, false);
+#undef MH_VSB
+    return hipGetLastError();
+}
+
+// A path whose MainLog overflowed: its adjoint replayed with L = its radiance
+// (prbvol_sample Mode 3, the NEE terms already charged), as k_prbvol_backward
+// does in place.
+template <bool InLds>
+__global__ void __launch_bounds__(256)
+k_pvb_replay_paths(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, VsBwdArgs bw,
+                   unsigned long long *counters) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    GradCtx g = make_grad_ctx(bw.ga);
+    uint32_t nc = 0, ns = 0;
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < min(*bw.ovf_count, bw.ovf_cap)) {
+        const float4 e = bw.ovf_paths[2 * (uint64_t)k], d = bw.ovf_paths[2 * (uint64_t)k + 1];
+        uint32_t lane, px, py;
+        lane_of(lm, __float_as_uint(e.w), lane, px, py);
+        Pcg r;
+        r.seed(seed_value, lane);
+        const float sx = (float)px + r.next_float(), sy = (float)py + r.next_float();
+        const RayT ray = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
+                                    __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+        prbvol_sample<3>(S, B, in, r, ray, v3(d.x, d.y, d.z), v3(e.x, e.y, e.z), &g, nc, ns);
+    }
+    flush_small_slots(g, bw.ga);
+    if (counters) {
+        wave_count(&counters[0], nc);
+        wave_count(&counters[1], ns);
+    }
+}
+
+// An NEE walk whose NeeLog overflowed: replayed with the sampler cloned at its
+// emitter sample, back-propagating dL * adj_emitted through every
+// tr_multiplier (prbvolpath.py:412-414; pvp_sample_emitter Mode 1).  The walk
+// reads of its vertex only the reference point, normal and shape.
+template <bool InLds>
+__global__ void __launch_bounds__(256)
+k_pvb_replay_walks(DScene S, VsBwdArgs bw, unsigned long long *counters) {
+    extern __shared__ uint4 lds[];
+    LdsBvh B = stage_bvh<InLds>(S, lds);
+    GradCtx g = make_grad_ctx(bw.ga);
+    uint32_t ns = 0;
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < min(*(bw.ovf_count + 1), bw.ovf_cap)) {
+        const float4 *r = bw.ovf_walks + (uint64_t)kPvbWalkRec * k;
+        const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4];
+        const uint32_t flags = __float_as_uint(r1.w);
+        MEI mei;
+        mei.p = v3(r0.x, r0.y, r0.z);
+        SI si;
+        si.valid = (flags & 2u) != 0;
+        si.p = mei.p;
+        si.n = v3(r1.x, r1.y, r1.z);
+        si.shape = __float_as_uint(r0.w);
+        Pcg rng;
+        rng.state = (uint64_t)__float_as_uint(r4.x) | ((uint64_t)__float_as_uint(r4.y) << 32);
+        rng.inc = (uint64_t)__float_as_uint(r4.z) | ((uint64_t)__float_as_uint(r4.w) << 32);
+        DirS ds;
+        pvp_sample_emitter<1>(S, B, mei, si, (flags & 1u) != 0, rng, __float_as_uint(r2.w), ds,
+                              v3(r2.x, r2.y, r2.z), v3(r3.x, r3.y, r3.z), &g, ns);
+    }
+    flush_small_slots(g, bw.ga);
+    if (counters) wave_count(&counters[1], ns);
+}
+
+hipError_t launch_vol_sched_bwd_replays(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
+                                        uint32_t seed_value, uint64_t n, const VsBwdArgs &bw,
+                                        unsigned long long *counters, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    // the lists' lengths stay on the device: every thread beyond them leaves at once
+    const size_t sh = lds_bytes(S, 256);
+    const uint32_t gp = (bw.ovf_cap + 255) / 256, gw = gp;
+    if (S.lds_bytes_bvh) {
+        hipLaunchKernelGGL(k_pvb_replay_paths<true>, dim3(gp), dim3(256), sh, st, S, in, lm, seed_value, bw, counters);
+        hipLaunchKernelGGL(k_pvb_replay_walks<true>, dim3(gw), dim3(256), sh, st, S, bw, counters);
+    } else {
+        hipLaunchKernelGGL(k_pvb_replay_paths<false>, dim3(gp), dim3(256), sh, st, S, in, lm, seed_value, bw, counters);
+        hipLaunchKernelGGL(k_pvb_replay_walks<false>, dim3(gw), dim3(256), sh, st, S, bw, counters);
+    }
     return hipGetLastError();
 }
 

@@ -368,20 +368,28 @@ def test_prbvolpath_per_sample_parity(kw, mode):
     assert close.mean() >= 0.999
 
 
-@pytest.mark.parametrize("nee", ["single", "main4", "twopass", "cap2", "replay"])
+@pytest.mark.parametrize("nee", ["single", "main4", "sched_nee2", "sched_off", "twopass", "cap2", "replay"])
 @pytest.mark.parametrize("kw", [{}, {"medium_type": "homogeneous", "sigma_t": 0.8, "scale": 1.0}])
 def test_prbvolpath_backward_parity(kw, nee, monkeypatch):
     """Gradients (sigma_t, albedo, floor reflectance) vs the oracle: same
     samples, float vs double accumulation and atomic order -> 2e-3.
-      single   one traversal: the L-dependent terms logged per thread
-               (MainLog) and charged once L_total is known, NEE walks logged
-               (NeeLog) -- the default
-      main4    4 MainLog entries per thread: most paths overflow and replay
-               their adjoint (without the NEE terms already charged)
-      twopass  primal + adjoint replay, NEE walks logged (MH_PVP_SINGLE=0)
-      cap2     two-pass with 2 NeeLog entries: most walks replay
-      replay   the reference's structure: two passes, NEE walks replayed"""
-    if nee == "replay":
+      single     one traversal on the phase scheduler (k_vol_sched<PvBwdMachine>):
+                 the L-dependent terms logged per lane (MainLog) and charged
+                 once L_total is known, NEE walks logged (NeeLog) -- the default
+      main4      4 MainLog entries: most paths overflow, and their adjoint is
+                 replayed from the overflow list (k_pvb_replay_paths) without
+                 the NEE terms already charged
+      sched_nee2 2 NeeLog entries on the scheduler: most walks overflow and are
+                 replayed from the overflow list (k_pvb_replay_walks)
+      sched_off  the same single pass on the per-sample kernel (k_prbvol_backward)
+      twopass    primal + adjoint replay, NEE walks logged (MH_PVP_SINGLE=0)
+      cap2       two-pass with 2 NeeLog entries: most walks replay
+      replay     the reference's structure: two passes, NEE walks replayed"""
+    if nee == "sched_nee2":
+        monkeypatch.setenv("MH_PVP_NEE_CAP", "2")
+    elif nee == "sched_off":
+        monkeypatch.setenv("MH_PVP_SCHED", "0")
+    elif nee == "replay":
         monkeypatch.setenv("MH_PVP_NEE_LOG", "0")
     elif nee == "cap2":
         monkeypatch.setenv("MH_PVP_NEE_CAP", "2")
