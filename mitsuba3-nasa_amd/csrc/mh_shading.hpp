@@ -2835,6 +2835,28 @@ struct MainLog {
     }
 };
 
+// Logs are read back in batches before their atomics are issued: on gfx950
+// stores and atomics retire through the same in-order vmcnt as loads, so a
+// load issued after a gradient scatter waits for the scatter's atomics (~3k
+// cycles with every CU issuing); one load per entry then paid that wait
+// once per entry, a batch pays it once.
+constexpr uint32_t kLogBatchMain = 2, kLogBatchWalk = 8;
+
+// the logged gradient steps of one NEE walk (NeeLog entries (p, coef) at
+// e[j * stride]): sigma_t's adjoint coef * K at every step, K = dL . adj_emitted
+MH_DEV void charge_walk_log(const DScene &S, const float4 *e, uint32_t stride, uint32_t n, uint32_t med, float K,
+                            GradCtx &g) {
+    for (uint32_t j0 = 0; j0 < n; j0 += kLogBatchWalk) {
+        float4 q[kLogBatchWalk];
+#pragma unroll
+        for (uint32_t b = 0; b < kLogBatchWalk; ++b)
+            if (j0 + b < n) q[b] = e[(uint64_t)(j0 + b) * stride];
+#pragma unroll
+        for (uint32_t b = 0; b < kLogBatchWalk; ++b)
+            if (j0 + b < n) sigma_t_backward(S, med, v3(q[b].x, q[b].y, q[b].z), q[b].w * K, g);
+    }
+}
+
 // Mode 0: primal; 1: adjoint replay (L = primal radiance); 2: primal + MainLog
 // + NEE gradients (single pass); 3: adjoint replay without the NEE gradients
 // (the fallback of a Mode-2 path whose log overflowed)
@@ -2990,10 +3012,7 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
             if (NeeGrad) {
                 if (logged && !nl->overflow) {  // the logged walk's steps: coef * (dL . adj_emitted)
                     const float K = (dL.x * contrib.x + dL.y * contrib.y) + dL.z * contrib.z;
-                    for (uint32_t j = 0; j < nl->n; ++j) {
-                        const float4 e = nl->buf[(uint64_t)j * nl->stride + nl->t];
-                        sigma_t_backward(S, nl->med, v3(e.x, e.y, e.z), e.w * K, *g);
-                    }
+                    charge_walk_log(S, nl->buf + nl->t, nl->stride, nl->n, nl->med, K, *g);
                 } else {
                     Pcg r2 = nee_rng;
                     DirS ds2;
@@ -3067,23 +3086,34 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
 
 // the logged L-dependent terms of a path whose radiance is now L_total
 MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &g) {
-    for (uint32_t j = 0; j < ml.n; ++j) {
-        const uint64_t o = (uint64_t)4 * j * ml.stride + ml.t;
-        const float4 q0 = ml.buf[o], q1 = ml.buf[o + ml.stride], q2 = ml.buf[o + 2 * (uint64_t)ml.stride],
-                     q3 = ml.buf[o + 3 * (uint64_t)ml.stride];
-        const uint32_t bits = __float_as_uint(q0.w), idx = bits >> 2;
-        const V3 Lsuf = Ltot - v3(q1.x, q1.y, q1.z);  // prbvolpath.py: L - (contributions so far)
-        const V3 up = v3(q2.x * Lsuf.x, q2.y * Lsuf.y, q2.z * Lsuf.z);
-        if (bits & 1u) {
-            const V3 adj = (up * kInvPi) * q3.x;
-            tex_backward(S, idx, q1.w, q2.w, adj, g);
-        } else {
-            const float gs = (up.x * q3.x + up.y * q3.y) + up.z * q3.z;
-            sigma_t_backward(S, idx, v3(q0.x, q0.y, q0.z), gs, g);
-            if (bits & 2u) albedo_backward(idx, up * q3.w, g);
+    for (uint32_t j0 = 0; j0 < ml.n; j0 += kLogBatchMain) {
+        float4 q[kLogBatchMain][4];
+#pragma unroll
+        for (uint32_t b = 0; b < kLogBatchMain; ++b) {
+            if (j0 + b >= ml.n) break;
+            const uint64_t o = (uint64_t)4 * (j0 + b) * ml.stride + ml.t;
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c) q[b][c] = ml.buf[o + c * (uint64_t)ml.stride];
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kLogBatchMain; ++b) {
+            if (j0 + b >= ml.n) break;
+            const float4 q0 = q[b][0], q1 = q[b][1], q2 = q[b][2], q3 = q[b][3];
+            const uint32_t bits = __float_as_uint(q0.w), idx = bits >> 2;
+            const V3 Lsuf = Ltot - v3(q1.x, q1.y, q1.z);  // prbvolpath.py: L - (contributions so far)
+            const V3 up = v3(q2.x * Lsuf.x, q2.y * Lsuf.y, q2.z * Lsuf.z);
+            if (bits & 1u) {
+                const V3 adj = (up * kInvPi) * q3.x;
+                tex_backward(S, idx, q1.w, q2.w, adj, g);
+            } else {
+                const float gs = (up.x * q3.x + up.y * q3.y) + up.z * q3.z;
+                sigma_t_backward(S, idx, v3(q0.x, q0.y, q0.z), gs, g);
+                if (bits & 2u) albedo_backward(idx, up * q3.w, g);
+            }
         }
     }
 }
+
 
 // small (register-accumulated) gradient slots: wave butterfly, then one
 // atomic per wave and component

@@ -1170,10 +1170,7 @@ struct PvBwdMachine {
                            float mis, V3 wo_s, uint32_t &n_shadow) {
         if (!v.nl_over) {  // the logged walk's steps: coef * (dL . adj_emitted)
             const float K = (v.dL.x * contrib.x + v.dL.y * contrib.y) + v.dL.z * contrib.z;
-            for (uint32_t j = 0; j < v.nl_n; ++j) {
-                const float4 e = a.nee_log[nee_base() + j];
-                sigma_t_backward(S, v.nl_med, v3(e.x, e.y, e.z), e.w * K, g);
-            }
+            charge_walk_log(S, a.nee_log + nee_base(), 1u, v.nl_n, v.nl_med, K, g);
         } else {  // the walk is replayed with the cloned sampler after the launch (k_pvb_replay_walks)
             const bool am = !v.e_surface;
             const V3 rp = am ? v.mei.p : v.si.p, rn = am ? v3(0.f, 0.f, 0.f) : v.si.n;
