@@ -228,7 +228,7 @@ def main():
         #                    written alike; the first bounce reads the sample's
         #                    grad / W texel (16 B)
         # with R = rays (sum of queue lengths), N = samples: survivors R - N.
-        # traffic / VALU issue from the PMC passes of profiles/r2_pmc.json
+        # traffic / VALU issue from the PMC passes of profiles/r3_pmc.json
         # (tools/profile_r2.sh: FETCH/WRITE corrected by the calib_fetch factors
         # for the kernel's access width; VALU issue = SQ_INSTS_VALU x 2 cycles /
         # (1024 SIMDs x launch time x measured clock)).
@@ -236,7 +236,9 @@ def main():
         avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
         n_local = H * W * args.spp
         pmc = {}
-        ppath = os.path.join(ROOT, "profiles", "r2_pmc.json")
+        ppath = os.path.join(ROOT, "profiles", "r3_pmc.json")  # tools/profile_r2.sh of this round's build
+        if not os.path.exists(ppath):
+            ppath = os.path.join(ROOT, "profiles", "r2_pmc.json")
         if os.path.exists(ppath):
             try:
                 pmc = json.load(open(ppath)).get("kernels", {})
