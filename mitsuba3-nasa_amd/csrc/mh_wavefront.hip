@@ -71,13 +71,20 @@ constexpr uint32_t kMaxWfBounces = (1u << (32 - kPidBits)) - 1u;
 // per-lane stack, broadcast node reads), per-lane while-while otherwise.
 // MH_TRAVERSAL=packet|lane overrides (tests cover both).
 constexpr uint32_t kPacketMaxPrims = 64;
-uint32_t wf_packet_max_prims() { return kPacketMaxPrims; }
+// MH_PACKET_MAX_PRIMS: experiments with larger packet scenes (read once)
+uint32_t wf_packet_max_prims() {
+    static const uint32_t v = [] {
+        const char *e = getenv("MH_PACKET_MAX_PRIMS");
+        return e ? (uint32_t)std::max(1, atoi(e)) : kPacketMaxPrims;
+    }();
+    return v;
+}
 static bool use_packet(const DScene &S) {
     const char *e = getenv("MH_TRAVERSAL");
-    if (S.n_prims > kPacketMaxPrims) return false;  // no pair records beyond (mh_api.hip)
+    if (S.n_prims > wf_packet_max_prims()) return false;  // no pair records beyond (mh_api.hip)
     if (e && !strcmp(e, "packet")) return true;
     if (e && !strcmp(e, "lane")) return false;
-    return S.n_prims <= kPacketMaxPrims;
+    return true;
 }
 // MH_WF_FUSED=0 keeps the three-kernel pipeline (trace / shade / shadow)
 static bool wf_unfused() {
