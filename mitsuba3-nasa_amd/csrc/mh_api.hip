@@ -109,6 +109,7 @@ struct mh_scene {
     DevBuf pvp_log;    // prbvolpath backward: per-thread NEE-walk step logs (NeeLog)
     DevBuf pvp_main;   // prbvolpath backward: per-thread path logs of the single pass (MainLog)
     DevBuf pvp_ovf;    // prbvolpath backward on the scheduler: overflow lists + their counters
+    DevBuf grid_corner;  // prbvolpath backward: per-cell corner blocks of the grid sigma_t slots
     // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
     // buffers of the sharded entry points (slab W image, staged peer sums,
     // slab gradients)
@@ -474,7 +475,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf,
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner,
                       &s->shard_w, &s->shard_tmp, &s->shard_g})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -1061,6 +1062,8 @@ struct Slots {
     std::vector<size_t> counts;
     std::vector<uint32_t> slot_of_param;
     uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0, bmp_tex = 0;
+    uint32_t grid_res[kMaxParams][3] = {};  // large sigma_t slots: the grid's resolution (x, y, z)
+    std::vector<float *> corner;            // their corner blocks (upload_slots, corners = true)
     std::vector<uint8_t> meta;  // host image of the meta block (uploaded by upload_slots when it changed)
 };
 
@@ -1112,6 +1115,8 @@ static int build_slots(const mh_scene *s, uint32_t n_params, const uint32_t *par
             if (kind == 0) P.bmp_tex = idx;
         }
         P.counts[slot] = cnt;
+        if (kind == MH_PARAM_MEDIUM_SIGMA_T && !small)
+            for (int a = 0; a < 3; ++a) P.grid_res[slot][a] = s->h_media[idx].grid_res[a];
         *owner = slot;
         P.slot_of_param[k] = (uint32_t)slot;
     }
@@ -1120,7 +1125,11 @@ static int build_slots(const mh_scene *s, uint32_t n_params, const uint32_t *par
 
 // per-slot device buffers (s->tmp_c, zeroed) and the meta block
 // slot_of_tex | is_rgb | bufs | sigma_slot | albedo_slot (s->grad_meta)
-static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vector<float *> &bufs, GradArgs &ga) {
+// corners: the grid sigma_t slots scatter into per-cell corner blocks
+// (s->grid_corner, zeroed; launch_corner_gather after the backward) unless
+// MH_GRID_CORNER=0, the block would exceed 16 GiB or cannot be allocated
+static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vector<float *> &bufs, GradArgs &ga,
+                               bool corners = false) {
     size_t total = 0;
     std::vector<size_t> off(kMaxParams, 0);
     for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += (P.counts[k] + 3) / 4 * 4; }
@@ -1130,10 +1139,31 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     if (e != hipSuccess) return e;
     bufs.assign(kMaxParams, nullptr);
     for (int k = 0; k < kMaxParams; ++k) bufs[k] = P.counts[k] ? s->tmp_c.as<float>() + off[k] : nullptr;
+    P.corner.assign(kMaxParams, nullptr);
+    const char *ec = getenv("MH_GRID_CORNER");
+    if (corners && !(ec && !strcmp(ec, "0"))) {
+        std::vector<size_t> coff(kMaxParams, 0);
+        std::vector<bool> use(kMaxParams, false);
+        size_t cfl = 0;
+        for (int k = 0; k < kMaxParams; ++k) {
+            const uint32_t *r = P.grid_res[k];
+            use[k] = r[0] && (uint64_t)(r[0] + 1) * (r[1] + 1) * (r[2] + 1) < (1ull << 32);
+            coff[k] = cfl;
+            if (use[k]) cfl += corner_floats(r);
+        }
+        if (cfl && cfl * 4 <= (16ull << 30) && s->grid_corner.alloc(cfl * 4) == hipSuccess) {
+            e = hipMemsetAsync(s->grid_corner.ptr, 0, cfl * 4, st);
+            if (e != hipSuccess) return e;
+            for (int k = 0; k < kMaxParams; ++k)
+                if (use[k]) P.corner[k] = s->grid_corner.as<float>() + coff[k];
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     auto al16 = [](size_t x) { return (x + 15) / 16 * 16; };
     const size_t o_slot = 0, o_isrgb = al16(P.slot_of_tex.size() * 4), o_bufs = al16(o_isrgb + kMaxParams * 4),
                  o_sig = al16(o_bufs + kMaxParams * 8), o_alb = al16(o_sig + P.sigma_slot.size() * 4),
-                 meta_bytes = al16(o_alb + P.albedo_slot.size() * 4);
+                 o_cor = al16(o_alb + P.albedo_slot.size() * 4), meta_bytes = al16(o_cor + kMaxParams * 8);
     std::vector<uint8_t> &meta = P.meta;
     meta.assign(meta_bytes, 0);
     memcpy(meta.data() + o_slot, P.slot_of_tex.data(), P.slot_of_tex.size() * 4);
@@ -1141,6 +1171,7 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     memcpy(meta.data() + o_bufs, bufs.data(), kMaxParams * 8);
     memcpy(meta.data() + o_sig, P.sigma_slot.data(), P.sigma_slot.size() * 4);
     memcpy(meta.data() + o_alb, P.albedo_slot.data(), P.albedo_slot.size() * 4);
+    memcpy(meta.data() + o_cor, P.corner.data(), kMaxParams * 8);
     // uploaded only when it changes (a new parameter set or reallocated slot
     // buffers), then with a stream sync; repeated calls with the same
     // parameters stay asynchronous
@@ -1160,6 +1191,9 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     ga.n_rgb = P.n_rgb;
     ga.sigma_slot = P.n_medium_params ? reinterpret_cast<const int32_t *>(mb + o_sig) : nullptr;
     ga.albedo_slot = P.n_medium_params ? reinterpret_cast<const int32_t *>(mb + o_alb) : nullptr;
+    bool any_corner = false;
+    for (float *c : P.corner) any_corner = any_corner || c;
+    ga.corner = any_corner ? reinterpret_cast<float *const *>(mb + o_cor) : nullptr;
     return hipSuccess;
 }
 
@@ -1192,7 +1226,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (rc_slots) return rc_slots;
     std::vector<float *> bufs;
     GradArgs ga;
-    MH_HIP(upload_slots(s, P, st, bufs, ga));
+    MH_HIP(upload_slots(s, P, st, bufs, ga, vol));
     const std::vector<size_t> &counts = P.counts;
     const std::vector<uint32_t> &slot_of_param = P.slot_of_param;
     const uint32_t n_rgb = P.n_rgb, n_bmp = P.n_bmp, bmp_tex = P.bmp_tex;
@@ -1396,6 +1430,8 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
     }
+    for (int k = 0; k < kMaxParams; ++k)
+        if (P.corner[k]) MH_HIP(launch_corner_gather(P.corner[k], bufs[k], P.grid_res[k], st));
     MH_HIP(hipEventRecord(s->ev1, st));
     if (wants_reduce(flags)) {  // the slot buffers are one block of s->tmp_c (upload_slots)
         size_t total = 0;

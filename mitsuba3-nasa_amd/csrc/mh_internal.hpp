@@ -34,6 +34,8 @@ struct GradArgs {
     int32_t lds_slot = -1;       // bitmap slot accumulated per workgroup in LDS (k_prb_backward replay)
     uint32_t lds_floats = 0;     // its size (floats)
     uint32_t lds_offset = 0;     // byte offset of the accumulator in dynamic LDS (set by the launcher)
+    float *const *corner = nullptr;  // device: slot -> per-cell corner block of a grid sigma_t slot or nullptr
+                                     // (prbvolpath; gathered into bufs[slot] by launch_corner_gather)
 };
 
 // ---- BVH builder (host, binned SAH) --------------------------------------
@@ -132,6 +134,9 @@ uint64_t grid_bricked_size(const uint32_t res[3]);
 void grid_to_bricks(const float *src, const uint32_t res[3], float *dst);
 hipError_t launch_grid_to_bricks(const float *src, const uint32_t res[3], float *dst, hipStream_t st);
 hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream_t st);  // dst += src
+// grid sigma_t gradient: per-cell corner block (GradArgs::corner) -> (z, y, x) gradient (+=)
+uint64_t corner_floats(const uint32_t res[3]);
+hipError_t launch_corner_gather(const float *corner, float *grad, const uint32_t res[3], hipStream_t st);
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,

@@ -1468,6 +1468,7 @@ struct GradCtx {
     float acc[kMaxRgbParams][3];  // per-lane accumulators for rgb params
     const int32_t *sigma_slot;    // prbvolpath: medium -> sigma_t slot or -1 (nullptr: none)
     const int32_t *albedo_slot;   // prbvolpath: medium -> albedo slot or -1 (nullptr: none)
+    float *const *corner;         // prbvolpath: slot -> per-cell corner block of a grid (nullptr: atomics into bufs)
     int32_t lds_slot;             // bitmap slot whose texels accumulate in LDS (-1: none)
     float *lds_acc;               // that slot's workgroup accumulator
     uint32_t lds_floats;          // its size (floats; checked under MH_DEBUG)
@@ -2641,6 +2642,39 @@ MH_DEV V3 volpath_sample(const DScene &S, const LdsBvh &B, const IntegratorParam
 //   Same operation order as the oracle restatement (oracle/mh_oracle.c,
 //   "PRBVolpathIntegrator" section).
 // ===========================================================================
+// Grid-gradient scatter into a per-cell corner block (GradArgs::corner): cell
+// (ix, iy, iz) of a lookup -- ix = floor(x - 0.5) clamped to [-1, rx - 1],
+// which keeps its clamped taps -- owns 8 contiguous floats, one per tap, and
+// launch_corner_gather folds them into the (z, y, x) gradient afterwards.
+// Float atomics execute at the memory side as one 64-B request per distinct
+// segment of a wave-instruction (MI355X_MICROARCH.md, global float atomics):
+// 8 atomics per lane into the linear grid put up to 64 rows in every
+// instruction.  Here the active lanes stage (cell, 8 values) in wave LDS and
+// issue the 8 x n adds transposed -- instruction j takes items j*n .. j*n+n-1
+// of the (lane rank, tap) order, the taps of ~n/8 cells, 32 B each.
+// Any exec mask (the call sites are divergent loops); kernels of <= 4 waves.
+constexpr int kCornerWaves = 4;
+MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8]) {
+    __shared__ float stage[kCornerWaves * 64 * 9];
+    float *sc = stage + (threadIdx.x >> 6) * (64 * 9);
+    const uint64_t m = __ballot(1);
+    const uint32_t n = (uint32_t)__popcll(m);
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    sc[r * 9] = __uint_as_float(cell);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) sc[r * 9 + 1 + c] = v[c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t t = j * n + r, src = t >> 3, c = t & 7u;
+        const uint32_t cc = __float_as_uint(sc[src * 9]);
+        unsafeAtomicAdd(cb + (size_t)cc * 8 + c, sc[src * 9 + 1 + c]);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // adjoint of sigma_t(p) = scale * Texture3f(grid).eval(p) (heterogeneous.cpp:192)
 // or scale * sigma_t (homogeneous.cpp:158); adj = d loss / d sigma_t(p)
 MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, GradCtx &g) {
@@ -2665,6 +2699,20 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
     const int32_t ys[2] = {min(max(iy, 0), ry - 1), min(max(iy + 1, 0), ry - 1)};
     const int32_t zs[2] = {min(max(iz, 0), rz - 1), min(max(iz + 1, 0), rz - 1)};
     float *buf = g.bufs[k];
+    if (!g.fwd && g.corner) {
+        if (float *cb = g.corner[k]) {
+            float v[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+                v[c] = as * (((bz ? w1z : w0z) * (by ? w1y : w0y)) * (bx ? w1x : w0x));
+            }
+            const uint32_t cx = (uint32_t)(min(max(ix, -1), rx - 1) + 1), cy = (uint32_t)(min(max(iy, -1), ry - 1) + 1),
+                           cz = (uint32_t)(min(max(iz, -1), rz - 1) + 1);
+            corner_scatter(cb, (cz * (uint32_t)(ry + 1) + cy) * (uint32_t)(rx + 1) + cx, v);
+            return;
+        }
+    }
     const uint64_t sy = (uint64_t)rx, sz = (uint64_t)rx * (uint64_t)ry;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -3140,6 +3188,7 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.is_rgb = ga.is_rgb;
     g.sigma_slot = ga.sigma_slot;
     g.albedo_slot = ga.albedo_slot;
+    g.corner = ga.corner;
     g.lds_slot = -1;
     g.lds_acc = nullptr;
     g.lds_floats = 0;

@@ -417,6 +417,36 @@ def test_prbvolpath_backward_parity(kw, nee, monkeypatch):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-7 + 2e-4 * np.abs(b).max(), err_msg=k)
 
 
+@pytest.mark.parametrize("shape", [(16, 16, 16), (7, 9, 5), (1, 3, 2)])
+def test_prbvolpath_grid_corner_scatter(shape, monkeypatch):
+    """The sigma_t grid gradient scattered per cell into corner blocks and
+    gathered afterwards (corner_scatter / k_corner_gather, the default)
+    equals the float atomics straight into the (z, y, x) gradient
+    (MH_GRID_CORNER=0) up to the float order of the adds, and the oracle
+    (heterogeneous.cpp:192 adjoint, prbvolpath.py:412-414 scatter).
+    Non-cubic and one-texel-thin grids exercise the clamped boundary cells."""
+    mi = _mi()
+    import torch
+    o = [(16 - n) // 2 for n in shape]  # the dense centre of the fBm cube
+    grid = np.ascontiguousarray(mi.fbm_grid(16)[o[0]:o[0] + shape[0], o[1]:o[1] + shape[1], o[2]:o[2] + shape[2]])
+    scene = _pvp_scene(mi, 24, 20, 8, grid=grid)
+    integ = scene.integrator()
+    params = mi.traverse(scene)
+    key = "medium1.sigma_t.data"
+    H, W = scene.height, scene.width
+    gi = np.random.default_rng(5).standard_normal((H, W, 3)).astype(np.float32)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MH_GRID_CORNER", mode)
+        out[mode] = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), [key], integ, seed=7,
+                                       spp=8)[0].cpu().numpy()
+    ref = O.render_backward(scene, integ, 7, 8, gi, [params.param_id(key)], [tuple(params[key].shape)])[0]
+    assert out["1"].shape == ref.shape and np.abs(ref).max() > 0
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(out["1"], out["0"], rtol=1e-4, atol=1e-6 * scale)
+    np.testing.assert_allclose(out["1"], ref, rtol=2e-3, atol=1e-7 + 2e-4 * scale)
+
+
 @pytest.mark.parametrize("alpha", [False, True])
 def test_prbvolpath_film_modes_agree(alpha):
     """mh_render of prbvolpath: the phase scheduler (default) against the
