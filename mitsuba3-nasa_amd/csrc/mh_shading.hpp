@@ -1465,7 +1465,8 @@ struct GradCtx {
     const int32_t *slot_of_tex;   // texture -> param slot or -1
     float *const *bufs;           // per slot gradient buffer
     const uint32_t *is_rgb;       // per slot
-    float acc[kMaxRgbParams][3];  // per-lane accumulators for rgb params
+    V3 acc0, acc1, acc2, acc3;    // per-lane accumulators of the small slots 0..3 (named, never indexed:
+                                  // one runtime-indexed access would put the whole context in scratch)
     const int32_t *sigma_slot;    // prbvolpath: medium -> sigma_t slot or -1 (nullptr: none)
     const int32_t *albedo_slot;   // prbvolpath: medium -> albedo slot or -1 (nullptr: none)
     float *const *corner;         // prbvolpath: slot -> per-cell corner block of a grid (nullptr: atomics into bufs)
@@ -1479,12 +1480,16 @@ struct GradCtx {
     float fsum;
 };
 
-// register accumulator of a small (rgb / scalar) parameter slot; the
-// unrolled compare keeps acc[][] in VGPRs (a runtime index would spill it)
+// register accumulator of a small (rgb / scalar) parameter slot
+static_assert(kMaxRgbParams == 4, "GradCtx names four small-slot accumulators");
 MH_DEV void acc_add(GradCtx &g, int32_t k, V3 a) {
-#pragma unroll
-    for (int kk = 0; kk < kMaxRgbParams; ++kk)
-        if (kk == k) { g.acc[kk][0] += a.x; g.acc[kk][1] += a.y; g.acc[kk][2] += a.z; }
+    if (k == 0) g.acc0 = g.acc0 + a;
+    else if (k == 1) g.acc1 = g.acc1 + a;
+    else if (k == 2) g.acc2 = g.acc2 + a;
+    else if (k == 3) g.acc3 = g.acc3 + a;
+}
+MH_DEV V3 acc_get(const GradCtx &g, int32_t k) {
+    return k == 0 ? g.acc0 : k == 1 ? g.acc1 : k == 2 ? g.acc2 : k == 3 ? g.acc3 : v3(0.f, 0.f, 0.f);
 }
 
 // ---------------------------------------------------------------------------
@@ -1569,9 +1574,7 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
     }
     const DTexture &tx = S.textures[tex];
     if (g.is_rgb[k]) {
-#pragma unroll
-        for (int kk = 0; kk < kMaxRgbParams; ++kk)
-            if (kk == k) { g.acc[kk][0] += adj.x; g.acc[kk][1] += adj.y; g.acc[kk][2] += adj.z; }
+        acc_add(g, k, adj);
         return;
     }
     Taps tp;
@@ -1968,6 +1971,14 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
     V3 prev_p = v3(0, 0, 0);
     float prev_bsdf_pdf = 1.f;
     bool prev_bsdf_delta = true;
+    // the small slots' accumulators as a local array for charge / add_slot
+    // (indexed only by unrolled constants), written back to g at the end
+    float acc[kMaxRgbParams][3];
+#pragma unroll
+    for (int kk = 0; kk < kMaxRgbParams; ++kk) {
+        const V3 a = acc_get(g, kk);
+        acc[kk][0] = a.x; acc[kk][1] = a.y; acc[kk][2] = a.z;
+    }
     float A[kMaxRgbParams][3];
 #pragma unroll
     for (int k = 0; k < kMaxRgbParams; ++k) A[k][0] = A[k][1] = A[k][2] = 0.f;
@@ -1988,7 +1999,7 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
             V3 le = v3(0, 0, 0);
             if (active_next)
                 le = emitter_eval(S, em, si);
-            charge(g.acc, A, n_rgb, dL * ((beta * mis) * le));
+            charge(acc, A, n_rgb, dL * ((beta * mis) * le));
         }
         active_next = active_next && (depth + 1 < in.max_depth) && si.valid;
         bool active_em = active_next && smooth;
@@ -2010,7 +2021,7 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
         diffuse_eval_pdf(rho, si.wi, wo_em, active_em, bsdf_value_em, bsdf_pdf_em);
         float mis_em = ds.delta ? 1.f : mis_weight(ds.pdf, bsdf_pdf_em);
         V3 beta_mis_em = beta * mis_em;
-        if (active_em) charge(g.acc, A, n_rgb, dL * ((beta_mis_em * bsdf_value_em) * em_weight));
+        if (active_em) charge(acc, A, n_rgb, dL * ((beta_mis_em * bsdf_value_em) * em_weight));
         (void)rng.next_float();
         float s2x = rng.next_float(), s2y = rng.next_float();
         V3 bs_wo = v3(0, 0, 0), bsdf_weight = v3(0, 0, 0);
@@ -2038,16 +2049,19 @@ MH_DEV void prb_fused(const DScene &S, const LdsBvh &B, const IntegratorParams &
             const int32_t slot = g.slot_of_tex[S.bsdf_tex[b]];
             if (slot >= 0) {
                 if (active_em && si.wi.z > 0.f && wo_em.z > 0.f)
-                    add_slot(g.acc, slot, (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi);
+                    add_slot(acc, slot, (((dL * em_weight) * beta_mis_em) * wo_em.z) * kInvPi);
                 add_slot(A, slot, prb_indirect_factor(active_next, si, to_local(si, ray.d), bsdf_weight, bs_pdf));
             }
         }
         if (si.valid) depth += 1;
         active = active_next;
     }
+    g.acc0 = v3(acc[0][0], acc[0][1], acc[0][2]);
+    g.acc1 = v3(acc[1][0], acc[1][1], acc[1][2]);
+    g.acc2 = v3(acc[2][0], acc[2][1], acc[2][2]);
+    g.acc3 = v3(acc[3][0], acc[3][1], acc[3][2]);
 }
 
-// ---------------------------------------------------------------------------
 // Forward-mode PRB (render_forward, common.py:696-826; prb.py:244-248
 // `δL += dr.forward_to(Lo)`) in the single-traversal form of prb_fused.  The
 // replay's tangent at vertex k is (D_k + (L_total - P_k) c_k / pi) * t_k with
@@ -2193,6 +2207,16 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     float f00 = __builtin_fmaf(w0x, v000, w1x * v100), f01 = __builtin_fmaf(w0x, v001, w1x * v101),
           f10 = __builtin_fmaf(w0x, v010, w1x * v110), f11 = __builtin_fmaf(w0x, v011, w1x * v111);
     float f0 = __builtin_fmaf(w0y, f00, w1y * f10), f1 = __builtin_fmaf(w0y, f01, w1y * f11);
+#ifdef MH_EXP_GRID2  // timing experiment: a second lookup's memory traffic (x mirrored), results unchanged
+    {
+        const int32_t xa = rx - 1 - x0, xb = rx - 1 - x1;
+        const float u = g[grid_index(xa, y0, z0, rx, ry)] + g[grid_index(xb, y0, z0, rx, ry)] +
+                        g[grid_index(xa, y1, z0, rx, ry)] + g[grid_index(xb, y1, z0, rx, ry)] +
+                        g[grid_index(xa, y0, z1, rx, ry)] + g[grid_index(xb, y0, z1, rx, ry)] +
+                        g[grid_index(xa, y1, z1, rx, ry)] + g[grid_index(xb, y1, z1, rx, ry)];
+        return __builtin_fmaf(w0z, f0, w1z * f1) + 0.f * u;
+    }
+#endif
     return __builtin_fmaf(w0z, f0, w1z * f1);
 }
 
@@ -3168,12 +3192,10 @@ MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &
 MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
     for (uint32_t p = 0; p < ga.n_rgb; ++p) {
         const int slot = (int)p;
+        const V3 a = acc_get(g, slot);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            float v = 0.f;
-#pragma unroll
-            for (int kk = 0; kk < kMaxRgbParams; ++kk)
-                if (kk == slot) v = g.acc[kk][c];
+            float v = c == 0 ? a.x : c == 1 ? a.y : a.z;
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
             if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(ga.bufs[slot] + c, v);
@@ -3194,8 +3216,7 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.lds_floats = 0;
     g.fwd = false;
     g.fsum = 0.f;
-#pragma unroll
-    for (int k = 0; k < kMaxRgbParams; ++k) g.acc[k][0] = g.acc[k][1] = g.acc[k][2] = 0.f;
+    g.acc0 = g.acc1 = g.acc2 = g.acc3 = v3(0.f, 0.f, 0.f);
     return g;
 }
 
