@@ -321,6 +321,9 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
             (a.grid_res[0] == 0 || a.grid_res[1] == 0 || a.grid_res[2] == 0 ||
              a.grid_offset + (uint64_t)a.grid_res[0] * a.grid_res[1] * a.grid_res[2] > desc->n_grid))
             return fail(MH_ERR_INVALID_ARGUMENT, "mh_scene_create: volume grid out of bounds");
+        // grid_eval indexes a grid's bricked texels with 32-bit offsets
+        if (a.type == MH_MEDIUM_HETEROGENEOUS && grid_bricked_size(a.grid_res) >= (1ull << 32))
+            return fail(MH_ERR_UNSUPPORTED, "mh_scene_create: volume grid above 2^32 texels");
         if (a.phase == MH_PHASE_HG && !(a.g > -1.f && a.g < 1.f))
             return fail(MH_ERR_INVALID_ARGUMENT, "The asymmetry parameter must lie in the interval (-1, 1)!");
     }

@@ -2200,10 +2200,17 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     return w0x * 0.3f + w1y * 0.2f + w0z * 0.1f + (float)(x0 + y1 + z0) * 1e-9f;
 #endif
     const float *g = S.grid + m.grid_offset;
-    float v000 = g[grid_index(x0, y0, z0, rx, ry)], v100 = g[grid_index(x1, y0, z0, rx, ry)];
-    float v010 = g[grid_index(x0, y1, z0, rx, ry)], v110 = g[grid_index(x1, y1, z0, rx, ry)];
-    float v001 = g[grid_index(x0, y0, z1, rx, ry)], v101 = g[grid_index(x1, y0, z1, rx, ry)];
-    float v011 = g[grid_index(x0, y1, z1, rx, ry)], v111 = g[grid_index(x1, y1, z1, rx, ry)];
+    // grid_index split per axis (brick-major part + texel-in-brick part, the
+    // bit fields disjoint), 32-bit (mh_scene_create caps a grid at 2^32 texels)
+    const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2, sy = nbx * 64u, sz = sy * nby;
+    const uint32_t ox0 = ((uint32_t)x0 >> 2) * 64u + ((uint32_t)x0 & 3u), ox1 = ((uint32_t)x1 >> 2) * 64u + ((uint32_t)x1 & 3u);
+    const uint32_t oy0 = ((uint32_t)y0 >> 2) * sy + (((uint32_t)y0 & 3u) << 2), oy1 = ((uint32_t)y1 >> 2) * sy + (((uint32_t)y1 & 3u) << 2);
+    const uint32_t oz0 = ((uint32_t)z0 >> 2) * sz + (((uint32_t)z0 & 3u) << 4), oz1 = ((uint32_t)z1 >> 2) * sz + (((uint32_t)z1 & 3u) << 4);
+    const uint32_t o00 = oy0 + oz0, o10 = oy1 + oz0, o01 = oy0 + oz1, o11 = oy1 + oz1;
+    float v000 = g[o00 + ox0], v100 = g[o00 + ox1];
+    float v010 = g[o10 + ox0], v110 = g[o10 + ox1];
+    float v001 = g[o01 + ox0], v101 = g[o01 + ox1];
+    float v011 = g[o11 + ox0], v111 = g[o11 + ox1];
     float f00 = __builtin_fmaf(w0x, v000, w1x * v100), f01 = __builtin_fmaf(w0x, v001, w1x * v101),
           f10 = __builtin_fmaf(w0x, v010, w1x * v110), f11 = __builtin_fmaf(w0x, v011, w1x * v111);
     float f0 = __builtin_fmaf(w0y, f00, w1y * f10), f1 = __builtin_fmaf(w0y, f01, w1y * f11);

@@ -511,15 +511,17 @@ MH_DEV uint32_t vs_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rn
     return (v.active && v.active_medium) ? kPhHead : kPhFree;
 }
 
-// HEAD: Russian roulette and free-flight sampling (volpath.cpp:143-165)
-MH_DEV uint32_t vs_head(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+// HEAD: Russian roulette and free-flight sampling (volpath.cpp:143-165), cut
+// at its medium sample: true with the sample's draw u when one is pending
+// (v.medium, v.ray), else the next phase in nph
+MH_DEV bool vs_head_pre(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v, uint32_t &nph, float &u) {
     bool active = nonzero(v.throughput);
     const float q = fminf(hmax(v.throughput) * (v.eta * v.eta), 0.95f);
     const bool perform_rr = v.depth > in.rr_depth;
     if (active) active = rng.next_float() < q || !perform_rr;
     if (perform_rr) v.throughput = v.throughput * rcp(q);
     active = active && v.depth < in.max_depth;
-    if (!active) return kPhFree;
+    if (!active) { nph = kPhFree; return false; }
     v.active = true;
     v.active_medium = v.medium != MH_INVALID;
     v.active_surface = !v.active_medium;
@@ -527,14 +529,23 @@ MH_DEV uint32_t vs_head(const DScene &S, const IntegratorParams &in, Pcg &rng, V
     v.nee_kind = kNeeNone;
     v.mei.valid = false;
     v.mei.t = __builtin_huge_valf();
-    if (v.active_medium) {
-        const DMedium &m = S.media[v.medium];
-        sample_interaction(S, v.medium, v.ray, rng.next_float(), v.mei);
-        if (m.type == MH_MEDIUM_HOMOGENEOUS && v.mei.valid) v.ray.maxt = v.mei.t;
-        if (v.needs_intersection) return kPhTraceM;
-        return vs_med_rest(S, in, rng, v);
-    }
-    return v.needs_intersection ? kPhTraceS : kPhSurf;
+    if (v.active_medium) { u = rng.next_float(); return true; }
+    nph = v.needs_intersection ? kPhTraceS : kPhSurf;
+    return false;
+}
+// the rest of HEAD once v.mei holds the medium sample
+MH_DEV uint32_t vs_head_post(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    const DMedium &m = S.media[v.medium];
+    if (m.type == MH_MEDIUM_HOMOGENEOUS && v.mei.valid) v.ray.maxt = v.mei.t;
+    if (v.needs_intersection) return kPhTraceM;
+    return vs_med_rest(S, in, rng, v);
+}
+MH_DEV uint32_t vs_head(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    uint32_t nph = kPhFree;
+    float u = 0.f;
+    if (!vs_head_pre(S, in, rng, v, nph, u)) return nph;
+    sample_interaction(S, v.medium, v.ray, u, v.mei);
+    return vs_head_post(S, in, rng, v);
 }
 
 // SCATTER: a real medium interaction (volpath.cpp:224-252)
@@ -638,23 +649,61 @@ MH_DEV bool walk_med_rest(const DScene &S, const DirS &ds, NeeState &ns, WMei &w
     return walk_tail(S, ns, active_medium, escaped, false, false, remaining);
 }
 
-// WALK: the start of a walk step, up to its intersection
-MH_DEV uint32_t vs_walk(const DScene &S, Pcg &rng, const DirS &ds, NeeState &ns, WMei &wm) {
+// WALK: the start of a walk step, up to its intersection; cut at its medium
+// sample like HEAD (pending: ns.medium, ns.ray and the draw u)
+MH_DEV bool vs_walk_pre(const DScene &S, Pcg &rng, NeeState &ns, uint32_t &nph, float &u) {
     const float remaining = ns.max_dist - ns.total_dist;
     ns.ray.maxt = remaining;
-    if (!(remaining > 0.f)) return kPhPost;
-    if (ns.medium != MH_INVALID) {
-        const DMedium &m = S.media[ns.medium];
-        MEI mei;
-        sample_interaction(S, ns.medium, ns.ray, rng.next_float(), mei);
-        if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ns.ray.maxt = fminf(mei.t, remaining);
-        wm.t = mei.t; wm.mint = mei.mint; wm.maj = mei.maj; wm.sigma_n = mei.sigma_n; wm.p = mei.p;
-        wm.valid = mei.valid;
-        if (ns.needs_intersection) return kPhTraceWM;
-        return walk_med_rest(S, ds, ns, wm) ? kPhWalk : kPhPost;
+    if (!(remaining > 0.f)) { nph = kPhPost; return false; }
+    if (ns.medium != MH_INVALID) { u = rng.next_float(); return true; }
+    if (ns.needs_intersection) { nph = kPhTraceWS; return false; }
+    nph = walk_tail(S, ns, false, false, true, false, remaining) ? kPhWalk : kPhPost;
+    return false;
+}
+MH_DEV uint32_t vs_walk_post(const DScene &S, const DirS &ds, NeeState &ns, WMei &wm, const MEI &mei) {
+    const float remaining = ns.max_dist - ns.total_dist;
+    const DMedium &m = S.media[ns.medium];
+    if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) ns.ray.maxt = fminf(mei.t, remaining);
+    wm.t = mei.t; wm.mint = mei.mint; wm.maj = mei.maj; wm.sigma_n = mei.sigma_n; wm.p = mei.p;
+    wm.valid = mei.valid;
+    if (ns.needs_intersection) return kPhTraceWM;
+    return walk_med_rest(S, ds, ns, wm) ? kPhWalk : kPhPost;
+}
+MH_DEV uint32_t vs_walk(const DScene &S, Pcg &rng, const DirS &ds, NeeState &ns, WMei &wm) {
+    uint32_t nph = kPhPost;
+    float u = 0.f;
+    if (!vs_walk_pre(S, rng, ns, nph, u)) return nph;
+    MEI mei;
+    sample_interaction(S, ns.medium, ns.ray, u, mei);
+    return vs_walk_post(S, ds, ns, wm, mei);
+}
+
+// HEAD and WALK lanes in one trip: both end in a medium sample (a grid
+// lookup, the trip's latency), so the pending lanes of both take it together
+// at one call site instead of one wave trip each.  Per lane the operations
+// and draws are vs_head's / vs_walk's.
+MH_DEV uint32_t vs_medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v, WMei &wm,
+                               uint32_t ph) {
+    uint32_t nph = kPhFree;
+    float u = 0.f;
+    const bool head = ph == kPhHead;
+    const bool pend = head ? vs_head_pre(S, in, rng, v, nph, u) : vs_walk_pre(S, rng, v.ns, nph, u);
+    if (!pend) return nph;
+    // the request as a select of values (a select of the two fields'
+    // addresses would pin the state in scratch)
+    const uint32_t mh = v.medium, mw = v.ns.medium;
+    const RayT rh = v.ray, rw = v.ns.ray;
+    RayT r;
+    r.o = v3(head ? rh.o.x : rw.o.x, head ? rh.o.y : rw.o.y, head ? rh.o.z : rw.o.z);
+    r.d = v3(head ? rh.d.x : rw.d.x, head ? rh.d.y : rw.d.y, head ? rh.d.z : rw.d.z);
+    r.maxt = head ? rh.maxt : rw.maxt;
+    MEI mei;
+    sample_interaction(S, head ? mh : mw, r, u, mei);
+    if (ph == kPhHead) {
+        v.mei = mei;
+        return vs_head_post(S, in, rng, v);
     }
-    if (ns.needs_intersection) return kPhTraceWS;
-    return walk_tail(S, ns, false, false, true, false, remaining) ? kPhWalk : kPhPost;
+    return vs_walk_post(S, v.ds, v.ns, wm, mei);
 }
 
 // TRACE: every lane pending an intersection traces it; then its continuation
@@ -829,15 +878,17 @@ MH_DEV uint32_t pv_med_rest(const DScene &S, const IntegratorParams &in, Pcg &rn
     return pv_mid(S, in, v, act_null, escaped, weight, P, fw, mt, hk);
 }
 
-// HEAD: Russian roulette (:142-149) and the medium sample (:157-163)
+// HEAD: Russian roulette (:142-149) and the medium sample (:157-163), cut at
+// the medium sample (as vs_head_pre: true with its draw u when one is
+// pending for v.med / v.ray, else the next phase in nph)
 template <class V, class Hk>
-MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk) {
+MH_DEV bool pv_head_pre(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk, uint32_t &nph, float &u) {
     bool active = nonzero(v.throughput);
     const float q = fminf(hmax(v.throughput) * (v.eta * v.eta), 0.99f);
     const bool perform_rr = v.depth > in.rr_depth;
     if (active) active = rng.next_float() < q || !perform_rr;
     if (perform_rr) v.throughput = v.throughput * rcp(q);
-    if (!active) return kPhFree;
+    if (!active) { nph = kPhFree; return false; }
     v.active = true;
     v.active_medium = v.medium != MH_INVALID;
     v.active_surface = !v.active_medium;
@@ -851,31 +902,44 @@ MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, V
     mei.sigma_t = 0.f;
     mei.p = v3(0.f, 0.f, 0.f);
     mei.sigma_s = v3(0.f, 0.f, 0.f);
-    if (v.active_medium) {
-        const DMedium &m = S.media[v.med];
-        sample_interaction(S, v.med, v.ray, rng.next_float(), mei);
-        if (m.type == MH_MEDIUM_HOMOGENEOUS && mei.valid) v.ray.maxt = mei.t;
-        if (v.needs_intersection) return kPhTraceM;
-        return pv_med_rest(S, in, rng, v, hk);
-    }
-    return pv_mid(S, in, v, false, false, v3(1.f, 1.f, 1.f), 1.f, 1.f, 0.f, hk);
+    if (v.active_medium) { u = rng.next_float(); return true; }
+    nph = pv_mid(S, in, v, false, false, v3(1.f, 1.f, 1.f), 1.f, 1.f, 0.f, hk);
+    return false;
+}
+// the rest of HEAD once v.mei holds the medium sample
+template <class V, class Hk>
+MH_DEV uint32_t pv_head_post(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk) {
+    const DMedium &m = S.media[v.med];
+    if (m.type == MH_MEDIUM_HOMOGENEOUS && v.mei.valid) v.ray.maxt = v.mei.t;
+    if (v.needs_intersection) return kPhTraceM;
+    return pv_med_rest(S, in, rng, v, hk);
+}
+template <class V, class Hk>
+MH_DEV uint32_t pv_head(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk) {
+    uint32_t nph = kPhFree;
+    float u = 0.f;
+    if (!pv_head_pre(S, in, rng, v, hk, nph, u)) return nph;
+    sample_interaction(S, v.med, v.ray, u, v.mei);
+    return pv_head_post(S, in, rng, v, hk);
 }
 
-// the walk step after its (optional) intersection (pvp_sample_emitter's loop)
-template <class V, class Hk>
-MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, V &v, float remaining_dist, Hk &hk) {
-    v.w_needs = false;
-    bool act_med = v.wmedium != MH_INVALID, act_surf = !act_med, escaped = false, hom = false;
-    float hom_t = 0.f;
-    MEI mei;
+// the walk step after its (optional) intersection (pvp_sample_emitter's loop),
+// from its medium sample on: mei holds it when the walk is in a medium
+// (v.wmedium valid), else the defaults below
+MH_DEV void pv_walk_mei_init(MEI &mei) {
     mei.valid = false;
     mei.t = 0.f;
     mei.maj = 1.f;
     mei.p = v3(0.f, 0.f, 0.f);
+}
+template <class V, class Hk>
+MH_DEV uint32_t pv_walk_fin(const DScene &S, V &v, float remaining_dist, Hk &hk, MEI &mei) {
+    v.w_needs = false;
+    bool act_med = v.wmedium != MH_INVALID, act_surf = !act_med, escaped = false, hom = false;
+    float hom_t = 0.f;
     V3 trm = v3(1.f, 1.f, 1.f);
     if (act_med) {
         const DMedium &m = S.media[v.wmedium];
-        sample_interaction(S, v.wmedium, v.wray, rng.next_float(), mei);
         if (v.wsi_t < mei.t) { mei.t = __builtin_huge_valf(); mei.valid = false; }
         if ((S.vol_flags & kVolNeeHomogeneous) && m.type == MH_MEDIUM_HOMOGENEOUS) {
             mei.t = fminf(remaining_dist, v.wsi_t);
@@ -911,17 +975,63 @@ MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, V &v, float remaining_di
     if (act_surf && is_medium_transition(S, v.wsi)) v.wmedium = target_medium(S, v.wsi, v.wray.d);
     return active ? kPhWalk : kPhPost;
 }
+template <class V, class Hk>
+MH_DEV uint32_t pv_walk_rest(const DScene &S, Pcg &rng, V &v, float remaining_dist, Hk &hk) {
+    MEI mei;
+    pv_walk_mei_init(mei);
+    if (v.wmedium != MH_INVALID) sample_interaction(S, v.wmedium, v.wray, rng.next_float(), mei);
+    return pv_walk_fin(S, v, remaining_dist, hk, mei);
+}
 
 MH_DEV float pv_remaining(const PvState &v) { return v.ds.dist * (1.f - kShadowEps) - v.total_dist; }
 
-// WALK: the head of one transmittance-loop trip
+// WALK: the head of one transmittance-loop trip, cut at its medium sample
+// (pending: v.wmedium, v.wray and the draw u)
 template <class V, class Hk>
-MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, V &v, Hk &hk) {
+MH_DEV bool pv_walk_pre(const DScene &S, Pcg &rng, V &v, Hk &hk, uint32_t &nph, float &u) {
     const float remaining_dist = pv_remaining(v);
     v.wray.maxt = remaining_dist;
-    if (!(remaining_dist > 0.f)) return kPhPost;
-    if (v.w_needs) return kPhTraceWS;
-    return pv_walk_rest(S, rng, v, remaining_dist, hk);
+    if (!(remaining_dist > 0.f)) { nph = kPhPost; return false; }
+    if (v.w_needs) { nph = kPhTraceWS; return false; }
+    if (v.wmedium != MH_INVALID) { u = rng.next_float(); return true; }
+    MEI mei;
+    pv_walk_mei_init(mei);
+    nph = pv_walk_fin(S, v, remaining_dist, hk, mei);
+    return false;
+}
+template <class V, class Hk>
+MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, V &v, Hk &hk) {
+    uint32_t nph = kPhPost;
+    float u = 0.f;
+    if (!pv_walk_pre(S, rng, v, hk, nph, u)) return nph;
+    MEI mei;
+    pv_walk_mei_init(mei);
+    sample_interaction(S, v.wmedium, v.wray, u, mei);
+    return pv_walk_fin(S, v, pv_remaining(v), hk, mei);
+}
+
+// HEAD and WALK lanes in one trip (vs_medium_step's form for prbvolpath)
+template <class V, class Hk>
+MH_DEV uint32_t pv_medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, V &v, Hk &hk, uint32_t ph) {
+    uint32_t nph = kPhFree;
+    float u = 0.f;
+    const bool head = ph == kPhHead;
+    const bool pend = head ? pv_head_pre(S, in, rng, v, hk, nph, u) : pv_walk_pre(S, rng, v, hk, nph, u);
+    if (!pend) return nph;
+    const uint32_t mh = v.med, mw = v.wmedium;
+    const RayT rh = v.ray, rw = v.wray;
+    RayT r;
+    r.o = v3(head ? rh.o.x : rw.o.x, head ? rh.o.y : rw.o.y, head ? rh.o.z : rw.o.z);
+    r.d = v3(head ? rh.d.x : rw.d.x, head ? rh.d.y : rw.d.y, head ? rh.d.z : rw.d.z);
+    r.maxt = head ? rh.maxt : rw.maxt;
+    MEI mei;
+    pv_walk_mei_init(mei);
+    sample_interaction(S, head ? mh : mw, r, u, mei);
+    if (head) {
+        v.mei = mei;
+        return pv_head_post(S, in, rng, v, hk);
+    }
+    return pv_walk_fin(S, v, pv_remaining(v), hk, mei);
 }
 
 // POST: the emitter sample's contribution (:256-270), phase sampling
@@ -1004,9 +1114,23 @@ MH_DEV uint32_t pv_trace(const DScene &S, const LdsBvh &B, const IntegratorParam
 // The integrators the phase scheduler runs: their state and phase steps.
 // Every machine is constructed once per thread from the kernel's backward
 // arguments (ignored by the primal machines) and offers the same calls.
+#ifndef MH_VS_MERGE
+#define MH_VS_MERGE 1
+#endif
+// prbvolpath's machines keep HEAD and WALK apart: merged (weight 4) the
+// config-4 forward measured 24.1 vs 24.1-24.4 ms and the backward 62.9 vs
+// 57.6 ms -- its walk steps alternate with their traces, so few walk lanes
+// meet a HEAD trip, while the hooks lengthen the divergent halves
+#ifndef MH_PV_MERGE
+#define MH_PV_MERGE 0
+#endif
+#ifndef MH_PVB_MERGE
+#define MH_PVB_MERGE 0
+#endif
 struct VolMachine {
     using State = VolState;
-    static constexpr bool kPrb = false, kWritesPos = true, kDeferEnd = false;
+    // kMergeMed: HEAD and WALK lanes share a trip (vs_medium_step)
+    static constexpr bool kPrb = false, kWritesPos = true, kDeferEnd = false, kMergeMed = MH_VS_MERGE != 0;
     MH_DEV VolMachine(const VsBwdArgs &, const LaneMap &, uint32_t) {}
     MH_DEV void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v, float, float) {
         volpath_init(S, in, rng, r, v);
@@ -1026,6 +1150,9 @@ struct VolMachine {
         return vs_surf(S, in, rng, v);
     }
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &wm) { return vs_walk(S, rng, v.ds, v.ns, wm); }
+    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &wm, uint32_t ph) {
+        return vs_medium_step(S, in, rng, v, wm, ph);
+    }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &, const IntegratorParams &in, Pcg &rng, State &v, uint32_t &) {
         return volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
     }
@@ -1038,7 +1165,7 @@ struct VolMachine {
 
 struct PvMachine {
     using State = PvState;
-    static constexpr bool kPrb = true, kWritesPos = true, kDeferEnd = false;
+    static constexpr bool kPrb = true, kWritesPos = true, kDeferEnd = false, kMergeMed = MH_PV_MERGE != 0;
     PvNoHook h;
     MH_DEV PvMachine(const VsBwdArgs &, const LaneMap &, uint32_t) {}
     MH_DEV void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &v, float, float) {
@@ -1059,6 +1186,9 @@ struct PvMachine {
         return pv_shade(S, in, rng, v, h);
     }
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, h); }
+    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph) {
+        return pv_medium_step(S, in, rng, v, h, ph);
+    }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
                          uint32_t &ns) {
         return pv_post(S, B, in, rng, v, h, ns);
@@ -1099,7 +1229,7 @@ struct PvBwdMachine {
     using State = PvBwdState;
     // the end-of-path log application is a phase of its own (kPhEnd): run
     // when a path ends, it would hold the wave for the few lanes that ended
-    static constexpr bool kPrb = true, kWritesPos = false, kDeferEnd = true;
+    static constexpr bool kPrb = true, kWritesPos = false, kDeferEnd = true, kMergeMed = MH_PVB_MERGE != 0;
     VsBwdArgs a;
     GradCtx g;
     LaneMap lm;
@@ -1223,6 +1353,9 @@ struct PvBwdMachine {
         return pv_shade(S, in, rng, v, *this);
     }
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, *this); }
+    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph) {
+        return pv_medium_step(S, in, rng, v, *this, ph);
+    }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
                          uint32_t &ns) {
         return pv_post(S, B, in, rng, v, *this, ns);
@@ -1255,6 +1388,11 @@ struct PvBwdMachine {
 #ifndef MH_VS_W
 #define MH_VS_W 8, 16, 12, 8, 8, 6, 12, 16   // free, head, trace, scatter, surf, walk, post (swept on config 4: 194 -> 214 Msamples/s), end
 #endif
+// the weight of the merged HEAD + WALK group (machines with kMergeMed; swept
+// on config 4: 16 -> 190, 6 -> 226, 4 -> 233, 3 -> 234 Msamples/s)
+#ifndef MH_VS_MERGE_W
+#define MH_VS_MERGE_W 4
+#endif
 // Tab: the shading tables (stage_tables) and the media records staged into
 // LDS: every trip reads the medium record (transform, bbox, majorant,
 // albedo) and the surface trips walk shape -> bsdf -> texture / emitter
@@ -1282,7 +1420,10 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         tab = vs_tab_bytes(S0) / 16u;
     }
     LdsBvh B = stage_bvh<InLds>(S0, lds + tab);
-    constexpr uint32_t W[kNGroups] = {MH_VS_W};
+    constexpr uint32_t W0[kNGroups] = {MH_VS_W};
+    uint32_t W[kNGroups];
+#pragma unroll
+    for (uint32_t k = 0; k < kNGroups; ++k) W[k] = (M::kMergeMed && k == kGHead) ? (uint32_t)MH_VS_MERGE_W : W0[k];
     constexpr uint32_t NG = M::kDeferEnd ? kNGroups : kGEnd;  // groups this machine uses
     const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
     uint32_t n_closest = 0, n_shadow = 0;
@@ -1324,7 +1465,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 #endif
     while (true) {
         uint32_t cnt[kNGroups];
-        const uint32_t g = ph_group(ph);
+        const uint32_t g = (M::kMergeMed && ph == kPhWalk) ? (uint32_t)kGHead : ph_group(ph);
 #pragma unroll
         for (uint32_t k = 0; k < NG; ++k) cnt[k] = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(g == k));
         if (drained && next >= end) cnt[kGFree] = 0;
@@ -1377,7 +1518,12 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             }
             next = std::min<uint64_t>(end, next + (uint64_t)__popcll(m));
         } else if (sel == kGHead) {
-            if (ph == kPhHead) { ph = mc.head(S, in, rng, v); ended = ph == kPhFree; }
+            if constexpr (M::kMergeMed) {
+                if (g == kGHead) { ph = mc.medium_step(S, in, rng, v, wm, ph); ended = ph == kPhFree; }
+            } else if (ph == kPhHead) {
+                ph = mc.head(S, in, rng, v);
+                ended = ph == kPhFree;
+            }
         } else if (sel == kGTrace) {
             if (g == kGTrace) {
                 ph = mc.template trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
