@@ -2701,6 +2701,9 @@ MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8]) {
     for (uint32_t j = 0; j < 8; ++j) {
         const uint32_t t = j * n + r, src = t >> 3, c = t & 7u;
         const uint32_t cc = __float_as_uint(sc[src * 9]);
+#ifdef MH_EXP_NO_SIGMA_ATOMIC  // diagnostic: cost of the grid-gradient scatter (wrong gradients)
+        if (sc[src * 9 + 1 + c] == 12345.f)
+#endif
         unsafeAtomicAdd(cb + (size_t)cc * 8 + c, sc[src * 9 + 1 + c]);
     }
     __builtin_amdgcn_wave_barrier();
