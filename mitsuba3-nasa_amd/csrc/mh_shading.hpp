@@ -2926,6 +2926,43 @@ constexpr uint32_t kLogBatchMain = 2, kLogBatchWalk = 8;
 
 // the logged gradient steps of one NEE walk (NeeLog entries (p, coef) at
 // e[j * stride]): sigma_t's adjoint coef * K at every step, K = dL . adj_emitted
+// Load-balanced wave loop over per-lane item counts (every lane of the wave
+// active): lane l owns cnt_l items, the wave takes 64 of them per step, and
+// f(owner, e, valid) runs on every lane with its item's owner lane and index
+// (valid false past the last item; f shuffles owner data first, then works
+// under `valid`).  The divergent per-lane loop it replaces ran max(cnt) steps
+// with the lanes that still had items.  scr: 64 words of the wave's LDS.
+MH_DEV uint32_t *flat_scratch() {
+    __shared__ uint32_t scr[kCornerWaves * 64];
+    return scr + (threadIdx.x >> 6) * 64u;
+}
+template <class F>
+MH_DEV void wave_flat(uint32_t cnt, uint32_t *scr, F &&f) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    if (total == 0) return;
+    scr[lane] = incl;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t base = 0; base < total; base += 64u) {
+        const uint32_t item = min(base + lane, total - 1u);
+        uint32_t o = 0;  // the first lane whose inclusive count exceeds item
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if (scr[o + step - 1] <= item) o += step;
+        const uint32_t start = o ? scr[o - 1] : 0u;
+        f(o, item - start, base + lane < total);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 MH_DEV void charge_walk_log(const DScene &S, const float4 *e, uint32_t stride, uint32_t n, uint32_t med, float K,
                             GradCtx &g) {
     for (uint32_t j0 = 0; j0 < n; j0 += kLogBatchWalk) {
@@ -3166,6 +3203,22 @@ MH_DEV V3 prbvol_sample(const DScene &S, const LdsBvh &B, const IntegratorParams
     return L;
 }
 
+// one logged L-dependent term (q0..q3: a MainLog entry) of a path whose
+// radiance is now L_total
+MH_DEV void pvp_log_entry(const DScene &S, float4 q0, float4 q1, float4 q2, float4 q3, V3 Ltot, GradCtx &g) {
+    const uint32_t bits = __float_as_uint(q0.w), idx = bits >> 2;
+    const V3 Lsuf = Ltot - v3(q1.x, q1.y, q1.z);  // prbvolpath.py: L - (contributions so far)
+    const V3 up = v3(q2.x * Lsuf.x, q2.y * Lsuf.y, q2.z * Lsuf.z);
+    if (bits & 1u) {
+        const V3 adj = (up * kInvPi) * q3.x;
+        tex_backward(S, idx, q1.w, q2.w, adj, g);
+    } else {
+        const float gs = (up.x * q3.x + up.y * q3.y) + up.z * q3.z;
+        sigma_t_backward(S, idx, v3(q0.x, q0.y, q0.z), gs, g);
+        if (bits & 2u) albedo_backward(idx, up * q3.w, g);
+    }
+}
+
 // the logged L-dependent terms of a path whose radiance is now L_total
 MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &g) {
     for (uint32_t j0 = 0; j0 < ml.n; j0 += kLogBatchMain) {
@@ -3180,18 +3233,7 @@ MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &
 #pragma unroll
         for (uint32_t b = 0; b < kLogBatchMain; ++b) {
             if (j0 + b >= ml.n) break;
-            const float4 q0 = q[b][0], q1 = q[b][1], q2 = q[b][2], q3 = q[b][3];
-            const uint32_t bits = __float_as_uint(q0.w), idx = bits >> 2;
-            const V3 Lsuf = Ltot - v3(q1.x, q1.y, q1.z);  // prbvolpath.py: L - (contributions so far)
-            const V3 up = v3(q2.x * Lsuf.x, q2.y * Lsuf.y, q2.z * Lsuf.z);
-            if (bits & 1u) {
-                const V3 adj = (up * kInvPi) * q3.x;
-                tex_backward(S, idx, q1.w, q2.w, adj, g);
-            } else {
-                const float gs = (up.x * q3.x + up.y * q3.y) + up.z * q3.z;
-                sigma_t_backward(S, idx, v3(q0.x, q0.y, q0.z), gs, g);
-                if (bits & 2u) albedo_backward(idx, up * q3.w, g);
-            }
+            pvp_log_entry(S, q[b][0], q[b][1], q[b][2], q[b][3], Ltot, g);
         }
     }
 }

@@ -1239,6 +1239,11 @@ struct PvBwdMachine {
     // entry-major layout (lanes writing their j-th entry as one 1-KiB run)
     // would scatter every 64-B entry over four lines here.
     uint32_t seed_value, t;
+    // charges deferred to the wave-wide, load-balanced loops that follow the
+    // trip's per-lane phase code (post_wave / end_wave): the NEE walk of a
+    // POST lane (its NeeLog steps, K, medium) and the MainLog of an ended path
+    uint32_t pend_walk = 0, pend_med = 0, pend_main = 0;
+    float pend_K = 0.f;
     MH_DEV PvBwdMachine(const VsBwdArgs &a_, const LaneMap &lm_, uint32_t sv)
         : a(a_), g(make_grad_ctx(a_.ga)), lm(lm_), seed_value(sv) {
         t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1298,9 +1303,10 @@ struct PvBwdMachine {
     }
     MH_DEV void nee_charge(const DScene &S, const LdsBvh &B, State &v, const Pcg &rng, V3 contrib, V3 emitted,
                            float mis, V3 wo_s, uint32_t &n_shadow) {
-        if (!v.nl_over) {  // the logged walk's steps: coef * (dL . adj_emitted)
-            const float K = (v.dL.x * contrib.x + v.dL.y * contrib.y) + v.dL.z * contrib.z;
-            charge_walk_log(S, a.nee_log + nee_base(), 1u, v.nl_n, v.nl_med, K, g);
+        if (!v.nl_over) {  // the logged walk's steps: coef * (dL . adj_emitted), in post_wave
+            pend_K = (v.dL.x * contrib.x + v.dL.y * contrib.y) + v.dL.z * contrib.z;
+            pend_walk = v.nl_n;
+            pend_med = v.nl_med;
         } else {  // the walk is replayed with the cloned sampler after the launch (k_pvb_replay_walks)
             const bool am = !v.e_surface;
             const V3 rp = am ? v.mei.p : v.si.p, rn = am ? v3(0.f, 0.f, 0.f) : v.si.n;
@@ -1363,9 +1369,8 @@ struct PvBwdMachine {
     // the path ended with radiance v.L: charge its logged terms, or replay
     MH_DEV void end(const DScene &S, const LdsBvh &B, const IntegratorParams &in, float *, uint64_t, uint32_t pid,
                     State &v, int, uint32_t &nc, uint32_t &ns) {
-        if (!v.ml_over) {
-            // MainLog's entry-major addressing with stride 1 and the lane's base: entry j at base + 4 j
-            pvp_log_apply(S, MainLog{a.main_log + main_base(), 1u, a.main_cap, 0u, v.ml_n, false}, v.L, g);
+        if (!v.ml_over) {  // charged by end_wave in this trip
+            pend_main = v.ml_n;
             return;
         }
         // the adjoint replayed after the launch (k_pvb_replay_paths)
@@ -1378,6 +1383,34 @@ struct PvBwdMachine {
         }
     }
     MH_DEV void finish() { flush_small_slots(g, a.ga); }
+    // ---- the wave-wide charge loops (every lane of the wave active)
+    MH_DEV uint64_t wave_t0() const { return (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); }
+    MH_DEV void post_wave(const DScene &S) {
+        const uint64_t t0 = wave_t0();
+        const uint32_t cnt = pend_walk, med = pend_med;
+        const float K = pend_K;
+        pend_walk = 0;
+        wave_flat(cnt, flat_scratch(), [&](uint32_t o, uint32_t e, bool valid) {
+            const float Ko = __shfl(K, (int)o);
+            const uint32_t mo = (uint32_t)__shfl((int)med, (int)o);
+            if (valid) {
+                const float4 q = a.nee_log[(t0 + o) * a.nee_cap + e];
+                sigma_t_backward(S, mo, v3(q.x, q.y, q.z), q.w * Ko, g);
+            }
+        });
+    }
+    MH_DEV void end_wave(const DScene &S, const State &v) {
+        const uint64_t t0 = wave_t0();
+        const uint32_t cnt = pend_main;
+        pend_main = 0;
+        wave_flat(cnt, flat_scratch(), [&](uint32_t o, uint32_t e, bool valid) {
+            const V3 L = v3(__shfl(v.L.x, (int)o), __shfl(v.L.y, (int)o), __shfl(v.L.z, (int)o));
+            if (valid) {  // MainLog entry e of thread t0 + o: float4 (t * main_cap + e) * 4
+                const float4 *q = a.main_log + ((t0 + o) * a.main_cap + e) * 4u;
+                pvp_log_entry(S, q[0], q[1], q[2], q[3], L, g);
+            }
+        });
+    }
 };
 
 #ifndef MH_VS_WAVES
@@ -1537,11 +1570,13 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             if (ph == kPhWalk) ph = mc.walk(S, rng, v, wm);
         } else if (sel == kGPost) {
             if (ph == kPhPost) { ph = mc.post(S, B, in, rng, v, n_shadow); ended = ph == kPhFree; }
+            if constexpr (M::kDeferEnd) mc.post_wave(S);
         } else if (M::kDeferEnd) {
             if (ph == kPhEnd) {
                 mc.end(S, B, in, out, plane, pid, v, alpha, n_closest, n_shadow);
                 ph = kPhFree;
             }
+            if constexpr (M::kDeferEnd) mc.end_wave(S, v);
         }
         if (ended) {
             if (M::kDeferEnd) ph = kPhEnd;
