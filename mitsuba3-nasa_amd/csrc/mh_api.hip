@@ -110,6 +110,7 @@ struct mh_scene {
     DevBuf pvp_main;   // prbvolpath backward: per-thread path logs of the single pass (MainLog)
     DevBuf pvp_ovf;    // prbvolpath backward on the scheduler: overflow lists + their counters
     DevBuf grid_corner;  // prbvolpath backward: per-cell corner blocks of the grid sigma_t slots
+    DevBuf fx_word;      // its deterministic pre-pass: the largest |item| (float bits)
     // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
     // buffers of the sharded entry points (slab W image, staged peer sums,
     // slab gradients)
@@ -478,7 +479,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner,
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word,
                       &s->shard_w, &s->shard_tmp, &s->shard_g})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -1067,6 +1068,7 @@ struct Slots {
     uint32_t n_rgb = 0, n_bmp = 0, n_medium_params = 0, bmp_tex = 0;
     uint32_t grid_res[kMaxParams][3] = {};  // large sigma_t slots: the grid's resolution (x, y, z)
     std::vector<float *> corner;            // their corner blocks (upload_slots, corners = true)
+    bool fx = false;                        // the blocks hold int64 fixed point (deterministic)
     std::vector<uint8_t> meta;  // host image of the meta block (uploaded by upload_slots when it changed)
 };
 
@@ -1131,8 +1133,10 @@ static int build_slots(const mh_scene *s, uint32_t n_params, const uint32_t *par
 // corners: the grid sigma_t slots scatter into per-cell corner blocks
 // (s->grid_corner, zeroed; launch_corner_gather after the backward) unless
 // MH_GRID_CORNER=0, the block would exceed 16 GiB or cannot be allocated
+// fx: MH_FLAG_DETERMINISTIC -- int64 corner blocks (twice the bytes), which
+// are then required (no direct-atomic fallback)
 static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vector<float *> &bufs, GradArgs &ga,
-                               bool corners = false) {
+                               bool corners = false, bool fx = false) {
     size_t total = 0;
     std::vector<size_t> off(kMaxParams, 0);
     for (int k = 0; k < kMaxParams; ++k) { off[k] = total; total += (P.counts[k] + 3) / 4 * 4; }
@@ -1144,7 +1148,8 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     for (int k = 0; k < kMaxParams; ++k) bufs[k] = P.counts[k] ? s->tmp_c.as<float>() + off[k] : nullptr;
     P.corner.assign(kMaxParams, nullptr);
     const char *ec = getenv("MH_GRID_CORNER");
-    if (corners && !(ec && !strcmp(ec, "0"))) {
+    P.fx = false;
+    if (corners && (fx || !(ec && !strcmp(ec, "0")))) {
         std::vector<size_t> coff(kMaxParams, 0);
         std::vector<bool> use(kMaxParams, false);
         size_t cfl = 0;
@@ -1154,11 +1159,14 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
             coff[k] = cfl;
             if (use[k]) cfl += corner_floats(r);
         }
-        if (cfl && cfl * 4 <= (16ull << 30) && s->grid_corner.alloc(cfl * 4) == hipSuccess) {
-            e = hipMemsetAsync(s->grid_corner.ptr, 0, cfl * 4, st);
+        const size_t eb = fx ? 8 : 4;  // bytes per corner value
+        if (cfl && cfl * eb <= (32ull << 30) && (fx || cfl * 4 <= (16ull << 30)) &&
+            s->grid_corner.alloc(cfl * eb) == hipSuccess) {
+            e = hipMemsetAsync(s->grid_corner.ptr, 0, cfl * eb, st);
             if (e != hipSuccess) return e;
             for (int k = 0; k < kMaxParams; ++k)
-                if (use[k]) P.corner[k] = s->grid_corner.as<float>() + coff[k];
+                if (use[k]) P.corner[k] = reinterpret_cast<float *>(s->grid_corner.as<uint8_t>() + coff[k] * eb);
+            P.fx = fx;
         } else {
             (void)hipGetLastError();
         }
@@ -1229,7 +1237,17 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (rc_slots) return rc_slots;
     std::vector<float *> bufs;
     GradArgs ga;
-    MH_HIP(upload_slots(s, P, st, bufs, ga, vol));
+    // MH_FLAG_DETERMINISTIC with a grid sigma_t parameter: the grid gradient in
+    // int64 fixed point (two passes, see the prbvolpath branch below)
+    bool any_grid = false;
+    for (int k = 0; k < kMaxParams; ++k) any_grid = any_grid || P.grid_res[k][0] != 0;
+    const bool fx = vol && any_grid && deterministic(flags);
+    MH_HIP(upload_slots(s, P, st, bufs, ga, vol, fx));
+    if (fx)
+        for (int k = 0; k < kMaxParams; ++k)
+            if (P.grid_res[k][0] && !P.corner[k])
+                return set_error(MH_ERR_OUT_OF_MEMORY,
+                                 "render_backward(): the deterministic grid gradient's corner block could not be allocated");
     const std::vector<size_t> &counts = P.counts;
     const std::vector<uint32_t> &slot_of_param = P.slot_of_param;
     const uint32_t n_rgb = P.n_rgb, n_bmp = P.n_bmp, bmp_tex = P.bmp_tex;
@@ -1302,6 +1320,26 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     const bool wavefront = ((fused && in->max_depth <= 64 && !mega) || bmp_wf);
     size_t wf_ctr_words = 0, wf_chunks = 0;
     uint32_t *pvb_lost = nullptr;  // prbvolpath on the scheduler: overflow entries that found their list full
+    double fx_inv = 1.0;           // deterministic grid gradient: 2^-S of the fixed point
+    // between the two passes of the deterministic grid gradient: the scale
+    // from pass 1's largest |item|; pass 1's rgb-slot adds and counters go
+    auto fx_between = [&](GradArgs &gp) -> hipError_t {
+        uint32_t mb = 0;
+        hipError_t e = hipMemcpyAsync(&mb, s->fx_word.ptr, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        float mx;
+        memcpy(&mx, &mb, 4);
+        int ex = 0;
+        if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &ex);  // mx < 2^ex
+        fx_inv = std::ldexp(1.0, ex - 31);
+        gp.fx_scale = std::ldexp(1.0, 31 - ex);
+        size_t total = 0;
+        for (int k = 0; k < kMaxParams; ++k) total += (counts[k] + 3) / 4 * 4;
+        e = hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st);
+        if (e == hipSuccess) e = hipMemsetAsync(s->counters.ptr, 0, 256, st);
+        return e;
+    };
     MH_HIP(hipEventRecord(s->ev0, st));
     if (wavefront) {
         int cus = 256;
@@ -1395,11 +1433,22 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         const uint32_t ovf_cap = (uint32_t)std::min<uint64_t>(n, 1ull << 26);
         sched = sched && main_cap && nee_ok &&
                 s->pvp_ovf.alloc((size_t)ovf_cap * (2 + kPvbWalkRec) * 16 + 256) == hipSuccess;
+        // MH_FLAG_DETERMINISTIC with a grid: pass 1 finds the largest |item| of
+        // the grid scatter (nothing is accumulated that survives), pass 2 adds
+        // round(item * 2^S) as int64, S = 31 - ceil(log2 max): |item| <= 2^31, so
+        // up to 2^31 items sum without overflow, and the sums are exact
+        if (fx) MH_HIP(s->fx_word.alloc(256));
+        for (uint32_t pass = fx ? 1u : 0u; pass <= (fx ? 2u : 0u); ++pass) {
+        GradArgs gp = ga;
+        gp.fx_mode = pass;
+        gp.fx_max = fx ? s->fx_word.as<uint32_t>() : nullptr;
+        if (pass == 1) MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 4, st));
+        if (pass == 2) MH_HIP(fx_between(gp));
         if (sched) {
             VsBwdArgs bw;
             bw.grad_in = g_in;
             bw.coalesce = L.spp_pp >= 4;
-            bw.ga = ga;
+            bw.ga = gp;
             bw.main_log = s->pvp_main.as<float4>();
             bw.nee_log = s->pvp_log.as<float4>();
             bw.main_cap = main_cap;
@@ -1424,17 +1473,35 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             }
         } else {
             MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
-                                       g_in, w, ga, fused, s->counters.as<unsigned long long>(), st,
+                                       g_in, w, gp, fused, s->counters.as<unsigned long long>(), st,
                                        nee_ok ? s->pvp_log.as<float4>() : nullptr, cap, blocks,
                                        s->counters.as<unsigned long long>() + kCtrPvpHead,
                                        main_cap ? s->pvp_main.as<float4>() : nullptr, main_cap));
+        }
+        }  // passes
+    } else if (fx) {  // prbvolpath replaying its NEE walks (MH_PVP_NEE_LOG=0), deterministic grid
+        MH_HIP(s->fx_word.alloc(256));
+        MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 4, st));
+        GradArgs gp = ga;
+        gp.fx_max = s->fx_word.as<uint32_t>();
+        for (uint32_t pass = 1; pass <= 2; ++pass) {
+            gp.fx_mode = pass;
+            if (pass == 2) MH_HIP(fx_between(gp));
+            MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
+                                       g_in, w, gp, fused, s->counters.as<unsigned long long>(), st));
         }
     } else {
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
     }
-    for (int k = 0; k < kMaxParams; ++k)
-        if (P.corner[k]) MH_HIP(launch_corner_gather(P.corner[k], bufs[k], P.grid_res[k], st));
+    for (int k = 0; k < kMaxParams; ++k) {
+        if (!P.corner[k]) continue;
+        if (P.fx)
+            MH_HIP(launch_corner_gather_fx(reinterpret_cast<const long long *>(P.corner[k]), bufs[k], P.grid_res[k],
+                                           fx_inv, st));
+        else
+            MH_HIP(launch_corner_gather(P.corner[k], bufs[k], P.grid_res[k], st));
+    }
     MH_HIP(hipEventRecord(s->ev1, st));
     if (wants_reduce(flags)) {  // the slot buffers are one block of s->tmp_c (upload_slots)
         size_t total = 0;

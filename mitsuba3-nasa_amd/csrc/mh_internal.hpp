@@ -36,6 +36,11 @@ struct GradArgs {
     uint32_t lds_offset = 0;     // byte offset of the accumulator in dynamic LDS (set by the launcher)
     float *const *corner = nullptr;  // device: slot -> per-cell corner block of a grid sigma_t slot or nullptr
                                      // (prbvolpath; gathered into bufs[slot] by launch_corner_gather)
+    // MH_FLAG_DETERMINISTIC on the corner blocks: 1 = pre-pass (the largest |item| into fx_max, no
+    // scatter), 2 = int64 fixed-point adds of round(item * fx_scale) (order-independent sums)
+    uint32_t fx_mode = 0;
+    uint32_t *fx_max = nullptr;
+    double fx_scale = 0.0;
 };
 
 // ---- BVH builder (host, binned SAH) --------------------------------------
@@ -137,6 +142,9 @@ hipError_t launch_accumulate(float *dst, const float *src, uint64_t n, hipStream
 // grid sigma_t gradient: per-cell corner block (GradArgs::corner) -> (z, y, x) gradient (+=)
 uint64_t corner_floats(const uint32_t res[3]);
 hipError_t launch_corner_gather(const float *corner, float *grad, const uint32_t res[3], hipStream_t st);
+// the int64 fixed-point form (fx_mode 2): grad += (float)(exact integer sum / fx_scale)
+hipError_t launch_corner_gather_fx(const long long *corner, float *grad, const uint32_t res[3], double inv_scale,
+                                   hipStream_t st);
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,

@@ -952,6 +952,44 @@ __global__ void k_corner_gather(const float *__restrict__ cb, float *__restrict_
     }
 }
 
+// the fixed-point form: exact int64 sums, one conversion per texel
+__global__ void k_corner_gather_fx(const long long *__restrict__ cb, float *__restrict__ grad, int32_t rx, int32_t ry,
+                                   int32_t rz, double inv_scale) {
+    const uint64_t n = (uint64_t)rx * ry * rz;
+    const uint64_t sy = (uint64_t)rx + 1, sz = sy * (uint64_t)(ry + 1);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t x = (int32_t)(i % rx), y = (int32_t)((i / rx) % ry), z = (int32_t)(i / ((uint64_t)rx * ry));
+        long long s = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int32_t b[3] = {c & 1, (c >> 1) & 1, c >> 2}, v[3] = {x, y, z}, r[3] = {rx, ry, rz};
+            int32_t cell[3][2], cnt[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                cell[a][0] = v[a] - b[a] + 1;
+                cnt[a] = 1;
+                if (b[a] == 0 && v[a] == 0) cell[a][cnt[a]++] = 0;
+                else if (b[a] == 1 && v[a] == r[a] - 1) cell[a][cnt[a]++] = r[a];
+            }
+            for (int kz = 0; kz < cnt[2]; ++kz)
+                for (int ky = 0; ky < cnt[1]; ++ky)
+                    for (int kx = 0; kx < cnt[0]; ++kx)
+                        s += cb[((uint64_t)cell[2][kz] * sz + (uint64_t)cell[1][ky] * sy + (uint64_t)cell[0][kx]) * 8 + c];
+        }
+        grad[i] += (float)((double)s * inv_scale);
+    }
+}
+
+hipError_t launch_corner_gather_fx(const long long *corner, float *grad, const uint32_t res[3], double inv_scale,
+                                   hipStream_t st) {
+    const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (uint32_t)std::min<uint64_t>(blocks_for(n, 256), 8192);
+    hipLaunchKernelGGL(k_corner_gather_fx, dim3(g), dim3(256), 0, st, corner, grad, (int32_t)res[0], (int32_t)res[1],
+                       (int32_t)res[2], inv_scale);
+    return hipGetLastError();
+}
+
 uint64_t corner_floats(const uint32_t res[3]) {
     return (uint64_t)(res[0] + 1) * (res[1] + 1) * (res[2] + 1) * 8u;
 }

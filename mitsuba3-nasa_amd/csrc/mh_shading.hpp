@@ -1470,6 +1470,9 @@ struct GradCtx {
     const int32_t *sigma_slot;    // prbvolpath: medium -> sigma_t slot or -1 (nullptr: none)
     const int32_t *albedo_slot;   // prbvolpath: medium -> albedo slot or -1 (nullptr: none)
     float *const *corner;         // prbvolpath: slot -> per-cell corner block of a grid (nullptr: atomics into bufs)
+    uint32_t fx_mode;             // GradArgs::fx_mode (deterministic grid gradient)
+    uint32_t *fx_max;
+    double fx_scale;
     int32_t lds_slot;             // bitmap slot whose texels accumulate in LDS (-1: none)
     float *lds_acc;               // that slot's workgroup accumulator
     uint32_t lds_floats;          // its size (floats; checked under MH_DEBUG)
@@ -2684,8 +2687,18 @@ MH_DEV V3 volpath_sample(const DScene &S, const LdsBvh &B, const IntegratorParam
 // issue the 8 x n adds transposed -- instruction j takes items j*n .. j*n+n-1
 // of the (lane rank, tap) order, the taps of ~n/8 cells, 32 B each.
 // Any exec mask (the call sites are divergent loops); kernels of <= 4 waves.
+// MH_FLAG_DETERMINISTIC (GradCtx::fx_mode): a pre-pass records the largest
+// |item| only; the real pass adds round(item * 2^S) as int64 (the block then
+// holds long longs), exact integer sums that no add order changes.
 constexpr int kCornerWaves = 4;
-MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8]) {
+MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8], const GradCtx &g) {
+    if (g.fx_mode == 1) {
+        float mx = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) mx = fmaxf(mx, fabsf(v[c]));
+        if (mx > 0.f) atomicMax(g.fx_max, __float_as_uint(mx));  // non-negative floats order as their bits
+        return;
+    }
     __shared__ float stage[kCornerWaves * 64 * 9];
     float *sc = stage + (threadIdx.x >> 6) * (64 * 9);
     const uint64_t m = __ballot(1);
@@ -2704,7 +2717,12 @@ MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8]) {
 #ifdef MH_EXP_NO_SIGMA_ATOMIC  // diagnostic: cost of the grid-gradient scatter (wrong gradients)
         if (sc[src * 9 + 1 + c] == 12345.f)
 #endif
-        unsafeAtomicAdd(cb + (size_t)cc * 8 + c, sc[src * 9 + 1 + c]);
+        if (g.fx_mode == 2) {
+            const long long q = __double2ll_rn((double)sc[src * 9 + 1 + c] * g.fx_scale);
+            atomicAdd(reinterpret_cast<unsigned long long *>(cb) + (size_t)cc * 8 + c, (unsigned long long)q);
+        } else {
+            unsafeAtomicAdd(cb + (size_t)cc * 8 + c, sc[src * 9 + 1 + c]);
+        }
     }
     __builtin_amdgcn_wave_barrier();
 }
@@ -2743,7 +2761,7 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
             }
             const uint32_t cx = (uint32_t)(min(max(ix, -1), rx - 1) + 1), cy = (uint32_t)(min(max(iy, -1), ry - 1) + 1),
                            cz = (uint32_t)(min(max(iz, -1), rz - 1) + 1);
-            corner_scatter(cb, (cz * (uint32_t)(ry + 1) + cy) * (uint32_t)(rx + 1) + cx, v);
+            corner_scatter(cb, (cz * (uint32_t)(ry + 1) + cy) * (uint32_t)(rx + 1) + cx, v, g);
             return;
         }
     }
@@ -3263,6 +3281,9 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.sigma_slot = ga.sigma_slot;
     g.albedo_slot = ga.albedo_slot;
     g.corner = ga.corner;
+    g.fx_mode = ga.fx_mode;
+    g.fx_max = ga.fx_max;
+    g.fx_scale = ga.fx_scale;
     g.lds_slot = -1;
     g.lds_acc = nullptr;
     g.lds_floats = 0;

@@ -447,6 +447,39 @@ def test_prbvolpath_grid_corner_scatter(shape, monkeypatch):
     np.testing.assert_allclose(out["1"], ref, rtol=2e-3, atol=1e-7 + 2e-4 * scale)
 
 
+@pytest.mark.parametrize("mode", ["sched", "sched_off", "replay"])
+def test_prbvolpath_deterministic_grid_gradient(mode, monkeypatch):
+    """MH_FLAG_DETERMINISTIC with a grid sigma_t parameter: the corner blocks
+    hold int64 fixed point (a pre-pass finds the largest item, the real pass
+    adds round(item * 2^S)), so repeated runs give the same bits whatever the
+    order of the adds; equal to the float-atomic gradient up to float order
+    and to the oracle at 2e-3.  On the scheduler (default), the per-sample
+    kernel (MH_PVP_SCHED=0) and the NEE-replaying kernel (MH_PVP_NEE_LOG=0)."""
+    if mode == "sched_off":
+        monkeypatch.setenv("MH_PVP_SCHED", "0")
+    elif mode == "replay":
+        monkeypatch.setenv("MH_PVP_NEE_LOG", "0")
+    mi = _mi()
+    import torch
+    scene = _pvp_scene(mi, 24, 20, 8)
+    integ = scene.integrator()
+    params = mi.traverse(scene)
+    key = "medium1.sigma_t.data"
+    H, W = scene.height, scene.width
+    gi = torch.from_numpy(np.random.default_rng(6).standard_normal((H, W, 3)).astype(np.float32)).cuda()
+    runs = [mi.render_backward(scene, params, gi, [key], integ, seed=3, spp=8, deterministic=True)[0]
+            for _ in range(3)]
+    for r in runs[1:]:
+        assert torch.equal(runs[0], r)
+    a = runs[0].cpu().numpy()
+    b = mi.render_backward(scene, params, gi, [key], integ, seed=3, spp=8)[0].cpu().numpy()
+    ref = O.render_backward(scene, integ, 3, 8, gi.cpu().numpy(), [params.param_id(key)], [tuple(params[key].shape)])[0]
+    scale = np.abs(ref).max()
+    assert scale > 0
+    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6 * scale)
+    np.testing.assert_allclose(a, ref, rtol=2e-3, atol=1e-7 + 2e-4 * scale)
+
+
 @pytest.mark.parametrize("alpha", [False, True])
 def test_prbvolpath_film_modes_agree(alpha):
     """mh_render of prbvolpath: the phase scheduler (default) against the
