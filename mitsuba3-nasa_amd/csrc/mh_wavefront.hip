@@ -1656,7 +1656,15 @@ hipError_t launch_wavefront_fwd(const DScene &S, const IntegratorParams &in, con
 // whose camera vertices all land on the same texels.  InLds: a
 // persistent grid accumulating into a per-workgroup LDS copy of the texture
 // (grouped ds_add_f32), flushed once with one global atomic per non-zero
-// texel; otherwise global atomics.
+// texel; otherwise global atomics, issued transposed: the wave's records
+// stage (4 tap bases, 12 values) in LDS and the wave adds items (record,
+// tap, channel) 64 at a time, so an instruction carries the two 24-B runs
+// of ~5 records instead of 64 lanes in 64 rows (the float-atomic shape
+// rule of corner_scatter; 1024^2 x 3 bitmap: 21.7 ms per scatter before).
+MH_DEV float *bmp_stage() {
+    __shared__ float st[4 * 64 * 16];
+    return st + (threadIdx.x >> 6) * (64 * 16);
+}
 template <bool InLds>
 __global__ void __launch_bounds__(256)
 k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restrict__ grad, uint32_t n_floats) {
@@ -1701,6 +1709,39 @@ k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restr
             float w4[4] = {1.f, 0.f, 0.f, 0.f};
             if (tp.n != 1) {
                 w4[0] = tp.w0y * tp.w0x; w4[1] = tp.w0y * tp.w1x; w4[2] = tp.w1y * tp.w0x; w4[3] = tp.w1y * tp.w1x;
+            }
+            if constexpr (!InLds) {
+                const uint64_t onm = __ballot(on);
+                const uint32_t n_on = (uint32_t)__popcll(onm);
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(onm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)onm, 0u));
+                const uint32_t nc = tx.channels == 3 ? 3u : 1u, per = 4u * nc;
+                float *st = bmp_stage();
+                if (on) {
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k)
+                        st[r * 16 + k] = __uint_as_float(k < tp.n ? (uint32_t)(tp.idx[k] - tx.data_offset) : 0xffffffffu);
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; ++k) {
+                        if (nc == 3) {
+                            st[r * 16 + 4 + k * 3 + 0] = adj.x * w4[k];
+                            st[r * 16 + 4 + k * 3 + 1] = adj.y * w4[k];
+                            st[r * 16 + 4 + k * 3 + 2] = adj.z * w4[k];
+                        } else {
+                            st[r * 16 + 4 + k * 3] = (adj.x + adj.y + adj.z) * w4[k];
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t total = n_on * per;
+                for (uint32_t t = lane; t < total; t += 64u) {
+                    const uint32_t src = t / per, rem = t - src * per, k = rem / nc, c = rem - k * nc;
+                    const uint32_t base = __float_as_uint(st[src * 16 + k]);
+                    if (base != 0xffffffffu) atomicAdd(grad + base + c, st[src * 16 + 4 + k * 3 + c]);
+                }
+                __builtin_amdgcn_wave_barrier();
+                continue;
             }
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {

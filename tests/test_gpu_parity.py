@@ -546,13 +546,16 @@ def test_prb_backward_bitmap_parity(spp, mode):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max())
 
 
+@pytest.mark.parametrize("lds", ["1", "0"])
 @pytest.mark.parametrize("channels,max_depth", [(3, 3), (1, 6), (3, 12)])
-def test_prb_bitmap_wavefront_chunks(channels, max_depth, monkeypatch):
+def test_prb_bitmap_wavefront_chunks(channels, max_depth, lds, monkeypatch):
     """Bitmap on the fused wavefront across several 4096-path chunks (the
     vertex records and L_total are per chunk), with two rgb slots beside it
     (the 4-slot kernel instance), a one-channel bitmap (adjoint summed over
-    r, g, b) and shallow / deep max_depth (record count max_depth - 1)."""
+    r, g, b) and shallow / deep max_depth (record count max_depth - 1); the
+    texel scatter in LDS and as transposed global atomics (MH_PRB_LDS_TEX=0)."""
     monkeypatch.setenv("MH_WF_CHUNK", "4096")
+    monkeypatch.setenv("MH_PRB_LDS_TEX", lds)
     mi = _mi()
     import torch
     from mitsuba_hip import _abi as A

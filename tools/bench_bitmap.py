@@ -15,11 +15,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--mode", default="auto")
+    ap.add_argument("--tex-res", type=int, default=64, help="bitmap resolution (> 73: the global-atomic scatter)")
     a = ap.parse_args()
     import torch
     import mitsuba_hip as mi
     mi.set_variant("hip_ad_rgb")
-    sb = mi.load_dict(mi.cornell_box_bitmap(64, 512, 512, 64))
+    sb = mi.load_dict(mi.cornell_box_bitmap(a.tex_res, 512, 512, 64))
     pb = mi.traverse(sb)
     prb = mi.load_dict({"type": "prb", "max_depth": 8})
     gi = torch.full((512, 512, 3), 1.0 / (512 * 512 * 3), dtype=torch.float32, device="cuda")
@@ -32,7 +33,7 @@ def main():
         f()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.reps
-    print(json.dumps({"config": f"3(b) ({a.mode})", "ms": round(dt * 1e3, 2),
+    print(json.dumps({"config": f"3(b) ({a.mode}, {a.tex_res}^2 x 3 bitmap)", "ms": round(dt * 1e3, 2),
                       "Msamples_s": round(512 * 512 * 64 / dt / 1e6, 1)}))
 
 
