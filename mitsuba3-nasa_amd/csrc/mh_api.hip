@@ -1310,13 +1310,26 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     const bool replay = (flags & MH_FLAG_PRB_REPLAY) || (env_replay && !strcmp(env_replay, "1"));
     const bool mega = (flags & MH_FLAG_MEGAKERNEL) || (env_mode && !strcmp(env_mode, "mega"));
     const bool fused = !vol && n_bmp == 0 && !replay;
-    // one bitmap parameter: the fused PRB wavefront logs its vertices and a
-    // scatter pass charges the texels (WfBmp, mh_wavefront.hip) -- packet-engine
-    // scenes, max_depth <= 32 (MH_PRB_BMP_WF=0: the replay megakernel)
+    // bitmap parameters: the fused PRB wavefront logs their vertices (with the
+    // bitmap's index) and a scatter pass charges the texels (WfBmp,
+    // mh_wavefront.hip) -- packet-engine scenes, max_depth <= 32
+    // (MH_PRB_BMP_WF=0: the replay megakernel)
     const char *env_bwf = getenv("MH_PRB_BMP_WF");
     const char *env_pvl = getenv("MH_PVP_NEE_LOG");  // 0: prbvolpath replays its NEE walks (no log)
-    const bool bmp_wf = !vol && n_bmp == 1 && !replay && !mega && wf_fused(s->S) && in->max_depth >= 1 &&
-                        in->max_depth <= 32 && !(env_bwf && !strcmp(env_bwf, "0"));
+    // (several bitmaps: all with the same channel count, as the scatter's
+    // transposed issue assumes)
+    bool bmp_same_ch = true;
+    {
+        uint32_t ch = 0;
+        for (uint32_t t = 0; t < (uint32_t)P.slot_of_tex.size(); ++t)
+            if (P.slot_of_tex[t] >= kMaxRgbParams) {
+                const uint32_t c = s->h_textures[t].channels;
+                bmp_same_ch = bmp_same_ch && (ch == 0 || ch == c);
+                ch = c;
+            }
+    }
+    const bool bmp_wf = !vol && n_bmp >= 1 && bmp_same_ch && !replay && !mega && wf_fused(s->S) &&
+                        in->max_depth >= 1 && in->max_depth <= 32 && !(env_bwf && !strcmp(env_bwf, "0"));
     const bool wavefront = ((fused && in->max_depth <= 64 && !mega) || bmp_wf);
     size_t wf_ctr_words = 0, wf_chunks = 0;
     uint32_t *pvb_lost = nullptr;  // prbvolpath on the scheduler: overflow entries that found their list full
@@ -1367,9 +1380,17 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             bmp.ws = s->wf_ws_bmp.ptr;
             bmp.n_depth = n_depth;
             bmp.slot = kMaxRgbParams;
-            bmp.tex = bmp_tex;
+            // every bitmap slot kMaxRgbParams + b: its texture and its offset in
+            // the bitmap slots' contiguous block of s->tmp_c (upload_slots)
+            size_t boff = 0;
+            for (int b = 0; b < kMaxBitmapParams; ++b) {
+                bmp.off[b] = (uint32_t)boff;
+                boff += (counts[kMaxRgbParams + b] + 3) / 4 * 4;
+            }
+            for (uint32_t t = 0; t < (uint32_t)P.slot_of_tex.size(); ++t)
+                if (P.slot_of_tex[t] >= kMaxRgbParams) bmp.tex[P.slot_of_tex[t] - kMaxRgbParams] = t;
             bmp.grad = bufs[kMaxRgbParams];
-            bmp.n_floats = (uint32_t)counts[kMaxRgbParams];
+            bmp.n_floats = (uint32_t)boff;
             bmp.lds_max = (env_lds && !strcmp(env_lds, "0")) ? 0u : (uint32_t)std::min(max_wg, 64 << 10);
             const size_t per_wg = std::max<size_t>((size_t)bmp.n_floats * 4, 1);
             const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (size_t)per_cu_lds / per_wg));

@@ -100,10 +100,11 @@ bool wf_fused(const DScene &S);  // launch_wavefront runs the fused bounce kerne
 struct WfBitmapArgs {
     void *ws = nullptr;      // wf_bmp_workspace_bytes(cap, n_depth)
     uint32_t n_depth = 0;    // vertex records per path: max_depth - 1
-    int32_t slot = -1;       // the bitmap's gradient slot (its slot_of_tex value)
-    uint32_t tex = 0;        // its texture index
-    float *grad = nullptr;   // its gradient buffer (device)
-    uint32_t n_floats = 0;   // texels x channels
+    int32_t slot = -1;       // the first bitmap gradient slot (kMaxRgbParams; -1: none)
+    uint32_t tex[kMaxBitmapParams] = {};  // texture of bitmap slot kMaxRgbParams + b
+    uint32_t off[kMaxBitmapParams] = {};  // its gradient's float offset in grad
+    float *grad = nullptr;   // the bitmap slots' block of gradient buffers (device)
+    uint32_t n_floats = 0;   // that block's floats (texels x channels, padded per slot)
     uint32_t lds_max = 0;    // per-workgroup LDS accumulation when n_floats * 4 <= lds_max
     uint32_t blocks = 0;     // scatter workgroups (persistent grid)
 };
@@ -114,7 +115,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                 void *ws, void *ws_prb, uint64_t cap, uint32_t *ctr, uint32_t n_bounces,
                                 uint32_t grid, float *partial, hipStream_t st,
                                 hipEvent_t *span = nullptr,               // span: 2 events around the bounce launches
-                                const WfBitmapArgs *bmp = nullptr,       // one bitmap parameter (or none)
+                                const WfBitmapArgs *bmp = nullptr,       // the bitmap parameters (or none)
                                 void *ws_det = nullptr);                 // deterministic rgb gradients (or none)
 size_t wf_det_workspace_bytes(uint64_t cap);
 // render_forward of `prb` on the fused wavefront (packet-engine scenes): the

@@ -1300,8 +1300,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             if (smooth) rho = tex_eval(S, S.bsdf_tex[b], si.uvx, si.uvy);
             const int32_t slot = smooth ? q.slot_of_tex[S.bsdf_tex[b]] : -1;
             if (Bm) {
-                bvtx = slot >= 0 && slot == bm.slot && depth < bm.n_depth;
-                depth_v = depth;
+                // every bitmap slot (kMaxRgbParams + b) records; b rides in depth_v's bits 8+
+                bvtx = slot >= (int32_t)kMaxRgbParams && depth < bm.n_depth;
+                depth_v = depth | (bvtx ? (uint32_t)(slot - (int32_t)kMaxRgbParams) << 8 : 0u);
                 b_uvx = si.uvx;
                 b_uvy = si.uvy;
             }
@@ -1406,10 +1407,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             Lrun = (Lrun + Le_b) + (unocc ? Lr_pot : v3(0, 0, 0));
             const V3 D = unocc ? D_pot : v3(0, 0, 0);
             if (bvtx && (nonzero(q_ind) || nonzero(D))) {
-                bm.r(depth_v, 0)[pid] = make_float4(Lrun.x, Lrun.y, Lrun.z, b_uvx);
-                bm.r(depth_v, 1)[pid] = make_float4(q_ind.x, q_ind.y, q_ind.z, b_uvy);
-                bm.r(depth_v, 2)[pid] = make_float4(D.x, D.y, D.z, 0.f);
-                vmask |= 1u << depth_v;
+                const uint32_t dv = depth_v & 0xffu;
+                bm.r(dv, 0)[pid] = make_float4(Lrun.x, Lrun.y, Lrun.z, b_uvx);
+                bm.r(dv, 1)[pid] = make_float4(q_ind.x, q_ind.y, q_ind.z, b_uvy);
+                bm.r(dv, 2)[pid] = make_float4(D.x, D.y, D.z, __uint_as_float(depth_v >> 8));
+                vmask |= 1u << dv;
             }
             if (alive) {
                 w.lx[nxt][slot_n] = Lrun.x; w.ly[nxt][slot_n] = Lrun.y; w.lz[nxt][slot_n] = Lrun.z;
@@ -1665,16 +1667,21 @@ MH_DEV float *bmp_stage() {
     __shared__ float st[4 * 64 * 16];
     return st + (threadIdx.x >> 6) * (64 * 16);
 }
+// the bitmap parameters of a scatter: record b (its r2.w) is texture tex[b],
+// whose texels sit at float offset off[b] of the slot block grad (the
+// bitmap slots' part of s->tmp_c, n_floats long with its padding)
+struct WfBmpTex {
+    uint32_t tex[kMaxBitmapParams], off[kMaxBitmapParams];
+};
 template <bool InLds>
 __global__ void __launch_bounds__(256)
-k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restrict__ grad, uint32_t n_floats) {
+k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restrict__ grad, uint32_t n_floats) {
     extern __shared__ uint4 lds[];
     LdsFloat *acc = (LdsFloat *)reinterpret_cast<float *>(lds);
     if (InLds) {
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x) acc[i] = 0.f;
         __syncthreads();
     }
-    const DTexture tx = S.textures[tex];
     // a workgroup owns whole 4096-path tiles (its waves take the tile's 64
     // columns in turn), so the 64 lines a wave's transposed load touches are
     // re-read by the same CU's next columns from its L1 / L2
@@ -1697,13 +1704,17 @@ k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restr
             mask &= mask - 1u;
             V3 adj = v3(0, 0, 0);
             float uvx = 0.f, uvy = 0.f;
+            uint32_t bi = 0;
             if (on) {
                 const float4 r0 = bm.r(d, 0)[pid], r1 = bm.r(d, 1)[pid], r2 = bm.r(d, 2)[pid];
                 const V3 Lsuf = Ltot - v3(r0.x, r0.y, r0.z);  // prb.py: L - Le - Lr_dir
                 adj = v3(r2.x, r2.y, r2.z) + ((dL * Lsuf) * v3(r1.x, r1.y, r1.z)) * kInvPi;
                 uvx = r0.w;
                 uvy = r1.w;
+                bi = min(__float_as_uint(r2.w), (uint32_t)kMaxBitmapParams - 1u);
             }
+            const DTexture tx = S.textures[bt.tex[bi]];
+            const uint32_t goff = bt.off[bi];
             Taps tp;
             bitmap_taps(tx, uvx, uvy, tp);
             float w4[4] = {1.f, 0.f, 0.f, 0.f};
@@ -1714,12 +1725,12 @@ k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restr
                 const uint64_t onm = __ballot(on);
                 const uint32_t n_on = (uint32_t)__popcll(onm);
                 const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(onm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)onm, 0u));
-                const uint32_t nc = tx.channels == 3 ? 3u : 1u, per = 4u * nc;
+                const uint32_t nc = tx.channels == 3 ? 3u : 1u, per = 4u * nc;  // every bitmap of a call has the same channel count
                 float *st = bmp_stage();
                 if (on) {
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k)
-                        st[r * 16 + k] = __uint_as_float(k < tp.n ? (uint32_t)(tp.idx[k] - tx.data_offset) : 0xffffffffu);
+                        st[r * 16 + k] = __uint_as_float(k < tp.n ? goff + (uint32_t)(tp.idx[k] - tx.data_offset) : 0xffffffffu);
 #pragma unroll
                     for (uint32_t k = 0; k < 4; ++k) {
                         if (nc == 3) {
@@ -1746,7 +1757,7 @@ k_wf_bitmap_scatter(DScene S, uint32_t tex, WfBmp bm, uint32_t n, float *__restr
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
                 const bool tap = on && k < tp.n;
-                const uint32_t base = (uint32_t)(tp.idx[k] - tx.data_offset);
+                const uint32_t base = goff + (uint32_t)(tp.idx[k] - tx.data_offset);
                 if (tx.channels == 3) {
                     const float v[3] = {adj.x * w4[k], adj.y * w4[k], adj.z * w4[k]};
                     if (InLds) lds_add_grouped<3>(acc, base, tap, v);
@@ -1900,12 +1911,14 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     if (with_bmp) {
         const bool in_lds = (size_t)bmp->n_floats * 4 <= bmp->lds_max;
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->blocks, (uint32_t)((n + 4095) / 4096)));
+        WfBmpTex bt;
+        for (int b = 0; b < kMaxBitmapParams; ++b) { bt.tex[b] = bmp->tex[b]; bt.off[b] = bmp->off[b]; }
         if (in_lds)
             hipLaunchKernelGGL(k_wf_bitmap_scatter<true>, dim3(blocks), dim3(256), (size_t)bmp->n_floats * 4, st, S,
-                               bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
+                               bt, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
         else
             hipLaunchKernelGGL(k_wf_bitmap_scatter<false>, dim3((uint32_t)((n + 4095) / 4096)), dim3(256), 0, st, S,
-                               bmp->tex, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
+                               bt, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
     }
     if (span) (void)hipEventRecord(span[1], st);
     if (det_on) {

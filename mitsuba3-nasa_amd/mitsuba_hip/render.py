@@ -256,9 +256,9 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
     Returns a list of gradient tensors (one per key, same shape as the param).
     mode: 'auto' (wavefront single-traversal kernels when the keys are rgb
-    constants and at most one bitmap -- a bitmap's vertices are logged and
-    scattered to its texels once the paths end -- else the per-lane primal +
-    adjoint replay), 'mega' (per-lane
+    constants and bitmaps of one channel count -- a bitmap's vertices are
+    logged and scattered to its texels once the paths end -- else the
+    per-lane primal + adjoint replay), 'mega' (per-lane
     single traversal) or 'replay' (per-lane primal + adjoint replay, the
     reference's own two-pass structure).
     deterministic: bit-reproducible rgb gradients on the fused wavefront (each

@@ -579,6 +579,42 @@ def test_prb_bitmap_wavefront_chunks(channels, max_depth, lds, monkeypatch):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max(), err_msg=k)
 
 
+@pytest.mark.parametrize("lds", ["1", "0"])
+@pytest.mark.parametrize("red_channels", [3, 1])
+def test_prb_two_bitmaps_wavefront(red_channels, lds, monkeypatch):
+    """Two bitmap parameters (white and red) plus an rgb slot: on the fused
+    wavefront every bitmap vertex is recorded with its bitmap index and the
+    scatter adds it to that bitmap's texels (LDS block of both, or transposed
+    global atomics).  Bitmaps of different channel counts take the replay
+    megakernel instead.  Gradients vs the oracle."""
+    monkeypatch.setenv("MH_WF_CHUNK", "4096")
+    monkeypatch.setenv("MH_PRB_LDS_TEX", lds)
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box_bitmap(tex_res=8, width=40, height=32, spp=16)
+    red = np.zeros((6, 5, red_channels), np.float32)
+    red[..., 0] = 0.57
+    if red_channels == 3:
+        red[..., 1], red[..., 2] = 0.04, 0.04
+    d["red"]["reflectance"] = {"type": "bitmap", "data": red, "filter_type": "bilinear", "wrap_mode": "repeat",
+                               "raw": True}
+    scene = mi.load_dict(d)
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    keys = ["white.reflectance.data", "red.reflectance.data", "green.reflectance.value"]
+    gi = np.random.default_rng(8).random((32, 40, 3)).astype(np.float32) / (32 * 40 * 3)
+    st = A.Stats()
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=23, spp=16, stats=st)
+    assert st.mode == (1 if red_channels == 3 else 0), st.mode
+    ref = O.render_backward(scene, integ, 23, 16, gi, [params.texture_of(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    for k, a, b in zip(keys, g, ref):
+        a = a.cpu().numpy()
+        assert a.shape == b.shape and np.abs(b).max() > 0, k
+        np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max(), err_msg=k)
+
+
 # ---------------------------------------------------------------------------
 # Config 5: W*H*spp > 2^32 -> passes of spp_per_pass samples, each lane's RNG
 # continuing across passes (integrator.cpp:281-295, 353-357)
