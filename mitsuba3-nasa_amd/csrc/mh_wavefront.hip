@@ -1380,7 +1380,12 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 }
         }
         // ---- visibility of the NEE sample; the record is charged if unoccluded
+#ifdef MH_EXP_NO_SHADOW  // timing experiment: no shadow traversal (every NEE sample unoccluded; wrong gradients)
+        Hit sh;
+        sh.shape = MH_INVALID;
+#else
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
+#endif
         const bool unocc = shadow && sh.shape == MH_INVALID;
         if (unocc) {
             float (&ga)[NR][3] = Det ? Pp : acc;
