@@ -1237,11 +1237,9 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (rc_slots) return rc_slots;
     std::vector<float *> bufs;
     GradArgs ga;
-    // MH_FLAG_DETERMINISTIC with a grid sigma_t parameter: the grid gradient in
-    // int64 fixed point (two passes, see the prbvolpath branch below)
-    bool any_grid = false;
-    for (int k = 0; k < kMaxParams; ++k) any_grid = any_grid || P.grid_res[k][0] != 0;
-    const bool fx = vol && any_grid && deterministic(flags);
+    // MH_FLAG_DETERMINISTIC on prbvolpath: the grid gradient and the small
+    // slots in int64 fixed point (two passes, see the prbvolpath branch below)
+    const bool fx = vol && deterministic(flags);  // also the small slots (acc_add_fx)
     MH_HIP(upload_slots(s, P, st, bufs, ga, vol, fx));
     if (fx)
         for (int k = 0; k < kMaxParams; ++k)
@@ -1334,23 +1332,51 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     size_t wf_ctr_words = 0, wf_chunks = 0;
     uint32_t *pvb_lost = nullptr;  // prbvolpath on the scheduler: overflow entries that found their list full
     double fx_inv = 1.0;           // deterministic grid gradient: 2^-S of the fixed point
+    double fx_small_inv[kMaxRgbParams] = {1.0, 1.0, 1.0, 1.0};  // and of the small slots
     // between the two passes of the deterministic grid gradient: the scale
     // from pass 1's largest |item|; pass 1's rgb-slot adds and counters go
-    auto fx_between = [&](GradArgs &gp) -> hipError_t {
-        uint32_t mb = 0;
-        hipError_t e = hipMemcpyAsync(&mb, s->fx_word.ptr, 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return e;
+    // fx_word: u32 max[0] (grid) and max[1 + k] (small slot k), double
+    // scale[k] at byte 64, int64 sums[3 k + c] at byte 192 (acc_add_fx)
+    auto fx_exp = [](uint32_t bits) {  // 2^S with |item| * 2^S < 2^31
         float mx;
-        memcpy(&mx, &mb, 4);
+        memcpy(&mx, &bits, 4);
         int ex = 0;
         if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &ex);  // mx < 2^ex
-        fx_inv = std::ldexp(1.0, ex - 31);
-        gp.fx_scale = std::ldexp(1.0, 31 - ex);
+        return 31 - ex;
+    };
+    auto fx_between = [&](GradArgs &gp) -> hipError_t {
+        uint32_t mb[1 + kMaxRgbParams] = {};
+        hipError_t e = hipMemcpyAsync(mb, s->fx_word.ptr, sizeof(mb), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        const int S0 = fx_exp(mb[0]);
+        fx_inv = std::ldexp(1.0, -S0);
+        gp.fx_scale = std::ldexp(1.0, S0);
+        double sc[kMaxRgbParams];
+        for (int k = 0; k < kMaxRgbParams; ++k) {
+            fx_small_inv[k] = std::ldexp(1.0, -fx_exp(mb[1 + k]));
+            sc[k] = std::ldexp(1.0, fx_exp(mb[1 + k]));
+        }
+        e = hipMemcpyAsync(s->fx_word.as<uint8_t>() + 64, sc, sizeof(sc), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemsetAsync(s->fx_word.as<uint8_t>() + 192, 0, 8 * 3 * kMaxRgbParams, st);
         size_t total = 0;
         for (int k = 0; k < kMaxParams; ++k) total += (counts[k] + 3) / 4 * 4;
-        e = hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st);
+        if (e == hipSuccess) e = hipMemsetAsync(s->tmp_c.ptr, 0, std::max<size_t>(total, 1) * 4, st);
         if (e == hipSuccess) e = hipMemsetAsync(s->counters.ptr, 0, 256, st);
+        return e;
+    };
+    // after pass 2: the small slots' exact sums into their buffers (which
+    // pass 2 left at zero: acc_add_fx bypasses the register accumulators)
+    auto fx_small_fold = [&]() -> hipError_t {
+        long long w[3 * kMaxRgbParams];
+        hipError_t e = hipMemcpyAsync(w, s->fx_word.as<uint8_t>() + 192, sizeof(w), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        for (uint32_t k = 0; e == hipSuccess && k < n_rgb; ++k) {
+            float v[3];
+            for (int c = 0; c < 3; ++c) v[c] = (float)((double)w[3 * k + c] * fx_small_inv[k]);
+            e = hipMemcpyAsync(bufs[k], v, std::min<size_t>(3, (counts[k] + 3) / 4 * 4) * 4, hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+        }
         return e;
     };
     MH_HIP(hipEventRecord(s->ev0, st));
@@ -1458,12 +1484,12 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         // the grid scatter (nothing is accumulated that survives), pass 2 adds
         // round(item * 2^S) as int64, S = 31 - ceil(log2 max): |item| <= 2^31, so
         // up to 2^31 items sum without overflow, and the sums are exact
-        if (fx) MH_HIP(s->fx_word.alloc(256));
+        if (fx) MH_HIP(s->fx_word.alloc(512));
         for (uint32_t pass = fx ? 1u : 0u; pass <= (fx ? 2u : 0u); ++pass) {
         GradArgs gp = ga;
         gp.fx_mode = pass;
         gp.fx_max = fx ? s->fx_word.as<uint32_t>() : nullptr;
-        if (pass == 1) MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 4, st));
+        if (pass == 1) MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 64, st));
         if (pass == 2) MH_HIP(fx_between(gp));
         if (sched) {
             VsBwdArgs bw;
@@ -1501,8 +1527,8 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         }
         }  // passes
     } else if (fx) {  // prbvolpath replaying its NEE walks (MH_PVP_NEE_LOG=0), deterministic grid
-        MH_HIP(s->fx_word.alloc(256));
-        MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 4, st));
+        MH_HIP(s->fx_word.alloc(512));
+        MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 64, st));
         GradArgs gp = ga;
         gp.fx_max = s->fx_word.as<uint32_t>();
         for (uint32_t pass = 1; pass <= 2; ++pass) {
@@ -1515,6 +1541,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
     }
+    if (fx) MH_HIP(fx_small_fold());
     for (int k = 0; k < kMaxParams; ++k) {
         if (!P.corner[k]) continue;
         if (P.fx)

@@ -1485,7 +1485,23 @@ struct GradCtx {
 
 // register accumulator of a small (rgb / scalar) parameter slot
 static_assert(kMaxRgbParams == 4, "GradCtx names four small-slot accumulators");
+// MH_FLAG_DETERMINISTIC on prbvolpath (GradCtx::fx_mode): the small slots go
+// to int64 fixed point like the grid; the words after fx_max hold the
+// per-slot scales (doubles at byte 64) and sums (int64 x 3 at byte 192)
+MH_DEV void acc_add_fx(GradCtx &g, int32_t k, V3 a) {
+    if (g.fx_mode == 1) {
+        const float m = fmaxf(fabsf(a.x), fmaxf(fabsf(a.y), fabsf(a.z)));
+        if (m > 0.f) atomicMax(g.fx_max + 1 + k, __float_as_uint(m));
+        return;
+    }
+    const double sc = reinterpret_cast<const double *>(reinterpret_cast<const uint8_t *>(g.fx_max) + 64)[k];
+    unsigned long long *w = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(g.fx_max) + 192) + 3 * k;
+    atomicAdd(w + 0, (unsigned long long)__double2ll_rn((double)a.x * sc));
+    atomicAdd(w + 1, (unsigned long long)__double2ll_rn((double)a.y * sc));
+    atomicAdd(w + 2, (unsigned long long)__double2ll_rn((double)a.z * sc));
+}
 MH_DEV void acc_add(GradCtx &g, int32_t k, V3 a) {
+    if (g.fx_mode) { acc_add_fx(g, k, a); return; }
     if (k == 0) g.acc0 = g.acc0 + a;
     else if (k == 1) g.acc1 = g.acc1 + a;
     else if (k == 2) g.acc2 = g.acc2 + a;

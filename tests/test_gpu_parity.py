@@ -449,12 +449,13 @@ def test_prbvolpath_grid_corner_scatter(shape, monkeypatch):
 
 @pytest.mark.parametrize("mode", ["sched", "sched_off", "replay"])
 def test_prbvolpath_deterministic_grid_gradient(mode, monkeypatch):
-    """MH_FLAG_DETERMINISTIC with a grid sigma_t parameter: the corner blocks
-    hold int64 fixed point (a pre-pass finds the largest item, the real pass
-    adds round(item * 2^S)), so repeated runs give the same bits whatever the
-    order of the adds; equal to the float-atomic gradient up to float order
-    and to the oracle at 2e-3.  On the scheduler (default), the per-sample
-    kernel (MH_PVP_SCHED=0) and the NEE-replaying kernel (MH_PVP_NEE_LOG=0)."""
+    """MH_FLAG_DETERMINISTIC on prbvolpath: the grid gradient's corner blocks
+    and the small slots (albedo, the floor's rgb reflectance) hold int64
+    fixed point (a pre-pass finds each one's largest item, the real pass adds
+    round(item * 2^S)), so repeated runs give the same bits whatever the order
+    of the adds; equal to the float-atomic gradients up to float order and to
+    the oracle at 2e-3.  On the scheduler (default), the per-sample kernel
+    (MH_PVP_SCHED=0) and the NEE-replaying kernel (MH_PVP_NEE_LOG=0)."""
     if mode == "sched_off":
         monkeypatch.setenv("MH_PVP_SCHED", "0")
     elif mode == "replay":
@@ -464,20 +465,22 @@ def test_prbvolpath_deterministic_grid_gradient(mode, monkeypatch):
     scene = _pvp_scene(mi, 24, 20, 8)
     integ = scene.integrator()
     params = mi.traverse(scene)
-    key = "medium1.sigma_t.data"
+    keys = ["medium1.sigma_t.data", "medium1.albedo.value", "floor.bsdf.reflectance.value"]
     H, W = scene.height, scene.width
     gi = torch.from_numpy(np.random.default_rng(6).standard_normal((H, W, 3)).astype(np.float32)).cuda()
-    runs = [mi.render_backward(scene, params, gi, [key], integ, seed=3, spp=8, deterministic=True)[0]
-            for _ in range(3)]
+    runs = [mi.render_backward(scene, params, gi, keys, integ, seed=3, spp=8, deterministic=True) for _ in range(3)]
     for r in runs[1:]:
-        assert torch.equal(runs[0], r)
-    a = runs[0].cpu().numpy()
-    b = mi.render_backward(scene, params, gi, [key], integ, seed=3, spp=8)[0].cpu().numpy()
-    ref = O.render_backward(scene, integ, 3, 8, gi.cpu().numpy(), [params.param_id(key)], [tuple(params[key].shape)])[0]
-    scale = np.abs(ref).max()
-    assert scale > 0
-    np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6 * scale)
-    np.testing.assert_allclose(a, ref, rtol=2e-3, atol=1e-7 + 2e-4 * scale)
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    flt = mi.render_backward(scene, params, gi, keys, integ, seed=3, spp=8)
+    ref = O.render_backward(scene, integ, 3, 8, gi.cpu().numpy(), [params.param_id(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    for k, a, b, r in zip(keys, runs[0], flt, ref):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        scale = np.abs(r).max()
+        assert scale > 0, k
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6 * scale, err_msg=k)
+        np.testing.assert_allclose(a, r, rtol=2e-3, atol=1e-7 + 2e-4 * scale, err_msg=k)
 
 
 @pytest.mark.parametrize("alpha", [False, True])
