@@ -2264,11 +2264,14 @@ MH_DEV bool bbox_ray_intersect(const float *mn, const float *mx, const RayT &r, 
     return active && maxt >= mint;
 }
 
-// Medium::sample_interaction (medium.cpp:40-86)
+// Medium::sample_interaction (medium.cpp:40-86).  Frame = false leaves the
+// interaction frame (fs, ft) to the caller (mei_frame), for callers that
+// need it only at a real scatter.
+template <bool Frame = true>
 MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, float u, MEI &mei) {
     const DMedium &m = S.media[med];
     mei.fn = ray.d;
-    coordinate_system(ray.d, mei.fs, mei.ft);
+    if (Frame) coordinate_system(ray.d, mei.fs, mei.ft);
     float mint, maxt;
     bool active;
     if (m.type == MH_MEDIUM_HOMOGENEOUS) {
@@ -2296,6 +2299,7 @@ MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, f
 }
 
 MH_DEV V3 mei_to_local(const MEI &m, V3 v) { return v3(dot(v, m.fs), dot(v, m.ft), dot(v, m.fn)); }
+MH_DEV void mei_frame(MEI &m) { coordinate_system(m.fn, m.fs, m.ft); }  // Frame3f(ray.d), as sample_interaction
 MH_DEV V3 mei_to_world(const MEI &m, V3 v) { return fma3s(m.fn, v.z, fma3s(m.ft, v.y, m.fs * v.x)); }
 
 // HGPhaseFunction (phase/hg.cpp:66-104), IsotropicPhaseFunction

@@ -550,6 +550,7 @@ MH_DEV uint32_t vs_head(const DScene &S, const IntegratorParams &in, Pcg &rng, V
 
 // SCATTER: a real medium interaction (volpath.cpp:224-252)
 MH_DEV uint32_t vs_scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v) {
+    mei_frame(v.mei);  // the merged medium step samples without it (identical values)
     const DMedium &m = S.media[v.medium];
     const MEI &mei = v.mei;
     const bool spectral = !(m.flags & MH_MEDIUM_NO_SPECTRAL_EXTINCTION);
@@ -697,8 +698,8 @@ MH_DEV uint32_t vs_medium_step(const DScene &S, const IntegratorParams &in, Pcg 
     r.o = v3(head ? rh.o.x : rw.o.x, head ? rh.o.y : rw.o.y, head ? rh.o.z : rw.o.z);
     r.d = v3(head ? rh.d.x : rw.d.x, head ? rh.d.y : rw.d.y, head ? rh.d.z : rw.d.z);
     r.maxt = head ? rh.maxt : rw.maxt;
-    MEI mei;
-    sample_interaction(S, head ? mh : mw, r, u, mei);
+    MEI mei;  // the frame only at a real scatter (vs_scatter)
+    sample_interaction<false>(S, head ? mh : mw, r, u, mei);
     if (ph == kPhHead) {
         v.mei = mei;
         return vs_head_post(S, in, rng, v);
