@@ -159,6 +159,34 @@ def test_render_backward_sharded_matches_one_call():
     np.testing.assert_allclose(outs[0][0].cpu().numpy(), ref.cpu().numpy(), rtol=1e-4)
 
 
+def test_render_backward_sharded_prbvolpath():
+    """The sharded backward of prbvolpath (grid sigma_t through the per-scene
+    corner blocks, albedo through the small slots): the slabs' gradients,
+    summed by device copies, equal one render_backward to float order."""
+    mi = _mi()
+    import torch
+    from mitsuba_hip.comm import render_backward_sharded
+    spp = 8
+
+    def vol():
+        d = mi.volume_cube(24, 20, spp, grid=mi.fbm_grid(16), scale=4.0, max_depth=6)
+        d["integrator"] = {"type": "prbvolpath", "max_depth": 6, "rr_depth": 5}
+        return mi.load_dict(d)
+
+    scenes = [vol() for _ in range(2)]
+    integ = scenes[0].integrator()
+    params = mi.traverse(scenes[0])
+    keys = ["medium1.sigma_t.data", "medium1.albedo.value"]
+    gi = torch.from_numpy(np.random.default_rng(2).standard_normal((20, 24, 3)).astype(np.float32)).cuda()
+    ref = mi.render_backward(scenes[0], params, gi, keys, integ, seed=4, spp=spp)
+    outs = render_backward_sharded(scenes, params, gi, keys, integ, 4, spp)
+    torch.cuda.synchronize()
+    for i, (k, r) in enumerate(zip(keys, ref)):
+        a, r = outs[0][i].cpu().numpy(), r.cpu().numpy()
+        assert np.abs(r).max() > 0, k
+        np.testing.assert_allclose(a, r, rtol=1e-4, atol=1e-6 * np.abs(r).max(), err_msg=k)
+
+
 def test_render_sharded_with_world1_comm_and_argument_checks():
     mi = _mi()
     import torch
