@@ -112,10 +112,11 @@ enum {
     MH_FLAG_DETERMINISTIC   = 1u << 6,  /* film / W-image splat as a fixed-order gather instead of float
                                            atomics: bit-reproducible films; mh_render_backward on the fused
                                            wavefront: rgb gradients summed per path and reduced in path-id
-                                           order, bit-reproducible; prbvolpath gradients (grid sigma_t and
-                                           the small slots) in int64 fixed point (a pre-pass sizes the
-                                           scales; the backward runs twice), bit-reproducible (bitmap
-                                           texels stay float atomics) (also env MH_DETERMINISTIC=1) */
+                                           order, and bitmap texels in int64 fixed point (a max pass sizes
+                                           the scale), bit-reproducible; prbvolpath gradients (grid sigma_t
+                                           and the small slots) in int64 fixed point (the backward runs
+                                           twice), bit-reproducible (the replay megakernel's texel atomics
+                                           stay float atomics) (also env MH_DETERMINISTIC=1) */
     /* multi-GPU (the scene has a communicator, mh_scene_set_comm; one host
        thread per rank): the call sums its result over the ranks in-call, on
        the scene's stream -- mh_render / mh_render_forward the film,

@@ -111,6 +111,7 @@ struct mh_scene {
     DevBuf pvp_ovf;    // prbvolpath backward on the scheduler: overflow lists + their counters
     DevBuf grid_corner;  // prbvolpath backward: per-cell corner blocks of the grid sigma_t slots
     DevBuf fx_word;      // its deterministic pre-pass: the largest |item| (float bits)
+    DevBuf bmp_fx;       // the deterministic bitmap scatter's max word + int64 texel sums
     // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
     // buffers of the sharded entry points (slab W image, staged peer sums,
     // slab gradients)
@@ -479,7 +480,7 @@ int mh_scene_destroy(mh_scene *s) {
     for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
-                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word,
+                      &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word, &s->bmp_fx,
                       &s->shard_w, &s->shard_tmp, &s->shard_g})
         b->release();
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
@@ -1418,13 +1419,18 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             bmp.grad = bufs[kMaxRgbParams];
             bmp.n_floats = (uint32_t)boff;
             bmp.lds_max = (env_lds && !strcmp(env_lds, "0")) ? 0u : (uint32_t)std::min(max_wg, 64 << 10);
+            if (deterministic(flags)) {  // fixed-point texel sums (k_wf_bitmap_scatter<false, Fx>)
+                MH_HIP(s->bmp_fx.alloc((size_t)bmp.n_floats * 8 + 256));
+                bmp.fx_word = s->bmp_fx.as<uint32_t>();
+                bmp.fx_acc = reinterpret_cast<unsigned long long *>(s->bmp_fx.as<uint8_t>() + 256);
+            }
             const size_t per_wg = std::max<size_t>((size_t)bmp.n_floats * 4, 1);
             const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (size_t)per_cu_lds / per_wg));
             bmp.blocks = (uint32_t)cus * per_cu;
         }
         // MH_FLAG_DETERMINISTIC: rgb slots summed per path and reduced in a
-        // fixed order (WfDet); a bitmap's texel scatter stays atomic
-        const bool det_grad = deterministic(flags) && !bmp_wf && n_rgb > 0;
+        // fixed order (WfDet); bitmap texels in int64 fixed point (bmp.fx_acc)
+        const bool det_grad = deterministic(flags) && n_rgb > 0;
         if (det_grad) MH_HIP(s->wf_ws_det.alloc(wf_det_workspace_bytes(cap)));
         MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
         MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));

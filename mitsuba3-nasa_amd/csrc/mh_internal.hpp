@@ -107,6 +107,10 @@ struct WfBitmapArgs {
     uint32_t n_floats = 0;   // that block's floats (texels x channels, padded per slot)
     uint32_t lds_max = 0;    // per-workgroup LDS accumulation when n_floats * 4 <= lds_max
     uint32_t blocks = 0;     // scatter workgroups (persistent grid)
+    // MH_FLAG_DETERMINISTIC: int64 sums (n_floats) and the max word of the
+    // fixed-point scatter (nullptr: float atomics)
+    unsigned long long *fx_acc = nullptr;
+    uint32_t *fx_word = nullptr;
 };
 size_t wf_bmp_workspace_bytes(uint64_t cap, uint32_t n_depth);
 hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,

@@ -20,6 +20,7 @@
 // between bounces: queue counts stay on the device).
 #include <algorithm>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 
 #include "mh_shading.hpp"
@@ -1152,7 +1153,6 @@ template <int NR, bool Gen, bool Bm, bool Det>
 __global__ void __launch_bounds__(256, Bm ? MH_BOUNCE_BMP_WAVES : MH_BOUNCE_PRB_WAVES)
 k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, WfState w, WfPrb q,
                 int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen, WfBmp bm, WfDet det) {
-    static_assert(!(Det && Bm), "deterministic gradients: rgb slots only");
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
     uint32_t n;
@@ -1675,12 +1675,20 @@ MH_DEV float *bmp_stage() {
 // the bitmap parameters of a scatter: record b (its r2.w) is texture tex[b],
 // whose texels sit at float offset off[b] of the slot block grad (the
 // bitmap slots' part of s->tmp_c, n_floats long with its padding)
+// Fx (MH_FLAG_DETERMINISTIC; the global path only): 1 = the largest |value|
+// into fx_max, nothing added; 2 = round(value * scale) as int64 into acc64
+// (exact sums, folded into grad by k_fx_fold)
 struct WfBmpTex {
     uint32_t tex[kMaxBitmapParams], off[kMaxBitmapParams];
+    unsigned long long *acc64;
+    uint32_t *fx_max;
+    double scale;
 };
-template <bool InLds>
+template <bool InLds, int Fx = 0>
 __global__ void __launch_bounds__(256)
 k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restrict__ grad, uint32_t n_floats) {
+    static_assert(!(InLds && Fx), "the fixed-point passes use the global path");
+    float fx_mx = 0.f;
     extern __shared__ uint4 lds[];
     LdsFloat *acc = (LdsFloat *)reinterpret_cast<float *>(lds);
     if (InLds) {
@@ -1754,7 +1762,12 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
                 for (uint32_t t = lane; t < total; t += 64u) {
                     const uint32_t src = t / per, rem = t - src * per, k = rem / nc, c = rem - k * nc;
                     const uint32_t base = __float_as_uint(st[src * 16 + k]);
-                    if (base != 0xffffffffu) atomicAdd(grad + base + c, st[src * 16 + 4 + k * 3 + c]);
+                    if (base == 0xffffffffu) continue;
+                    const float val = st[src * 16 + 4 + k * 3 + c];
+                    if constexpr (Fx == 1) fx_mx = fmaxf(fx_mx, fabsf(val));
+                    else if constexpr (Fx == 2)
+                        atomicAdd(bt.acc64 + base + c, (unsigned long long)__double2ll_rn((double)val * bt.scale));
+                    else atomicAdd(grad + base + c, val);
                 }
                 __builtin_amdgcn_wave_barrier();
                 continue;
@@ -1784,6 +1797,17 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x)
             if (acc[i] != 0.f) atomicAdd(grad + i, acc[i]);
     }
+    if constexpr (Fx == 1) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) fx_mx = fmaxf(fx_mx, __shfl_xor(fx_mx, off));
+        if ((threadIdx.x & 63u) == 0 && fx_mx > 0.f) atomicMax(bt.fx_max, __float_as_uint(fx_mx));
+    }
+}
+
+// grad += the exact int64 sums of the fixed-point scatter, once per texel float
+__global__ void k_fx_fold(const long long *__restrict__ acc, float *__restrict__ grad, uint32_t n, double inv) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        grad[i] += (float)((double)acc[i] * inv);
 }
 
 template <bool InLds, bool Packet, int NR>
@@ -1857,7 +1881,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     if (with_bmp && (!fused || bmp->n_depth > 31 || bmp->n_depth + 1 < n_bounces || !bmp->ws)) return hipErrorInvalidValue;
     const WfBmp bm = with_bmp ? carve_bmp(bmp->ws, cap, bmp->n_depth, bmp->slot) : WfBmp{};
     const bool det_on = ws_det != nullptr;
-    if (det_on && (with_bmp || !fused)) return hipErrorInvalidValue;
+    if (det_on && !fused) return hipErrorInvalidValue;
     const WfDet det = det_on ? carve_det(ws_det, cap) : WfDet{};
     if (det_on) {  // paths whose id is never written (segment gaps) add zeros
         e = hipMemsetAsync(det.fin_host(0), 0, (size_t)n_rgb * 3 * det.stride * 4, st);
@@ -1880,7 +1904,10 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
-            if (with_bmp) {
+            if (with_bmp && det_on) {
+                if (b == 0) MH_BOUNCE_PRB_NR(true, true, true);
+                else MH_BOUNCE_PRB_NR(false, true, true);
+            } else if (with_bmp) {
                 if (b == 0) MH_BOUNCE_PRB_NR(true, true, false);
                 else MH_BOUNCE_PRB_NR(false, true, false);
             } else if (det_on) {
@@ -1918,7 +1945,32 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->blocks, (uint32_t)((n + 4095) / 4096)));
         WfBmpTex bt;
         for (int b = 0; b < kMaxBitmapParams; ++b) { bt.tex[b] = bmp->tex[b]; bt.off[b] = bmp->off[b]; }
-        if (in_lds)
+        bt.acc64 = bmp->fx_acc;
+        bt.fx_max = bmp->fx_word;
+        bt.scale = 0.0;
+        const dim3 g_all((uint32_t)((n + 4095) / 4096));
+        if (bmp->fx_acc) {  // deterministic: max pass, then int64 pass, then fold (this chunk's own scale)
+            e = hipMemsetAsync(bmp->fx_word, 0, 4, st);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_wf_bitmap_scatter<false, 1>), g_all, dim3(256), 0, st, S, bt, bm, (uint32_t)n,
+                               bmp->grad, bmp->n_floats);
+            uint32_t mb = 0;
+            e = hipMemcpyAsync(&mb, bmp->fx_word, 4, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            float mx;
+            memcpy(&mx, &mb, 4);
+            int ex = 0;
+            if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &ex);
+            bt.scale = std::ldexp(1.0, 31 - ex);
+            e = hipMemsetAsync(bmp->fx_acc, 0, (size_t)bmp->n_floats * 8, st);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((k_wf_bitmap_scatter<false, 2>), g_all, dim3(256), 0, st, S, bt, bm, (uint32_t)n,
+                               bmp->grad, bmp->n_floats);
+            hipLaunchKernelGGL(k_fx_fold, dim3(std::max<uint32_t>(1, std::min<uint32_t>(4096, (bmp->n_floats + 255) / 256))),
+                               dim3(256), 0, st, reinterpret_cast<const long long *>(bmp->fx_acc), bmp->grad,
+                               bmp->n_floats, std::ldexp(1.0, ex - 31));
+        } else if (in_lds)
             hipLaunchKernelGGL(k_wf_bitmap_scatter<true>, dim3(blocks), dim3(256), (size_t)bmp->n_floats * 4, st, S,
                                bt, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
         else
