@@ -882,6 +882,9 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpai
         // rectangles [0, nrect) densely (nearly every ray overlaps the room),
         // then the triangle run
         uint32_t i = 0;
+#ifdef MH_EXP_SHADOW_NORECT  // timing experiment: shadow queries skip the rectangles (not exact in general)
+        if (Shadow) i = nrect;
+#endif
         for (; i + 1u < nrect; i += 2u) rect_pair<Shadow>(gpairs, c + i, hit & (!Shadow || !ph.occl), r, ph);
         if (i < nrect) {
             rect_one<Shadow>(gprims, c + i, hit & (!Shadow || !ph.occl), r, ph);
