@@ -1,4 +1,4 @@
-"""CPU, world_size 2 over gloo: the sample-slab sharding + all-reduce
+"""CPU, world_size 2 and 4 over gloo: the sample-slab sharding + all-reduce
 orchestration that bench.py runs over RCCL (mitsuba_hip.distributed), with
 the CPU oracle standing in for the HIP entry points.  The union of the two
 ranks' slabs must reproduce the single-process render and PRB gradient."""
@@ -53,7 +53,7 @@ def _worker(rank, world, port, out_dir):
     from mitsuba_hip import distributed as D
     dist.init_process_group("gloo", rank=rank, world_size=world)
     scene = _scene(mi)
-    slab = D.sample_slab(rank, world, 4)
+    slab = D.sample_slab(rank, world, 8 // world)
     img, grads = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7)
     # the same step with the W image computed locally on every rank (no W
     # all-reduce) and the film summed onto rank 0 only
@@ -74,18 +74,22 @@ def test_sample_slab():
         D.sample_slab(4, 4, 64)
 
 
-def test_two_rank_gloo_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_ranks_match_single_process(world, tmp_path):
     import torch
     import torch.multiprocessing as mp
     import mitsuba_hip as mi
     import oracle_py as O
     from mitsuba_hip import distributed as D
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    r0, r1 = (np.load(tmp_path / f"r{i}.npz") for i in range(2))
-    assert (int(r0["begin"]), int(r0["end"]), int(r1["begin"]), int(r1["end"])) == (0, 4, 4, 8)
-    assert float(r0["t"]) == float(r1["t"]) == 1.5  # max over ranks
-    assert np.array_equal(r0["img"], r1["img"]) and np.array_equal(r0["g"], r1["g"])
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    rs = [np.load(tmp_path / f"r{i}.npz") for i in range(world)]
+    per = 8 // world
+    assert [(int(r["begin"]), int(r["end"])) for r in rs] == [(i * per, (i + 1) * per) for i in range(world)]
+    assert all(float(r["t"]) == world - 0.5 for r in rs)  # max over ranks
+    r0, r1 = rs[0], rs[-1]
+    for r in rs[1:]:
+        assert np.array_equal(r0["img"], r["img"]) and np.array_equal(r0["g"], r["g"])
     # single process, all 8 samples per pixel
     scene = _scene(mi)
     img, grads = D.fwd_grad_step(_ops(mi, O, scene, torch), D.sample_slab(0, 1, 8), seed=7)
