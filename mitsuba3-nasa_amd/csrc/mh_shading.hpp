@@ -167,6 +167,10 @@ struct LdsBvh {
     const Prim *prims;
     uint32_t *stack;  // this lane's column
     uint32_t stride;
+    // packet engine with sparse-run deferral (k_vol_sched): LDS pair records and
+    // this wave's deferral scratch (nullptr: dense packet tests only)
+    const float *recs = nullptr;
+    uint8_t *dscr = nullptr;
 };
 
 // InLds = true: BVH resident in LDS (compile-time choice, so hipcc emits
@@ -2343,14 +2347,18 @@ MH_DEV uint32_t target_medium(const DScene &S, const SI &si, V3 d) {
 // Pk: the wave-coherent packet engine (small scenes with pair records; the
 // lanes that reach this call trace together, control stays scalar) instead
 // of the per-lane traversal; same hits (closest, exact-t ties to the lower key)
+// the surface interaction of a closest hit and its distance
+MH_DEV void si_from_hit(const DScene &S, const RayT &ray, const Hit &h, SI &si, float &si_t) {
+    compute_si(S, ray, h, si);
+    si_t = si.valid ? h.t : __builtin_huge_valf();
+}
 template <bool Pk = false>
 MH_DEV void trace_si(const DScene &S, const LdsBvh &B, const RayT &ray, SI &si, float &si_t) {
     Hit h;
     if (Pk) h = packet_batch<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B.stack - (threadIdx.x & 63u), B.stride,
                                     ray, true);
     else traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
-    compute_si(S, ray, h, si);
-    si_t = si.valid ? h.t : __builtin_huge_valf();
+    si_from_hit(S, ray, h, si, si_t);
 }
 
 // volpath.cpp:333-450: emitter sample + ratio-tracked transmittance, split

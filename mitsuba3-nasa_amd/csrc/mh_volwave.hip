@@ -708,14 +708,36 @@ MH_DEV uint32_t vs_medium_step(const DScene &S, const IntegratorParams &in, Pcg 
 }
 
 // TRACE: every lane pending an intersection traces it; then its continuation
+MH_DEV uint32_t vs_trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, VolState &v,
+                             WMei &wm, const Hit &h, const RayT &ray, uint32_t &n_closest, uint32_t &n_shadow);
 template <bool Pk>
 MH_DEV uint32_t vs_trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, uint32_t ph,
                          VolState &v, WMei &wm, uint32_t &n_closest, uint32_t &n_shadow) {
     const bool walk = ph == kPhTraceWM || ph == kPhTraceWS;
     const RayT ray = walk ? v.ns.ray : v.ray;
+    Hit h;
+    if (Pk) h = packet_batch<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B.stack - (threadIdx.x & 63u), B.stride,
+                                    ray, true);
+    else traverse<false>(B.nodes, B.prims, B.stack, B.stride, ray, h);
+    return vs_trace_hit(S, in, rng, ph, v, wm, h, ray, n_closest, n_shadow);
+}
+// the ray a TRACE lane traces (selected as values, not as one of two fields)
+MH_DEV RayT vs_trace_ray(const VolState &v, uint32_t ph) {
+    const bool walk = ph == kPhTraceWM || ph == kPhTraceWS;
+    const RayT a = v.ns.ray, b = v.ray;
+    RayT r;
+    r.o = v3(walk ? a.o.x : b.o.x, walk ? a.o.y : b.o.y, walk ? a.o.z : b.o.z);
+    r.d = v3(walk ? a.d.x : b.d.x, walk ? a.d.y : b.d.y, walk ? a.d.z : b.d.z);
+    r.maxt = walk ? a.maxt : b.maxt;
+    return r;
+}
+// TRACE after the traversal: the hit's interaction, then its continuation
+MH_DEV uint32_t vs_trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, VolState &v,
+                             WMei &wm, const Hit &h, const RayT &ray, uint32_t &n_closest, uint32_t &n_shadow) {
+    const bool walk = ph == kPhTraceWM || ph == kPhTraceWS;
     SI si;
     float si_t;
-    trace_si<Pk>(S, B, ray, si, si_t);
+    si_from_hit(S, ray, h, si, si_t);
     if (walk) {
         v.ns.si = si;
         v.ns.si_t = si_t;
@@ -1098,6 +1120,30 @@ MH_DEV uint32_t pv_post(const DScene &S, const LdsBvh &B, const IntegratorParams
     return (v.active && (v.active_surface || v.active_medium)) ? kPhHead : kPhFree;
 }
 
+// the wave-wide TRACE (k_vol_sched): the lane's ray, then its hit's continuation
+template <class V>
+MH_DEV RayT pv_trace_ray(const V &v, uint32_t ph) {
+    const bool ws = ph == kPhTraceWS;
+    const RayT a = v.wray, b = v.ray;
+    RayT r;
+    r.o = v3(ws ? a.o.x : b.o.x, ws ? a.o.y : b.o.y, ws ? a.o.z : b.o.z);
+    r.d = v3(ws ? a.d.x : b.d.x, ws ? a.d.y : b.d.y, ws ? a.d.z : b.d.z);
+    r.maxt = ws ? a.maxt : b.maxt;
+    return r;
+}
+template <class V, class Hk>
+MH_DEV uint32_t pv_trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, V &v, const Hit &h,
+                             const RayT &r, uint32_t &n_closest, uint32_t &n_shadow, Hk &hk) {
+    if (ph == kPhTraceWS) {
+        si_from_hit(S, r, h, v.wsi, v.wsi_t);
+        ++n_shadow;
+        return pv_walk_rest(S, rng, v, pv_remaining(v), hk);
+    }
+    si_from_hit(S, r, h, v.si, v.si_t);
+    ++n_closest;
+    if (ph == kPhTraceM) return pv_med_rest(S, in, rng, v, hk);
+    return kPhSurf;
+}
 template <bool Pk, class V, class Hk>
 MH_DEV uint32_t pv_trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, uint32_t ph,
                          V &v, uint32_t &n_closest, uint32_t &n_shadow, Hk &hk) {
@@ -1154,6 +1200,11 @@ struct VolMachine {
     MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &wm, uint32_t ph) {
         return vs_medium_step(S, in, rng, v, wm, ph);
     }
+    MH_DEV RayT trace_ray(const State &v, uint32_t ph) const { return vs_trace_ray(v, ph); }
+    MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &wm,
+                              const Hit &h, const RayT &r, uint32_t &nc, uint32_t &ns) {
+        return vs_trace_hit(S, in, rng, ph, v, wm, h, r, nc, ns);
+    }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &, const IntegratorParams &in, Pcg &rng, State &v, uint32_t &) {
         return volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
     }
@@ -1189,6 +1240,11 @@ struct PvMachine {
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, h); }
     MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph) {
         return pv_medium_step(S, in, rng, v, h, ph);
+    }
+    MH_DEV RayT trace_ray(const State &v, uint32_t ph) const { return pv_trace_ray(v, ph); }
+    MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &,
+                              const Hit &hh, const RayT &r, uint32_t &nc, uint32_t &ns) {
+        return pv_trace_hit(S, in, rng, ph, v, hh, r, nc, ns, h);
     }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
                          uint32_t &ns) {
@@ -1363,6 +1419,11 @@ struct PvBwdMachine {
     MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph) {
         return pv_medium_step(S, in, rng, v, *this, ph);
     }
+    MH_DEV RayT trace_ray(const State &v, uint32_t ph) const { return pv_trace_ray(v, ph); }
+    MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &,
+                              const Hit &hh, const RayT &r, uint32_t &nc, uint32_t &ns) {
+        return pv_trace_hit(S, in, rng, ph, v, hh, r, nc, ns, *this);
+    }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
                          uint32_t &ns) {
         return pv_post(S, B, in, rng, v, *this, ns);
@@ -1417,6 +1478,13 @@ struct PvBwdMachine {
 #ifndef MH_VS_WAVES
 #define MH_VS_WAVES 2
 #endif
+// TRACE as one wave-wide packet traversal with sparse-run deferral (packet scenes)
+#ifndef MH_VS_DEFER
+#define MH_VS_DEFER 1
+#endif
+__host__ __device__ inline uint32_t vs_defer_bytes(const DScene &S) {
+    return MH_VS_DEFER ? 16u + align16(S.n_prims * kPairRecFloats * 4u) + 4u * kDeferScratch : 0u;
+}
 // phase weights (x16): a phase runs when its pending lanes x weight is the
 // largest; heavy phases wait for more lanes
 #ifndef MH_VS_W
@@ -1454,6 +1522,14 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         tab = vs_tab_bytes(S0) / 16u;
     }
     LdsBvh B = stage_bvh<InLds>(S0, lds + tab);
+    if (Pk && MH_VS_DEFER) {  // pair records + deferral scratch after the stacks (vs_defer_bytes)
+        const uint32_t off = (tab * 16u + S0.lds_bytes_bvh + S0.stack_size * blockDim.x * 4u + 15u) & ~15u;
+        float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + off);
+        stage_pair_records(S0, recs);
+        __syncthreads();
+        B.recs = recs;
+        B.dscr = reinterpret_cast<uint8_t *>(recs) + align16(S0.n_prims * kPairRecFloats * 4u) + (threadIdx.x >> 6) * kDeferScratch;
+    }
     constexpr uint32_t W0[kNGroups] = {MH_VS_W};
     uint32_t W[kNGroups];
 #pragma unroll
@@ -1559,7 +1635,20 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 ended = ph == kPhFree;
             }
         } else if (sel == kGTrace) {
-            if (g == kGTrace) {
+            if constexpr (Pk && MH_VS_DEFER) {
+                // every lane of the wave in the traversal (the deferral hands
+                // sparse leaves' (ray, pair) items to all 64 lanes); TRACE lanes
+                // carry their rays, the others ride along inactive
+                const bool act = g == kGTrace;
+                RayT r{v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 1.f), -1.f};
+                if (act) r = mc.trace_ray(v, ph);
+                const Hit h = packet_batch<false, true>(S.nodes, S.prims, S.prim_pairs, S.key_sp,
+                                                        B.stack - (threadIdx.x & 63u), B.stride, r, act, B.recs, B.dscr);
+                if (act) {
+                    ph = mc.trace_hit(S, in, rng, ph, v, wm, h, r, n_closest, n_shadow);
+                    ended = ph == kPhFree;
+                }
+            } else if (g == kGTrace) {
                 ph = mc.template trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
                 ended = ph == kPhFree;
             }
@@ -1650,7 +1739,7 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     const bool pk = S.n_prims > 0 && S.n_prims <= wf_packet_max_prims() && !(te && !strcmp(te, "lane"));
     const bool tab = S.tab_bytes != 0 && !getenv("MH_VS_NOTAB");
 #define MH_VS1(Mc, L, P, T)                                                                                   \
-    hipLaunchKernelGGL((k_vol_sched<Mc, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), st, S, \
+    hipLaunchKernelGGL((k_vol_sched<Mc, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u) + (P ? vs_defer_bytes(S) : 0u), st, S, \
                        in, lm, seed_value, n, plane, out, counters, work, alpha, VsBwdArgs{})
 #define MH_VS(L, P, T)                                                  \
     do {                                                                \
@@ -1686,7 +1775,7 @@ hipError_t launch_vol_sched_bwd(const DScene &S, const IntegratorParams &in, con
     hipError_t e = hipMemsetAsync(work, 0, 8 * 128, st);
     if (e != hipSuccess) return e;
 #define MH_VSB(L, P, T)                                                                                        \
-    hipLaunchKernelGGL((k_vol_sched<PvBwdMachine, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u), \
+    hipLaunchKernelGGL((k_vol_sched<PvBwdMachine, L, P, T>), dim3(grid), dim3(256), sh + (T ? vs_tab_bytes(S) : 0u) + (P ? vs_defer_bytes(S) : 0u), \
                        st, S, in, lm, seed_value, n, (uint64_t)0, (float *)nullptr, counters, work, 0, bw)
     if (pk && tab) MH_VSB(false, true, true);
     else if (pk) MH_VSB(false, true, false);
