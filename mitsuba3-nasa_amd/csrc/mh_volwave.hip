@@ -1488,12 +1488,15 @@ __host__ __device__ inline uint32_t vs_defer_bytes(const DScene &S) {
 // phase weights (x16): a phase runs when its pending lanes x weight is the
 // largest; heavy phases wait for more lanes
 #ifndef MH_VS_W
-#define MH_VS_W 8, 16, 12, 8, 8, 6, 12, 16   // free, head, trace, scatter, surf, walk, post (swept on config 4: 194 -> 214 Msamples/s), end
+// free, head, trace, scatter, surf, walk, post, end (swept on config 4: 194 -> 214 Msamples/s;
+// trace 12 -> 8 re-swept after the wave-wide TRACE: 32 / 20 / 12 / 8 / 6 / 4 -> 240 / 244 / 246 / 247 / 246 / 242)
+#define MH_VS_W 8, 16, 8, 8, 8, 6, 12, 16
 #endif
 // the weight of the merged HEAD + WALK group (machines with kMergeMed; swept
-// on config 4: 16 -> 190, 6 -> 226, 4 -> 233, 3 -> 234 Msamples/s)
+// on config 4: 16 -> 190, 6 -> 226, 4 -> 233, 3 -> 234 Msamples/s; with the
+// wave-wide TRACE at weight 8: 6 -> 237, 4 -> 246, 3 -> 250.5)
 #ifndef MH_VS_MERGE_W
-#define MH_VS_MERGE_W 4
+#define MH_VS_MERGE_W 3
 #endif
 // Tab: the shading tables (stage_tables) and the media records staged into
 // LDS: every trip reads the medium record (transform, bbox, majorant,
