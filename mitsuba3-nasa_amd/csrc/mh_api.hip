@@ -38,6 +38,7 @@ using namespace mh;
 namespace {
 
 thread_local std::string g_error;
+thread_local bool g_call_issued = false;  // the current entry point has passed its argument checks
 
 int set_error(int code, const std::string &msg) {
     g_error = msg;
@@ -98,7 +99,7 @@ struct mh_scene {
     bool own_stream = false;
     DScene S{};
     // device buffers
-    DevBuf nodes, nodes4, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
+    DevBuf nodes, nodes4, primsc, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, film4, alpha_px, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     std::vector<uint8_t> meta_host;  // the bytes last uploaded to grad_meta (upload_slots)
@@ -440,16 +441,28 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     // wide BVH for the stream engine when the BVH lives in global memory
     // (mh_bvh.cpp collapse_bvh4; MH_BVH4=0 keeps BVH2 everywhere)
     S.nodes4 = nullptr;
+    S.qnodes = nullptr;
+    S.primsc = nullptr;
     {
-        const char *e4 = getenv("MH_BVH4");
+        // the float BVH4 (round 1); MH_BVH4Q=1: the quantised BVH4 + compact
+        // primitives (round 4, measured slower so far: DESIGN.md §3);
+        // MH_BVH4=0: BVH2
+        const char *e4 = getenv("MH_BVH4"), *eq = getenv("MH_BVH4Q");
         if (S.lds_bytes_bvh == 0 && bvh.n_prims > 64 && !(e4 && !strcmp(e4, "0"))) {
-            std::vector<uint8_t> n4;
+            std::vector<uint8_t> n4, pc;
             uint32_t cnt4 = 0, depth4 = 0;
-            collapse_bvh4(bvh, n4, cnt4, depth4);
+            const bool quant = (eq && !strcmp(eq, "1")) && build_qbvh4(bvh, n4, pc, cnt4, depth4);
+            if (!quant) collapse_bvh4(bvh, n4, cnt4, depth4);
             const uint32_t stack4 = 3u * depth4 + 2u;
             if ((size_t)std::max(S.stack_size, stack4) * 256 * 4 <= 65536 &&
-                upload(s->nodes4, n4.data(), n4.size(), st) == hipSuccess) {
-                S.nodes4 = reinterpret_cast<const Node4 *>(s->nodes4.ptr);
+                upload(s->nodes4, n4.data(), n4.size(), st) == hipSuccess &&
+                (!quant || upload(s->primsc, pc.data(), pc.size(), st) == hipSuccess)) {
+                if (quant) {
+                    S.qnodes = reinterpret_cast<const QNode4 *>(s->nodes4.ptr);
+                    S.primsc = reinterpret_cast<const PrimC *>(s->primsc.ptr);
+                } else {
+                    S.nodes4 = reinterpret_cast<const Node4 *>(s->nodes4.ptr);
+                }
                 S.stack_size = std::max(S.stack_size, stack4);
             }
         }
@@ -475,9 +488,10 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
 
 int mh_scene_destroy(mh_scene *s) {
     if (!s) return MH_OK;
+    if (s->comm) comm_attach(s->comm, -1);
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
+    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->primsc, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word, &s->bmp_fx,
@@ -727,13 +741,31 @@ static int reduce_result(mh_scene *s, uint32_t flags, float *buf, uint64_t count
     return comm_reduce_one(s->comm, s->device, buf, count, st, root);
 }
 
+// The waits of a call whose collectives are in flight: with MH_FLAG_REDUCE a
+// deadline-bounded poll that also watches the communicator's async error and
+// aborts it on a failure (mh_comm.cpp comm_wait), so a rank whose peer failed
+// before issuing its collective returns an error instead of hanging in
+// hipStreamSynchronize; otherwise a plain stream sync.
+static hipError_t wait_stream(mh_scene *s, uint32_t flags, hipStream_t st) {
+    if (wants_reduce(flags) && s->comm) return comm_wait(s->comm, st, "collective call") == MH_OK ? hipSuccess : hipErrorLaunchTimeOut;
+    return hipStreamSynchronize(st);
+}
+#define MH_WAIT(s, flags, st)                                                                         \
+    do {                                                                                              \
+        if (wants_reduce(flags) && (s)->comm) {                                                       \
+            if (int _rc = comm_wait((s)->comm, st, __func__)) return _rc;                             \
+        } else {                                                                                      \
+            MH_HIP(hipStreamSynchronize(st));                                                         \
+        }                                                                                             \
+    } while (0)
+
 // MH_FLAG_DEVICE_POINTERS | MH_FLAG_NO_SYNC without stats: nothing is read
 // back to the host, so the call returns with its work enqueued on the stream
 static bool async_call(uint32_t flags, const mh_stats *stats) {
     return (flags & MH_FLAG_DEVICE_POINTERS) && (flags & MH_FLAG_NO_SYNC) && !stats;
 }
 
-int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
               uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
     ScopedPhase phase_("Render");
     if (!s || !in || !film_rgbw) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: NULL argument");
@@ -749,6 +781,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     int rc = make_layout(s, spp, spp_begin, spp_end, L, ad);
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
+    g_call_issued = true;  // past argument validation: a failure from here aborts the communicator
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
     // film storage: RGBW, or R G B A W for alpha films; the kernels splat into
@@ -868,7 +901,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     // enqueued on the scene's stream, as a stream-ordered library op does
     if (async_call(flags, stats)) return MH_OK;
     if (!stats && !getenv("MH_VW_DEBUG")) {  // nothing to read back: the call's own sync + the bounds word
-        MH_HIP(hipStreamSynchronize(st));
+        MH_WAIT(s, flags, st);
         return check_bounds_counter(s, "mh_render");
     }
     unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
@@ -882,7 +915,7 @@ int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
     unsigned long long iv[2] = {0, 0};  // [kCtrInvalid], [kCtrBounds]
     static_assert(kCtrBounds == kCtrInvalid + 1, "one read-back of both words");
     MH_HIP(hipMemcpyAsync(iv, invalid, sizeof(iv), hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));  // the stats counters are read back
+    MH_WAIT(s, flags, st);  // the stats counters are read back
     n_invalid = iv[0];
     if (iv[1])
         return set_error(MH_ERR_HIP, "mh_render: " + std::to_string(iv[1]) +
@@ -1025,7 +1058,7 @@ int mh_develop(mh_scene *s, const float *film_rgbw, float *image_rgb, uint32_t f
 // ---------------------------------------------------------------------------
 // PRB backward
 // ---------------------------------------------------------------------------
-int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
+static int prb_weights_impl(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
                    float *weights, uint32_t flags) {
     ScopedPhase phase_("ImageBlockPut");
     if (!s || !weights) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_prb_weights: NULL argument");
@@ -1035,6 +1068,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
+    g_call_issued = true;  // past argument validation: a failure from here aborts the communicator
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
     float *w = weights;
@@ -1052,7 +1086,7 @@ int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin,
     if (int rc = reduce_result(s, flags, w, n_px, st, false)) return rc;
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
         MH_HIP(hipMemcpyAsync(weights, w, n_px * 4, hipMemcpyDeviceToHost, st));
-    if (!async_call(flags, nullptr)) MH_HIP(hipStreamSynchronize(st));
+    if (!async_call(flags, nullptr)) MH_WAIT(s, flags, st);
     return MH_OK;
 }
 
@@ -1209,7 +1243,7 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     return hipSuccess;
 }
 
-int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
+static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
                        uint32_t spp_begin, uint32_t spp_end, const float *grad_in,
                        const float *weights, uint32_t n_params, const uint32_t *param_tex,
                        float *const *grads, uint32_t flags, mh_stats *stats) {
@@ -1228,6 +1262,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
+    g_call_issued = true;  // past argument validation: a failure from here aborts the communicator
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
     const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
@@ -1348,7 +1383,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     auto fx_between = [&](GradArgs &gp) -> hipError_t {
         uint32_t mb[1 + kMaxRgbParams] = {};
         hipError_t e = hipMemcpyAsync(mb, s->fx_word.ptr, sizeof(mb), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = wait_stream(s, flags, st);
         if (e != hipSuccess) return e;
         const int S0 = fx_exp(mb[0]);
         fx_inv = std::ldexp(1.0, -S0);
@@ -1371,12 +1406,12 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     auto fx_small_fold = [&]() -> hipError_t {
         long long w[3 * kMaxRgbParams];
         hipError_t e = hipMemcpyAsync(w, s->fx_word.as<uint8_t>() + 192, sizeof(w), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = wait_stream(s, flags, st);
         for (uint32_t k = 0; e == hipSuccess && k < n_rgb; ++k) {
             float v[3];
             for (int c = 0; c < 3; ++c) v[c] = (float)((double)w[3 * k + c] * fx_small_inv[k]);
             e = hipMemcpyAsync(bufs[k], v, std::min<size_t>(3, (counts[k] + 3) / 4 * 4) * 4, hipMemcpyHostToDevice, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e == hipSuccess) e = wait_stream(s, flags, st);
         }
         return e;
     };
@@ -1518,7 +1553,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             MH_HIP(launch_vol_sched_bwd_replays(s->S, *in, lm0, s->S.sampler_seed + seed, n, bw,
                                                 s->counters.as<unsigned long long>(), st));
             if (getenv("MH_VW_DEBUG")) {
-                MH_HIP(hipStreamSynchronize(st));
+                MH_WAIT(s, flags, st);
                 if (int rc2 = print_vs_phases(s)) return rc2;
                 uint32_t oc[3];
                 MH_HIP(hipMemcpy(oc, bw.ovf_count, sizeof(oc), hipMemcpyDeviceToHost));
@@ -1572,7 +1607,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         } else {
             host_tmp.resize(c);
             MH_HIP(hipMemcpyAsync(host_tmp.data(), bufs[slot], c * 4, hipMemcpyDeviceToHost, st));
-            MH_HIP(hipStreamSynchronize(st));
+            MH_WAIT(s, flags, st);
             for (size_t i = 0; i < c; ++i) grads[k][i] += host_tmp[i];
         }
     }
@@ -1587,7 +1622,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         return MH_OK;
     };
     if (!stats) {
-        MH_HIP(hipStreamSynchronize(st));
+        MH_WAIT(s, flags, st);
         return check_lost();
     }
     unsigned long long ctr[2] = {0, 0};
@@ -1596,7 +1631,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(hipMemcpyAsync(wctr.data(), s->wf_ctr.ptr, wctr.size() * 4, hipMemcpyDeviceToHost, st));
     else
         MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
+    MH_WAIT(s, flags, st);
     if (int rc_lost = check_lost()) return rc_lost;
     if (wavefront) {
         const size_t per_bounce = wf_ctr_words / (in->max_depth + 1), nseg = per_bounce / 32;
@@ -1632,7 +1667,7 @@ int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
 // ---------------------------------------------------------------------------
 // Forward-mode derivative: RBIntegrator.render_forward (common.py:696-826)
 // ---------------------------------------------------------------------------
-int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+static int render_forward_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
                       uint32_t spp_end, uint32_t n_params, const uint32_t *param_tex, const float *const *tangents,
                       float *film_rgbw, uint32_t flags, mh_stats *stats) {
     ScopedPhase phase_("RenderForward");
@@ -1649,6 +1684,7 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);  // prepare(): one wavefront of <= 2^32
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
+    g_call_issued = true;  // past argument validation: a failure from here aborts the communicator
     hipStream_t st = s->stream;
     const bool dev = flags & MH_FLAG_DEVICE_POINTERS;
     Slots P;
@@ -1733,12 +1769,12 @@ int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint3
     if (!dev) MH_HIP(hipMemcpyAsync(film_rgbw, film, film_bytes, hipMemcpyDeviceToHost, st));
     if (async_call(flags, stats)) return MH_OK;
     if (!stats) {
-        MH_HIP(hipStreamSynchronize(st));
+        MH_WAIT(s, flags, st);
         return check_bounds_counter(s, "mh_render_forward");
     }
     unsigned long long ctr[2] = {0, 0};
     MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
-    MH_HIP(hipStreamSynchronize(st));
+    MH_WAIT(s, flags, st);
     if (int rc = check_bounds_counter(s, "mh_render_forward")) return rc;
     if (stats) {
         float ms = 0.f;
@@ -1844,6 +1880,68 @@ int mh_trace_shadow(mh_scene *s, uint64_t n, const float *rays, uint32_t *occlud
 // (src/render/integrator.cpp:276-390): its sample loop is cut into per-device
 // slabs of every pixel, whose union is sample-identical to one render.
 // ===========================================================================
+// The entry points with in-call collectives: a call that fails with
+// MH_FLAG_REDUCE aborts the scene's communicator (comm_abort), since it has
+// issued only part of the call's collectives and its peers' streams wait on
+// the rest: their waits then end in an error (comm_wait), and later
+// collectives on this communicator fail at once instead of pairing with a
+// peer's different collective.
+static int abort_on_failure(mh_scene *s, uint32_t flags, int rc) {
+    const bool issued = g_call_issued;  // argument errors (before any work) leave the communicator usable
+    g_call_issued = false;
+#ifdef MH_DEBUG
+    // the debug build's device bounds guards (MH_GUARD) fail the call
+    if (rc == MH_OK && issued && s) {
+        (void)hipSetDevice(s->device);
+        unsigned long long g[2][kGuardCount] = {};
+        if (hipDeviceSynchronize() != hipSuccess || guard_read_wf(g[0]) != hipSuccess || guard_read_k(g[1]) != hipSuccess)
+            rc = set_error(MH_ERR_HIP, "MH_DEBUG: the device guard counters could not be read");
+        static const char *what[kGuardCount] = {"queue item beyond its segment", "path id beyond the chunk",
+                                                "appended slot beyond its segment", "sample-plane index beyond the plane",
+                                                "generated pixel outside the film", "LDS accumulator index beyond its size", "", ""};
+        for (int k = 0; rc == MH_OK && k < kGuardCount; ++k)
+            if (g[0][k] + g[1][k])
+                rc = set_error(MH_ERR_HIP, std::string("MH_DEBUG device guard: ") + what[k] + " (" +
+                                               std::to_string(g[0][k] + g[1][k]) + " lanes)");
+    }
+#endif
+    if (rc != MH_OK && issued && s && s->comm && wants_reduce(flags)) {
+        const std::string why = g_error;
+        comm_abort(s->comm);
+        set_error(rc, why + " (the scene's communicator was aborted)");
+    }
+    return rc;
+}
+
+int mh_render(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+              uint32_t spp_end, float *film_rgbw, uint32_t flags, mh_stats *stats) {
+    g_call_issued = false;
+    return abort_on_failure(s, flags, render_impl(s, in, seed, spp, spp_begin, spp_end, film_rgbw, flags, stats));
+}
+
+int mh_prb_weights(mh_scene *s, uint32_t seed, uint32_t spp, uint32_t spp_begin, uint32_t spp_end,
+                   float *weights, uint32_t flags) {
+    g_call_issued = false;
+    return abort_on_failure(s, flags, prb_weights_impl(s, seed, spp, spp_begin, spp_end, weights, flags));
+}
+
+int mh_render_backward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp,
+                       uint32_t spp_begin, uint32_t spp_end, const float *grad_in,
+                       const float *weights, uint32_t n_params, const uint32_t *param_tex,
+                       float *const *grads, uint32_t flags, mh_stats *stats) {
+    g_call_issued = false;
+    return abort_on_failure(s, flags, render_backward_impl(s, in, seed, spp, spp_begin, spp_end, grad_in, weights,
+                                                           n_params, param_tex, grads, flags, stats));
+}
+
+int mh_render_forward(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
+                      uint32_t spp_end, uint32_t n_params, const uint32_t *param_tex, const float *const *tangents,
+                      float *film_rgbw, uint32_t flags, mh_stats *stats) {
+    g_call_issued = false;
+    return abort_on_failure(s, flags, render_forward_impl(s, in, seed, spp, spp_begin, spp_end, n_params, param_tex,
+                                                          tangents, film_rgbw, flags, stats));
+}
+
 int mh_scene_set_comm(mh_scene *s, mh_comm *comm) {
     if (!s) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_set_comm: NULL scene");
     if (comm) {
@@ -1852,7 +1950,9 @@ int mh_scene_set_comm(mh_scene *s, mh_comm *comm) {
         if (dev != s->device)
             return set_error(MH_ERR_INVALID_ARGUMENT, "mh_scene_set_comm: the communicator's device is not the scene's");
     }
+    if (s->comm) comm_attach(s->comm, -1);
     s->comm = comm;
+    if (comm) comm_attach(comm, +1);
     return MH_OK;
 }
 

@@ -474,4 +474,171 @@ void collapse_bvh4(const BvhOut &b2, std::vector<uint8_t> &nodes4, uint32_t &n4,
     memcpy(nodes4.data(), c.out.data(), nodes4.size());
 }
 
+// ---------------------------------------------------------------------------
+// Quantised wide BVH (round 4).  The stream engine on a large mesh is bound
+// by dependent node / primitive fetches from the Infinity Cache, so the bytes
+// per fetch and the lines a ray touches are what to cut:
+//  - 64-B nodes (QNode4) instead of 128-B Node4: child boxes as 8-bit
+//    offsets in a per-node power-of-two grid;
+//  - the inner children of a node are stored contiguously, parents before
+//    children, depth first over sibling groups, so a node's children (the
+//    next fetch) sit in one or two cache lines;
+//  - 48-B primitive records (PrimC) instead of 64 B.
+// Conservative by construction: every decoded bound fma(q, 2^e, o) computed
+// in float, exactly as the device decodes it, is checked against the padded
+// float box of the BVH2 and moved outward until it contains it, so the slab
+// test enters every child the float boxes would (the hit set of a ray, and
+// with the closest-hit rule its result, do not change).
+// ---------------------------------------------------------------------------
+namespace {
+struct QBuild {
+    const Node *n2;
+    struct CNode { Entry e[4]; int k; uint32_t child[4]; };
+    std::vector<CNode> cn;   // collapsed nodes, in creation order
+    uint32_t depth = 0;
+    uint32_t collapse(uint32_t i, uint32_t d) {
+        depth = std::max(depth, d);
+        Collapser c;
+        c.n2 = n2;
+        CNode x;
+        c.entries_of(i, x.e);
+        int k = 2;
+        while (k < 4) {   // open the inner child of largest area (as collapse_bvh4)
+            int best = -1;
+            for (int j = 0; j < k; ++j)
+                if (x.e[j].inner != ~0u && (best < 0 || x.e[j].area() > x.e[best].area())) best = j;
+            if (best < 0) break;
+            Entry sub[2];
+            c.entries_of(x.e[best].inner, sub);
+            x.e[best] = sub[0];
+            x.e[k++] = sub[1];
+        }
+        x.k = k;
+        const uint32_t me = (uint32_t)cn.size();
+        cn.push_back(x);
+        for (int j = 0; j < k; ++j) {
+            const uint32_t ch = x.e[j].inner != ~0u ? collapse(x.e[j].inner, d + 1) : ~0u;
+            cn[me].child[j] = ch;
+        }
+        return me;
+    }
+};
+
+// one axis of a node: exponent byte and the 8-bit bounds of its k children
+// (lo rounded down, hi up, each checked on the float decode); false if the
+// extent cannot be represented (non-finite boxes)
+bool quantise_axis(float o, const float *lo, const float *hi, int k, uint32_t &ebyte, uint8_t *qlo, uint8_t *qhi) {
+    float ext = 0.f;
+    for (int c = 0; c < k; ++c) ext = std::max(ext, hi[c] - o);
+    if (!std::isfinite(ext) || !std::isfinite(o)) return false;
+    int e = -126;
+    if (ext > 0.f) {
+        int ex;
+        std::frexp((double)ext / 255.0, &ex);   // ext / 255 < 2^ex
+        e = std::max(-126, ex);
+    }
+    for (; e <= 127; ++e) {
+        const float s = std::ldexp(1.0f, e);
+        bool ok = true;
+        for (int c = 0; c < k && ok; ++c) {
+            double fl = std::floor(((double)lo[c] - (double)o) / (double)s);
+            int ql = (int)std::min(255.0, std::max(0.0, fl));
+            while (ql > 0 && std::fmaf((float)ql, s, o) > lo[c]) --ql;
+            double ch = std::ceil(((double)hi[c] - (double)o) / (double)s);
+            int qh = (int)std::min(256.0, std::max(0.0, ch));
+            while (qh <= 255 && std::fmaf((float)qh, s, o) < hi[c]) ++qh;
+            if (qh > 255 || std::fmaf((float)ql, s, o) > lo[c]) { ok = false; break; }
+            qlo[c] = (uint8_t)ql;
+            qhi[c] = (uint8_t)qh;
+        }
+        if (ok) { ebyte = (uint32_t)(e + 127); return true; }
+    }
+    return false;
+}
+}  // namespace
+
+bool build_qbvh4(const BvhOut &b2, std::vector<uint8_t> &qnodes, std::vector<uint8_t> &primsc, uint32_t &n4,
+                 uint32_t &depth4) {
+    qnodes.clear();
+    primsc.clear();
+    n4 = depth4 = 0;
+    if (b2.n_nodes == 0 || b2.n_prims >= (1u << 26)) return false;
+    QBuild qb;
+    qb.n2 = reinterpret_cast<const Node *>(b2.nodes.data());
+    qb.cn.reserve(b2.n_nodes / 2 + 1);
+    qb.collapse(0, 1);
+    const uint32_t n = (uint32_t)qb.cn.size();
+    // children-contiguous depth-first order: the root, then each node's inner
+    // children as one group, then the groups below the first child, ...
+    std::vector<uint32_t> pos(n, ~0u);
+    pos[0] = 0;
+    uint32_t next = 1;
+    std::vector<uint32_t> todo{0};   // nodes whose children are not placed yet (a stack: depth first)
+    while (!todo.empty()) {
+        const uint32_t c = todo.back();
+        todo.pop_back();
+        const QBuild::CNode &x = qb.cn[c];
+        for (int j = 0; j < x.k; ++j)
+            if (x.child[j] != ~0u) pos[x.child[j]] = next++;
+        for (int j = x.k - 1; j >= 0; --j)
+            if (x.child[j] != ~0u) todo.push_back(x.child[j]);
+    }
+    std::vector<QNode4> out(n);
+    for (uint32_t c = 0; c < n; ++c) {
+        const QBuild::CNode &x = qb.cn[c];
+        QNode4 q;
+        memset(&q, 0, sizeof(q));
+        float o[3];
+        for (int a = 0; a < 3; ++a) {
+            o[a] = FLT_MAX;
+            for (int j = 0; j < x.k; ++j) o[a] = std::min(o[a], x.e[j].lo[a]);
+        }
+        uint32_t eb[3];
+        uint8_t ql[3][4] = {}, qh[3][4] = {};
+        for (int a = 0; a < 3; ++a) {
+            float lo[4], hi[4];
+            for (int j = 0; j < x.k; ++j) { lo[j] = x.e[j].lo[a]; hi[j] = x.e[j].hi[a]; }
+            if (!quantise_axis(o[a], lo, hi, x.k, eb[a], ql[a], qh[a])) return false;
+        }
+        q.ox = o[0]; q.oy = o[1]; q.oz = o[2];
+        q.ebits = eb[0] | eb[1] << 8 | eb[2] << 16;
+        uint32_t lo32[3] = {0, 0, 0}, hi32[3] = {0, 0, 0};
+        uint32_t ref[4];
+        for (int j = 0; j < 4; ++j) {
+            if (j >= x.k) { ref[j] = kEmptyRef; continue; }   // empty slot: rejected by its ref
+            for (int a = 0; a < 3; ++a) {
+                lo32[a] |= (uint32_t)ql[a][j] << (8 * j);
+                hi32[a] |= (uint32_t)qh[a][j] << (8 * j);
+            }
+            const Entry &e = x.e[j];
+            ref[j] = e.inner == ~0u ? (kLeafRef | (e.first << 5) | e.count) : pos[x.child[j]];
+        }
+        q.qlo[0] = lo32[0]; q.qlo[1] = lo32[1]; q.qlo[2] = lo32[2];
+        q.qhi_x = hi32[0]; q.qhi_y = hi32[1]; q.qhi_z = hi32[2];
+        for (int j = 0; j < 4; ++j) q.ref[j] = ref[j];
+        out[pos[c]] = q;
+    }
+    // compact primitive records, same (leaf) order as Prim
+    const Prim *P = reinterpret_cast<const Prim *>(b2.prims.data());
+    std::vector<PrimC> pc(b2.n_prims);
+    for (uint32_t i = 0; i < b2.n_prims; ++i) {
+        PrimC &r = pc[i];
+        memset(&r, 0, sizeof(r));
+        const Prim &p = P[i];
+        r.v0x = p.a.x; r.v0y = p.a.y; r.v0z = p.a.z;
+        r.e1x = p.b.x; r.e1y = p.b.y; r.e1z = p.b.z;
+        r.e2x = p.c.x; r.e2y = p.c.y; r.e2z = p.c.z;
+        r.key = p.info.w;
+        r.prim = p.info.y;
+        r.shape = p.info.x | (p.info.z == MH_SHAPE_RECTANGLE ? kPrimCRect : 0u);
+    }
+    n4 = n;
+    depth4 = qb.depth;
+    qnodes.resize(sizeof(QNode4) * n);
+    memcpy(qnodes.data(), out.data(), qnodes.size());
+    primsc.resize(sizeof(PrimC) * pc.size());
+    memcpy(primsc.data(), pc.data(), primsc.size());
+    return true;
+}
+
 }  // namespace mh

@@ -16,8 +16,11 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -27,6 +30,8 @@
 struct mh_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    int users = 0;         // scenes this communicator is attached to (mh_scene_set_comm)
+    bool aborted = false;  // aborted after a failure: every later collective fails fast
 };
 
 namespace {
@@ -44,6 +49,7 @@ struct Rccl {
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
     decltype(&ncclCommGetAsyncError) async_error = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
 };
 
 Rccl &rccl() {
@@ -76,6 +82,7 @@ Rccl &rccl() {
         bind(R.group_end, "ncclGroupEnd");
         bind(R.error_string, "ncclGetErrorString");
         bind(R.async_error, "ncclCommGetAsyncError");
+        bind(R.abort, "ncclCommAbort");
         R.ok = all;
     });
     return R;
@@ -155,6 +162,10 @@ int mh_comm_create_all(int ndev, const int *devices, mh_comm **out) {
 
 int mh_comm_destroy(mh_comm *c) {
     if (!c) return MH_OK;
+    if (c->users > 0)  // a scene still holds it (mh_scene_set_comm): destroying it would leave the scene dangling
+        return mh_report_error(MH_ERR_INVALID_ARGUMENT, "mh_comm_destroy: the communicator is still attached to " +
+                                                            std::to_string(c->users) +
+                                                            " scene(s); detach them first (mh_scene_set_comm(scene, NULL))");
     if (c->comm && rccl().ok) {
         (void)hipSetDevice(c->device);
         (void)rccl().destroy(c->comm);
@@ -178,6 +189,10 @@ int mh_comm_reduce(mh_comm *const *comms, int n, float *const *bufs, uint64_t co
         if (!comms[i] || !bufs[i]) return mh_report_error(MH_ERR_INVALID_ARGUMENT, "mh_comm_reduce: NULL entry");
     if (root >= comms[0]->nranks)
         return mh_report_error(MH_ERR_INVALID_ARGUMENT, "mh_comm_reduce: root out of [0, nranks)");
+    for (int i = 0; i < n; ++i)
+        if (comms[i]->aborted)
+            return mh_report_error(MH_ERR_HIP, "mh_comm_reduce: the communicator was aborted after an earlier failure "
+                                               "of a collective call (create a new one)");
     if (count == 0) return MH_OK;
     if (int rc = need_rccl("mh_comm_reduce")) return rc;
     Rccl &R = rccl();
@@ -204,6 +219,62 @@ int mh_comm_reduce(mh_comm *const *comms, int n, float *const *bufs, uint64_t co
 }
 
 }  // extern "C"
+
+// ---- failure handling of the in-call collectives (mh_api.hip) ----
+// A rank that fails inside a MH_FLAG_REDUCE call returns before it has issued
+// every collective of the call, while its peers have queued theirs: the
+// peers' streams can then never drain.  So (1) a rank waits for its stream
+// through comm_wait, which polls the stream and the communicator's async error
+// with a deadline (MH_COMM_TIMEOUT_S, default 1800 s) instead of blocking in
+// hipStreamSynchronize, and (2) a rank whose call fails aborts its
+// communicator (comm_abort), as does a rank whose wait runs out: every rank
+// then returns an error, and every later collective on that communicator
+// fails at once instead of pairing with the wrong collective of a peer.
+void comm_abort(mh_comm *c) {
+    if (!c || c->aborted) return;
+    c->aborted = true;
+    if (c->comm && rccl().ok) {
+        (void)hipSetDevice(c->device);
+        (void)rccl().abort(c->comm);
+    }
+    c->comm = nullptr;
+}
+
+int comm_wait(mh_comm *c, hipStream_t st, const char *api) {
+    static const double timeout_s = [] {
+        const char *e = getenv("MH_COMM_TIMEOUT_S");
+        return e ? std::max(0.001, atof(e)) : 1800.0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 0;; ++it) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) return MH_OK;
+        if (q != hipErrorNotReady) {
+            comm_abort(c);
+            return mh_report_error(MH_ERR_HIP, std::string(api) + ": " + hipGetErrorString(q));
+        }
+        if (c && !c->aborted && c->comm && rccl().ok) {
+            ncclResult_t r = ncclSuccess;
+            if (rccl().async_error(c->comm, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
+                comm_abort(c);
+                return mh_report_error(MH_ERR_HIP, std::string(api) + ": a collective failed: " + rccl().error_string(r));
+            }
+        }
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt > timeout_s) {
+            comm_abort(c);
+            return mh_report_error(MH_ERR_HIP, std::string(api) + ": the call's collectives did not complete within " +
+                                                   std::to_string(timeout_s) + " s (a peer rank failed?); "
+                                                   "the communicator was aborted");
+        }
+        if (it < 2000) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+void comm_attach(mh_comm *c, int delta) {
+    if (c) c->users += delta;
+}
 
 // in-call reduction of one rank (mh_api.hip: MH_FLAG_REDUCE / MH_FLAG_REDUCE_ROOT)
 int comm_reduce_one(mh_comm *c, int device, float *buf, uint64_t count, hipStream_t st, int root) {

@@ -17,6 +17,31 @@ namespace mh {
 
 #define MH_DEV __device__ __forceinline__
 
+// Debug build (tools/build_variant.sh <name> -DMH_DEBUG): device bounds
+// guards.  A failed check counts into this translation unit's g_mh_guard[k];
+// the entry points read every unit's counters after the call (guard_read_*)
+// and fail it when one is nonzero.  Release builds compile them away.
+enum {
+    kGuardQueueSlot = 0,   // a queue item beyond its segment's capacity
+    kGuardPathId = 1,      // a path id beyond the chunk's paths
+    kGuardAppendSlot = 2,  // a compacted (appended) slot beyond the segment's capacity
+    kGuardPlane = 3,       // a sample-plane index beyond the plane
+    kGuardPixel = 4,       // a generated sample's pixel outside the film
+    kGuardLds = 5,         // an LDS texel accumulator index beyond the accumulator
+    kGuardCount = 8
+};
+#ifdef MH_DEBUG
+static __device__ unsigned long long g_mh_guard[kGuardCount];
+#define MH_GUARD(cond, k)                                           \
+    do {                                                            \
+        if (!(cond)) atomicAdd(&g_mh_guard[(k)], 1ull);             \
+    } while (0)
+#else
+#define MH_GUARD(cond, k) \
+    do {                  \
+    } while (0)
+#endif
+
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInvPi = 0.31830988618379067154f;
 constexpr float kRayEps = 1500.0f * 5.9604644775390625e-08f;  // core/math.h:18-23
@@ -46,6 +71,32 @@ struct alignas(16) Prim {       // 64 B primitive record
     float4 a, b, c;             // triangle: v0, e1 = v1 - v0, e2 = v2 - v0; rectangle: to_object rows
     uint4 info;                 // x: shape, y: prim index (face; ~0 for rectangles), z: type, w: scene-order key
 };
+
+// 64 B: the quantised wide node of the stream engine (round 4; mh_bvh.cpp
+// build_qbvh4).  Child c's box on axis a is [o_a + qlo_a[c] * s_a, o_a +
+// qhi_a[c] * s_a] with s_a = 2^(ebits byte a - 127), decoded by one fma per
+// bound (exact product, one rounding); the host picks each byte so that the
+// decoded float box contains the padded float box of the BVH2, so the slab
+// test stays conservative and hits stay bit-identical.  Byte c of qlo[a] /
+// qhi[a] is child c.  ref: as Node4.  A node's inner children are contiguous
+// (children-contiguous depth-first order).
+struct alignas(16) QNode4 {
+    float ox, oy, oz;
+    uint32_t ebits;
+    uint32_t qlo[3], qhi_x;
+    uint32_t qhi_y, qhi_z, pad0, pad1;
+    uint32_t ref[4];
+};
+
+// 48 B: the compact primitive record of the stream engine, in the leaf order
+// of Prim (same index): v0, e1, e2 of a triangle, the scene-order key, the
+// face index and the shape (kPrimCRect set for a rectangle, whose test reads
+// the full Prim of the same index).
+struct alignas(16) PrimC {
+    float v0x, v0y, v0z, e1x, e1y, e1z, e2x, e2y, e2z;
+    uint32_t key, prim, shape;
+};
+constexpr uint32_t kPrimCRect = 0x80000000u;
 
 struct DShape {                 // shading-time shape record
     uint32_t type, bsdf, emitter, face_offset;
@@ -103,6 +154,8 @@ struct DScene {                 // kernel argument (by value)
     const Node4 *nodes4;           // wide BVH of the stream engine (nullptr: BVH2 only)
     const uint2 *key_sp;           // scene-order key -> (shape, prim) (packet engine)
     const Prim *prim_pairs;        // interleaved pair records of the packet engine (mh_shading.hpp pp())
+    const QNode4 *qnodes;          // quantised wide BVH of the stream engine (nullptr: Node4 / BVH2)
+    const PrimC *primsc;           // its compact primitive records (with qnodes)
     uint32_t n_nodes, n_prims, n_emitters, environment;
     uint32_t n_media, camera_medium;
     uint32_t vol_flags;            // prbvolpath prepare_scene flags (kVol*)

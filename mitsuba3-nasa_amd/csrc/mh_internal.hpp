@@ -59,6 +59,10 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf 
 // BVH4 collapsed from a BVH2 (greedy: open the largest-area inner child until
 // four children); depth4 = max Node4 nesting
 void collapse_bvh4(const BvhOut &b2, std::vector<uint8_t> &nodes4, uint32_t &n4, uint32_t &depth4);
+// the same BVH4 quantised (QNode4, children-contiguous order) + compact
+// primitive records (PrimC); false when a box cannot be quantised
+bool build_qbvh4(const BvhOut &b2, std::vector<uint8_t> &qnodes, std::vector<uint8_t> &primsc, uint32_t &n4,
+                 uint32_t &depth4);
 
 // ---- kernel launchers (mh_kernels.hip) -------------------------------------
 size_t lds_bytes(const DScene &S, uint32_t block);
@@ -151,6 +155,10 @@ hipError_t launch_corner_gather(const float *corner, float *grad, const uint32_t
 hipError_t launch_corner_gather_fx(const long long *corner, float *grad, const uint32_t res[3], double inv_scale,
                                    hipStream_t st);
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
+#ifdef MH_DEBUG
+hipError_t guard_read_wf(unsigned long long *out);  // kGuardCount words each, read and reset
+hipError_t guard_read_k(unsigned long long *out);
+#endif
 hipError_t launch_develop(uint64_t n_px, const float *film, float *rgb, uint32_t fmt, hipStream_t st);
 hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, const LaneMap &lm,
                                uint32_t seed_value, uint64_t n, int coalesce,
@@ -216,3 +224,9 @@ hipError_t launch_volwave(const DScene &S, const IntegratorParams &in, const Lan
 int mh_report_error(int code, const std::string &msg);
 // one rank's in-call sum over its communicator (root < 0: all-reduce), stream-ordered on st
 int comm_reduce_one(mh_comm *c, int device, float *buf, uint64_t count, hipStream_t st, int root);
+// wait for st with a deadline, watching the communicator's async error (aborts it on a failure)
+int comm_wait(mh_comm *c, hipStream_t st, const char *api);
+// abort after a failed collective call (later collectives on it fail at once)
+void comm_abort(mh_comm *c);
+// scenes holding the communicator (mh_comm_destroy refuses while > 0)
+void comm_attach(mh_comm *c, int delta);

@@ -25,6 +25,15 @@ namespace mh {
 // ===========================================================================
 // Kernels
 // ===========================================================================
+// this wave's contiguous share of n items (the stream engine refills lanes
+// from it); wave-uniform
+MH_DEV void stream_wave_range(uint64_t n, uint32_t &r0, uint32_t &r1) {
+    const uint32_t waves = gridDim.x * (blockDim.x / 64u), w = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
+    const uint64_t per = (n + waves - 1) / waves;
+    r0 = (uint32_t)std::min<uint64_t>(n, (uint64_t)w * per);
+    r1 = (uint32_t)std::min<uint64_t>(n, (uint64_t)r0 + per);
+}
+
 template <bool InLds>
 __global__ void __launch_bounds__(256)
 k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__restrict__ t_out,
@@ -32,18 +41,18 @@ k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__r
                 uint32_t *__restrict__ shape_out, uint32_t *__restrict__ inst_out) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    // the OptiX payload (scene_optix.inl:602-657, optix/common.h:43-58):
+    // prim_index 0 for rectangles (rectangle.cuh:42) and for misses (the
+    // payload's initial value; the miss program sets only t and shape),
+    // prim_uv (0, 0) on a miss; no instancing: instance = null
+    auto load = [&](uint64_t i) {
         RayT r;
         r.o = v3(rays[i], rays[n + i], rays[2 * n + i]);
         r.d = v3(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
         r.maxt = fminf(rays[6 * n + i], kFloatMax);
-        Hit h;
-        traverse<false>(B.nodes, B.prims, B.stack, B.stride, r, h);
-        // the OptiX payload (scene_optix.inl:602-657, optix/common.h:43-58):
-        // prim_index 0 for rectangles (rectangle.cuh:42) and for misses (the
-        // payload's initial value; the miss program sets only t and shape),
-        // prim_uv (0, 0) on a miss; no instancing: instance = null
+        return r;
+    };
+    auto store = [&](uint64_t i, const Hit &h, bool) {
         const bool hit = h.shape != MH_INVALID;
         t_out[i] = h.t;
         u_out[i] = hit ? h.u : 0.f;
@@ -51,6 +60,20 @@ k_trace_closest(DScene S, uint64_t n, const float *__restrict__ rays, float *__r
         prim_out[i] = hit && h.prim != MH_INVALID ? h.prim : 0u;
         shape_out[i] = h.shape;
         if (inst_out) inst_out[i] = MH_INVALID;
+    };
+    if (!InLds && (B.qnodes || B.nodes4)) {
+        // a BVH in global memory: the wavefront's per-lane stream engine (the
+        // launcher keeps n < 2^32), items in contiguous per-wave ranges
+        uint32_t r0, r1;
+        stream_wave_range(n, r0, r1);
+        trace_stream_any<false>(B, r0, r1, load, store);
+        return;
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        Hit h;
+        traverse<false>(B.nodes, B.prims, B.stack, B.stride, load(i), h);
+        store(i, h, true);
     }
 }
 
@@ -59,14 +82,23 @@ __global__ void __launch_bounds__(256)
 k_trace_shadow(DScene S, uint64_t n, const float *__restrict__ rays, uint32_t *__restrict__ occ) {
     extern __shared__ uint4 lds[];
     LdsBvh B = stage_bvh<InLds>(S, lds);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    auto load = [&](uint64_t i) {
         RayT r;
         r.o = v3(rays[i], rays[n + i], rays[2 * n + i]);
         r.d = v3(rays[3 * n + i], rays[4 * n + i], rays[5 * n + i]);
         r.maxt = fminf(rays[6 * n + i], kFloatMax);
+        return r;
+    };
+    if (!InLds && (B.qnodes || B.nodes4)) {
+        uint32_t r0, r1;
+        stream_wave_range(n, r0, r1);
+        trace_stream_any<true>(B, r0, r1, load, [&](uint64_t i, const Hit &, bool f) { occ[i] = f ? 1u : 0u; });
+        return;
+    }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         Hit h;
-        occ[i] = traverse<true>(B.nodes, B.prims, B.stack, B.stride, r, h) ? 1u : 0u;
+        occ[i] = traverse<true>(B.nodes, B.prims, B.stack, B.stride, load(i), h) ? 1u : 0u;
     }
 }
 
@@ -724,6 +756,16 @@ k_prbvol_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value
 // ===========================================================================
 static inline uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
+#ifdef MH_DEBUG
+// this unit's device guard counters (mh_device.hpp MH_GUARD), read and reset
+hipError_t guard_read_k(unsigned long long *out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mh_guard), sizeof(g_mh_guard));
+    const unsigned long long z[kGuardCount] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_mh_guard), z, sizeof(z));
+    return e;
+}
+#endif
+
 size_t lds_bytes(const DScene &S, uint32_t block) {
     return (size_t)S.lds_bytes_bvh + (size_t)S.stack_size * block * sizeof(uint32_t);
 }
@@ -736,6 +778,7 @@ hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *r
     if (g == 0) return hipSuccess;
     size_t sh = lds_bytes(S, bs);
     const bool lds = S.lds_bytes_bvh != 0;
+    if (!lds && (S.qnodes || S.nodes4) && n >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit stream items
     if (shadow) {
         if (lds) hipLaunchKernelGGL(k_trace_shadow<true>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
         else hipLaunchKernelGGL(k_trace_shadow<false>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);

@@ -24,8 +24,7 @@ struct RayT {
 };
 
 // Moeller-Trumbore (render/mesh.h:430-453), e1/e2 precomputed bit-identically
-MH_DEV bool tri_test(const Prim &p, const RayT &r, float &t, float &u, float &v) {
-    V3 v0 = v3(p.a.x, p.a.y, p.a.z), e1 = v3(p.b.x, p.b.y, p.b.z), e2 = v3(p.c.x, p.c.y, p.c.z);
+MH_DEV bool tri_test_v(V3 v0, V3 e1, V3 e2, const RayT &r, float &t, float &u, float &v) {
     V3 pvec = cross(r.d, e2);
     float inv_det = rcp(dot(e1, pvec));
     V3 tvec = r.o - v0;
@@ -36,6 +35,9 @@ MH_DEV bool tri_test(const Prim &p, const RayT &r, float &t, float &u, float &v)
     // Non-short-circuit masks: every lane evaluates the whole test, so the
     // compiler emits v_cmp/s_and instead of exec-mask branches.
     return (u >= 0.f) & (u <= 1.f) & (v >= 0.f) & (u + v <= 1.f) & (t >= 0.f) & (t <= r.maxt);
+}
+MH_DEV bool tri_test(const Prim &p, const RayT &r, float &t, float &u, float &v) {
+    return tri_test_v(v3(p.a.x, p.a.y, p.a.z), v3(p.b.x, p.b.y, p.b.z), v3(p.c.x, p.c.y, p.c.z), r, t, u, v);
 }
 
 // Rectangle::ray_intersect_preliminary_impl (shapes/rectangle.cpp:446-470)
@@ -164,6 +166,8 @@ MH_DEV bool traverse(const Node *nodes, const Prim *prims, uint32_t *stk, uint32
 struct LdsBvh {
     const Node *nodes;
     const Node4 *nodes4;  // wide BVH (global memory), nullptr when absent
+    const QNode4 *qnodes; // quantised wide BVH + compact primitives (global memory), nullptr when absent
+    const PrimC *primsc;
     const Prim *prims;
     uint32_t *stack;  // this lane's column
     uint32_t stride;
@@ -193,6 +197,8 @@ MH_DEV LdsBvh stage_bvh(const DScene &S, uint4 *lds) {
         b.prims = S.prims;
     }
     b.nodes4 = InLds ? nullptr : S.nodes4;
+    b.qnodes = InLds ? nullptr : S.qnodes;
+    b.primsc = InLds ? nullptr : S.primsc;
     b.stack = reinterpret_cast<uint32_t *>(lds + nq) + threadIdx.x;
     b.stride = blockDim.x;
     return b;
@@ -402,6 +408,59 @@ MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, uint32_t *stk, uin
     trav_take(t, rc[0]);
 }
 
+// the same step on the quantised node (QNode4, 64 B = four 16-B loads): each
+// child bound decoded by one fma (v_cvt_f32_ubyte of its byte, the node's
+// power-of-two scale, the node's origin), then the float slab test of
+// trav_inner_step4 on the decoded box
+MH_DEV float qscale(uint32_t ebits, uint32_t a) { return __uint_as_float(((ebits >> (8u * a)) & 0xffu) << 23); }
+MH_DEV float qbyte(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); }
+MH_DEV void trav_inner_step_q(TravLane &t, const QNode4 *nodes, uint32_t *stk, uint32_t stride) {
+    if (t.node == kNoNode) {
+        if (t.sp == 0) { t.node = kDone; return; }
+        --t.sp;
+        const uint32_t ref = stk[t.sp * stride];
+        trav_take(t, ref);
+        if (t.node == kNoNode || (t.node & kLeafBit)) return;
+    }
+    const uint4 *q = reinterpret_cast<const uint4 *>(nodes + t.node);
+    const uint4 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+    const float ox = __uint_as_float(w0.x), oy = __uint_as_float(w0.y), oz = __uint_as_float(w0.z);
+    const float sx = qscale(w0.w, 0), sy = qscale(w0.w, 1), sz = qscale(w0.w, 2);
+    const uint32_t rf[4] = {w3.x, w3.y, w3.z, w3.w};
+    float tc[4];
+    uint32_t rc[4];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float lx = __builtin_fmaf(qbyte(w1.x, c), sx, ox), hx = __builtin_fmaf(qbyte(w1.w, c), sx, ox);
+        const float ly = __builtin_fmaf(qbyte(w1.y, c), sy, oy), hy = __builtin_fmaf(qbyte(w2.x, c), sy, oy);
+        const float lz = __builtin_fmaf(qbyte(w1.z, c), sz, oz), hz = __builtin_fmaf(qbyte(w2.y, c), sz, oz);
+        const float a0 = __builtin_fmaf(lx, t.inv.x, -t.ood.x), b0 = __builtin_fmaf(hx, t.inv.x, -t.ood.x);
+        const float a1 = __builtin_fmaf(ly, t.inv.y, -t.ood.y), b1 = __builtin_fmaf(hy, t.inv.y, -t.ood.y);
+        const float a2 = __builtin_fmaf(lz, t.inv.z, -t.ood.z), b2 = __builtin_fmaf(hz, t.inv.z, -t.ood.z);
+        const float lo = fmaxf(fmaxf(fminf(a0, b0), fminf(a1, b1)), fmaxf(fminf(a2, b2), 0.f));
+        const float hi = fminf(fminf(fmaxf(a0, b0), fmaxf(a1, b1)), fminf(fmaxf(a2, b2), t.best));
+        const bool h = lo <= hi && rf[c] != 0xffffffffu;
+        tc[c] = h ? lo : __builtin_huge_valf();
+        rc[c] = rf[c];
+        cnt += h ? 1u : 0u;
+    }
+#define MH_CSWAP(i, j)                                                           \
+    {                                                                            \
+        const bool sw = tc[j] < tc[i];                                           \
+        const float ta = sw ? tc[j] : tc[i], tb = sw ? tc[i] : tc[j];            \
+        const uint32_t ra = sw ? rc[j] : rc[i], rb = sw ? rc[i] : rc[j];         \
+        tc[i] = ta; tc[j] = tb; rc[i] = ra; rc[j] = rb;                          \
+    }
+    MH_CSWAP(0, 1) MH_CSWAP(2, 3) MH_CSWAP(0, 2) MH_CSWAP(1, 3) MH_CSWAP(1, 2)
+#undef MH_CSWAP
+    if (cnt == 0) { t.node = kNoNode; return; }
+    if (cnt > 3) { stk[t.sp * stride] = rc[3]; ++t.sp; }
+    if (cnt > 2) { stk[t.sp * stride] = rc[2]; ++t.sp; }
+    if (cnt > 1) { stk[t.sp * stride] = rc[1]; ++t.sp; }
+    trav_take(t, rc[0]);
+}
+
 template <bool Shadow>
 MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
     RayT r{t.o, t.d, t.maxt};
@@ -418,9 +477,39 @@ MH_DEV void trav_leaf(TravLane &t, const Prim *prims) {
     if (t.node != kDone && t.node != kNoNode && (t.node & kLeafBit)) trav_take(t, t.node);
 }
 
+// the leaf on compact records (PrimC: three 16-B loads per triangle; a
+// rectangle reads its full Prim); the same tests and update rule as trav_leaf
+template <bool Shadow>
+MH_DEV void trav_leaf_c(TravLane &t, const PrimC *pc, const Prim *prims) {
+    RayT r{t.o, t.d, t.maxt};
+    for (uint32_t i = 0; i < t.nleaf; ++i) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(pc + t.leaf + i);
+        const uint4 a = q[0], b = q[1], c = q[2];
+        float tt, u, v;
+        bool ok;
+        if (c.w & kPrimCRect) {
+            ok = rect_test(prims[t.leaf + i], r, tt, u, v);
+        } else {
+            ok = tri_test_v(v3(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)),
+                            v3(__uint_as_float(a.w), __uint_as_float(b.x), __uint_as_float(b.y)),
+                            v3(__uint_as_float(b.z), __uint_as_float(b.w), __uint_as_float(c.x)), r, tt, u, v);
+        }
+        if (ok && (Shadow || (tt < t.hit.t) | ((tt == t.hit.t) & (c.y < t.hit.key)))) {
+            t.hit.t = tt; t.hit.u = u; t.hit.v = v; t.hit.prim = c.z; t.hit.shape = c.w & ~kPrimCRect; t.hit.key = c.y;
+            t.best = tt;
+            if (Shadow) { t.node = kDone; t.sp = 0; break; }
+        }
+    }
+    t.nleaf = 0;
+    if (t.node != kDone && t.node != kNoNode && (t.node & kLeafBit)) trav_take(t, t.node);
+}
+
+// node formats of the per-lane stream engine
+enum { kEngBvh2 = 0, kEngWide = 1, kEngQuant = 2 };
+
 // Traces items [r0, r1) of this wave.  load(item) -> RayT, store(item, hit,
 // found).  Must be called by all 64 lanes of the wave (uniform r0, r1).
-template <bool Shadow, bool Wide = false, class Load, class Store>
+template <bool Shadow, int Eng = kEngBvh2, class Load, class Store>
 MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, Store store) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool empty = B.nodes == nullptr;
@@ -436,12 +525,16 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
             const bool ready = !has || t.nleaf != 0 || t.node == kDone;
             if (!__any(inner) || __all(ready)) break;
             if (inner) {
-                if (Wide) trav_inner_step4(t, B.nodes4, B.stack, B.stride);
+                if (Eng == kEngQuant) trav_inner_step_q(t, B.qnodes, B.stack, B.stride);
+                else if (Eng == kEngWide) trav_inner_step4(t, B.nodes4, B.stack, B.stride);
                 else trav_inner_step(t, B.nodes, B.stack, B.stride);
             }
         }
         // grouped leaf phase
-        if (has && t.nleaf) trav_leaf<Shadow>(t, B.prims);
+        if (has && t.nleaf) {
+            if (Eng == kEngQuant) trav_leaf_c<Shadow>(t, B.primsc, B.prims);
+            else trav_leaf<Shadow>(t, B.prims);
+        }
         if (has && t.node == kNoNode && t.sp == 0 && t.nleaf == 0) t.node = kDone;
         // retire finished lanes and refill them from the wave's range
         const bool fin = has && t.node == kDone && t.nleaf == 0;
@@ -459,6 +552,15 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
         }
         fetched += (uint32_t)__popcll(m);
     }
+}
+
+// the stream engine on whichever node format the scene carries (quantised
+// BVH4, float BVH4, BVH2); B is wave-uniform, so the branch is scalar
+template <bool Shadow, class Load, class Store>
+MH_DEV void trace_stream_any(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, Store store) {
+    if (B.qnodes) trace_stream<Shadow, kEngQuant>(B, r0, r1, load, store);
+    else if (B.nodes4) trace_stream<Shadow, kEngWide>(B, r0, r1, load, store);
+    else trace_stream<Shadow, kEngBvh2>(B, r0, r1, load, store);
 }
 
 // ---------------------------------------------------------------------------
@@ -1617,9 +1719,7 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
         if (j >= tp.n) break;
         uint64_t base = tp.idx[j] - tx.data_offset;
         if (in_lds) {  // ds_add_f32 (an LDS-qualified pointer, not a flat atomic)
-#ifdef MH_DEBUG
-            assert(base + tx.channels <= g.lds_floats);
-#endif
+            MH_GUARD(base + tx.channels <= g.lds_floats, kGuardLds);
             // (not lds_add_grouped: the replay's lanes are divergent here)
             LdsFloat *l = (LdsFloat *)(buf + base);
             if (tx.channels == 3) {

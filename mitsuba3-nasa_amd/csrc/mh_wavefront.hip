@@ -110,6 +110,16 @@ static bool wf_unfused() {
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 uint32_t wf_counter_words(uint32_t n_bounces) { return kCtrStride * (n_bounces + 1); }
+
+#ifdef MH_DEBUG
+// this unit's device guard counters (mh_device.hpp MH_GUARD), read and reset
+hipError_t guard_read_wf(unsigned long long *out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mh_guard), sizeof(g_mh_guard));
+    const unsigned long long z[kGuardCount] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_mh_guard), z, sizeof(z));
+    return e;
+}
+#endif
 uint64_t wf_max_chunk() { return 1ull << kPidBits; }
 
 size_t wf_workspace_bytes(uint64_t cap) {
@@ -288,8 +298,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
         w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
     };
     if (Packet) trace_packet<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
-    else if (B.nodes4) trace_stream<false, true>(B, r0, r1, load, store);
-    else trace_stream<false>(B, r0, r1, load, store);
+    else trace_stream_any<false>(B, r0, r1, load, store);
 }
 
 // one iteration of PathIntegrator::sample for every queued path
@@ -477,6 +486,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         const uint32_t i = base + lane_id();
         const bool has = i < n;
         const uint32_t j = sbase + i;
+        MH_GUARD(!has || i < seg_cap, kGuardQueueSlot);
         bool alive = false, shadow = false;
         uint32_t pid = 0, depth = 0;
         RayT ray{v3(0, 0, 0), v3(0, 0, 1), -1.f}, sray{v3(0, 0, 0), v3(0, 0, 1), -1.f};
@@ -489,6 +499,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 pid = j;
                 uint32_t lane, px, py;
                 lane_of(lm, pid, lane, px, py);
+                MH_GUARD(px < S0.width && py < S0.height, kGuardPixel);
                 Pcg g;
                 if (pass == 0) {
                     g.seed(seed_value, lane);
@@ -512,6 +523,8 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 ray.d = v3(q1.x, q1.y, q1.z);
                 ray.maxt = q0.w;
             }
+            MH_GUARD(pid < n_total, kGuardPathId);
+            MH_GUARD(pid < plane, kGuardPlane);
         }
         const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has, recs, dscr);
 #ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
@@ -612,6 +625,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         // ---- compaction: the survivor's next-bounce state leaves registers
         // before the shadow trace (only L and the NEE product stay live across it)
         const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        MH_GUARD(!alive || slot - sbase < seg_cap, kGuardAppendSlot);
         const float rng_hi = __uint_as_float((uint32_t)(rng.state >> 32));
         if (alive) {
             w.pl(nxt, 0)[slot] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
@@ -667,8 +681,7 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
         out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
     };
     if (Packet) trace_packet<true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
-    else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
-    else trace_stream<true>(B, r0, r1, load, store);
+    else trace_stream_any<true>(B, r0, r1, load, store);
 }
 
 // ---------------------------------------------------------------------------
@@ -1191,6 +1204,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         for (int kk = 0; kk < NR; ++kk) Pp[kk][0] = Pp[kk][1] = Pp[kk][2] = 0.f;
         Pcg rng;
         const uint32_t j = sbase + i;
+        MH_GUARD(i >= n || i < seg_cap, kGuardQueueSlot);
         uint64_t gen_state = 0, gen_inc = 0;
         // Bm: running radiance, this vertex's Le / potential Lr_dir / record
         V3 Lrun = v3(0, 0, 0), Le_b = v3(0, 0, 0), Lr_pot = v3(0, 0, 0), D_pot = v3(0, 0, 0), q_ind = v3(0, 0, 0);
@@ -1202,6 +1216,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 pid = j;
                 uint32_t lane, px, py;
                 lane_of(lm, pid, lane, px, py);
+                MH_GUARD(px < S0.width && py < S0.height, kGuardPixel);
                 Pcg g;
                 g.seed(seed_value, lane);
                 const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
@@ -1226,6 +1241,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 ray.d = v3(w.dx[cur][j], w.dy[cur][j], w.dz[cur][j]);
                 ray.maxt = w.mt[cur][j];
             }
+            MH_GUARD(pid < gen.n_total, kGuardPathId);
         }
         const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n, recs, dscr);
         if (i < n) {
@@ -1360,6 +1376,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             alive = active_next;
         }
         const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        MH_GUARD(!alive || slot_n - sbase < seg_cap, kGuardAppendSlot);
         if (alive) {
             w.pd[nxt][slot_n] = pid | (depth << kPidBits);
             w.ox[nxt][slot_n] = ray.o.x; w.oy[nxt][slot_n] = ray.o.y; w.oz[nxt][slot_n] = ray.o.z;
@@ -1841,8 +1858,7 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
             }
     };
     if (Packet) trace_packet<true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
-    else if (B.nodes4) trace_stream<true, true>(B, r0, r1, load, store);
-    else trace_stream<true>(B, r0, r1, load, store);
+    else trace_stream_any<true>(B, r0, r1, load, store);
     flush_partial(acc, q);
 }
 

@@ -72,8 +72,11 @@ class Comm:
         return t
 
     def close(self):
+        """Destroy the communicator.  The library refuses while a scene still
+        holds it (mh_scene_set_comm); detach it first (scene_set_comm(scene,
+        None)) or release the scene."""
         if self._h:
-            A.lib().mh_comm_destroy(self._h)
+            A.check(A.lib().mh_comm_destroy(self._h))
             self._h = C.c_void_p()
 
     def __del__(self):
@@ -84,44 +87,66 @@ class Comm:
 
 
 def scene_set_comm(scene, comm: Optional[Comm], device: int = 0):
+    """Attach `comm` to the scene's handle on `device` (None: detach).  The
+    scene keeps a reference to the Comm while it is attached, so the
+    communicator cannot be destroyed under it."""
     A.check(A.lib().mh_scene_set_comm(scene.handle(device), comm.handle if comm is not None else None))
+    held = scene.__dict__.setdefault("_comms", {})
+    if comm is None:
+        held.pop(device, None)
+    else:
+        held[device] = comm
 
 
-def _handles(scenes, device):
-    return (C.c_void_p * len(scenes))(*[s.handle(device).value for s in scenes])
+def _devices(scenes, device) -> List[int]:
+    """One device per scene: `device` is an int (every scene on it) or a list."""
+    if isinstance(device, int):
+        return [device] * len(scenes)
+    if len(device) != len(scenes):
+        raise A.MitsubaHipError("the device list needs one entry per scene")
+    return list(device)
 
 
-def render_sharded(scenes, integrator, seed: int, spp: int, films, device: int = 0, reduce_all: bool = True,
+def _handles(scenes, devices):
+    return (C.c_void_p * len(scenes))(*[s.handle(d).value for s, d in zip(scenes, devices)])
+
+
+def render_sharded(scenes, integrator, seed: int, spp: int, films, device=0, reduce_all: bool = True,
                    deterministic: bool = False, stats=None):
     """mh_render_sharded: scene i renders the slab [spp*i/n, spp*(i+1)/n) of
-    every pixel into films[i] (device tensors); the films are summed into
+    every pixel into films[i] (device tensors on scene i's device; `device`:
+    one int for all scenes or one per scene); the films are summed into
     every film (reduce_all) or into films[0] only."""
     n = len(scenes)
+    devs = _devices(scenes, device)
     ic = integrator.c()
     fp = (C.c_void_p * n)(*[f.data_ptr() for f in films])
     flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_REDUCE if reduce_all else 0)
     flags |= A.FLAG_DETERMINISTIC if deterministic else 0
     st = (A.Stats * n)() if stats is not None else None
-    A.check(A.lib().mh_render_sharded(_handles(scenes, device), n, C.byref(ic), seed, spp, fp, flags, st))
+    A.check(A.lib().mh_render_sharded(_handles(scenes, devs), n, C.byref(ic), seed, spp, fp, flags, st))
     if stats is not None:
         stats[:] = list(st)
     return films
 
 
-def render_backward_sharded(scenes, params, grad_in, keys, integrator, seed: int, spp: int, device: int = 0,
+def render_backward_sharded(scenes, params, grad_in, keys, integrator, seed: int, spp: int, device=0,
                             local_weights: bool = False):
     """mh_render_backward_sharded: every scene differentiates its slab with
-    the summed W image; returns per scene the list of summed gradients."""
+    the summed W image; returns per scene the list of summed gradients, each
+    on that scene's device (`device`: one int for all scenes or one per
+    scene; grad_in is copied to every scene's device)."""
     import torch
     n = len(scenes)
+    devs = _devices(scenes, device)
     ic = integrator.c()
-    gi = [grad_in.to(torch.float32).contiguous() for _ in range(n)]
+    gi = [grad_in.to(device=f"cuda:{d}", dtype=torch.float32).contiguous() for d in devs]
     gptr = (C.c_void_p * n)(*[g.data_ptr() for g in gi])
     ids = (C.c_uint32 * max(len(keys), 1))(*[params.param_id(k) for k in keys])
-    outs = [[torch.zeros(params[k].shape, dtype=torch.float32, device=grad_in.device) for k in keys]
-            for _ in range(n)]
+    outs = [[torch.zeros(params[k].shape, dtype=torch.float32, device=f"cuda:{d}") for k in keys]
+            for d in devs]
     optr = (C.c_void_p * max(n * len(keys), 1))(*[o.data_ptr() for row in outs for o in row])
     flags = A.FLAG_DEVICE_POINTERS | (A.FLAG_LOCAL_WEIGHTS if local_weights else 0)
-    A.check(A.lib().mh_render_backward_sharded(_handles(scenes, device), n, C.byref(ic), seed, spp, gptr,
+    A.check(A.lib().mh_render_backward_sharded(_handles(scenes, devs), n, C.byref(ic), seed, spp, gptr,
                                                len(keys), ids, optr, flags, None))
     return outs

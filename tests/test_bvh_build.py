@@ -3,7 +3,9 @@ slot of scene_optix.inl:449-514): binned SAH with the O(n) passes of large
 ranges split over threads and subtrees built by workers.  tools/bvh_check.cpp
 builds a clustered synthetic soup and checks every primitive sits in exactly
 one leaf whose box (and every ancestor's) contains it; the node / primitive
-arrays must not depend on the thread count."""
+arrays must not depend on the thread count.  The quantised BVH4 of the
+stream engine (build_qbvh4) is checked the same way on its float-decoded
+child boxes."""
 import json
 import os
 import subprocess
@@ -35,5 +37,6 @@ def test_bvh_valid_and_thread_independent(bvh_check, n):
     a = run(bvh_check, n, 1)
     b = run(bvh_check, n, 4)
     assert a["bad"] == 0 and b["bad"] == 0
+    assert a["qbad"] == 0 and b["qbad"] == 0   # the quantised BVH4 is conservative and complete
     assert a["hash"] == b["hash"], (a, b)
     assert a["leaves"] == a["nodes"] + 1 and a["depth"] < 48

@@ -2,7 +2,9 @@
 // synthetic triangle soup: every primitive in exactly one leaf, every child
 // box containing its subtree, and a hash of the node + primitive arrays (the
 // same for any MH_BVH_THREADS).  usage: bvh_check <n_tris> [seed]
+#include <cfloat>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -77,7 +79,69 @@ int main(int argc, char **argv) {
     uint64_t h = 1469598103934665603ull;
     for (uint8_t b : out.nodes) h = (h ^ b) * 1099511628211ull;
     for (uint8_t b : out.prims) h = (h ^ b) * 1099511628211ull;
-    printf("{\"n\": %u, \"ms\": %.1f, \"nodes\": %u, \"leaves\": %llu, \"depth\": %u, \"bad\": %d, \"hash\": \"%016llx\"}\n",
-           n, ms, out.n_nodes, (unsigned long long)leaves, out.depth, bad, (unsigned long long)h);
-    return bad ? 1 : 0;
+    // the quantised BVH4 (build_qbvh4): every child box, decoded in float as
+    // the device decodes it (fma(byte, 2^e, origin)), contains every primitive
+    // below it; every primitive in exactly one leaf; inner children contiguous
+    // and after their parent; compact records equal to the Prim fields
+    std::vector<uint8_t> qn, qp;
+    uint32_t nq = 0, dq = 0;
+    int qbad = 0;
+    if (build_qbvh4(out, qn, qp, nq, dq)) {
+        const QNode4 *Q = reinterpret_cast<const QNode4 *>(qn.data());
+        const PrimC *PC = reinterpret_cast<const PrimC *>(qp.data());
+        std::vector<int> qseen(n, 0);
+        struct Bx { float lo[3], hi[3]; };
+        auto dec = [&](const QNode4 &q, int c, Bx &b) {
+            const float o[3] = {q.ox, q.oy, q.oz};
+            const uint32_t lo[3] = {q.qlo[0], q.qlo[1], q.qlo[2]}, hi[3] = {q.qhi_x, q.qhi_y, q.qhi_z};
+            for (int a = 0; a < 3; ++a) {
+                float sc;
+                const uint32_t bits = ((q.ebits >> (8 * a)) & 0xffu) << 23;
+                memcpy(&sc, &bits, 4);
+                b.lo[a] = std::fmaf((float)((lo[a] >> (8 * c)) & 0xffu), sc, o[a]);
+                b.hi[a] = std::fmaf((float)((hi[a] >> (8 * c)) & 0xffu), sc, o[a]);
+            }
+        };
+        struct It { uint32_t node; Bx box; int depth; };
+        std::vector<It> qs{{0u, Bx{{-FLT_MAX, -FLT_MAX, -FLT_MAX}, {FLT_MAX, FLT_MAX, FLT_MAX}}, 0}};
+        // each primitive must be inside every decoded box on its path: carry the intersection
+        while (!qs.empty()) {
+            const It it = qs.back();
+            qs.pop_back();
+            if (it.node >= nq) { ++qbad; continue; }
+            const QNode4 &q = Q[it.node];
+            uint32_t prev_inner = ~0u;
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t r = q.ref[c];
+                if (r == 0xffffffffu) continue;
+                Bx b;
+                dec(q, c, b);
+                for (int a = 0; a < 3; ++a) { b.lo[a] = std::max(b.lo[a], it.box.lo[a]); b.hi[a] = std::min(b.hi[a], it.box.hi[a]); }
+                if (r & 0x80000000u) {
+                    const uint32_t first = (r & 0x7fffffffu) >> 5, cnt = r & 31u;
+                    for (uint32_t j = first; j < first + cnt; ++j) {
+                        const uint32_t id = pr[j].info.w;
+                        const PrimC &pc = PC[j];
+                        const bool rec_ok = pc.key == id && pc.prim == pr[j].info.y && (pc.shape & 0x7fffffffu) == pr[j].info.x &&
+                                            pc.v0x == pr[j].a.x && pc.e1y == pr[j].b.y && pc.e2z == pr[j].c.z;
+                        if (id >= n || !rec_ok) { ++qbad; continue; }
+                        for (int a = 0; a < 3; ++a)
+                            if (!(b.lo[a] <= prims[id].lo[a] && b.hi[a] >= prims[id].hi[a])) { ++qbad; break; }
+                        qseen[id]++;
+                    }
+                } else {
+                    if (r <= it.node || (prev_inner != ~0u && r != prev_inner + 1)) ++qbad;  // contiguous, after the parent
+                    prev_inner = r;
+                    qs.push_back(It{r, b, it.depth + 1});
+                }
+            }
+        }
+        for (uint32_t i = 0; i < n; ++i) qbad += qseen[i] != (n == 1 ? 2 : 1);
+        for (uint8_t b : qn) h = (h ^ b) * 1099511628211ull;
+    } else {
+        qbad = -1;  // not built
+    }
+    printf("{\"n\": %u, \"ms\": %.1f, \"nodes\": %u, \"leaves\": %llu, \"depth\": %u, \"bad\": %d, \"qnodes\": %u, \"qdepth\": %u, \"qbad\": %d, \"hash\": \"%016llx\"}\n",
+           n, ms, out.n_nodes, (unsigned long long)leaves, out.depth, bad, nq, dq, qbad, (unsigned long long)h);
+    return (bad || qbad) ? 1 : 0;
 }

@@ -1,0 +1,210 @@
+// Host statistics of the stream engine's two wide-BVH formats on the
+// displaced-sphere mesh of tools/bench_mesh.py: per ray, inner-node visits,
+// distinct 128-B node lines, leaf primitive tests and distinct primitive
+// lines, for the float Node4 (collapse_bvh4) and the quantised QNode4 +
+// PrimC (build_qbvh4), the same closest-hit traversal as trav_inner_step4 /
+// trav_inner_step_q (entry-distance order).  usage: qbvh_stats <n_tris> [rays]
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <set>
+#include <vector>
+
+#include "../mitsuba3-nasa_amd/csrc/mh_device.hpp"
+#include "../mitsuba3-nasa_amd/csrc/mh_internal.hpp"
+
+using namespace mh;
+
+struct Stats { double nodes = 0, node_lines = 0, prims = 0, prim_lines = 0; };
+
+static bool slab(const float lo[3], const float hi[3], const float inv[3], const float ood[3], float tmax, float &tl) {
+    float a[3], b[3];
+    for (int k = 0; k < 3; ++k) { a[k] = std::fmaf(lo[k], inv[k], -ood[k]); b[k] = std::fmaf(hi[k], inv[k], -ood[k]); }
+    float l = std::fmax(std::fmax(std::fmin(a[0], b[0]), std::fmin(a[1], b[1])), std::fmax(std::fmin(a[2], b[2]), 0.f));
+    float h = std::fmin(std::fmin(std::fmax(a[0], b[0]), std::fmax(a[1], b[1])), std::fmin(std::fmax(a[2], b[2]), tmax));
+    tl = l;
+    return l <= h;
+}
+
+static bool tri(const Prim &p, const float o[3], const float d[3], float tmax, float &t) {
+    const float *v0 = &p.a.x, *e1 = &p.b.x, *e2 = &p.c.x;
+    float pv[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
+    float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+    float inv = 1.f / det;
+    float tv[3] = {o[0] - v0[0], o[1] - v0[1], o[2] - v0[2]};
+    float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
+    float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
+    float v = (d[0] * qv[0] + d[1] * qv[1] + d[2] * qv[2]) * inv;
+    t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
+    return u >= 0 && u <= 1 && v >= 0 && u + v <= 1 && t >= 0 && t <= tmax;
+}
+
+static float g_best;
+template <bool Q>
+static void trace(const void *nodes, const Prim *P, const float o[3], const float d[3], bool shadow, Stats &s) {
+    float inv[3], ood[3];
+    for (int k = 0; k < 3; ++k) {
+        float dd = std::fabs(d[k]) > 0x1p-80f ? d[k] : std::copysign(0x1p-80f, d[k]);
+        inv[k] = 1.f / dd;
+        ood[k] = o[k] * inv[k];
+    }
+    float best = FLT_MAX;
+    std::vector<uint32_t> st{0u};
+    std::set<uint64_t> nl, pl;
+    const size_t nsz = Q ? sizeof(QNode4) : sizeof(Node4), psz = Q ? sizeof(PrimC) : sizeof(Prim);
+    while (!st.empty()) {
+        uint32_t r = st.back();
+        st.pop_back();
+        if (r & 0x80000000u) {
+            const uint32_t first = (r & 0x7fffffffu) >> 5, cnt = r & 31u;
+            for (uint32_t j = first; j < first + cnt; ++j) {
+                s.prims += 1;
+                for (uint64_t b = j * psz / 128; b <= ((j + 1) * psz - 1) / 128; ++b) pl.insert(b);
+                float t;
+                if (tri(P[j], o, d, best, t)) {
+                    best = t;
+                    if (shadow) { st.clear(); break; }
+                }
+            }
+            continue;
+        }
+        s.nodes += 1;
+        for (uint64_t b = r * nsz / 128; b <= ((r + 1) * nsz - 1) / 128; ++b) nl.insert(b);
+        float lo[4][3], hi[4][3];
+        uint32_t ref[4];
+        if (Q) {
+            const QNode4 &q = reinterpret_cast<const QNode4 *>(nodes)[r];
+            const float og[3] = {q.ox, q.oy, q.oz};
+            const uint32_t ql[3] = {q.qlo[0], q.qlo[1], q.qlo[2]}, qh[3] = {q.qhi_x, q.qhi_y, q.qhi_z};
+            for (int c = 0; c < 4; ++c) {
+                for (int a = 0; a < 3; ++a) {
+                    uint32_t bits = ((q.ebits >> (8 * a)) & 0xffu) << 23;
+                    float sc;
+                    memcpy(&sc, &bits, 4);
+                    lo[c][a] = std::fmaf((float)((ql[a] >> (8 * c)) & 0xff), sc, og[a]);
+                    hi[c][a] = std::fmaf((float)((qh[a] >> (8 * c)) & 0xff), sc, og[a]);
+                }
+                ref[c] = q.ref[c];
+            }
+        } else {
+            const Node4 &n = reinterpret_cast<const Node4 *>(nodes)[r];
+            const float *L[3] = {&n.lox.x, &n.loy.x, &n.loz.x}, *H[3] = {&n.hix.x, &n.hiy.x, &n.hiz.x};
+            for (int c = 0; c < 4; ++c) {
+                for (int a = 0; a < 3; ++a) { lo[c][a] = L[a][c]; hi[c][a] = H[a][c]; }
+                ref[c] = (&n.ref.x)[c];
+            }
+        }
+        float tc[4];
+        uint32_t rc[4];
+        int k = 0;
+        for (int c = 0; c < 4; ++c) {
+            float tl;
+            if (ref[c] != 0xffffffffu && slab(lo[c], hi[c], inv, ood, best, tl)) { tc[k] = tl; rc[k] = ref[c]; ++k; }
+        }
+        for (int i = 0; i < k; ++i)
+            for (int j = i + 1; j < k; ++j)
+                if (tc[j] < tc[i]) { std::swap(tc[i], tc[j]); std::swap(rc[i], rc[j]); }
+        for (int i = k - 1; i >= 0; --i) st.push_back(rc[i]);
+    }
+    s.node_lines += nl.size();
+    s.prim_lines += pl.size();
+    g_best = best;
+}
+static float hit_t(const void *n4, const Prim *P, const float o[3], const float d[3]) {
+    Stats s;
+    trace<false>(n4, P, o, d, false, s);
+    return g_best;
+}
+
+static float hit_t(const void *n4, const Prim *P, const float o[3], const float d[3]);
+
+int main(int argc, char **argv) {
+    const uint32_t n_tri = argc > 1 ? atoi(argv[1]) : 1000000;
+    const int n_rays = argc > 2 ? atoi(argv[2]) : 20000;
+    // the displaced sphere of tools/bench_mesh.py, scaled 0.45 at (0, -0.45, 0)
+    const int m = std::max(8, (int)std::sqrt(n_tri / 4.0));
+    std::vector<float> V;
+    for (int i = 0; i <= m; ++i)
+        for (int j = 0; j <= 2 * m; ++j) {
+            double th = M_PI * i / m, ph = 2 * M_PI * j / (2 * m);
+            double r = 1.0 + 0.08 * std::sin(7 * th) * std::cos(9 * ph) + 0.03 * std::sin(23 * ph + 3 * th);
+            V.push_back((float)(0.45 * r * std::sin(th) * std::cos(ph)));
+            V.push_back((float)(0.45 * r * std::cos(th) - 0.45));
+            V.push_back((float)(0.45 * r * std::sin(th) * std::sin(ph)));
+        }
+    std::vector<BuildPrim> bp;
+    auto add = [&](int a, int b, int c) {
+        BuildPrim p{};
+        const float *v[3] = {&V[3 * a], &V[3 * b], &V[3 * c]};
+        for (int k = 0; k < 3; ++k) {
+            p.lo[k] = std::min(v[0][k], std::min(v[1][k], v[2][k]));
+            p.hi[k] = std::max(v[0][k], std::max(v[1][k], v[2][k]));
+            p.rec[k] = v[0][k];
+            p.rec[4 + k] = v[1][k] - v[0][k];
+            p.rec[8 + k] = v[2][k] - v[0][k];
+        }
+        p.type = MH_SHAPE_MESH;
+        p.prim = (uint32_t)bp.size();
+        bp.push_back(p);
+    };
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < 2 * m; ++j) {
+            int a = i * (2 * m + 1) + j;
+            add(a, a + 2 * m + 1, a + 1);
+            add(a + 1, a + 2 * m + 1, a + 2 * m + 2);
+        }
+    const char *el = getenv("MH_BVH_LEAF"), *ec = getenv("MH_BVH_CT");
+    BvhOut b;
+    build_bvh(bp, b, el ? atoi(el) : 8, ec ? (float)atof(ec) : 2.f);
+    std::vector<uint8_t> n4, qn, qp;
+    uint32_t c4, d4, cq, dq;
+    collapse_bvh4(b, n4, c4, d4);
+    build_qbvh4(b, qn, qp, cq, dq);
+    const Prim *P = reinterpret_cast<const Prim *>(b.prims.data());
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    for (int shadow = 0; shadow < 2; ++shadow) {
+        Stats sf, sq;
+        for (int i = 0; i < n_rays; ++i) {
+            // diffuse secondaries leaving the blob's surface: a point on the
+            // displaced sphere (radius 0.45 +- 8 %), offset outward, a random
+            // direction in the outer hemisphere
+            float o[3], d[3];
+            float l2;
+            do { d[0] = U(rng); d[1] = U(rng); d[2] = U(rng); l2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2]; } while (l2 > 1 || l2 < 1e-4);
+            for (int k = 0; k < 3; ++k) d[k] /= std::sqrt(l2);
+            const float rr = 0.45f * 1.12f;
+            o[0] = d[0] * rr; o[1] = d[1] * rr - 0.45f; o[2] = d[2] * rr;
+            if (i % 2) {  // half of them on the surface itself: march inward to the first hit
+                float din[3] = {-d[0], -d[1], -d[2]};
+                Stats tmp;
+                float t = hit_t(n4.data(), P, o, din);
+                if (t < FLT_MAX) for (int k = 0; k < 3; ++k) o[k] += din[k] * t * 0.999f;
+            }
+            float nrm[3] = {d[0], d[1], d[2]};
+            do { d[0] = U(rng); d[1] = U(rng); d[2] = U(rng); l2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2]; } while (l2 > 1 || l2 < 1e-4);
+            for (int k = 0; k < 3; ++k) d[k] /= std::sqrt(l2);
+            if (d[0] * nrm[0] + d[1] * nrm[1] + d[2] * nrm[2] < 0) for (int k = 0; k < 3; ++k) d[k] = -d[k];
+            if (shadow) {  // toward the ceiling light
+                float t[3] = {U(rng) * 0.23f - o[0], 0.99f - o[1], U(rng) * 0.19f - o[2]};
+                float L = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+                for (int k = 0; k < 3; ++k) d[k] = t[k] / L;
+            }
+            trace<false>(n4.data(), P, o, d, shadow, sf);
+            trace<true>(qn.data(), P, o, d, shadow, sq);
+        }
+        auto pr = [&](const char *nm, const Stats &s, size_t nsz, size_t psz) {
+            printf("%-7s %-6s nodes %.2f  node lines %.2f (%.0f B)  prims %.2f  prim lines %.2f (%.0f B)  total %.0f B/ray\n",
+                   shadow ? "shadow" : "closest", nm, s.nodes / n_rays, s.node_lines / n_rays, s.nodes / n_rays * nsz,
+                   s.prims / n_rays, s.prim_lines / n_rays, s.prims / n_rays * psz,
+                   128.0 * (s.node_lines + s.prim_lines) / n_rays);
+        };
+        pr("float", sf, sizeof(Node4), sizeof(Prim));
+        pr("quant", sq, sizeof(QNode4), sizeof(PrimC));
+    }
+    printf("bvh2 nodes %u, node4 %u (%.1f MB), qnode4 %u (%.1f MB), prims %u (%.1f / %.1f MB)\n", b.n_nodes, c4,
+           c4 * 128 / 1e6, cq, cq * 64 / 1e6, b.n_prims, b.n_prims * 64 / 1e6, b.n_prims * 48 / 1e6);
+}
