@@ -14,8 +14,18 @@ max-over-ranks step time.  Inputs (the scene) are resident in HBM before the
 timed region; the timed region ends with the image and gradients on the
 device.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Per step two collectives (packed, the default): the film and the W image
+(which depends only on the gradient seed's jitters) are summed in ONE
+all-reduce, the gradients in another (mitsuba_hip.distributed.fwd_grad_step).
+
+--config 5 is BASELINE.json configs[4]: cornell_box 2048x2048 @ 1024 spp
+TOTAL (strong scaling: rank r takes samples [1024 r / N, 1024 (r + 1) / N) of
+every pixel; the forward runs 2 passes of 512 spp, integrator.cpp:281-295, the
+gradient one AD wavefront of 2^32 samples), max_depth 8, same JSON line.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5]
        torchrun --nproc-per-node N bench.py --gpus N ...   (the driver)
+       torchrun --nproc-per-node 8 bench.py --gpus 8 --config 5
 """
 import argparse
 import ctypes as C
@@ -46,6 +56,11 @@ def parse():
                    help="every rank computes the whole W image (no W all-reduce; N x the W splat work)")
     p.add_argument("--film-all-reduce", action="store_true",
                    help="all-reduce the film to every rank instead of reducing it onto rank 0")
+    p.add_argument("--config", type=int, default=2, choices=(2, 5),
+                   help="2: 512^2 @ 256 spp per GPU (weak scaling, the headline); 5: 2048^2 @ 1024 spp total "
+                        "split over the ranks (strong scaling)")
+    p.add_argument("--unpacked", action="store_true",
+                   help="separate film and W collectives (3 per step) instead of one packed film + W all-reduce")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' to rehearse "
                         "several ranks on one GPU)")
@@ -122,11 +137,13 @@ def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
             "cpu_model": model, "nproc": nproc, "affinity": aff, "threads": threads}
 
 
-def build_step(res, spp, max_depth, rank, world, dev):
+def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     """The bench's hot-path wiring (also driven by tests/test_gpu_multirank.py):
     cornell_box res^2, `path` forward + `prb` backward wrt white's rgb
     reflectance, the rank's sample slab of a spp * world render, through the
-    HIP C-ABI wrappers of mitsuba_hip."""
+    HIP C-ABI wrappers of mitsuba_hip.  fwd_passes: the forward's passes
+    (integrator.cpp:281-295; its slab counts lanes of one pass).  One device
+    buffer holds the film and the W image (StepOps.packed)."""
     import torch
     import mitsuba_hip as mi
     from mitsuba_hip import _abi as A
@@ -143,17 +160,23 @@ def build_step(res, spp, max_depth, rank, world, dev):
     grad_in = torch.full((res, res, 3), 1.0 / (res * res * 3), dtype=torch.float32, device=dev)
     st_f, st_b = A.Stats(), A.Stats()
     film = torch.empty((res, res, 4), dtype=torch.float32, device=dev)
+    packed = torch.empty(res * res * 5, dtype=torch.float32, device=dev)  # film (RGBW) | W image
+    views = (packed, packed[:res * res * 4].view(res, res, 4), packed[res * res * 4:].view(res, res))
     ops = D.StepOps(
-        render_film=lambda seed, spp_, b, e: mi.render_film(scene, fwd, seed=seed, spp=spp_, spp_begin=b,
-                                                            spp_end=e, film=film, stats=st_f),
+        render_film=lambda seed, spp_, b, e, out=None: mi.render_film(
+            scene, fwd, seed=seed, spp=spp_, spp_begin=b, spp_end=e, film=film if out is None else out, stats=st_f),
         develop=lambda f: mi.develop(scene, f),
-        prb_weights=lambda seed, spp_, b, e: mi.prb_weights(scene, seed, spp_, b, e),
+        prb_weights=lambda seed, spp_, b, e, out=None: mi.prb_weights(scene, seed, spp_, b, e, out=out),
         render_backward=lambda seed, spp_, b, e, w: mi.render_backward(
             scene, params, grad_in, [key], prb, seed=seed, spp=spp_, spp_begin=b, spp_end=e, weights=w,
             stats=st_b),
-        seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0])
+        seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0],
+        packed=lambda: views)
+    slab = D.sample_slab(rank, world, spp)
+    fs = D.sample_slab(rank, world, spp // fwd_passes)
+    fwd_slab = D.Slab(slab.spp_total, fs.begin, fs.end)
     return {"scene": scene, "fwd": fwd, "prb": prb, "key": key, "ops": ops,
-            "slab": D.sample_slab(rank, world, spp), "st_f": st_f, "st_b": st_b}
+            "slab": slab, "fwd_slab": fwd_slab, "st_f": st_f, "st_b": st_b}
 
 
 def main():
@@ -179,15 +202,22 @@ def main():
 
     from mitsuba_hip import _abi as A
     from mitsuba_hip import distributed as D
-    w = build_step(args.res, args.spp, args.max_depth, rank, world, dev)
-    scene, fwd, prb, key, ops, slab, st_f, st_b = (w[k] for k in ("scene", "fwd", "prb", "key", "ops", "slab",
-                                                                   "st_f", "st_b"))
+    if args.config == 5:  # BASELINE.json configs[4]: 2048^2 @ 1024 spp in total, strong scaling
+        if 512 % world:
+            raise SystemExit("--config 5 needs a rank count that divides 512")
+        args.res, args.spp, fwd_passes = 2048, 1024 // world, 2
+    else:
+        fwd_passes = 1
+    w = build_step(args.res, args.spp, args.max_depth, rank, world, dev, fwd_passes)
+    scene, fwd, prb, key, ops, slab, fwd_slab, st_f, st_b = (
+        w[k] for k in ("scene", "fwd", "prb", "key", "ops", "slab", "fwd_slab", "st_f", "st_b"))
     H = W = args.res
     spp_total = args.spp * world
+    packed = not (args.unpacked or args.local_weights or args.fwd_only)
 
     def step(i):
         return D.fwd_grad_step(ops, slab, i, with_grad=not args.fwd_only, local_weights=args.local_weights,
-                               film_to_root=not args.film_all_reduce)
+                               film_to_root=not args.film_all_reduce, packed=packed, fwd_slab=fwd_slab)
 
     for i in range(args.warmup):
         step(1000 + i)
@@ -286,20 +316,37 @@ def main():
         roofline_other = roofs[1][1] if len(roofs) > 1 else None
         cpu = None
         if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N = 1 only
-            cpu = cpu_baseline(scene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)
+            cscene = scene
+            if args.res > 512:  # a bounded sample: the same scene at 512^2 (per-sample work is resolution-free)
+                import mitsuba_hip as mi
+                d = mi.cornell_box()
+                d["sensor"]["film"]["width"] = d["sensor"]["film"]["height"] = 512
+                cscene = mi.load_dict(d)
+            cpu = cpu_baseline(cscene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)
+        coll = ("RCCL" if args.backend == "nccl" else args.backend)
+        if packed:
+            par = f"sample-slab x{world} + {coll} all-reduce (film + W, one packed buffer) + all-reduce (gradient)"
+        else:
+            par = (f"sample-slab x{world} + {coll}" +
+                   (" all-reduce (film)" if args.film_all_reduce else " reduce to rank 0 (film)") +
+                   (", local W" if args.local_weights else ", all-reduce (W)") + ", all-reduce (gradient)")
+        cfg5 = args.config == 5
         line = {
             "metric": "Msamples/s (pixels×spp/s) fwd + PRB grad, cornell_box 512²; 1/2/4/8 GPU",
             "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic (cornell_box scene, seeded PCG32)",
-            "config": {"workload": f"cornell_box {W}x{H} @ {args.spp} spp/GPU: path fwd (max_depth {args.max_depth})"
+            "scaling": "strong" if cfg5 else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (cornell_box scene, seeded PCG32)",
+            "config": {"workload": (f"config 5: cornell_box {W}x{H} @ {spp_total} spp total ({args.spp}/GPU; "
+                                    f"forward in 2 passes): path fwd (max_depth {args.max_depth})" if cfg5 else
+                                    f"cornell_box {W}x{H} @ {args.spp} spp/GPU: path fwd (max_depth {args.max_depth})")
                                    + ("" if args.fwd_only else f" + prb backward wrt '{key}'"),
                        "film": f"{W}x{H}", "spp_per_gpu": args.spp, "spp_total": spp_total,
-                       "parallelism": f"sample-slab x{world} + " +
-                                      ("RCCL" if args.backend == "nccl" else args.backend) +
-                                      (" all-reduce (film)" if args.film_all_reduce else " reduce to rank 0 (film)") +
-                                      (", local W" if args.local_weights else ", all-reduce (W)") +
-                                      ", all-reduce (gradient)"},
+                       "parallelism": par,
+                       "collectives_per_step": (2 if packed else (1 if args.fwd_only else (2 if args.local_weights else 3))),
+                       "collective_bytes": ({"film+W": H * W * 20, "gradient": 12} if packed else
+                                            {"film": H * W * 16, "W": 0 if args.local_weights else H * W * 4,
+                                             "gradient": 12})},
             "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
             "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
             "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),

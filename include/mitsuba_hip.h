@@ -414,6 +414,8 @@ typedef struct mh_comm mh_comm;
 int mh_comm_unique_id(uint8_t id[MH_COMM_ID_BYTES]);
 int mh_comm_create(const uint8_t id[MH_COMM_ID_BYTES], int nranks, int rank, int device, mh_comm **out);
 int mh_comm_create_all(int ndev, const int *devices, mh_comm **out);
+/* Fails (MH_ERR_INVALID_ARGUMENT, nothing destroyed) while a scene still
+ * holds the communicator (mh_scene_set_comm): detach it first. */
 int mh_comm_destroy(mh_comm *comm);
 int mh_comm_info(const mh_comm *comm, int *nranks, int *rank, int *device);
 /*
@@ -426,7 +428,14 @@ int mh_comm_info(const mh_comm *comm, int *nranks, int *rank, int *device);
 int mh_comm_reduce(mh_comm *const *comms, int n, float *const *bufs, uint64_t count, void *const *streams,
                    int root);
 /* The scene's communicator for MH_FLAG_REDUCE / MH_FLAG_REDUCE_ROOT (NULL
- * detaches); its device must be the scene's. */
+ * detaches); its device must be the scene's.  The scene holds it until it is
+ * detached or the scene is destroyed.
+ * Failure handling of the in-call collectives: a call that fails after its
+ * argument checks aborts the communicator (ncclCommAbort; later collectives
+ * on it fail at once), and a call waits for its collectives with a deadline
+ * (MH_COMM_TIMEOUT_S, default 1800 s) while watching the communicator's
+ * async error, so a rank whose peer failed returns an error instead of
+ * waiting forever.  Create a new communicator after such a failure. */
 int mh_scene_set_comm(mh_scene *scene, mh_comm *comm);
 /* Wait for the scene's stream (after MH_FLAG_NO_SYNC calls). */
 int mh_scene_synchronize(mh_scene *scene);

@@ -99,7 +99,7 @@ struct mh_scene {
     bool own_stream = false;
     DScene S{};
     // device buffers
-    DevBuf nodes, nodes4, primsc, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
+    DevBuf nodes, nodes4, primsc, stack_ovf, prims, prim_pairs, key_sp, shapes, bsdf_type, bsdf_tex, textures, emitters, positions, normals,
         texcoords, faces, texels, media, grid;
     DevBuf work, film_tmp, film4, alpha_px, counters, grad_meta, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e, weights_tmp;
     std::vector<uint8_t> meta_host;  // the bytes last uploaded to grad_meta (upload_slots)
@@ -467,6 +467,32 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
             }
         }
     }
+    // The stream engine's stack (round 4): the bound 3 * depth4 + 2 of a
+    // wide-BVH traversal (44-50 entries on 1M-4M triangles) put 48 KiB of LDS
+    // stack in every 256-thread workgroup and held the trace kernels at 3
+    // waves per SIMD; the stacks rays really build stay far shallower
+    // (tools/qbvh_stats: at most 14 entries on those meshes).  So the first
+    // kStreamStack entries live in LDS and deeper ones in a global overflow
+    // region, one column per thread of the largest stream-kernel grid: exact
+    // for any depth, and 5 waves per SIMD (1M triangles: 403 -> 537
+    // Msamples/s measured with a 24-entry LDS stack).  MH_STREAM_STACK overrides.
+    S.stream_stack = S.stack_size;
+    S.stack_ovf = nullptr;
+    S.ovf_threads = 0;
+    if (S.lds_bytes_bvh == 0 && (S.nodes4 || S.qnodes)) {
+        const char *es = getenv("MH_STREAM_STACK");
+        const uint32_t cap = es ? (uint32_t)std::max(4, atoi(es)) : 24u;
+        if (cap < S.stack_size) {
+            int cus = 256;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+            const uint32_t threads = wf_blocks(cus) * 256u;
+            if (upload(s->stack_ovf, (const uint32_t *)nullptr, (size_t)(S.stack_size - cap) * threads, st) == hipSuccess) {
+                S.stream_stack = cap;
+                S.stack_ovf = s->stack_ovf.as<uint32_t>();
+                S.ovf_threads = threads;
+            }
+        }
+    }
     if ((size_t)S.stack_size * 256 * 4 + S.lds_bytes_bvh > 65536)
         return fail(MH_ERR_UNSUPPORTED, "mh_scene_create: BVH too deep for the LDS traversal stack");
     memcpy(S.cam_to_world, sn.to_world, sizeof(S.cam_to_world));
@@ -491,7 +517,7 @@ int mh_scene_destroy(mh_scene *s) {
     if (s->comm) comm_attach(s->comm, -1);
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->primsc, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
+    for (DevBuf *b : {&s->nodes, &s->nodes4, &s->primsc, &s->stack_ovf, &s->prims, &s->prim_pairs, &s->key_sp, &s->shapes, &s->bsdf_type, &s->bsdf_tex, &s->textures,
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word, &s->bmp_fx,

@@ -154,8 +154,6 @@ struct DScene {                 // kernel argument (by value)
     const Node4 *nodes4;           // wide BVH of the stream engine (nullptr: BVH2 only)
     const uint2 *key_sp;           // scene-order key -> (shape, prim) (packet engine)
     const Prim *prim_pairs;        // interleaved pair records of the packet engine (mh_shading.hpp pp())
-    const QNode4 *qnodes;          // quantised wide BVH of the stream engine (nullptr: Node4 / BVH2)
-    const PrimC *primsc;           // its compact primitive records (with qnodes)
     uint32_t n_nodes, n_prims, n_emitters, environment;
     uint32_t n_media, camera_medium;
     uint32_t vol_flags;            // prbvolpath prepare_scene flags (kVol*)
@@ -173,6 +171,15 @@ struct DScene {                 // kernel argument (by value)
     float rfilter_radius;
     float filter_coeff[10];
     uint32_t sampler_seed;
+    // (last: the fused bounce kernels never read them, and fields ahead of
+    // the ones they do read shift the kernel-argument layout they are tuned on)
+    const QNode4 *qnodes;          // quantised wide BVH of the stream engine (nullptr: Node4 / BVH2)
+    const PrimC *primsc;           // its compact primitive records (with qnodes)
+    // the per-lane stream engine's stack: stream_stack entries per lane in
+    // LDS (<= stack_size), the deeper ones in stack_ovf (entry k of global
+    // thread g at (k - stream_stack) * ovf_threads + g; nullptr: none needed)
+    uint32_t *stack_ovf;
+    uint32_t stream_stack, ovf_threads;
 };
 
 // lane -> (pixel, sample) map of one render call (sample-slab aware)

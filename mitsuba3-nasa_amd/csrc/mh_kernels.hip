@@ -776,9 +776,11 @@ hipError_t launch_trace(const DScene &S, bool shadow, uint64_t n, const float *r
     const uint32_t bs = 256;
     uint32_t g = grid ? grid : blocks_for(n, bs);
     if (g == 0) return hipSuccess;
-    size_t sh = lds_bytes(S, bs);
-    const bool lds = S.lds_bytes_bvh != 0;
-    if (!lds && (S.qnodes || S.nodes4) && n >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit stream items
+    const bool lds = S.lds_bytes_bvh != 0, stream = !lds && (S.qnodes || S.nodes4);
+    if (stream && n >= (1ull << 32)) return hipErrorInvalidValue;  // 32-bit stream items
+    // the stream engine: its LDS stack, and at most one overflow column per thread
+    if (stream && S.stack_ovf) g = std::min<uint32_t>(g, S.ovf_threads / bs);
+    const size_t sh = stream ? stream_lds_bytes(S, bs) : lds_bytes(S, bs);
     if (shadow) {
         if (lds) hipLaunchKernelGGL(k_trace_shadow<true>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);
         else hipLaunchKernelGGL(k_trace_shadow<false>, dim3(g), dim3(bs), sh, st, S, n, rays, occ);

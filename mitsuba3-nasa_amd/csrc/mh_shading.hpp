@@ -175,6 +175,24 @@ struct LdsBvh {
     // this wave's deferral scratch (nullptr: dense packet tests only)
     const float *recs = nullptr;
     uint8_t *dscr = nullptr;
+    // the stream engine's stack beyond `scap` LDS entries: this lane's column
+    // of the scene's overflow region (DScene::stack_ovf), stride sgstride
+    uint32_t scap = 0;
+    uint32_t *sglb = nullptr;
+    uint32_t sgstride = 0;
+    MH_DEV void push(uint32_t sp, uint32_t v) const {
+        if (__builtin_expect(sp >= scap, 0)) {
+            sglb[(sp - scap) * sgstride] = v;
+            return;
+        }
+        stack[sp * stride] = v;
+    }
+    MH_DEV uint32_t pop(uint32_t sp) const {
+        uint32_t v;
+        if (__builtin_expect(sp >= scap, 0)) v = sglb[(sp - scap) * sgstride];
+        else v = stack[sp * stride];
+        return v;
+    }
 };
 
 // InLds = true: BVH resident in LDS (compile-time choice, so hipcc emits
@@ -201,7 +219,18 @@ MH_DEV LdsBvh stage_bvh(const DScene &S, uint4 *lds) {
     b.primsc = InLds ? nullptr : S.primsc;
     b.stack = reinterpret_cast<uint32_t *>(lds + nq) + threadIdx.x;
     b.stride = blockDim.x;
+    // the stream engine: S.stream_stack entries in LDS (the launch allocates
+    // stream_lds_bytes), the rest in the global overflow region
+    const bool ovf = !InLds && S.stack_ovf != nullptr;
+    b.scap = ovf ? S.stream_stack : S.stack_size;
+    b.sglb = ovf ? S.stack_ovf + (blockIdx.x * blockDim.x + threadIdx.x) : nullptr;
+    b.sgstride = S.ovf_threads;
     return b;
+}
+// dynamic LDS of the stream-engine kernels (k_wf_trace / k_wf_shadow /
+// k_trace_*): the BVH when LDS-resident, and stream_stack entries per thread
+__host__ __device__ inline size_t stream_lds_bytes(const DScene &S, uint32_t block) {
+    return (size_t)S.lds_bytes_bvh + (size_t)(S.lds_bytes_bvh || !S.stack_ovf ? S.stack_size : S.stream_stack) * block * 4u;
 }
 
 // ---------------------------------------------------------------------------
@@ -330,11 +359,11 @@ MH_DEV void trav_take(TravLane &t, uint32_t ref) {
 }
 
 // one inner step: pop if needed, then visit one inner node
-MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint32_t stride) {
+MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, const LdsBvh &stk) {
     if (t.node == kNoNode) {
         if (t.sp == 0) { t.node = kDone; return; }  // (only reached without a held leaf)
         --t.sp;
-        const uint32_t ref = stk[t.sp * stride];
+        const uint32_t ref = stk.pop(t.sp);
         trav_take(t, ref);
         if (t.node == kNoNode || (t.node & kLeafBit)) return;
     }
@@ -348,7 +377,7 @@ MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint3
     const uint32_t r1 = n1 ? (kLeafBit | (c1 << 5) | n1) : c1;
     if (h0 && h1) {
         const bool swap = t1 < t0;
-        stk[t.sp * stride] = swap ? r0 : r1;
+        stk.push(t.sp, swap ? r0 : r1);
         ++t.sp;
         trav_take(t, swap ? r1 : r0);
     } else if (h0) {
@@ -363,11 +392,11 @@ MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, uint32_t *stk, uint3
 // one inner step on the wide BVH: the four child boxes of a Node4 (one
 // 128-B record, SoA planes), the hit children sorted near to far, the nearest
 // taken and the others pushed far-first (at most 3 pushes per step)
-MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, uint32_t *stk, uint32_t stride) {
+MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, const LdsBvh &stk) {
     if (t.node == kNoNode) {
         if (t.sp == 0) { t.node = kDone; return; }
         --t.sp;
-        const uint32_t ref = stk[t.sp * stride];
+        const uint32_t ref = stk.pop(t.sp);
         trav_take(t, ref);
         if (t.node == kNoNode || (t.node & kLeafBit)) return;
     }
@@ -402,9 +431,9 @@ MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, uint32_t *stk, uin
     MH_CSWAP(0, 1) MH_CSWAP(2, 3) MH_CSWAP(0, 2) MH_CSWAP(1, 3) MH_CSWAP(1, 2)
 #undef MH_CSWAP
     if (cnt == 0) { t.node = kNoNode; return; }
-    if (cnt > 3) { stk[t.sp * stride] = rc[3]; ++t.sp; }
-    if (cnt > 2) { stk[t.sp * stride] = rc[2]; ++t.sp; }
-    if (cnt > 1) { stk[t.sp * stride] = rc[1]; ++t.sp; }
+    if (cnt > 3) { stk.push(t.sp, rc[3]); ++t.sp; }
+    if (cnt > 2) { stk.push(t.sp, rc[2]); ++t.sp; }
+    if (cnt > 1) { stk.push(t.sp, rc[1]); ++t.sp; }
     trav_take(t, rc[0]);
 }
 
@@ -414,11 +443,11 @@ MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, uint32_t *stk, uin
 // trav_inner_step4 on the decoded box
 MH_DEV float qscale(uint32_t ebits, uint32_t a) { return __uint_as_float(((ebits >> (8u * a)) & 0xffu) << 23); }
 MH_DEV float qbyte(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); }
-MH_DEV void trav_inner_step_q(TravLane &t, const QNode4 *nodes, uint32_t *stk, uint32_t stride) {
+MH_DEV void trav_inner_step_q(TravLane &t, const QNode4 *nodes, const LdsBvh &stk) {
     if (t.node == kNoNode) {
         if (t.sp == 0) { t.node = kDone; return; }
         --t.sp;
-        const uint32_t ref = stk[t.sp * stride];
+        const uint32_t ref = stk.pop(t.sp);
         trav_take(t, ref);
         if (t.node == kNoNode || (t.node & kLeafBit)) return;
     }
@@ -455,9 +484,9 @@ MH_DEV void trav_inner_step_q(TravLane &t, const QNode4 *nodes, uint32_t *stk, u
     MH_CSWAP(0, 1) MH_CSWAP(2, 3) MH_CSWAP(0, 2) MH_CSWAP(1, 3) MH_CSWAP(1, 2)
 #undef MH_CSWAP
     if (cnt == 0) { t.node = kNoNode; return; }
-    if (cnt > 3) { stk[t.sp * stride] = rc[3]; ++t.sp; }
-    if (cnt > 2) { stk[t.sp * stride] = rc[2]; ++t.sp; }
-    if (cnt > 1) { stk[t.sp * stride] = rc[1]; ++t.sp; }
+    if (cnt > 3) { stk.push(t.sp, rc[3]); ++t.sp; }
+    if (cnt > 2) { stk.push(t.sp, rc[2]); ++t.sp; }
+    if (cnt > 1) { stk.push(t.sp, rc[1]); ++t.sp; }
     trav_take(t, rc[0]);
 }
 
@@ -525,9 +554,9 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
             const bool ready = !has || t.nleaf != 0 || t.node == kDone;
             if (!__any(inner) || __all(ready)) break;
             if (inner) {
-                if (Eng == kEngQuant) trav_inner_step_q(t, B.qnodes, B.stack, B.stride);
-                else if (Eng == kEngWide) trav_inner_step4(t, B.nodes4, B.stack, B.stride);
-                else trav_inner_step(t, B.nodes, B.stack, B.stride);
+                if (Eng == kEngQuant) trav_inner_step_q(t, B.qnodes, B);
+                else if (Eng == kEngWide) trav_inner_step4(t, B.nodes4, B);
+                else trav_inner_step(t, B.nodes, B);
             }
         }
         // grouped leaf phase

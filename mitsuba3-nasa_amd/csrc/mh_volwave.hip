@@ -1307,9 +1307,22 @@ struct PvBwdMachine {
     }
     MH_DEV uint64_t main_base() const { return (uint64_t)t * a.main_cap * 4; }
     MH_DEV uint64_t nee_base() const { return (uint64_t)t * a.nee_cap; }
+    // traffic diagnostics (wrong gradients, timing / byte counts only):
+    // MH_EXP_PVB_MAIN_FIXED / MH_EXP_PVB_NEE_FIXED keep every MainLog / NeeLog
+    // entry of a thread at its entry 0 (cache-resident), so the log's HBM bytes drop out
+#ifdef MH_EXP_PVB_MAIN_FIXED
+    static constexpr uint32_t kMainStep = 0;
+#else
+    static constexpr uint32_t kMainStep = 1;
+#endif
+#ifdef MH_EXP_PVB_NEE_FIXED
+    static constexpr uint32_t kNeeStep = 0;
+#else
+    static constexpr uint32_t kNeeStep = 1;
+#endif
     MH_DEV void log_main(State &v, float4 q0, float4 q1, float4 q2, float4 q3) {
         if (v.ml_n >= a.main_cap) { v.ml_over = true; return; }
-        float4 *e = a.main_log + main_base() + (uint64_t)4 * v.ml_n;
+        float4 *e = a.main_log + main_base() + (uint64_t)4 * v.ml_n * kMainStep;
         e[0] = q0;
         e[1] = q1;
         e[2] = q2;
@@ -1351,7 +1364,7 @@ struct PvBwdMachine {
     }
     MH_DEV void walk_step(State &v, V3 p, float coef) {
         if (v.nl_n < a.nee_cap && (v.nl_n == 0 || v.nl_med == v.wmedium)) {
-            a.nee_log[nee_base() + v.nl_n] = make_float4(p.x, p.y, p.z, coef);
+            a.nee_log[nee_base() + v.nl_n * kNeeStep] = make_float4(p.x, p.y, p.z, coef);
             v.nl_med = v.wmedium;
             ++v.nl_n;
         } else {
@@ -1456,7 +1469,7 @@ struct PvBwdMachine {
             const float Ko = __shfl(K, (int)o);
             const uint32_t mo = (uint32_t)__shfl((int)med, (int)o);
             if (valid) {
-                const float4 q = a.nee_log[(t0 + o) * a.nee_cap + e];
+                const float4 q = a.nee_log[(t0 + o) * a.nee_cap + e * kNeeStep];
                 sigma_t_backward(S, mo, v3(q.x, q.y, q.z), q.w * Ko, g);
             }
         });
@@ -1468,7 +1481,7 @@ struct PvBwdMachine {
         wave_flat(cnt, flat_scratch(), [&](uint32_t o, uint32_t e, bool valid) {
             const V3 L = v3(__shfl(v.L.x, (int)o), __shfl(v.L.y, (int)o), __shfl(v.L.z, (int)o));
             if (valid) {  // MainLog entry e of thread t0 + o: float4 (t * main_cap + e) * 4
-                const float4 *q = a.main_log + ((t0 + o) * a.main_cap + e) * 4u;
+                const float4 *q = a.main_log + ((t0 + o) * a.main_cap + e * kMainStep) * 4u;
                 pvp_log_entry(S, q[0], q[1], q[2], q[3], L, g);
             }
         });

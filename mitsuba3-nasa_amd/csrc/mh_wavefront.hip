@@ -732,10 +732,11 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
     const WfPacked pk = carve_packed(ws, nullptr, cap);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
-    const size_t sh = lds_bytes(S, 256);
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
+    const size_t sh = packet ? lds_bytes(S, 256) : stream_lds_bytes(S, 256);
     const uint32_t seg_cap = seg_len(n);
     grid = std::max<uint32_t>(kSeg, grid / kSeg * kSeg);  // whole number of blocks per segment
+    if (S.stack_ovf && (uint64_t)grid * 256 > S.ovf_threads) return hipErrorInvalidValue;  // overflow columns
     if (!fused)  // the fused first bounce generates its camera rays itself
         hipLaunchKernelGGL(k_wf_raygen, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, S, lm,
                            seed_value, n, plane, out, w, ctr);
@@ -1888,11 +1889,12 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     WfPrb q = carve_prb(ws_prb, cap, partial, slot_of_tex, n_rgb);
     hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t) * kCtrStride * (n_bounces + 1), st);
     if (e != hipSuccess) return e;
-    const size_t sh = lds_bytes(S, 256);
     const bool lds = S.lds_bytes_bvh != 0, packet = use_packet(S);
+    const size_t sh = packet ? lds_bytes(S, 256) : stream_lds_bytes(S, 256);
     const uint32_t seg_cap = seg_len(n);
     const bool fused = packet && S.tab_bytes != 0 && !wf_unfused();
     const size_t sh_fused = fused_lds_bytes(S);
+    if (S.stack_ovf && (uint64_t)grid * 256 > S.ovf_threads) return hipErrorInvalidValue;  // overflow columns
     const bool with_bmp = bmp != nullptr;
     if (with_bmp && (!fused || bmp->n_depth > 31 || bmp->n_depth + 1 < n_bounces || !bmp->ws)) return hipErrorInvalidValue;
     const WfBmp bm = with_bmp ? carve_bmp(bmp->ws, cap, bmp->n_depth, bmp->slot) : WfBmp{};

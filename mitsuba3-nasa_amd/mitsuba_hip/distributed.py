@@ -12,9 +12,17 @@ only coupling is additive:
             dL gather (common.py:936-947), then each rank's gradient slab
             -> all-reduce(sum)
 
+The W image depends only on the gradient seed's pixel jitters, not on the
+forward's radiance, so a step can compute it before the forward exchange and
+sum film and W in ONE collective (`packed`, the default of bench.py): one
+all-reduce of film + W (5 MiB at 512², 80 MiB at 2048²) and one of the
+gradients (12 B per rgb parameter) per step.  Unpacked, the film is reduced
+(or all-reduced) and W all-reduced separately, or W is computed locally on
+every rank (local_weights: no W exchange, N times the W splat).
+
 One process per GPU; torch.distributed with backend "nccl" (= RCCL over xGMI
 on ROCm), or "gloo" for the CPU tests.  No collective sits inside a kernel
-loop: three all-reduces per step, sized 4 MiB / 1 MiB / 12 B at 512².
+loop.
 """
 from __future__ import annotations
 
@@ -70,30 +78,72 @@ class StepOps:
     render_backward: Callable  # (seed, spp_total, begin, end, weights) -> [grad tensors]; weights None:
                                # the W image of every sample computed in-call (local W)
     seed_grad: Callable        # (seed) -> seed of the differential pass (TEA(seed, 1).v0)
+    # optional: () -> (buffer, film view, W view), one device buffer holding the
+    # film and the W image; render_film / prb_weights then take out= (their
+    # output view), so the packed exchange needs no copy.  None: the packed
+    # step concatenates the two.
+    packed: Optional[Callable] = None
+
+
+def all_reduce_list_(ts: List) -> List:
+    """Sum a list of tensors over ranks in ONE collective (concatenated when
+    there are several); returns the summed tensors (in place for one)."""
+    d = _dist()
+    if d is None or not ts:
+        return ts
+    if len(ts) == 1:
+        d.all_reduce(ts[0])
+        return ts
+    import torch
+    flat = torch.cat([t.reshape(-1) for t in ts])
+    d.all_reduce(flat)
+    out, o = [], 0
+    for t in ts:
+        out.append(flat[o:o + t.numel()].view_as(t))
+        o += t.numel()
+    return out
 
 
 def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, local_weights: bool = False,
-                  film_to_root: bool = False):
+                  film_to_root: bool = False, packed: bool = False, fwd_slab: Optional[Slab] = None):
     """One benchmark step: forward render of the rank's slab + film
     all-reduce + develop; then (with_grad) PRB render_backward of the slab
     with the globally all-reduced W image and an all-reduced gradient.
 
+    packed: the W image of the gradient seed is computed before the forward
+    exchange and summed together with the film in one all-reduce (two
+    collectives per step: film + W, gradients).
     local_weights: every rank computes the whole W image itself (all
     spp_total samples of every pixel) instead of its slab's W + an
     all-reduce -- one collective fewer for N times the W splat work.
     film_to_root: the film is summed onto rank 0 only (a reduce, not an
-    all-reduce); only rank 0's image is then defined."""
-    film = ops.render_film(seed, slab.spp_total, slab.begin, slab.end)
+    all-reduce); only rank 0's image is then defined.
+    fwd_slab: the forward's slab when it differs from the gradient's (a
+    multi-pass forward counts its slab in lanes of one pass)."""
+    fs = fwd_slab or slab
+    if with_grad and packed and not local_weights:
+        sg = ops.seed_grad(seed)
+        if ops.packed is not None:
+            buf, fv, wv = ops.packed()
+            film = ops.render_film(seed, fs.spp_total, fs.begin, fs.end, out=fv)
+            w = ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end, out=wv)
+            all_reduce_(buf)  # film + W: one collective
+        else:
+            film = ops.render_film(seed, fs.spp_total, fs.begin, fs.end)
+            w = ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end)
+            film, w = all_reduce_list_([film, w])
+        img = ops.develop(film)
+        grads: List = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
+        return img, all_reduce_list_(grads)
+    film = ops.render_film(seed, fs.spp_total, fs.begin, fs.end)
     film = reduce_to_root_(film) if film_to_root else all_reduce_(film)
     img = ops.develop(film)
     if not with_grad:
         return img, None
     sg = ops.seed_grad(seed)
     w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end))
-    grads: List = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
-    for g in grads:
-        all_reduce_(g)
-    return img, grads
+    grads = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
+    return img, all_reduce_list_(grads)
 
 
 def max_over_ranks(x: float, device=None) -> float:

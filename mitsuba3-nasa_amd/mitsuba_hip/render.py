@@ -214,11 +214,21 @@ def develop(scene: Scene, film, device=None):
     return out
 
 
-def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, device=None, deterministic=False):
+def prb_weights(scene: Scene, seed: int, spp: int, spp_begin=0, spp_end=0, device=None, deterministic=False,
+                out=None):
+    """The W image of render_backward (common.py:936-947): the filter weight
+    sum of samples [spp_begin, spp_end) of every pixel, (H, W) on the device
+    (into `out` when given, a contiguous float32 device tensor of H*W)."""
     torch = _torch()
     dev = _device_index(device)
     h = scene.handle(dev, torch.cuda.current_stream(dev).cuda_stream)
-    w = torch.empty((scene.height, scene.width), dtype=torch.float32, device=f"cuda:{dev}")
+    if out is not None:
+        if out.dtype != torch.float32 or not out.is_cuda or not out.is_contiguous() or \
+                out.numel() != scene.height * scene.width:
+            raise A.MitsubaHipError("prb_weights: out must be a contiguous float32 device tensor of H*W")
+        w = out
+    else:
+        w = torch.empty((scene.height, scene.width), dtype=torch.float32, device=f"cuda:{dev}")
     A.check(A.lib().mh_prb_weights(h, seed, spp, spp_begin, spp_end, _ptr(w),
                                    A.FLAG_DEVICE_POINTERS | _NO_SYNC |
                                    (A.FLAG_DETERMINISTIC if deterministic else 0)))

@@ -58,9 +58,12 @@ def _worker(rank, world, port, out_dir):
     # the same step with the W image computed locally on every rank (no W
     # all-reduce) and the film summed onto rank 0 only
     img2, grads2 = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7, local_weights=True, film_to_root=True)
+    # packed: film and W summed in one all-reduce (bench.py's default step)
+    img3, grads3 = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7, packed=True)
     t = D.max_over_ranks(float(rank) + 0.5)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), img=img.numpy(), g=grads[0].numpy(), t=t,
-             begin=slab.begin, end=slab.end, img2=img2.numpy(), g2=grads2[0].numpy())
+             begin=slab.begin, end=slab.end, img2=img2.numpy(), g2=grads2[0].numpy(), img3=img3.numpy(),
+             g3=grads3[0].numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -100,3 +103,15 @@ def test_gloo_ranks_match_single_process(world, tmp_path):
     np.testing.assert_allclose(r0["img2"], img.numpy(), rtol=2e-6, atol=1e-7)
     assert np.array_equal(r0["g2"], r1["g2"])
     np.testing.assert_allclose(r0["g2"], grads[0].numpy(), rtol=1e-5, atol=1e-9)
+    # one packed film + W all-reduce: every rank's image and gradient equal the single-process step
+    for r in rs:
+        np.testing.assert_allclose(r["img3"], img.numpy(), rtol=2e-6, atol=1e-7)
+        np.testing.assert_allclose(r["g3"], grads[0].numpy(), rtol=1e-5, atol=1e-9)
+
+
+def test_all_reduce_list_single_rank():
+    import torch
+    from mitsuba_hip import distributed as D
+    ts = [torch.ones(3), torch.arange(4.0)]
+    out = D.all_reduce_list_(ts)  # no process group: unchanged
+    assert all(torch.equal(a, b) for a, b in zip(out, ts))

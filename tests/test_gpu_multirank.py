@@ -65,3 +65,7 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     np.testing.assert_allclose(r0["img2"], img, rtol=1e-5, atol=1e-7)
     np.testing.assert_array_equal(r0["g2"], r1["g2"])
     np.testing.assert_allclose(r0["g2"], g, rtol=1e-4)
+    # the packed film + W all-reduce (bench.py's default step)
+    for r in (r0, r1):
+        np.testing.assert_allclose(r["img3"], img, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(r["g3"], g, rtol=1e-4)

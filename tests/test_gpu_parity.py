@@ -869,12 +869,15 @@ def _blob_scene(mi, n_tri=6000, w=24, h=24, spp=8, max_depth=6):
     return mi.load_dict(d)
 
 
-@pytest.mark.parametrize("bvh4", ["1", "q", "0"])
+@pytest.mark.parametrize("bvh4", ["1", "q", "0", "1-ovf"])
 def test_large_mesh_trace_parity(bvh4, monkeypatch):
     # the trace entry points run the wavefront's stream engine on a global-
-    # memory BVH: float BVH4, quantised BVH4 (MH_BVH4Q=1) or BVH2
+    # memory BVH: float BVH4, quantised BVH4 (MH_BVH4Q=1) or BVH2; "-ovf": a
+    # 4-entry LDS stack, so most rays take the global overflow region too
     monkeypatch.setenv("MH_BVH4", "0" if bvh4 == "0" else "1")
     monkeypatch.setenv("MH_BVH4Q", "1" if bvh4 == "q" else "0")
+    if bvh4.endswith("-ovf"):
+        monkeypatch.setenv("MH_STREAM_STACK", "4")
     mi = _mi()
     scene = _blob_scene(mi)
     rays = random_rays(scene, 1 << 16, seed=4)
@@ -887,10 +890,12 @@ def test_large_mesh_trace_parity(bvh4, monkeypatch):
     assert (rshape == 8).mean() > 0.02      # the blob is hit
 
 
-@pytest.mark.parametrize("bvh4,fused", [("1", "1"), ("1", "0"), ("q", "1"), ("q", "0"), ("0", "1")])
+@pytest.mark.parametrize("bvh4,fused", [("1", "1"), ("1", "0"), ("q", "1"), ("q", "0"), ("0", "1"), ("1-ovf", "0")])
 def test_large_mesh_per_sample_parity(bvh4, fused, monkeypatch):
     monkeypatch.setenv("MH_BVH4", "0" if bvh4 == "0" else "1")
     monkeypatch.setenv("MH_BVH4Q", "1" if bvh4 == "q" else "0")
+    if bvh4.endswith("-ovf"):
+        monkeypatch.setenv("MH_STREAM_STACK", "4")
     monkeypatch.setenv("MH_WF_FUSED", fused)
     mi = _mi()
     from mitsuba_hip import _abi as A

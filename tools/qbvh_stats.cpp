@@ -18,7 +18,7 @@
 
 using namespace mh;
 
-struct Stats { double nodes = 0, node_lines = 0, prims = 0, prim_lines = 0; };
+struct Stats { double nodes = 0, node_lines = 0, prims = 0, prim_lines = 0; size_t max_sp = 0; std::vector<uint64_t> sp_hist = std::vector<uint64_t>(128, 0); };
 
 static bool slab(const float lo[3], const float hi[3], const float inv[3], const float ood[3], float tmax, float &tl) {
     float a[3], b[3];
@@ -55,7 +55,9 @@ static void trace(const void *nodes, const Prim *P, const float o[3], const floa
     std::vector<uint32_t> st{0u};
     std::set<uint64_t> nl, pl;
     const size_t nsz = Q ? sizeof(QNode4) : sizeof(Node4), psz = Q ? sizeof(PrimC) : sizeof(Prim);
+    size_t ray_max = 0;
     while (!st.empty()) {
+        ray_max = std::max(ray_max, st.size());
         uint32_t r = st.back();
         st.pop_back();
         if (r & 0x80000000u) {
@@ -111,6 +113,8 @@ static void trace(const void *nodes, const Prim *P, const float o[3], const floa
     }
     s.node_lines += nl.size();
     s.prim_lines += pl.size();
+    s.max_sp = std::max(s.max_sp, ray_max);
+    s.sp_hist[std::min<size_t>(127, ray_max)]++;
     g_best = best;
 }
 static float hit_t(const void *n4, const Prim *P, const float o[3], const float d[3]) {
@@ -203,6 +207,16 @@ int main(int argc, char **argv) {
                    128.0 * (s.node_lines + s.prim_lines) / n_rays);
         };
         pr("float", sf, sizeof(Node4), sizeof(Prim));
+        {
+            uint64_t tot = 0, over[4] = {0, 0, 0, 0};
+            const size_t caps[4] = {16, 20, 24, 32};
+            for (size_t k = 0; k < 128; ++k) {
+                tot += sf.sp_hist[k];
+                for (int c = 0; c < 4; ++c) if (k > caps[c]) over[c] += sf.sp_hist[k];
+            }
+            printf("  max stack %zu (bound 3*depth4+2 = %u); rays over 16/20/24/32: %llu %llu %llu %llu of %llu\n", sf.max_sp, 3 * d4 + 2,
+                   (unsigned long long)over[0], (unsigned long long)over[1], (unsigned long long)over[2], (unsigned long long)over[3], (unsigned long long)tot);
+        }
         pr("quant", sq, sizeof(QNode4), sizeof(PrimC));
     }
     printf("bvh2 nodes %u, node4 %u (%.1f MB), qnode4 %u (%.1f MB), prims %u (%.1f / %.1f MB)\n", b.n_nodes, c4,
