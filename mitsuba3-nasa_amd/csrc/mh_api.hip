@@ -474,14 +474,16 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     // (tools/qbvh_stats: at most 14 entries on those meshes).  So the first
     // kStreamStack entries live in LDS and deeper ones in a global overflow
     // region, one column per thread of the largest stream-kernel grid: exact
-    // for any depth, and 5 waves per SIMD (1M triangles: 403 -> 537
-    // Msamples/s measured with a 24-entry LDS stack).  MH_STREAM_STACK overrides.
+    // for any depth, and 6 waves per SIMD.  Same box, path 512^2 @ 64 on the
+    // 1M / 4M-triangle meshes: 386 / 317 Msamples/s with the full LDS stack,
+    // 522 / 434 capped at 12-20 entries (5 waves), 534-538 / 446-451 at 6
+    // waves (MH_STREAM_WAVES).  MH_STREAM_STACK overrides the cap.
     S.stream_stack = S.stack_size;
     S.stack_ovf = nullptr;
     S.ovf_threads = 0;
     if (S.lds_bytes_bvh == 0 && (S.nodes4 || S.qnodes)) {
         const char *es = getenv("MH_STREAM_STACK");
-        const uint32_t cap = es ? (uint32_t)std::max(4, atoi(es)) : 24u;
+        const uint32_t cap = es ? (uint32_t)std::max(4, atoi(es)) : 20u;
         if (cap < S.stack_size) {
             int cus = 256;
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);

@@ -392,6 +392,7 @@ MH_DEV void trav_inner_step(TravLane &t, const Node *nodes, const LdsBvh &stk) {
 // one inner step on the wide BVH: the four child boxes of a Node4 (one
 // 128-B record, SoA planes), the hit children sorted near to far, the nearest
 // taken and the others pushed far-first (at most 3 pushes per step)
+template <bool Shadow>
 MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, const LdsBvh &stk) {
     if (t.node == kNoNode) {
         if (t.sp == 0) { t.node = kDone; return; }
@@ -421,6 +422,21 @@ MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, const LdsBvh &stk)
         cnt += h ? 1u : 0u;
     }
     // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance
+    if (Shadow) {
+        // any hit: the visiting order changes only which occluder is found
+        // first, not whether one is, so the hit children go as they come --
+        // the first is taken, the others pushed (no sort)
+        if (cnt == 0) { t.node = kNoNode; return; }
+        uint32_t first = kNoNode;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (tc[c] == __builtin_huge_valf()) continue;
+            if (first == kNoNode) first = rc[c];
+            else { stk.push(t.sp, rc[c]); ++t.sp; }
+        }
+        trav_take(t, first);
+        return;
+    }
 #define MH_CSWAP(i, j)                                                           \
     {                                                                            \
         const bool sw = tc[j] < tc[i];                                           \
@@ -443,6 +459,7 @@ MH_DEV void trav_inner_step4(TravLane &t, const Node4 *nodes, const LdsBvh &stk)
 // trav_inner_step4 on the decoded box
 MH_DEV float qscale(uint32_t ebits, uint32_t a) { return __uint_as_float(((ebits >> (8u * a)) & 0xffu) << 23); }
 MH_DEV float qbyte(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); }
+template <bool Shadow>
 MH_DEV void trav_inner_step_q(TravLane &t, const QNode4 *nodes, const LdsBvh &stk) {
     if (t.node == kNoNode) {
         if (t.sp == 0) { t.node = kDone; return; }
@@ -473,6 +490,21 @@ MH_DEV void trav_inner_step_q(TravLane &t, const QNode4 *nodes, const LdsBvh &st
         tc[c] = h ? lo : __builtin_huge_valf();
         rc[c] = rf[c];
         cnt += h ? 1u : 0u;
+    }
+    if (Shadow) {
+        // any hit: the visiting order changes only which occluder is found
+        // first, not whether one is, so the hit children go as they come --
+        // the first is taken, the others pushed (no sort)
+        if (cnt == 0) { t.node = kNoNode; return; }
+        uint32_t first = kNoNode;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (tc[c] == __builtin_huge_valf()) continue;
+            if (first == kNoNode) first = rc[c];
+            else { stk.push(t.sp, rc[c]); ++t.sp; }
+        }
+        trav_take(t, first);
+        return;
     }
 #define MH_CSWAP(i, j)                                                           \
     {                                                                            \
@@ -535,6 +567,10 @@ MH_DEV void trav_leaf_c(TravLane &t, const PrimC *pc, const Prim *prims) {
 
 // node formats of the per-lane stream engine
 enum { kEngBvh2 = 0, kEngWide = 1, kEngQuant = 2 };
+#ifndef MH_SHADOW_UNSORTED
+#define MH_SHADOW_UNSORTED 1  // shadow rays skip the near-to-far sort of the wide nodes' children
+#endif
+constexpr bool kShadowUnsorted = MH_SHADOW_UNSORTED != 0;
 
 // Traces items [r0, r1) of this wave.  load(item) -> RayT, store(item, hit,
 // found).  Must be called by all 64 lanes of the wave (uniform r0, r1).
@@ -554,8 +590,8 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
             const bool ready = !has || t.nleaf != 0 || t.node == kDone;
             if (!__any(inner) || __all(ready)) break;
             if (inner) {
-                if (Eng == kEngQuant) trav_inner_step_q(t, B.qnodes, B);
-                else if (Eng == kEngWide) trav_inner_step4(t, B.nodes4, B);
+                if (Eng == kEngQuant) trav_inner_step_q<Shadow && kShadowUnsorted>(t, B.qnodes, B);
+                else if (Eng == kEngWide) trav_inner_step4<Shadow && kShadowUnsorted>(t, B.nodes4, B);
                 else trav_inner_step(t, B.nodes, B);
             }
         }

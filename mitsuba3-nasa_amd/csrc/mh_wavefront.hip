@@ -268,12 +268,14 @@ MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1
     r1 = min(n, r0 + per);
 }
 
-// occupancy target of the unfused trace kernels (experiments: -DMH_STREAM_WAVES=n)
-#ifdef MH_STREAM_WAVES
-#define MH_STREAM_LB __launch_bounds__(256, MH_STREAM_WAVES)
-#else
-#define MH_STREAM_LB __launch_bounds__(256)
+// occupancy target of the unfused trace kernels (experiments: -DMH_STREAM_WAVES=n).
+// With the LDS stack capped (DScene::stream_stack) registers set it: 6 waves
+// per SIMD (80 VGPRs, 2 spilled) measured +3-4 % over 5 on 1M / 4M-triangle
+// meshes (522 -> 536 / 434 -> 450 Msamples/s), 8 waves (64 VGPRs) -10 %.
+#ifndef MH_STREAM_WAVES
+#define MH_STREAM_WAVES 6
 #endif
+#define MH_STREAM_LB __launch_bounds__(256, MH_STREAM_WAVES)
 
 // Packet: wave-coherent engine (small BVHs) instead of the per-lane stream engine
 template <bool InLds, bool Packet>
@@ -1829,7 +1831,7 @@ __global__ void k_fx_fold(const long long *__restrict__ acc, float *__restrict__
 }
 
 template <bool InLds, bool Packet, int NR>
-__global__ void __launch_bounds__(256)
+__global__ void MH_STREAM_LB
 k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
