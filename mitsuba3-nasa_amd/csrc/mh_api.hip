@@ -462,6 +462,14 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
                     S.primsc = reinterpret_cast<const PrimC *>(s->primsc.ptr);
                 } else {
                     S.nodes4 = reinterpret_cast<const Node4 *>(s->nodes4.ptr);
+                    // MH_PRIMC=1: the compact 48-B triangle records with the float BVH4
+                    const char *epc = getenv("MH_PRIMC");
+                    if (epc && !strcmp(epc, "1")) {
+                        std::vector<uint8_t> qn, pc2;
+                        uint32_t c2 = 0, d2 = 0;
+                        if (build_qbvh4(bvh, qn, pc2, c2, d2) && upload(s->primsc, pc2.data(), pc2.size(), st) == hipSuccess)
+                            S.primsc = reinterpret_cast<const PrimC *>(s->primsc.ptr);
+                    }
                 }
                 S.stack_size = std::max(S.stack_size, stack4);
             }

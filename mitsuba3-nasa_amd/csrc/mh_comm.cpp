@@ -281,5 +281,12 @@ int comm_reduce_one(mh_comm *c, int device, float *buf, uint64_t count, hipStrea
     if (c->device != device)
         return mh_report_error(MH_ERR_INVALID_ARGUMENT, "MH_FLAG_REDUCE: the communicator's device is not the scene's");
     void *sp = st;
-    return mh_comm_reduce(&c, 1, &buf, count, &sp, root);
+    int rc = mh_comm_reduce(&c, 1, &buf, count, &sp, root);
+    // test hook (tests/test_gpu_comm.py): a one-rank sum leaves the data as it
+    // is, so a wrong extent, buffer or root would go unseen; MH_TEST_COMM_SCALE
+    // doubles exactly the reduced extent (buf += buf) at world size 1
+    if (rc == MH_OK && c->nranks == 1 && count && getenv("MH_TEST_COMM_SCALE"))
+        if (mh::launch_accumulate(buf, buf, count, st) != hipSuccess)
+            rc = mh_report_error(MH_ERR_HIP, "MH_TEST_COMM_SCALE: launch failed");
+    return rc;
 }

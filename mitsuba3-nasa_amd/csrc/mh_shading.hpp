@@ -300,6 +300,11 @@ MH_DEV DScene stage_tables(const DScene &S, uint4 *lds) {
     return T;
 }
 
+// rank of this lane among the lanes set in m below it (v_mbcnt_lo / _hi)
+MH_DEV uint32_t lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // ---------------------------------------------------------------------------
 // Stream traversal engine for the wavefront kernels: while-while traversal
 // (inner-node phase until every lane holds a leaf, then a grouped leaf phase)
@@ -566,7 +571,7 @@ MH_DEV void trav_leaf_c(TravLane &t, const PrimC *pc, const Prim *prims) {
 }
 
 // node formats of the per-lane stream engine
-enum { kEngBvh2 = 0, kEngWide = 1, kEngQuant = 2 };
+enum { kEngBvh2 = 0, kEngWide = 1, kEngQuant = 2, kEngWideC = 3 };  // WideC: float BVH4 + PrimC
 #ifndef MH_SHADOW_UNSORTED
 #define MH_SHADOW_UNSORTED 1  // shadow rays skip the near-to-far sort of the wide nodes' children
 #endif
@@ -591,13 +596,15 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
             if (!__any(inner) || __all(ready)) break;
             if (inner) {
                 if (Eng == kEngQuant) trav_inner_step_q<Shadow && kShadowUnsorted>(t, B.qnodes, B);
-                else if (Eng == kEngWide) trav_inner_step4<Shadow && kShadowUnsorted>(t, B.nodes4, B);
+                else if (Eng == kEngWide || Eng == kEngWideC) trav_inner_step4<Shadow && kShadowUnsorted>(t, B.nodes4, B);
                 else trav_inner_step(t, B.nodes, B);
             }
         }
         // grouped leaf phase
         if (has && t.nleaf) {
-            if (Eng == kEngQuant) trav_leaf_c<Shadow>(t, B.primsc, B.prims);
+            // compact 48-B triangle records when the scene carries them (the
+            // quantised BVH always; the float BVH4 with MH_PRIMC=1)
+            if (Eng == kEngQuant || Eng == kEngWideC) trav_leaf_c<Shadow>(t, B.primsc, B.prims);
             else trav_leaf<Shadow>(t, B.prims);
         }
         if (has && t.node == kNoNode && t.sp == 0 && t.nleaf == 0) t.node = kDone;
@@ -606,7 +613,7 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
         if (fin) store(item, t.hit, t.hit.shape != MH_INVALID);
         const bool need = fin || !has;
         const unsigned long long m = __ballot(need);
-        const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        const uint32_t rank = lane_rank(m);
         if (need) {
             const uint32_t cand = fetched + rank;
             has = cand < r1;
@@ -619,11 +626,17 @@ MH_DEV void trace_stream(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, S
     }
 }
 
+// the stream engine's node format of a scene (host: kernel dispatch)
+__host__ __device__ inline int stream_engine(const DScene &S) {
+    return S.qnodes ? kEngQuant : S.nodes4 ? (S.primsc ? kEngWideC : kEngWide) : kEngBvh2;
+}
+
 // the stream engine on whichever node format the scene carries (quantised
 // BVH4, float BVH4, BVH2); B is wave-uniform, so the branch is scalar
 template <bool Shadow, class Load, class Store>
 MH_DEV void trace_stream_any(const LdsBvh &B, uint32_t r0, uint32_t r1, Load load, Store store) {
     if (B.qnodes) trace_stream<Shadow, kEngQuant>(B, r0, r1, load, store);
+    else if (B.nodes4 && B.primsc) trace_stream<Shadow, kEngWideC>(B, r0, r1, load, store);
     else if (B.nodes4) trace_stream<Shadow, kEngWide>(B, r0, r1, load, store);
     else trace_stream<Shadow, kEngBvh2>(B, r0, r1, load, store);
 }
@@ -911,9 +924,6 @@ struct Defer {
     uint32_t first[kMaxDefer], ntri[kMaxDefer], pc[kMaxDefer];
 };
 
-MH_DEV uint32_t lane_rank(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
 // The triangle run [first, first + count) for the lanes `live`: dense packet
 // test, or deferred when few lanes overlap the leaf.

@@ -92,19 +92,33 @@ static bool wf_unfused() {
     const char *e = getenv("MH_WF_FUSED");
     return e && !strcmp(e, "0");
 }
+// the stream kernels are instantiated per node format (Eng), so each one's
+// register allocation is that of its own traversal engine
 #define MH_WF_DISPATCH(K, ...)                                                                        \
     do {                                                                                              \
-        if (lds && packet) hipLaunchKernelGGL((K<true, true>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);   \
-        else if (lds) hipLaunchKernelGGL((K<true, false>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);     \
-        else if (packet) hipLaunchKernelGGL((K<false, true>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);  \
-        else hipLaunchKernelGGL((K<false, false>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);             \
+        const dim3 g_(grid), b_(256);                                                                 \
+        if (lds && packet) hipLaunchKernelGGL((K<true, true, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__);         \
+        else if (lds) hipLaunchKernelGGL((K<true, false, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__);           \
+        else if (packet) hipLaunchKernelGGL((K<false, true, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__);        \
+        else switch (stream_engine(S)) {                                                              \
+            case kEngQuant: hipLaunchKernelGGL((K<false, false, kEngQuant>), g_, b_, sh, st, __VA_ARGS__); break; \
+            case kEngWideC: hipLaunchKernelGGL((K<false, false, kEngWideC>), g_, b_, sh, st, __VA_ARGS__); break; \
+            case kEngWide: hipLaunchKernelGGL((K<false, false, kEngWide>), g_, b_, sh, st, __VA_ARGS__); break;   \
+            default: hipLaunchKernelGGL((K<false, false, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__); break;        \
+        }                                                                                             \
     } while (0)
 #define MH_WF_DISPATCH_NR(K, NR, ...)                                                                 \
     do {                                                                                              \
-        if (lds && packet) hipLaunchKernelGGL((K<true, true, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);   \
-        else if (lds) hipLaunchKernelGGL((K<true, false, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);     \
-        else if (packet) hipLaunchKernelGGL((K<false, true, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);  \
-        else hipLaunchKernelGGL((K<false, false, NR>), dim3(grid), dim3(256), sh, st, __VA_ARGS__);             \
+        const dim3 g_(grid), b_(256);                                                                 \
+        if (lds && packet) hipLaunchKernelGGL((K<true, true, NR, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__);     \
+        else if (lds) hipLaunchKernelGGL((K<true, false, NR, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__);       \
+        else if (packet) hipLaunchKernelGGL((K<false, true, NR, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__);    \
+        else switch (stream_engine(S)) {                                                              \
+            case kEngQuant: hipLaunchKernelGGL((K<false, false, NR, kEngQuant>), g_, b_, sh, st, __VA_ARGS__); break; \
+            case kEngWideC: hipLaunchKernelGGL((K<false, false, NR, kEngWideC>), g_, b_, sh, st, __VA_ARGS__); break; \
+            case kEngWide: hipLaunchKernelGGL((K<false, false, NR, kEngWide>), g_, b_, sh, st, __VA_ARGS__); break;   \
+            default: hipLaunchKernelGGL((K<false, false, NR, kEngBvh2>), g_, b_, sh, st, __VA_ARGS__); break;        \
+        }                                                                                             \
     } while (0)
 
 static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -208,7 +222,9 @@ MH_DEV uint32_t wave_append(uint32_t *count, bool pred) {
     uint32_t base = 0;
     if (lane_id() == 0 && tot) base = atomicAdd(count, tot);
     base = __builtin_amdgcn_readfirstlane(base);
-    const uint32_t off = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+    // the lanes below this one (v_mbcnt: no 64-bit lane mask kept live across
+    // the kernel's loop, which the PRB bounce spilled to scratch)
+    const uint32_t off = lane_rank(m);
     return base + off;
 }
 
@@ -278,7 +294,7 @@ MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1
 #define MH_STREAM_LB __launch_bounds__(256, MH_STREAM_WAVES)
 
 // Packet: wave-coherent engine (small BVHs) instead of the per-lane stream engine
-template <bool InLds, bool Packet>
+template <bool InLds, bool Packet, int Eng>
 __global__ void MH_STREAM_LB
 k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -300,7 +316,7 @@ k_wf_trace(DScene S, WfState w, int cur, uint32_t seg_cap, uint32_t *ctr) {
         w.ht[j] = h.t; w.hu[j] = h.u; w.hv[j] = h.v; w.hp[j] = h.prim; w.hs[j] = h.shape;
     };
     if (Packet) trace_packet<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
-    else trace_stream_any<false>(B, r0, r1, load, store);
+    else trace_stream<false, Eng>(B, r0, r1, load, store);
 }
 
 // one iteration of PathIntegrator::sample for every queued path
@@ -660,7 +676,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
 }
 
-template <bool InLds, bool Packet>
+template <bool InLds, bool Packet, int Eng>
 __global__ void MH_STREAM_LB
 k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -683,7 +699,7 @@ k_wf_shadow(DScene S, WfState w, uint64_t plane, float *out, uint32_t seg_cap, u
         out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
     };
     if (Packet) trace_packet<true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
-    else trace_stream_any<true>(B, r0, r1, load, store);
+    else trace_stream<true, Eng>(B, r0, r1, load, store);
 }
 
 // ---------------------------------------------------------------------------
@@ -1830,7 +1846,7 @@ __global__ void k_fx_fold(const long long *__restrict__ acc, float *__restrict__
         grad[i] += (float)((double)acc[i] * inv);
 }
 
-template <bool InLds, bool Packet, int NR>
+template <bool InLds, bool Packet, int NR, int Eng>
 __global__ void MH_STREAM_LB
 k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
     extern __shared__ uint4 lds[];
@@ -1861,7 +1877,7 @@ k_wf_shadow_prb(DScene S, WfState w, WfPrb q, uint32_t seg_cap, uint32_t *ctr) {
             }
     };
     if (Packet) trace_packet<true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, B, r0, r1, load, store);
-    else trace_stream_any<true>(B, r0, r1, load, store);
+    else trace_stream<true, Eng>(B, r0, r1, load, store);
     flush_partial(acc, q);
 }
 

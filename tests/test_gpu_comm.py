@@ -115,6 +115,100 @@ def test_render_reduce_flags_world1_match_plain_calls():
     comm.close()
 
 
+def test_reduce_extents_with_scale_hook(monkeypatch):
+    """Which extents the in-call reductions cover: with MH_TEST_COMM_SCALE a
+    one-rank sum doubles its buffer (mh_comm.cpp comm_reduce_one), so the film
+    (MH_FLAG_REDUCE and _ROOT), the W image and the gradients -- rgb, bitmap,
+    and prbvolpath's grid (corner-gathered) + albedo -- must come out exactly
+    twice the plain calls' (local W: no W reduction), and the backward with
+    the in-call W reduction exactly equal to the plain one (2 W halves dL,
+    the gradient sum doubles it back).  Deterministic mode: bit-comparable."""
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip.comm import Comm, scene_set_comm
+    D = A.FLAG_DETERMINISTIC
+    tex = np.random.default_rng(1).uniform(0.2, 0.8, (8, 8, 3)).astype(np.float32)
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"] = d["sensor"]["film"]["height"] = 32
+    d["red"]["reflectance"] = {"type": "bitmap", "data": tex, "filter_type": "bilinear", "wrap_mode": "repeat",
+                               "raw": True}
+    scene = mi.load_dict(d)
+    integ = mi.load_dict({"type": "path", "max_depth": 5})
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    scene_set_comm(scene, comm)
+    monkeypatch.setenv("MH_TEST_COMM_SCALE", "1")
+    plain, red, root = _film(scene, torch), _film(scene, torch), _film(scene, torch)
+    _render(A, scene, integ, 5, 16, plain, D)
+    _render(A, scene, integ, 5, 16, red, D | A.FLAG_REDUCE)
+    _render(A, scene, integ, 5, 16, root, D | A.FLAG_REDUCE_ROOT)
+    torch.cuda.synchronize()
+    assert float(plain.abs().max()) > 0
+    assert torch.equal(red, 2 * plain) and torch.equal(root, 2 * plain)
+    # W image
+    w0 = torch.zeros((32, 32), device="cuda:0")
+    w1 = torch.zeros((32, 32), device="cuda:0")
+    for w, f in ((w0, 0), (w1, A.FLAG_REDUCE)):
+        A.check(A.lib().mh_prb_weights(scene.handle(0), 9, 16, 0, 0, C.c_void_p(w.data_ptr()),
+                                       A.FLAG_DEVICE_POINTERS | D | f))
+    torch.cuda.synchronize()
+    assert torch.equal(w1, 2 * w0)
+    # gradients: an rgb slot and a bitmap slot
+    prb = mi.load_dict({"type": "prb", "max_depth": 5})
+    params = mi.traverse(scene)
+    keys = ["white.reflectance.value", "red.reflectance.data"]
+    gi = torch.full((32, 32, 3), 1.0 / (32 * 32 * 3), device="cuda:0")
+
+    def bwd(sc, ps, ks, integrator, flags, gin):
+        tex_ids = (C.c_uint32 * len(ks))(*[ps.param_id(k) for k in ks])
+        outs = [torch.zeros(ps[k].shape, dtype=torch.float32, device="cuda:0") for k in ks]
+        ptr = (C.c_void_p * len(ks))(*[o.data_ptr() for o in outs])
+        ic = integrator.c()
+        A.check(A.lib().mh_render_backward(sc.handle(0), C.byref(ic), 9, 16, 0, 0, C.c_void_p(gin.data_ptr()),
+                                           None, len(ks), tex_ids, ptr, A.FLAG_DEVICE_POINTERS | D | flags, None))
+        torch.cuda.synchronize()
+        return [o.cpu().numpy() for o in outs]
+
+    g0 = bwd(scene, params, keys, prb, 0, gi)
+    g_local = bwd(scene, params, keys, prb, A.FLAG_REDUCE | A.FLAG_LOCAL_WEIGHTS, gi)
+    g_red = bwd(scene, params, keys, prb, A.FLAG_REDUCE, gi)
+    for k, a, b, c in zip(keys, g0, g_local, g_red):
+        assert np.abs(a).max() > 0, k
+        np.testing.assert_allclose(b, 2 * a, rtol=1e-6, atol=0, err_msg=k)
+        np.testing.assert_allclose(c, a, rtol=1e-6, atol=0, err_msg=k)
+    scene_set_comm(scene, None)
+    # prbvolpath: the grid sigma_t (corner blocks) and the albedo
+    dv = mi.volume_cube(24, 20, 8, grid=mi.fbm_grid(16), scale=4.0, max_depth=6)
+    dv["integrator"] = {"type": "prbvolpath", "max_depth": 6, "rr_depth": 5}
+    vs = mi.load_dict(dv)
+    scene_set_comm(vs, comm)
+    vp = mi.traverse(vs)
+    vkeys = ["medium1.sigma_t.data", "medium1.albedo.value"]
+    gv = torch.from_numpy(np.random.default_rng(2).standard_normal((20, 24, 3)).astype(np.float32)).cuda()
+    v0 = bwd(vs, vp, vkeys, vs.integrator(), 0, gv)
+    v_local = bwd(vs, vp, vkeys, vs.integrator(), A.FLAG_REDUCE | A.FLAG_LOCAL_WEIGHTS, gv)
+    for k, a, b in zip(vkeys, v0, v_local):
+        assert np.abs(a).max() > 0, k
+        np.testing.assert_allclose(b, 2 * a, rtol=1e-6, atol=0, err_msg=k)
+    scene_set_comm(vs, None)
+    comm.close()
+
+
+def test_comm_destroy_refused_while_attached():
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip.comm import Comm, scene_set_comm
+    scene = _scene(mi)
+    c = Comm(Comm.unique_id(), 1, 0, 0)
+    scene_set_comm(scene, c)
+    assert scene._comms[0] is c  # the scene keeps the Comm alive
+    with pytest.raises(A.MitsubaHipError, match="still attached"):
+        c.close()
+    scene_set_comm(scene, None)
+    assert 0 not in scene._comms
+    c.close()
+
+
 @pytest.mark.parametrize("n", [2, 3])
 def test_render_sharded_slabs_sum_to_one_render(n):
     mi = _mi()
