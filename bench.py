@@ -56,9 +56,11 @@ def parse():
                    help="every rank computes the whole W image (no W all-reduce; N x the W splat work)")
     p.add_argument("--film-all-reduce", action="store_true",
                    help="all-reduce the film to every rank instead of reducing it onto rank 0")
-    p.add_argument("--config", type=int, default=2, choices=(2, 5),
-                   help="2: 512^2 @ 256 spp per GPU (weak scaling, the headline); 5: 2048^2 @ 1024 spp total "
-                        "split over the ranks (strong scaling)")
+    p.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5),
+                   help="BASELINE.json configs[i-1]: 2 (default, the headline): 512^2 @ 256 spp per GPU fwd + PRB "
+                        "grad, weak scaling; 5: 2048^2 @ 1024 spp total split over the ranks (strong scaling); "
+                        "1: path 256^2 @ 16 (CPU leg: the scalar_rgb restatement); 3: prb gradient wrt a 64^2x3 "
+                        "albedo bitmap, 512^2 @ 64; 4: volpath, 256^3 fBm medium + HG, 256^2 @ 64")
     p.add_argument("--unpacked", action="store_true",
                    help="separate film and W collectives (3 per step) instead of one packed film + W all-reduce")
     p.add_argument("--backend", default="nccl",
@@ -179,6 +181,86 @@ def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
             "slab": slab, "fwd_slab": fwd_slab, "st_f": st_f, "st_b": st_b}
 
 
+def single_op(args, rank, world, dev):
+    """BASELINE configs 1, 3 and 4 as one-op steps on the rank's sample slab
+    (weak scaling; the film or gradient summed over the ranks): 1 = `path`
+    256^2 @ 16 (its CPU leg the scalar_rgb restatement, oracle_render_scalar),
+    3 = `prb` render_backward wrt a 64^2 x 3 albedo bitmap, 512^2 @ 64,
+    4 = `volpath` on the 256^3 fBm medium + HG, 256^2 @ 64."""
+    import torch
+    import mitsuba_hip as mi
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip import distributed as D
+    mi.set_variant("hip_ad_rgb")
+    st = A.Stats()
+    c = args.config
+    if c == 1:
+        res, spp = 256, 16
+        d = mi.cornell_box()
+        d["sensor"]["film"]["width"] = d["sensor"]["film"]["height"] = res
+        scene = mi.load_dict(d)
+        integ = mi.load_dict({"type": "path", "max_depth": args.max_depth})
+        work = f"config 1: cornell_box {res}x{res} @ {spp} spp/GPU, path fwd (max_depth {args.max_depth})"
+    elif c == 3:
+        res, spp = 512, 64
+        scene = mi.load_dict(mi.cornell_box_bitmap(64, res, res, spp))
+        integ = mi.load_dict({"type": "prb", "max_depth": args.max_depth})
+        params = mi.traverse(scene)
+        key = "white.reflectance.data"
+        grad_in = torch.full((res, res, 3), 1.0 / (res * res * 3), dtype=torch.float32, device=dev)
+        work = (f"config 3: cornell_box {res}x{res} @ {spp} spp/GPU, prb render_backward (max_depth "
+                f"{args.max_depth}) wrt '{key}' (64x64x3 bitmap)")
+    else:
+        res, spp = 256, 64
+        scene = mi.load_dict(mi.volume_cube(res, res, spp, grid=mi.fbm_grid(256)))
+        integ = scene.integrator()
+        work = f"config 4: volpath, 256^3 fBm heterogeneous medium + HG, {res}x{res} @ {spp} spp/GPU"
+    slab = D.sample_slab(rank, world, spp)
+
+    def step(i):
+        if c == 3:
+            (g,) = mi.render_backward(scene, params, grad_in, [key], integ, seed=i, spp=slab.spp_total,
+                                      spp_begin=slab.begin, spp_end=slab.end, stats=st)
+            return D.all_reduce_(g)
+        return D.all_reduce_(mi.render_film(scene, integ, seed=i, spp=slab.spp_total, spp_begin=slab.begin,
+                                            spp_end=slab.end, stats=st))
+
+    return scene, integ, res, spp, work, step, st
+
+
+def cpu_single_op(args, scene, integ, res, spp):
+    """The CPU leg of configs 1 / 3 / 4 (rank 0, N = 1): the oracle on all the
+    job's threads at a bounded spp (config 1: the scalar_rgb restatement)."""
+    import numpy as np
+    import oracle_py as O
+    threads = cpu_threads()
+    model, nproc, aff = cpu_info()
+    c = args.config
+    params = None
+
+    def run(s):
+        t0 = time.perf_counter()
+        if c == 1:
+            O.render_scalar(scene, integ, seed=0, spp=s, threads=threads)
+        elif c == 3:
+            gi = np.full((res, res, 3), 1.0 / (res * res * 3), np.float32)
+            O.render_backward(scene, integ, 1, s, gi, [scene.params["white.reflectance.data"][1]],
+                              [(64, 64, 3)], threads=threads)
+        else:
+            O.render(scene, integ, seed=0, spp=s, threads=threads)
+        return time.perf_counter() - t0
+
+    t1 = run(1)
+    s = int(max(1, min(spp, args.cpu_seconds / 4 / max(t1, 1e-3))))
+    s = 1 << max(0, s.bit_length() - 1)
+    best = min(run(s) for _ in range(2)) if s > 1 else t1
+    kind = "scalar_rgb restatement (oracle_render_scalar)" if c == 1 else "CPU restatement of llvm_ad_rgb"
+    return {"value": round(res * res * s / best / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{res}x{res} @ {s} spp on {threads} threads; min of 2 runs after 1 warm-up, {best:.2f} s each",
+            "label": f"{kind} (oracle/libmh_oracle.so: scalar C, no SIMD)", "cpu_model": model, "nproc": nproc,
+            "affinity": aff, "threads": threads}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -202,6 +284,8 @@ def main():
 
     from mitsuba_hip import _abi as A
     from mitsuba_hip import distributed as D
+    if args.config in (1, 3, 4):
+        return main_single_op(args, rank, world, dev, dist_on)
     if args.config == 5:  # BASELINE.json configs[4]: 2048^2 @ 1024 spp in total, strong scaling
         if 512 % world:
             raise SystemExit("--config 5 needs a rank count that divides 512")
@@ -355,6 +439,50 @@ def main():
             "rays_shadow_per_sample_prb": (round(st_b.rays_shadow / max(1, n_local), 4)
                                            if not args.fwd_only else None),
             "roofline": roofline, "roofline_other": roofline_other, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+
+
+def main_single_op(args, rank, world, dev, dist_on):
+    import torch
+    import torch.distributed as dist
+    from mitsuba_hip import distributed as D
+    scene, integ, res, spp, work, step, st = single_op(args, rank, world, dev)
+    for i in range(args.warmup):
+        step(1000 + i)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kms = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+        kms.append(st.ms_kernel)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    ms_step = elapsed / args.steps * 1e3
+    value = world * res * res * spp / (ms_step / 1e3) / 1e6
+    if rank == 0:
+        cpu = None if (args.no_cpu or world > 1) else cpu_single_op(args, scene, integ, res, spp)
+        names = {1: "path fwd", 3: "PRB grad (bitmap albedo)", 4: "volpath fwd"}
+        line = {
+            "metric": f"Msamples/s (pixels×spp/s) {names[args.config]}, BASELINE config {args.config}",
+            "value": round(value, 2), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded PCG32; procedural fBm grid for config 4)",
+            "config": {"workload": work, "film": f"{res}x{res}", "spp_per_gpu": spp, "spp_total": spp * world,
+                       "parallelism": f"sample-slab x{world}" + (" + all-reduce" if world > 1 else "")},
+            "kernel_ms": round(sum(kms) / len(kms), 3),
+            "rays_closest_per_sample": round(st.rays_closest / max(1, res * res * spp), 4),
+            "rays_shadow_per_sample": round(st.rays_shadow / max(1, res * res * spp), 4),
+            "roofline": None, "roofline_note": "rooflines of these kernels: DESIGN.md §3 and profiles/",
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist_on:
