@@ -46,12 +46,16 @@ struct WfState {
 };
 
 // Queues are split into kSeg statically partitioned segments (paths never
-// change segment).  Workgroup b serves segment b % kSeg, so a segment's state
+// change segment).  Workgroup b serves one segment (seg_iter), so a segment's state
 // stays on one XCD's L2 (blocks b, b+8, ... share an XCD) and every segment
 // has its own counters on a private 128-B line: no single-word atomic hot
 // spot (MI355X_MICROARCH.md "dequeue": one word saturates at ~88 ops/us).
 // Per bounce: kSeg x 32 uint32: [s*32 + 0] queue length, [s*32 + 1] shadow length.
 constexpr uint32_t kSeg = 64;
+#ifndef MH_SEG_XCD
+#define MH_SEG_XCD 1
+#endif
+static_assert(kSeg == 64, "seg_iter's XCD-contiguous map assumes 64 segments over 8 XCDs");
 #ifndef MH_BOUNCE_WAVES
 #define MH_BOUNCE_WAVES 5  // fused bounce kernels: waves per SIMD the register budget targets
 #endif
@@ -207,7 +211,17 @@ struct SegIter {
 };
 MH_DEV SegIter seg_iter() {
     SegIter it;
+    // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md:
+    // b and b + 8 share one).  MH_SEG_XCD = 1: the 8 segments of one XCD are
+    // consecutive (XCD x serves segments 8x .. 8x + 7: one contiguous eighth
+    // of the chunk's pixels, so its L2 caches one region's nodes and state);
+    // 0: segment b % 64 (XCD x serves x, x + 8, ...: bands spread over the
+    // image).  Either map gives a segment the blocks b = s' + 64 k.
+#if MH_SEG_XCD
+    it.seg = (blockIdx.x & 7u) * 8u + ((blockIdx.x >> 3) & 7u);
+#else
     it.seg = blockIdx.x % kSeg;
+#endif
     const uint32_t wpb = blockDim.x / 64u;
     it.wave = (blockIdx.x / kSeg) * wpb + threadIdx.x / 64u;
     it.nwaves = (gridDim.x / kSeg) * wpb;
