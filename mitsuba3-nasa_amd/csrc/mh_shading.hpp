@@ -1672,6 +1672,14 @@ static_assert(kMaxRgbParams == 4, "GradCtx names four small-slot accumulators");
 // MH_FLAG_DETERMINISTIC on prbvolpath (GradCtx::fx_mode): the small slots go
 // to int64 fixed point like the grid; the words after fx_max hold the
 // per-slot scales (doubles at byte 64) and sums (int64 x 3 at byte 192)
+// Pass 2 sums each wave's contributions in LDS (ds_add_u64: integer adds are
+// exact, so their order does not matter) and adds them to the global words
+// once per wave and component at the flush (flush_small_slots), instead of
+// three global int64 atomics on one word per contribution.  Every kernel that
+// builds a GradCtx does so and flushes it with whole waves.
+constexpr uint32_t kFxWaveWords = 3 * kMaxRgbParams, kFxMaxWaves = 16;  // blocks of up to 1024 threads
+static __shared__ unsigned long long g_fx_wave[kFxMaxWaves * kFxWaveWords];
+MH_DEV unsigned long long *fx_wave_sums() { return g_fx_wave + (threadIdx.x >> 6) * kFxWaveWords; }
 MH_DEV void acc_add_fx(GradCtx &g, int32_t k, V3 a) {
     if (g.fx_mode == 1) {
         const float m = fmaxf(fabsf(a.x), fmaxf(fabsf(a.y), fabsf(a.z)));
@@ -1679,7 +1687,7 @@ MH_DEV void acc_add_fx(GradCtx &g, int32_t k, V3 a) {
         return;
     }
     const double sc = reinterpret_cast<const double *>(reinterpret_cast<const uint8_t *>(g.fx_max) + 64)[k];
-    unsigned long long *w = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(g.fx_max) + 192) + 3 * k;
+    unsigned long long *w = fx_wave_sums() + 3 * k;
     atomicAdd(w + 0, (unsigned long long)__double2ll_rn((double)a.x * sc));
     atomicAdd(w + 1, (unsigned long long)__double2ll_rn((double)a.y * sc));
     atomicAdd(w + 2, (unsigned long long)__double2ll_rn((double)a.z * sc));
@@ -3466,6 +3474,16 @@ MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &
 // small (register-accumulated) gradient slots: wave butterfly, then one
 // atomic per wave and component
 MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
+    if (g.fx_mode == 2) {  // the wave's exact int64 sums -> the global words (acc_add_fx)
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t j = threadIdx.x & 63u;
+        if (j < 3u * ga.n_rgb) {
+            const unsigned long long v = fx_wave_sums()[j];
+            unsigned long long *w = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(g.fx_max) + 192);
+            if (v) atomicAdd(w + j, v);
+        }
+        return;
+    }
     for (uint32_t p = 0; p < ga.n_rgb; ++p) {
         const int slot = (int)p;
         const V3 a = acc_get(g, slot);
@@ -3480,6 +3498,10 @@ MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
 }
 
 MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
+    if (ga.fx_mode == 2) {  // this wave's LDS sums of acc_add_fx start at zero
+        if ((threadIdx.x & 63u) < kFxWaveWords) fx_wave_sums()[threadIdx.x & 63u] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+    }
     GradCtx g;
     g.slot_of_tex = ga.slot_of_tex;
     g.bufs = ga.bufs;
