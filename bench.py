@@ -342,7 +342,7 @@ def main():
         #                    written alike; the first bounce reads the sample's
         #                    grad / W texel (16 B)
         # with R = rays (sum of queue lengths), N = samples: survivors R - N.
-        # traffic / VALU issue from the PMC passes of profiles/r3_pmc.json
+        # traffic / VALU issue from the PMC passes of profiles/r4_pmc.json (r3 / r2 before)
         # (tools/profile_r2.sh: FETCH/WRITE corrected by the calib_fetch factors
         # for the kernel's access width; VALU issue = SQ_INSTS_VALU x 2 cycles /
         # (1024 SIMDs x launch time x measured clock)).
@@ -350,9 +350,9 @@ def main():
         avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
         n_local = H * W * args.spp
         pmc = {}
-        ppath = os.path.join(ROOT, "profiles", "r3_pmc.json")  # tools/profile_r2.sh of this round's build
-        if not os.path.exists(ppath):
-            ppath = os.path.join(ROOT, "profiles", "r2_pmc.json")
+        # tools/profile_r2.sh of the latest round's build
+        ppath = next((q for q in (os.path.join(ROOT, "profiles", f"r{r}_pmc.json") for r in (4, 3, 2))
+                      if os.path.exists(q)), "")
         if os.path.exists(ppath):
             try:
                 pmc = json.load(open(ppath)).get("kernels", {})

@@ -53,7 +53,7 @@ struct WfState {
 // Per bounce: kSeg x 32 uint32: [s*32 + 0] queue length, [s*32 + 1] shadow length.
 constexpr uint32_t kSeg = 64;
 #ifndef MH_SEG_XCD
-#define MH_SEG_XCD 1
+#define MH_SEG_XCD 0  // 1 measured slower: bench 1,859 -> 1,806, 1M-triangle mesh 558 -> 500 Msamples/s (round 4)
 #endif
 static_assert(kSeg == 64, "seg_iter's XCD-contiguous map assumes 64 segments over 8 XCDs");
 #ifndef MH_BOUNCE_WAVES
@@ -212,11 +212,12 @@ struct SegIter {
 MH_DEV SegIter seg_iter() {
     SegIter it;
     // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md:
-    // b and b + 8 share one).  MH_SEG_XCD = 1: the 8 segments of one XCD are
-    // consecutive (XCD x serves segments 8x .. 8x + 7: one contiguous eighth
-    // of the chunk's pixels, so its L2 caches one region's nodes and state);
-    // 0: segment b % 64 (XCD x serves x, x + 8, ...: bands spread over the
-    // image).  Either map gives a segment the blocks b = s' + 64 k.
+    // b and b + 8 share one).  Default: segment b % 64 (XCD x serves segments
+    // x, x + 8, ...: pixel bands spread over the image, so every XCD gets a
+    // share of every region's work).  MH_SEG_XCD = 1: XCD x serves segments
+    // 8x .. 8x + 7, one contiguous eighth of the pixels, for L2 locality --
+    // measured slower on the bench and the large meshes (the per-XCD loads
+    // become uneven).  Either map gives a segment the blocks b = s' + 64 k.
 #if MH_SEG_XCD
     it.seg = (blockIdx.x & 7u) * 8u + ((blockIdx.x >> 3) & 7u);
 #else
