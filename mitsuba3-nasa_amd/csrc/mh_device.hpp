@@ -41,6 +41,10 @@ static __device__ unsigned long long g_mh_guard[kGuardCount];
     do {                  \
     } while (0)
 #endif
+#ifdef MH_EXP_LOOKUPS
+// diagnostic build: density-grid lookups of this translation unit's kernels
+static __device__ unsigned long long g_mh_lookups;
+#endif
 
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInvPi = 0.31830988618379067154f;

@@ -2409,6 +2409,12 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     return w0x * 0.3f + w1y * 0.2f + w0z * 0.1f + (float)(x0 + y1 + z0) * 1e-9f;
 #endif
     const float *g = S.grid + m.grid_offset;
+#ifdef MH_EXP_LOOKUPS  // diagnostic build: count the lookups (one add per wave; results unchanged)
+    {
+        const unsigned long long ex = __builtin_amdgcn_read_exec();
+        if (lane_rank(ex) == 0) atomicAdd(&g_mh_lookups, (unsigned long long)__builtin_popcountll(ex));
+    }
+#endif
     // grid_index split per axis (brick-major part + texel-in-brick part, the
     // bit fields disjoint), 32-bit (mh_scene_create caps a grid at 2^32 texels)
     const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2, sy = nbx * 64u, sz = sy * nby;

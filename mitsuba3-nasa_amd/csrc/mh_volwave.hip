@@ -1765,12 +1765,25 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     unsigned long long *work = counters + 32;  // the 8 queue heads of this launch (128 B apart)
     hipError_t e = hipMemsetAsync(work, 0, 8 * 128, st);
     if (e != hipSuccess) return e;
+#ifdef MH_EXP_LOOKUPS
+    const unsigned long long zero = 0;
+    if ((e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mh_lookups), &zero, 8, 0, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+#endif
     if (pk && tab) MH_VS(false, true, true);
     else if (pk) MH_VS(false, true, false);
     else if (lds) MH_VS(true, false, false);
     else MH_VS(false, false, false);
 #undef MH_VS
 #undef MH_VS1
+#ifdef MH_EXP_LOOKUPS
+    {
+        unsigned long long nl = 0;
+        if ((e = hipMemcpyFromSymbolAsync(&nl, HIP_SYMBOL(g_mh_lookups), 8, 0, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return e;
+        fprintf(stderr, "MH_LOOKUPS k_vol_sched samples %llu lookups %llu\n", (unsigned long long)n, nl);
+    }
+#endif
     return hipGetLastError();
 }
 

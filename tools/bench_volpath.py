@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--integrator", default="volpath", choices=["volpath", "prbvolpath"])
     ap.add_argument("--no-nee", action="store_true", help="medium sample_emitters = false (diagnostic)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="prbvolpath: MH_FLAG_DETERMINISTIC backward (int64 fixed-point grid + albedo gradients)")
     a = ap.parse_args()
     import torch
     import mitsuba_hip as mi
@@ -77,7 +79,8 @@ def bench_prbvolpath(a, mi, A, scene, t_load):
 
     def step(seed):
         film = mi.render_film(scene, seed=seed, spp=a.spp, stats=sf)
-        g = mi.render_backward(scene, params, gi, keys, seed=seed + 1, spp=a.spp, stats=sb)
+        g = mi.render_backward(scene, params, gi, keys, seed=seed + 1, spp=a.spp, stats=sb,
+                               deterministic=a.deterministic)
         return film, g
 
     step(100)
@@ -95,6 +98,7 @@ def bench_prbvolpath(a, mi, A, scene, t_load):
            "unit": "Msamples/s", "ms_per_step": round(dt * 1e3, 3),
            "fwd_kernel_ms": round(sum(kf) / len(kf), 3), "bwd_kernel_ms": round(sum(kb) / len(kb), 3),
            "grad_sigma_t_abs_sum": float(g[0].abs().sum()), "grad_albedo": [float(x) for x in g[1]],
+           "deterministic": a.deterministic,
            "config": {"film": f"{a.res}x{a.res}", "spp": a.spp, "grid": f"{a.grid}^3 fBm",
                       "scene_load_s": round(t_load, 2)}}
     if not a.no_cpu:
