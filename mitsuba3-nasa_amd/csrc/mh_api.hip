@@ -434,6 +434,9 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.n_nodes = bvh.n_nodes;
     S.n_prims = bvh.n_prims;
     S.n_emitters = desc->n_emitters;
+    S.inv_n_emitters = 1.f / (float)S.n_emitters;  // inf for 0: never read then
+    S.n_emitters_f = (float)S.n_emitters;
+    S.env_pdf = kInv4Pi * S.inv_n_emitters;
     S.environment = desc->environment;
     S.stack_size = bvh.depth + 2;
     const size_t bvh_bytes = bvh.nodes.size() + bvh.prims.size();
@@ -511,6 +514,8 @@ int mh_scene_create(const mh_scene_desc *desc, int device, void *stream, mh_scen
     S.far_clip = sn.far_clip;
     S.width = sn.width;
     S.height = sn.height;
+    S.inv_width = 1.f / (float)S.width;
+    S.inv_height = 1.f / (float)S.height;
     S.rfilter = sn.rfilter;
     S.rfilter_radius = sn.rfilter_radius;
     memcpy(S.filter_coeff, sn.filter_coeff, sizeof(S.filter_coeff));

@@ -184,6 +184,10 @@ struct DScene {                 // kernel argument (by value)
     // thread g at (k - stream_stack) * ovf_threads + g; nullptr: none needed)
     uint32_t *stack_ovf;
     uint32_t stream_stack, ovf_threads;
+    // 1 / (float)width, 1 / (float)height, 1 / (float)n_emitters: divided on the host (correctly rounded,
+    // as the device's division), so the bounce kernels hold no per-lane loop-invariant quotients
+    float inv_width, inv_height, inv_n_emitters;
+    float n_emitters_f, env_pdf;  // (float)n_emitters; kInv4Pi * inv_n_emitters (a constant emitter's pdf)
 };
 
 // lane -> (pixel, sample) map of one render call (sample-slab aware)

@@ -124,7 +124,7 @@ k_render(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint32_
         lane_of(lm, k, lane, px, py);
         Pcg rng;
         rng.seed(seed_value, lane);
-        const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
+        const float sw = S.inv_width, sh = S.inv_height;
         for (uint32_t pass = 0; pass < n_passes; ++pass) {
             float jx = rng.next_float(), jy = rng.next_float();
             float sx = (float)px + jx, sy = (float)py + jy;
@@ -588,8 +588,8 @@ k_render_forward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         Pcg rng;
         rng.seed(seed_value, lane);
         const float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
-        RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                            __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+        RayT r = camera_ray(S, __builtin_fmaf(sx, S.inv_width, -0.f),
+                            __builtin_fmaf(sy, S.inv_height, -0.f));
         V3 dL;
         bool valid = false;
         if (Vol) {
@@ -656,8 +656,8 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
         Pcg rng;
         rng.seed(seed_value, lane);
         float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
-        RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                            __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+        RayT r = camera_ray(S, __builtin_fmaf(sx, S.inv_width, -0.f),
+                            __builtin_fmaf(sy, S.inv_height, -0.f));
         V3 dL = gather_dL_wave(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
         if (Fused) {
             prb_fused(S, B, in, rng, r, dL, ga.n_rgb, g, n_closest, n_shadow);
@@ -726,8 +726,8 @@ k_prbvol_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value
             Pcg rng;
             rng.seed(seed_value, lane);
             float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
-            RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                                __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+            RayT r = camera_ray(S, __builtin_fmaf(sx, S.inv_width, -0.f),
+                                __builtin_fmaf(sy, S.inv_height, -0.f));
             V3 dL = gather_dL_wave(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W (k_grad_over_w)
             Pcg rng_primal = rng;  // sampler.clone()
             if (wk.main) {  // single pass: primal + logged adjoint terms, replay only on overflow

@@ -1385,7 +1385,7 @@ MH_DEV float emitter_hit_pdf(const DScene &S, uint32_t em, const SI &si, V3 prev
     V3 rel = si.p - prev_p;
     ds.dist = norm(rel);
     ds.d = si.valid ? vdiv(rel, ds.dist) : -si.wi;
-    return area_pdf_direction(S, em, ds) * (1.f / (float)S.n_emitters);
+    return area_pdf_direction(S, em, ds) * S.inv_n_emitters;
 }
 
 // AreaLight::sample_direction -> Shape::sample_direction -> Rectangle::sample_position
@@ -1458,11 +1458,11 @@ MH_DEV V3 scene_sample_emitter_direction(const DScene &S, V3 ref_p, float sx, fl
     const uint32_t n = S.n_emitters;
     if (n == 0) return v3(0, 0, 0);
     if (n == 1) return emitter_sample_direction(S, 0, ref_p, sx, sy, ds);
-    const float nf = (float)n, scaled = sx * nf;
+    const float nf = S.n_emitters_f, scaled = sx * nf;  // (float)n, converted on the host
     uint32_t idx = (uint32_t)scaled;
     if (idx > n - 1) idx = n - 1;
     V3 spec = emitter_sample_direction(S, idx, ref_p, scaled - (float)idx, sy, ds);
-    ds.pdf *= 1.f / nf;
+    ds.pdf *= S.inv_n_emitters;  // 1 / nf, divided on the host
     return spec * nf;
 }
 
@@ -1478,7 +1478,7 @@ MH_DEV V3 emitter_eval(const DScene &S, uint32_t em, const SI &si) {
 MH_DEV float emitter_pdf_direction(const DScene &S, uint32_t em, const SI &si, V3 ref_p) {
     const DEmitter &e = S.emitters[em];
     if (e.type == MH_EMITTER_AREA) return emitter_hit_pdf(S, em, si, ref_p);
-    if (e.type == MH_EMITTER_CONSTANT) return kInv4Pi * (1.f / (float)S.n_emitters);
+    if (e.type == MH_EMITTER_CONSTANT) return S.env_pdf;  // kInv4Pi * inv_n_emitters, multiplied on the host
     return 0.f;
 }
 
@@ -1528,13 +1528,18 @@ MH_DEV RayT camera_ray(const DScene &S, float ax, float ay) {
 
 
 MH_DEV void lane_of(const LaneMap &m, uint64_t k, uint32_t &lane, uint32_t &px, uint32_t &py) {
+    // k < 2^32: a wavefront holds at most 2^32 samples (make_layout).  The
+    // divisions stay the compiler's: multiply-high forms with host-made
+    // multipliers freed the generating kernels' spills but measured 0.3-0.6 %
+    // slower on the bench (same box, 2 runs each)
+    const uint32_t k32 = (uint32_t)k;
     uint32_t pl, sl;
-    if (m.log_S < 32) { pl = (uint32_t)(k >> m.log_S); sl = (uint32_t)(k & ((1u << m.log_S) - 1u)); }
-    else { pl = (uint32_t)(k / m.S); sl = (uint32_t)(k - (uint64_t)pl * m.S); }
+    if (m.log_S < 32) { pl = k32 >> m.log_S; sl = k32 & ((1u << m.log_S) - 1u); }
+    else { pl = k32 / m.S; sl = k32 - pl * m.S; }
     uint32_t pixel = m.pixel_begin + pl;
     lane = pixel * m.spp_pp + (m.s_begin + sl);
     // recompute the reference's own mapping from the lane index
-    uint32_t pix2 = m.log_spp < 32 ? (lane >> m.log_spp) : (lane / m.spp_pp);
+    uint32_t pix2 = m.log_spp < 32 ? (lane >> m.log_spp) : lane / m.spp_pp;
     py = pix2 / m.W;
     px = pix2 - m.W * py;
 }
@@ -1680,10 +1685,16 @@ static_assert(kMaxRgbParams == 4, "GradCtx names four small-slot accumulators");
 constexpr uint32_t kFxWaveWords = 3 * kMaxRgbParams, kFxMaxWaves = 16;  // blocks of up to 1024 threads
 static __shared__ unsigned long long g_fx_wave[kFxMaxWaves * kFxWaveWords];
 MH_DEV unsigned long long *fx_wave_sums() { return g_fx_wave + (threadIdx.x >> 6) * kFxWaveWords; }
+// Pass 1 keeps the wave's maxima (the grid's, then each small slot's, as the
+// bits of non-negative floats) in the same LDS words and flushes them with one
+// global atomicMax per wave and word: every lane of every wave maxing one
+// global word serialised the pass on that word's L2 channel (config 4: the
+// deterministic backward 198 ms against 35 ms).
+MH_DEV unsigned int *fx_wave_max() { return reinterpret_cast<unsigned int *>(fx_wave_sums()); }
 MH_DEV void acc_add_fx(GradCtx &g, int32_t k, V3 a) {
     if (g.fx_mode == 1) {
         const float m = fmaxf(fabsf(a.x), fmaxf(fabsf(a.y), fabsf(a.z)));
-        if (m > 0.f) atomicMax(g.fx_max + 1 + k, __float_as_uint(m));
+        if (m > 0.f) atomicMax(fx_wave_max() + 1 + k, __float_as_uint(m));
         return;
     }
     const double sc = reinterpret_cast<const double *>(reinterpret_cast<const uint8_t *>(g.fx_max) + 64)[k];
@@ -2916,7 +2927,7 @@ MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8], const 
         float mx = 0.f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) mx = fmaxf(mx, fabsf(v[c]));
-        if (mx > 0.f) atomicMax(g.fx_max, __float_as_uint(mx));  // non-negative floats order as their bits
+        if (mx > 0.f) atomicMax(fx_wave_max(), __float_as_uint(mx));  // non-negative floats order as their bits
         return;
     }
     __shared__ float stage[kCornerWaves * 64 * 9];
@@ -3480,6 +3491,15 @@ MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &
 // small (register-accumulated) gradient slots: wave butterfly, then one
 // atomic per wave and component
 MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
+    if (g.fx_mode == 1) {  // the wave's maxima (corner_scatter, acc_add_fx) -> fx_max[0 .. n_rgb]
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t j = threadIdx.x & 63u;
+        if (j <= ga.n_rgb) {
+            const unsigned int v = fx_wave_max()[j];
+            if (v) atomicMax(g.fx_max + j, v);
+        }
+        return;
+    }
     if (g.fx_mode == 2) {  // the wave's exact int64 sums -> the global words (acc_add_fx)
         __builtin_amdgcn_wave_barrier();
         const uint32_t j = threadIdx.x & 63u;
@@ -3504,7 +3524,7 @@ MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
 }
 
 MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
-    if (ga.fx_mode == 2) {  // this wave's LDS sums of acc_add_fx start at zero
+    if (ga.fx_mode) {  // this wave's LDS maxima (pass 1) / sums (pass 2) start at zero
         if ((threadIdx.x & 63u) < kFxWaveWords) fx_wave_sums()[threadIdx.x & 63u] = 0ull;
         __builtin_amdgcn_wave_barrier();
     }

@@ -227,7 +227,7 @@ k_vw_main(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64
     vw_range(it, count, r0, r1);
     const uint64_t base = (uint64_t)it.seg * seg_cap;
     uint32_t *ctr_next = ctr_out + it.seg * 32;
-    const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
+    const float sw = S.inv_width, sh = S.inv_height;
     uint32_t n_closest = 0;
 #ifdef MH_EXP_VWCNT  // diagnostic build: loop trips / walk steps / wave iterations per round
     uint32_t n_trips = 0, n_iter = 0;
@@ -1551,7 +1551,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 #pragma unroll
     for (uint32_t k = 0; k < kNGroups; ++k) W[k] = (M::kMergeMed && k == kGHead) ? (uint32_t)MH_VS_MERGE_W : W0[k];
     constexpr uint32_t NG = M::kDeferEnd ? kNGroups : kGEnd;  // groups this machine uses
-    const float sw = 1.f / (float)S.width, sh = 1.f / (float)S.height;
+    const float sw = S.inv_width, sh = S.inv_height;
     uint32_t n_closest = 0, n_shadow = 0;
     M mc(bw, lm, seed_value);
     typename M::State v;
@@ -1833,8 +1833,8 @@ k_pvb_replay_paths(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_valu
         Pcg r;
         r.seed(seed_value, lane);
         const float sx = (float)px + r.next_float(), sy = (float)py + r.next_float();
-        const RayT ray = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                                    __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+        const RayT ray = camera_ray(S, __builtin_fmaf(sx, S.inv_width, -0.f),
+                                    __builtin_fmaf(sy, S.inv_height, -0.f));
         prbvol_sample<3>(S, B, in, r, ray, v3(d.x, d.y, d.z), v3(e.x, e.y, e.z), &g, nc, ns);
     }
     flush_small_slots(g, bw.ga);

@@ -265,8 +265,8 @@ k_wf_raygen(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plan
     Pcg rng;
     rng.seed(seed_value, lane);
     float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
-    RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                        __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+    RayT r = camera_ray(S, __builtin_fmaf(sx, S.inv_width, -0.f),
+                        __builtin_fmaf(sy, S.inv_height, -0.f));
     // slot k of buffer 0 == path k (segment s holds ids [s*L, (s+1)*L))
     w.pd[0][k] = (uint32_t)k;  // depth 0: prev_bsdf_delta = true on the first bounce
     w.ox[0][k] = r.o.x; w.oy[0][k] = r.o.y; w.oz[0][k] = r.o.z;
@@ -541,8 +541,8 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                     g.inc = pcg_inc(seed_value, lane);
                 }
                 const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
-                ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
-                                 __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
+                ray = camera_ray(S0, __builtin_fmaf(sx, S0.inv_width, -0.f),
+                                 __builtin_fmaf(sy, S0.inv_height, -0.f));
                 gen_state = g.state;
                 gen_inc = g.inc;  // the TEA of this lane, reused below
                 out[3 * plane + pid] = sx;
@@ -956,8 +956,8 @@ k_wf_raygen_prb(DScene S, LaneMap lm, uint32_t seed_value, uint64_t n, int coale
     Pcg rng;
     rng.seed(seed_value, lane);
     float sx = (float)px + rng.next_float(), sy = (float)py + rng.next_float();
-    RayT r = camera_ray(S, __builtin_fmaf(sx, 1.f / (float)S.width, -0.f),
-                        __builtin_fmaf(sy, 1.f / (float)S.height, -0.f));
+    RayT r = camera_ray(S, __builtin_fmaf(sx, S.inv_width, -0.f),
+                        __builtin_fmaf(sy, S.inv_height, -0.f));
     V3 dL = gather_dL(S, coalesce, grad_in, sx, sy);  // grad_in: pre-divided by W
     w.pd[0][k] = (uint32_t)k;
     w.ox[0][k] = r.o.x; w.oy[0][k] = r.o.y; w.oz[0][k] = r.o.z;
@@ -1254,8 +1254,8 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 Pcg g;
                 g.seed(seed_value, lane);
                 const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
-                ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
-                                 __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
+                ray = camera_ray(S0, __builtin_fmaf(sx, S0.inv_width, -0.f),
+                                 __builtin_fmaf(sy, S0.inv_height, -0.f));
                 gen_state = g.state;
                 gen_inc = g.inc;  // the TEA of this lane, reused below
 #ifdef MH_EXP_NO_GATHER  // diagnostic: cost of the first bounce's dL gather
@@ -1549,8 +1549,8 @@ k_wf_bounce_fwd(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 Pcg g;
                 g.seed(seed_value, lane);
                 const float sx = (float)px + g.next_float(), sy = (float)py + g.next_float();
-                ray = camera_ray(S0, __builtin_fmaf(sx, 1.f / (float)S0.width, -0.f),
-                                 __builtin_fmaf(sy, 1.f / (float)S0.height, -0.f));
+                ray = camera_ray(S0, __builtin_fmaf(sx, S0.inv_width, -0.f),
+                                 __builtin_fmaf(sy, S0.inv_height, -0.f));
                 gen_state = g.state;
                 gen_inc = g.inc;
                 fo.out[3 * fo.plane + pid] = sx;
