@@ -99,6 +99,8 @@ def bench_prbvolpath(a, mi, A, scene, t_load):
            "fwd_kernel_ms": round(sum(kf) / len(kf), 3), "bwd_kernel_ms": round(sum(kb) / len(kb), 3),
            "grad_sigma_t_abs_sum": float(g[0].abs().sum()), "grad_albedo": [float(x) for x in g[1]],
            "deterministic": a.deterministic,
+           "fwd_rays_closest_per_sample": round(sf.rays_closest / n, 3),
+           "fwd_rays_shadow_per_sample": round(sf.rays_shadow / n, 3),
            "config": {"film": f"{a.res}x{a.res}", "spp": a.spp, "grid": f"{a.grid}^3 fBm",
                       "scene_load_s": round(t_load, 2)}}
     if not a.no_cpu:
