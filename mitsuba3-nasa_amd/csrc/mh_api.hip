@@ -113,6 +113,7 @@ struct mh_scene {
     DevBuf grid_corner;  // prbvolpath backward: per-cell corner blocks of the grid sigma_t slots
     DevBuf fx_word;      // its deterministic pre-pass: the largest |item| (float bits)
     DevBuf bmp_fx;       // the deterministic bitmap scatter's max word + int64 texel sums
+    DevBuf replay_fx;    // the deterministic replay kernel: int64 mirror of the slot block (bitmap texels)
     // multi-GPU: the communicator of MH_FLAG_REDUCE (not owned), and the
     // buffers of the sharded entry points (slab W image, staged peer sums,
     // slab gradients)
@@ -1406,10 +1407,25 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
     const bool bmp_wf = !vol && n_bmp >= 1 && bmp_same_ch && !replay && !mega && wf_fused(s->S) &&
                         in->max_depth >= 1 && in->max_depth <= 32 && !(env_bwf && !strcmp(env_bwf, "0"));
     const bool wavefront = ((fused && in->max_depth <= 64 && !mega) || bmp_wf);
+    // MH_FLAG_DETERMINISTIC on the replay kernel (bitmaps the wavefront cannot
+    // take, MH_FLAG_PRB_REPLAY, megakernel): the int64 two-pass form of
+    // prbvolpath -- small slots through acc_add_fx, bitmap texels through
+    // bmp_add_fx into an int64 mirror of the slot block (no LDS accumulator)
+    const bool det_replay = deterministic(flags) && !vol && !wavefront;
+    const bool fxr = fx || det_replay;
+    if (det_replay) {
+        size_t total = 0;
+        for (int k = 0; k < kMaxParams; ++k) total += (counts[k] + 3) / 4 * 4;
+        MH_HIP(s->replay_fx.alloc(std::max<size_t>(total, 1) * 8));
+        MH_HIP(hipMemsetAsync(s->replay_fx.ptr, 0, std::max<size_t>(total, 1) * 8, st));
+        ga.fx_i64 = s->replay_fx.as<long long>();
+        ga.fx_f32 = s->tmp_c.as<float>();
+        ga.lds_slot = -1;
+    }
     size_t wf_ctr_words = 0, wf_chunks = 0;
     uint32_t *pvb_lost = nullptr;  // prbvolpath on the scheduler: overflow entries that found their list full
     double fx_inv = 1.0;           // deterministic grid gradient: 2^-S of the fixed point
-    double fx_small_inv[kMaxRgbParams] = {1.0, 1.0, 1.0, 1.0};  // and of the small slots
+    double fx_small_inv[kMaxParams] = {1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0};  // and of each slot
     // between the two passes of the deterministic grid gradient: the scale
     // from pass 1's largest |item|; pass 1's rgb-slot adds and counters go
     // fx_word: u32 max[0] (grid) and max[1 + k] (small slot k), double
@@ -1422,15 +1438,15 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         return 31 - ex;
     };
     auto fx_between = [&](GradArgs &gp) -> hipError_t {
-        uint32_t mb[1 + kMaxRgbParams] = {};
+        uint32_t mb[1 + kMaxParams] = {};  // words 1 + k: slot k (small slots; bitmaps on the replay)
         hipError_t e = hipMemcpyAsync(mb, s->fx_word.ptr, sizeof(mb), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = wait_stream(s, flags, st);
         if (e != hipSuccess) return e;
         const int S0 = fx_exp(mb[0]);
         fx_inv = std::ldexp(1.0, -S0);
         gp.fx_scale = std::ldexp(1.0, S0);
-        double sc[kMaxRgbParams];
-        for (int k = 0; k < kMaxRgbParams; ++k) {
+        double sc[kMaxParams];
+        for (int k = 0; k < kMaxParams; ++k) {
             fx_small_inv[k] = std::ldexp(1.0, -fx_exp(mb[1 + k]));
             sc[k] = std::ldexp(1.0, fx_exp(mb[1 + k]));
         }
@@ -1608,7 +1624,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
                                        main_cap ? s->pvp_main.as<float4>() : nullptr, main_cap));
         }
         }  // passes
-    } else if (fx) {  // prbvolpath replaying its NEE walks (MH_PVP_NEE_LOG=0), deterministic grid
+    } else if (fxr) {  // deterministic: prbvolpath replaying its NEE walks (MH_PVP_NEE_LOG=0), or the prb replay
         MH_HIP(s->fx_word.alloc(512));
         MH_HIP(hipMemsetAsync(s->fx_word.ptr, 0, 64, st));
         GradArgs gp = ga;
@@ -1623,7 +1639,12 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         MH_HIP(launch_prb_backward(s->S, *in, lane_map(L, 0), s->S.sampler_seed + seed, n, L.spp_pp >= 4,
                                    g_in, w, ga, fused, s->counters.as<unsigned long long>(), st));
     }
-    if (fx) MH_HIP(fx_small_fold());
+    if (fxr) MH_HIP(fx_small_fold());
+    if (det_replay)
+        for (int k = kMaxRgbParams; k < kMaxParams; ++k)
+            if (counts[k])
+                MH_HIP(launch_fx_to_float(s->replay_fx.as<long long>() + (bufs[k] - s->tmp_c.as<float>()), bufs[k],
+                                          counts[k], fx_small_inv[k], st));
     for (int k = 0; k < kMaxParams; ++k) {
         if (!P.corner[k]) continue;
         if (P.fx)

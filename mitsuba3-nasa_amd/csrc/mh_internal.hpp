@@ -41,6 +41,10 @@ struct GradArgs {
     uint32_t fx_mode = 0;
     uint32_t *fx_max = nullptr;
     double fx_scale = 0.0;
+    // MH_FLAG_DETERMINISTIC on the replay kernel: bitmap texel sums as int64,
+    // element i of the slot block (s->tmp_c) at fx_i64[i] (fx_f32 = the block)
+    long long *fx_i64 = nullptr;
+    const float *fx_f32 = nullptr;
 };
 
 // ---- BVH builder (host, binned SAH) --------------------------------------
@@ -154,6 +158,8 @@ hipError_t launch_corner_gather(const float *corner, float *grad, const uint32_t
 // the int64 fixed-point form (fx_mode 2): grad += (float)(exact integer sum / fx_scale)
 hipError_t launch_corner_gather_fx(const long long *corner, float *grad, const uint32_t res[3], double inv_scale,
                                    hipStream_t st);
+// deterministic bitmap texels of the replay kernel (GradArgs::fx_i64): grad += (float)(fx / scale)
+hipError_t launch_fx_to_float(const long long *fx, float *grad, uint64_t n, double inv_scale, hipStream_t st);
 hipError_t launch_grad_over_w(uint64_t n_px, const float *grad_in, const float *w, float *out, hipStream_t st);
 #ifdef MH_DEBUG
 hipError_t guard_read_wf(unsigned long long *out);  // kGuardCount words each, read and reset

@@ -626,7 +626,7 @@ k_render_forward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 // PRB backward: dL gather + primal + adjoint per lane (common.py:900-983)
 // ---------------------------------------------------------------------------
 #ifndef MH_PRB_WAVES
-#define MH_PRB_WAVES 4  // replay backward: 127-128 VGPRs (4 waves/SIMD) instead of 129 (3), no spills
+#define MH_PRB_WAVES 4  // replay backward: 128 VGPRs (4 waves/SIMD, ~28 spilled) measured faster than 3 waves
 #endif
 template <bool InLds, bool Fused>
 __global__ void __launch_bounds__(256, Fused ? 1 : MH_PRB_WAVES)
@@ -1032,6 +1032,19 @@ hipError_t launch_corner_gather_fx(const long long *corner, float *grad, const u
     const uint32_t g = (uint32_t)std::min<uint64_t>(blocks_for(n, 256), 8192);
     hipLaunchKernelGGL(k_corner_gather_fx, dim3(g), dim3(256), 0, st, corner, grad, (int32_t)res[0], (int32_t)res[1],
                        (int32_t)res[2], inv_scale);
+    return hipGetLastError();
+}
+
+// deterministic bitmap texels (replay kernel): grad[i] += (float)(fx[i] / scale)
+__global__ void k_fx_to_float(const long long *__restrict__ fx, float *__restrict__ grad, uint64_t n, double inv_scale) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (const long long q = fx[i]) grad[i] += (float)((double)q * inv_scale);
+}
+
+hipError_t launch_fx_to_float(const long long *fx, float *grad, uint64_t n, double inv_scale, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint32_t g = (uint32_t)std::min<uint64_t>(blocks_for(n, 256), 8192);
+    hipLaunchKernelGGL(k_fx_to_float, dim3(g), dim3(256), 0, st, fx, grad, n, inv_scale);
     return hipGetLastError();
 }
 

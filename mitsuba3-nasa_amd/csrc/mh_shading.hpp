@@ -1662,6 +1662,8 @@ struct GradCtx {
     uint32_t fx_mode;             // GradArgs::fx_mode (deterministic grid gradient)
     uint32_t *fx_max;
     double fx_scale;
+    long long *fx_i64;            // GradArgs::fx_i64 / fx_f32 (deterministic bitmap texels, replay kernel)
+    const float *fx_f32;
     int32_t lds_slot;             // bitmap slot whose texels accumulate in LDS (-1: none)
     float *lds_acc;               // that slot's workgroup accumulator
     uint32_t lds_floats;          // its size (floats; checked under MH_DEBUG)
@@ -1702,6 +1704,19 @@ MH_DEV void acc_add_fx(GradCtx &g, int32_t k, V3 a) {
     atomicAdd(w + 0, (unsigned long long)__double2ll_rn((double)a.x * sc));
     atomicAdd(w + 1, (unsigned long long)__double2ll_rn((double)a.y * sc));
     atomicAdd(w + 2, (unsigned long long)__double2ll_rn((double)a.z * sc));
+}
+// a bitmap texel's charge in fixed point (MH_FLAG_DETERMINISTIC on the replay
+// kernel): pass 1 the slot's largest |item| (wave max in LDS, word 1 + k),
+// pass 2 round(item * scale_k) added as int64 at the texel's mirror in fx_i64
+MH_DEV void bmp_add_fx(const GradCtx &g, int32_t k, const float *dst, float v) {
+    if (g.fx_mode == 1) {
+        const float a = fabsf(v);
+        if (a > 0.f) atomicMax(fx_wave_max() + 1 + k, __float_as_uint(a));
+        return;
+    }
+    const double sc = reinterpret_cast<const double *>(reinterpret_cast<const uint8_t *>(g.fx_max) + 64)[k];
+    atomicAdd(reinterpret_cast<unsigned long long *>(g.fx_i64 + (dst - g.fx_f32)),
+              (unsigned long long)__double2ll_rn((double)v * sc));
 }
 MH_DEV void acc_add(GradCtx &g, int32_t k, V3 a) {
     if (g.fx_mode) { acc_add_fx(g, k, a); return; }
@@ -1822,6 +1837,16 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
                 __hip_atomic_fetch_add(l + 2, adj.z * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
                 __hip_atomic_fetch_add(l, (adj.x + adj.y + adj.z) * w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            continue;
+        }
+        if (g.fx_mode) {  // deterministic replay (the host keeps such a slot out of LDS)
+            if (tx.channels == 3) {
+                bmp_add_fx(g, k, buf + base + 0, adj.x * w[j]);
+                bmp_add_fx(g, k, buf + base + 1, adj.y * w[j]);
+                bmp_add_fx(g, k, buf + base + 2, adj.z * w[j]);
+            } else {
+                bmp_add_fx(g, k, buf + base, (adj.x + adj.y + adj.z) * w[j]);
             }
             continue;
         }
@@ -3490,11 +3515,20 @@ MH_DEV void pvp_log_apply(const DScene &S, const MainLog &ml, V3 Ltot, GradCtx &
 
 // small (register-accumulated) gradient slots: wave butterfly, then one
 // atomic per wave and component
-MH_DEV void flush_small_slots(const GradCtx &g, const GradArgs &ga) {
-    if (g.fx_mode == 1) {  // the wave's maxima (corner_scatter, acc_add_fx) -> fx_max[0 .. n_rgb]
+MH_DEV void flush_small_slots(GradCtx &g, const GradArgs &ga) {
+    if (g.fx_mode) {
+        // a lane's own float sums (prb_fused accumulates in registers, not
+        // through acc_add): per lane in a fixed order, so fold them exactly
+        for (uint32_t p = 0; p < ga.n_rgb; ++p) {
+            const V3 a = acc_get(g, (int32_t)p);
+            if (a.x != 0.f || a.y != 0.f || a.z != 0.f) acc_add_fx(g, (int32_t)p, a);
+        }
+        g.acc0 = g.acc1 = g.acc2 = g.acc3 = v3(0.f, 0.f, 0.f);
+    }
+    if (g.fx_mode == 1) {  // the wave's maxima (corner_scatter, acc_add_fx, bmp_add_fx) -> fx_max[0 .. kMaxParams]
         __builtin_amdgcn_wave_barrier();
         const uint32_t j = threadIdx.x & 63u;
-        if (j <= ga.n_rgb) {
+        if (j <= (uint32_t)kMaxParams) {
             const unsigned int v = fx_wave_max()[j];
             if (v) atomicMax(g.fx_max + j, v);
         }
@@ -3538,6 +3572,8 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.fx_mode = ga.fx_mode;
     g.fx_max = ga.fx_max;
     g.fx_scale = ga.fx_scale;
+    g.fx_i64 = ga.fx_i64;
+    g.fx_f32 = ga.fx_f32;
     g.lds_slot = -1;
     g.lds_acc = nullptr;
     g.lds_floats = 0;

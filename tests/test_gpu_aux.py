@@ -219,3 +219,46 @@ def test_async_entry_points_match_synchronous():
     assert np.array_equal(f0, f1) and np.array_equal(w0, w1)
     assert f0.min() >= 0.0 and w0.min() > 0.0
     np.testing.assert_allclose(g1, g0, rtol=1e-5)
+
+
+@pytest.mark.parametrize("case", ["bitmap_replay", "bitmap_replay_global", "rgb_mega"])
+def test_deterministic_prb_replay_bit_reproducible(case, monkeypatch):
+    """MH_FLAG_DETERMINISTIC on the replay kernel (the bitmap path of scenes
+    the fused wavefront does not take; MH_PRB_REPLAY=1 forces it here) and on
+    the rgb megakernel (MH_MODE=mega): a max pass and an int64 fixed-point
+    pass, bitmap texels into an int64 mirror of the slot block, the lanes'
+    small-slot sums folded exactly; repeated runs give the same bits, equal
+    to the float build and to the oracle within tolerance (prb.py:245-246)."""
+    if case == "rgb_mega":
+        monkeypatch.setenv("MH_MODE", "mega")
+    else:
+        monkeypatch.setenv("MH_PRB_REPLAY", "1")
+    if case == "bitmap_replay_global":
+        monkeypatch.setenv("MH_PRB_LDS_TEX", "0")
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    if case == "rgb_mega":
+        scene = mi.load_dict(_cbox(mi, 40, 32, 16))
+        keys = ["white.reflectance.value", "red.reflectance.value"]
+    else:
+        scene = mi.load_dict(mi.cornell_box_bitmap(tex_res=8, width=40, height=32, spp=16))
+        keys = ["white.reflectance.data", "red.reflectance.value"]
+    prb = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(scene)
+    gi = torch.from_numpy(np.random.default_rng(4).random((32, 40, 3)).astype(np.float32) / (32 * 40 * 3)).cuda()
+    st = A.Stats()
+    runs = [mi.render_backward(scene, params, gi, keys, prb, seed=3, spp=16, deterministic=True, stats=st)
+            for _ in range(3)]
+    assert st.mode == 0  # the replay / megakernel, not the wavefront
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert torch.equal(a, b)
+    flt = mi.render_backward(scene, params, gi, keys, prb, seed=3, spp=16)
+    ref = O.render_backward(scene, prb, 3, 16, gi.cpu().numpy(), [params.texture_of(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    for k, a, b, r in zip(keys, runs[0], flt, ref):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.abs(r).max() > 0, k
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6 * np.abs(r).max(), err_msg=k)
+        np.testing.assert_allclose(a, r, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(r).max(), err_msg=k)
