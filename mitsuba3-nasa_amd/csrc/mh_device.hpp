@@ -44,6 +44,7 @@ static __device__ unsigned long long g_mh_guard[kGuardCount];
 #ifdef MH_EXP_LOOKUPS
 // diagnostic build: density-grid lookups of this translation unit's kernels
 static __device__ unsigned long long g_mh_lookups;
+static __device__ unsigned long long g_mh_pf_hits;  // of which served by a prefetch (GridPf)
 #endif
 
 constexpr float kPi = 3.14159265358979323846f;

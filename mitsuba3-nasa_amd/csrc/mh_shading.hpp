@@ -2429,20 +2429,55 @@ __host__ __device__ __forceinline__ uint64_t grid_index(int32_t x, int32_t y, in
     return brick * 64u + ((((uint32_t)z & 3u) << 4) | (((uint32_t)y & 3u) << 2) | ((uint32_t)x & 3u));
 }
 
-// [drjit] Texture3f::eval_nonaccel, linear, clamp, 1 channel (grid.cpp:545-558)
-MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
+// [drjit] Texture3f::eval_nonaccel, linear, clamp, 1 channel (grid.cpp:545-558),
+// in three parts: the tap offsets and weights, the 8 loads, the interpolation
+// (so that a lookup's loads can be issued ahead of it: GridPf)
+struct GridLookup {
+    float w0x, w0y, w0z, w1x, w1y, w1z;
+    uint32_t o[8];  // tap (bx, by, bz) at o[bx | by << 1 | bz << 2] in the bricked grid
+};
+MH_DEV void grid_setup(const DMedium &m, V3 p, GridLookup &L) {
     V3 q = xf_point(m.to_local, p);
     const int32_t rx = (int32_t)m.res[0], ry = (int32_t)m.res[1], rz = (int32_t)m.res[2];
     float px = __builtin_fmaf(q.x, (float)rx, -0.5f), py = __builtin_fmaf(q.y, (float)ry, -0.5f),
           pz = __builtin_fmaf(q.z, (float)rz, -0.5f);
     int32_t ix = (int32_t)floorf(px), iy = (int32_t)floorf(py), iz = (int32_t)floorf(pz);
-    float w1x = px - (float)ix, w1y = py - (float)iy, w1z = pz - (float)iz;
-    float w0x = 1.f - w1x, w0y = 1.f - w1y, w0z = 1.f - w1z;
+    L.w1x = px - (float)ix; L.w1y = py - (float)iy; L.w1z = pz - (float)iz;
+    L.w0x = 1.f - L.w1x; L.w0y = 1.f - L.w1y; L.w0z = 1.f - L.w1z;
     const int32_t x0 = min(max(ix, 0), rx - 1), x1 = min(max(ix + 1, 0), rx - 1);
     const int32_t y0 = min(max(iy, 0), ry - 1), y1 = min(max(iy + 1, 0), ry - 1);
     const int32_t z0 = min(max(iz, 0), rz - 1), z1 = min(max(iz + 1, 0), rz - 1);
+    // grid_index split per axis (brick-major part + texel-in-brick part, the
+    // bit fields disjoint), 32-bit (mh_scene_create caps a grid at 2^32 texels)
+    const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2, sy = nbx * 64u, sz = sy * nby;
+    const uint32_t ox0 = ((uint32_t)x0 >> 2) * 64u + ((uint32_t)x0 & 3u), ox1 = ((uint32_t)x1 >> 2) * 64u + ((uint32_t)x1 & 3u);
+    const uint32_t oy0 = ((uint32_t)y0 >> 2) * sy + (((uint32_t)y0 & 3u) << 2), oy1 = ((uint32_t)y1 >> 2) * sy + (((uint32_t)y1 & 3u) << 2);
+    const uint32_t oz0 = ((uint32_t)z0 >> 2) * sz + (((uint32_t)z0 & 3u) << 4), oz1 = ((uint32_t)z1 >> 2) * sz + (((uint32_t)z1 & 3u) << 4);
+    const uint32_t o00 = oy0 + oz0, o10 = oy1 + oz0, o01 = oy0 + oz1, o11 = oy1 + oz1;
+    L.o[0] = o00 + ox0; L.o[1] = o00 + ox1; L.o[2] = o10 + ox0; L.o[3] = o10 + ox1;
+    L.o[4] = o01 + ox0; L.o[5] = o01 + ox1; L.o[6] = o11 + ox0; L.o[7] = o11 + ox1;
+}
+MH_DEV float grid_interp(const GridLookup &L, const float (&v)[8]) {
+    float f00 = __builtin_fmaf(L.w0x, v[0], L.w1x * v[1]), f01 = __builtin_fmaf(L.w0x, v[4], L.w1x * v[5]),
+          f10 = __builtin_fmaf(L.w0x, v[2], L.w1x * v[3]), f11 = __builtin_fmaf(L.w0x, v[6], L.w1x * v[7]);
+    float f0 = __builtin_fmaf(L.w0y, f00, L.w1y * f10), f1 = __builtin_fmaf(L.w0y, f01, L.w1y * f11);
+    return __builtin_fmaf(L.w0z, f0, L.w1z * f1);
+}
+// The 8 taps of a medium sample's lookup, loaded a trip ahead (k_vol_sched:
+// a lane that continues a null-collision chain or a ratio-tracking walk
+// issues its next sample's loads at the end of this one, so that the next
+// medium trip finds them in registers).  key = the lookup's first tap
+// offset, checked at the use: the values are the grid's own, so a match of
+// the cell within the same medium is exact whatever produced the prefetch.
+struct GridPf {
+    uint32_t key;  // ~0u: none
+    float v[8];
+};
+MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p, const GridPf *pf = nullptr) {
+    GridLookup L;
+    grid_setup(m, p, L);
 #ifdef MH_EXP_NOGRID  // timing experiment: no grid memory traffic (wrong results)
-    return w0x * 0.3f + w1y * 0.2f + w0z * 0.1f + (float)(x0 + y1 + z0) * 1e-9f;
+    return L.w0x * 0.3f + L.w1y * 0.2f + L.w0z * 0.1f + (float)(L.o[0] + L.o[7]) * 1e-9f;
 #endif
     const float *g = S.grid + m.grid_offset;
 #ifdef MH_EXP_LOOKUPS  // diagnostic build: count the lookups (one add per wave; results unchanged)
@@ -2451,31 +2486,29 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
         if (lane_rank(ex) == 0) atomicAdd(&g_mh_lookups, (unsigned long long)__builtin_popcountll(ex));
     }
 #endif
-    // grid_index split per axis (brick-major part + texel-in-brick part, the
-    // bit fields disjoint), 32-bit (mh_scene_create caps a grid at 2^32 texels)
-    const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2, sy = nbx * 64u, sz = sy * nby;
-    const uint32_t ox0 = ((uint32_t)x0 >> 2) * 64u + ((uint32_t)x0 & 3u), ox1 = ((uint32_t)x1 >> 2) * 64u + ((uint32_t)x1 & 3u);
-    const uint32_t oy0 = ((uint32_t)y0 >> 2) * sy + (((uint32_t)y0 & 3u) << 2), oy1 = ((uint32_t)y1 >> 2) * sy + (((uint32_t)y1 & 3u) << 2);
-    const uint32_t oz0 = ((uint32_t)z0 >> 2) * sz + (((uint32_t)z0 & 3u) << 4), oz1 = ((uint32_t)z1 >> 2) * sz + (((uint32_t)z1 & 3u) << 4);
-    const uint32_t o00 = oy0 + oz0, o10 = oy1 + oz0, o01 = oy0 + oz1, o11 = oy1 + oz1;
-    float v000 = g[o00 + ox0], v100 = g[o00 + ox1];
-    float v010 = g[o10 + ox0], v110 = g[o10 + ox1];
-    float v001 = g[o01 + ox0], v101 = g[o01 + ox1];
-    float v011 = g[o11 + ox0], v111 = g[o11 + ox1];
-    float f00 = __builtin_fmaf(w0x, v000, w1x * v100), f01 = __builtin_fmaf(w0x, v001, w1x * v101),
-          f10 = __builtin_fmaf(w0x, v010, w1x * v110), f11 = __builtin_fmaf(w0x, v011, w1x * v111);
-    float f0 = __builtin_fmaf(w0y, f00, w1y * f10), f1 = __builtin_fmaf(w0y, f01, w1y * f11);
-#ifdef MH_EXP_GRID2  // timing experiment: a second lookup's memory traffic (x mirrored), results unchanged
+    float v[8];
+    if (pf && pf->key == L.o[0]) {
+#ifdef MH_EXP_LOOKUPS
+        {
+            const unsigned long long ex = __builtin_amdgcn_read_exec();
+            if (lane_rank(ex) == 0) atomicAdd(&g_mh_pf_hits, (unsigned long long)__builtin_popcountll(ex));
+        }
+#endif
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = pf->v[c];
+    } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = g[L.o[c]];
+    }
+#ifdef MH_EXP_GRID2  // timing experiment: a second lookup's memory traffic (results unchanged)
     {
-        const int32_t xa = rx - 1 - x0, xb = rx - 1 - x1;
-        const float u = g[grid_index(xa, y0, z0, rx, ry)] + g[grid_index(xb, y0, z0, rx, ry)] +
-                        g[grid_index(xa, y1, z0, rx, ry)] + g[grid_index(xb, y1, z0, rx, ry)] +
-                        g[grid_index(xa, y0, z1, rx, ry)] + g[grid_index(xb, y0, z1, rx, ry)] +
-                        g[grid_index(xa, y1, z1, rx, ry)] + g[grid_index(xb, y1, z1, rx, ry)];
-        return __builtin_fmaf(w0z, f0, w1z * f1) + 0.f * u;
+        float u = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) u += g[L.o[c] ^ 64u];
+        return grid_interp(L, v) + 0.f * u;
     }
 #endif
-    return __builtin_fmaf(w0z, f0, w1z * f1);
+    return grid_interp(L, v);
 }
 
 // BoundingBox3f::ray_intersect (core/bbox.h:303-327)
@@ -2499,11 +2532,9 @@ MH_DEV bool bbox_ray_intersect(const float *mn, const float *mx, const RayT &r, 
 // Medium::sample_interaction (medium.cpp:40-86).  Frame = false leaves the
 // interaction frame (fs, ft) to the caller (mei_frame), for callers that
 // need it only at a real scatter.
-template <bool Frame = true>
-MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, float u, MEI &mei) {
-    const DMedium &m = S.media[med];
-    mei.fn = ray.d;
-    if (Frame) coordinate_system(ray.d, mei.fs, mei.ft);
+// the free-flight part of Medium::sample_interaction: the sampled distance
+// and position, and whether it lies inside the medium's segment (valid)
+MH_DEV bool free_flight(const DMedium &m, const RayT &ray, float u, float &mint_o, float &t_o, V3 &p_o) {
     float mint, maxt;
     bool active;
     if (m.type == MH_MEDIUM_HOMOGENEOUS) {
@@ -2515,19 +2546,47 @@ MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, f
     if (!active) { mint = 0.f; maxt = __builtin_huge_valf(); }
     mint = fmaxf(0.f, mint);
     maxt = fminf(ray.maxt, maxt);
+    const float sampled_t = mint + (-log_dr(1.f - u) / m.maj);
+    mint_o = mint;
+    t_o = sampled_t;
+    p_o = fma3s(ray.d, sampled_t, ray.o);
+    return active && sampled_t <= maxt;
+}
+template <bool Frame = true>
+MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, float u, MEI &mei,
+                               const GridPf *pf = nullptr) {
+    const DMedium &m = S.media[med];
+    mei.fn = ray.d;
+    if (Frame) coordinate_system(ray.d, mei.fs, mei.ft);
+    float mint, sampled_t;
+    V3 p;
+    const bool valid = free_flight(m, ray, u, mint, sampled_t, p);
     const float maj = m.maj;
-    const float sampled_t = mint + (-log_dr(1.f - u) / maj);
-    const bool valid = active && sampled_t <= maxt;
     mei.valid = valid;
     mei.t = valid ? sampled_t : __builtin_huge_valf();
-    mei.p = fma3s(ray.d, sampled_t, ray.o);
+    mei.p = p;
     mei.mint = mint;
     mei.maj = maj;
     float st = 0.f;
-    if (valid) st = m.type == MH_MEDIUM_HOMOGENEOUS ? m.sigma_t_const * m.scale : m.scale * grid_eval(S, m, mei.p);
+    if (valid) st = m.type == MH_MEDIUM_HOMOGENEOUS ? m.sigma_t_const * m.scale : m.scale * grid_eval(S, m, mei.p, pf);
     mei.sigma_t = st;
     mei.sigma_s = valid ? v3(m.albedo[0], m.albedo[1], m.albedo[2]) * st : v3(0, 0, 0);
     mei.sigma_n = m.type == MH_MEDIUM_HOMOGENEOUS ? 0.f : maj - st;
+}
+// the loads of the medium sample a lane will take next (GridPf): the same
+// free flight as sample_interaction's, its 8 taps issued now
+MH_DEV void grid_prefetch(const DScene &S, uint32_t med, const RayT &ray, float u, GridPf &pf) {
+    const DMedium &m = S.media[med];
+    if (m.type == MH_MEDIUM_HOMOGENEOUS) return;
+    float mint, t;
+    V3 p;
+    if (!free_flight(m, ray, u, mint, t, p)) return;
+    GridLookup L;
+    grid_setup(m, p, L);
+    const float *g = S.grid + m.grid_offset;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) pf.v[c] = g[L.o[c]];
+    pf.key = L.o[0];
 }
 
 MH_DEV V3 mei_to_local(const MEI &m, V3 v) { return v3(dot(v, m.fs), dot(v, m.ft), dot(v, m.fn)); }
@@ -2709,6 +2768,7 @@ struct VolState {
     float pend_w;       // medium: MIS weight applied after the emitted radiance
     DirS ds;
     NeeState ns;
+    GridPf pf;          // k_vol_sched: the next medium sample's taps, loaded a trip ahead (key ~0u: none)
 };
 
 MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT ray, VolState &v) {
@@ -2727,6 +2787,7 @@ MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, 
     v.last_p = v3(0, 0, 0);
     v.last_pdf = 1.f;
     v.mode = kVolPre;
+    v.pf.key = ~0u;
 }
 
 // pre: false when the path ends at the loop head
