@@ -115,8 +115,9 @@ enum {
                                            order, and bitmap texels in int64 fixed point (a max pass sizes
                                            the scale), bit-reproducible; prbvolpath gradients (grid sigma_t
                                            and the small slots) in int64 fixed point (the backward runs
-                                           twice), bit-reproducible (the replay megakernel's texel atomics
-                                           stay float atomics) (also env MH_DETERMINISTIC=1) */
+                                           twice), bit-reproducible; the replay kernel and the rgb
+                                           megakernel the same way (bitmap texels into an int64 mirror)
+                                           (also env MH_DETERMINISTIC=1) */
     /* multi-GPU (the scene has a communicator, mh_scene_set_comm; one host
        thread per rank): the call sums its result over the ranks in-call, on
        the scene's stream -- mh_render / mh_render_forward the film,
