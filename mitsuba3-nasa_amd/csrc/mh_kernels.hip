@@ -334,6 +334,9 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 #pragma unroll
             for (int c = (Mode == 0 ? 0 : 3); c < 4; ++c) acc[ys][xs][c] = row16_sum(acc[ys][xs][c]);
     if (g != 0) return;
+#ifdef MH_EXP_SPLAT_NOATOMIC  // timing experiment: the footprint sums are not added (wrong film)
+    if (acc[2][2][3] != 12345.f) return;
+#endif
 #pragma unroll
     for (int ys = 0; ys < 5; ++ys) {
         uint32_t yy = py - 2 + ys;
@@ -350,6 +353,118 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
                 atomicAdd(film + (uint64_t)yy * W + xx, acc[ys][xs][3]);
             }
         }
+    }
+}
+
+// The film splat (mode 0) on 4 x 4 tiles of source pixels: a 256-thread
+// workgroup is 16 pixel rows of kSplatLanes lanes, as in k_splat_px, but the
+// rows' footprint sums go to the tile's 8 x 8 film block in LDS (ds_add_f32)
+// and the block is added to the film once, coalesced: 256 lanes, one float
+// each, film rows of 8 pixels x 4 channels contiguous.  k_splat_px issues
+// 100 memory-side atomics per source pixel from 4 lanes of a wave; this
+// issues 16 (the film's halo pixels still receive up to four tiles' adds).
+// Same values and filter as k_splat_px; only the float summation order
+// differs (as between any two atomic runs).
+#ifndef MH_SPLAT_TILE
+#define MH_SPLAT_TILE 1
+#endif
+constexpr uint32_t kSplatTile = 4;                    // source pixels per tile side
+constexpr uint32_t kSplatTileFilm = kSplatTile + 4;   // film pixels per tile side (the 5 x 5 footprint)
+__global__ void __launch_bounds__(256)
+k_splat_tile(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row_first, uint32_t tiles_x, uint32_t Sn,
+             uint32_t n_passes, uint64_t n, uint64_t plane, const float *__restrict__ in, float *__restrict__ film,
+             unsigned long long *__restrict__ invalid, uint64_t in_lim, unsigned long long *__restrict__ viol) {
+    __shared__ float tile[kSplatTileFilm * kSplatTileFilm * 4];
+    const uint32_t W = S.width, H = S.height;
+    const uint32_t tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const uint32_t grp = threadIdx.x / kSplatLanes, g = threadIdx.x % kSplatLanes;
+    const uint32_t ti = grp % kSplatTile, tj = grp / kSplatTile;
+    const uint32_t px = tx * kSplatTile + ti, py = row_first + ty * kSplatTile + tj;
+    tile[threadIdx.x] = 0.f;
+    if (threadIdx.x < kSplatTileFilm * kSplatTileFilm * 4 - 256) tile[256 + threadIdx.x] = 0.f;
+    const uint32_t pixel = py * W + px;
+    bool live = px < W && py < H && pixel >= pixel_begin && pixel - pixel_begin < n_pix;
+    const uint32_t pl = pixel - pixel_begin;
+    if (live) {  // the bounds guard of k_splat_px: a row that would read past the planes leaves whole
+        const uint64_t last = (uint64_t)(n_passes - 1) * n + (uint64_t)(pl + 1) * Sn - 1 + 4 * plane;
+        if (last >= in_lim) {
+            if (g == 0) atomicAdd(viol, 1ull);
+            live = false;
+        }
+    }
+    __syncthreads();
+    uint32_t n_bad = 0;
+    float acc[5][5][4];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[i][j][c] = 0.f;
+    if (live) {
+        for (uint32_t pass = 0; pass < n_passes; ++pass) {
+            const float *src = in + (uint64_t)pass * n + (uint64_t)pl * Sn;
+            float nv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+            if (g < Sn) {
+#pragma unroll
+                for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + g];
+            }
+            for (uint32_t j = g; j < Sn; j += kSplatLanes) {
+                float vals[4] = {nv[0], nv[1], nv[2], 1.f};
+                const float sx = nv[3], sy = nv[4];
+                n_bad += sample_invalid(vals) ? 1u : 0u;
+                const uint32_t jn = j + kSplatLanes;
+                if (jn < Sn) {
+#pragma unroll
+                    for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + jn];
+                }
+                const int32_t fx = (int32_t)floorf(sx), fy = (int32_t)floorf(sy);
+                if (fx != (int32_t)px || fy != (int32_t)py) {  // jitter rounded onto the next pixel
+                    splat_one_atomic(S, film, sx, sy, vals, 4, 0);
+                    continue;
+                }
+                const float relx = ((float)(fx - 2) + 0.5f) - sx, rely = ((float)(fy - 2) + 0.5f) - sy;
+                float wx[5], wy[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    wx[i] = gaussian_eval(S.filter_coeff, relx + (float)i);
+                    wy[i] = gaussian_eval(S.filter_coeff, rely + (float)i);
+                }
+#pragma unroll
+                for (int ys = 0; ys < 5; ++ys)
+#pragma unroll
+                    for (int xs = 0; xs < 5; ++xs) {
+                        const float w = wx[xs] * wy[ys];
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) acc[ys][xs][c] += vals[c] * w;
+                    }
+            }
+        }
+    }
+    if (invalid && n_bad) atomicAdd(invalid, (unsigned long long)n_bad);  // rare: no reduction
+#pragma unroll
+    for (int ys = 0; ys < 5; ++ys)
+#pragma unroll
+        for (int xs = 0; xs < 5; ++xs)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[ys][xs][c] = row16_sum(acc[ys][xs][c]);
+    if (live && g == 0) {
+#pragma unroll
+        for (int ys = 0; ys < 5; ++ys)
+#pragma unroll
+            for (int xs = 0; xs < 5; ++xs)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    atomicAdd(&tile[((tj + ys) * kSplatTileFilm + (ti + xs)) * 4 + c], acc[ys][xs][c]);
+    }
+    __syncthreads();
+    // the film block: element e = (row, column, channel) of the tile's 8 x 8 x 4
+    const int32_t ox = (int32_t)(tx * kSplatTile) - 2, oy = (int32_t)(row_first + ty * kSplatTile) - 2;
+    for (uint32_t e = threadIdx.x; e < kSplatTileFilm * kSplatTileFilm * 4; e += 256) {
+        const float v = tile[e];
+        const int32_t x = ox + (int32_t)((e >> 2) % kSplatTileFilm), y = oy + (int32_t)((e >> 2) / kSplatTileFilm);
+        if (v != 0.f && x >= 0 && y >= 0 && (uint32_t)x < W && (uint32_t)y < H)
+            atomicAdd(film + ((uint64_t)y * W + (uint32_t)x) * 4 + (e & 3u), v);
     }
 }
 
@@ -864,6 +979,12 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
         if (mode == kSplatFilm && invalid)  // the sample check of the atomic path, counted by the generic kernel's rule
             hipLaunchKernelGGL(k_count_invalid, dim3(blocks_for(n * n_passes, 256)), dim3(256), 0, st, n * n_passes,
                                n, plane, in, invalid);
+    } else if (fast && mode == kSplatFilm && MH_SPLAT_TILE) {
+        const uint32_t r_first = lm.pixel_begin / S.width, r_last = (lm.pixel_begin + n_pix - 1) / S.width;
+        const uint32_t tiles_x = (S.width + kSplatTile - 1) / kSplatTile;
+        const uint32_t tiles_y = (r_last - r_first + 1 + kSplatTile - 1) / kSplatTile;
+        hipLaunchKernelGGL(k_splat_tile, dim3(tiles_x * tiles_y), dim3(256), 0, st, S, lm.pixel_begin, n_pix, r_first,
+                           tiles_x, lm.S, n_passes, n, plane, in, film, invalid, in_floats, viol);
     } else if (fast) {
         const uint32_t bs = 128;
         const uint64_t lanes = (uint64_t)n_pix * kSplatLanes;
