@@ -262,3 +262,25 @@ def test_deterministic_prb_replay_bit_reproducible(case, monkeypatch):
         assert np.abs(r).max() > 0, k
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6 * np.abs(r).max(), err_msg=k)
         np.testing.assert_allclose(a, r, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(r).max(), err_msg=k)
+
+
+@pytest.mark.parametrize("size,chunk", [((37, 29), None), ((37, 29), "3136"), ((64, 9), "1200"), ((5, 70), None)])
+def test_tiled_film_splat_matches_gather(size, chunk, monkeypatch):
+    """The film splat on 4 x 4 source tiles with an LDS film block
+    (k_splat_tile): film sizes that are not multiples of the tile, chunks
+    that start and end inside a row (MH_WF_CHUNK, in samples) -- equal to the
+    fixed-order gather (MH_FLAG_DETERMINISTIC) up to float summation order,
+    and to the oracle (imageblock.cpp:418-531)."""
+    if chunk:
+        monkeypatch.setenv("MH_WF_CHUNK", chunk)
+    mi = _mi()
+    w, h = size
+    scene = mi.load_dict(_cbox(mi, w, h, 16))
+    integ = scene.integrator()
+    tiled = mi.render_film(scene, integ, seed=6, spp=16).cpu().numpy()
+    gather = mi.render_film(scene, integ, seed=6, spp=16, deterministic=True).cpu().numpy()
+    assert tiled.shape == (h, w, 4) and np.abs(gather).max() > 0
+    np.testing.assert_allclose(tiled, gather, rtol=1e-5, atol=1e-6)
+    ref = O.render(scene, integ, seed=6, spp=16)
+    ok = np.all(np.abs(tiled - ref) <= 1e-4 * np.maximum(1.0, np.abs(ref)), axis=-1)
+    assert ok.mean() >= 0.995
