@@ -2519,7 +2519,11 @@ MH_DEV bool bbox_ray_intersect(const float *mn, const float *mx, const RayT &r, 
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         active = active && (d[i] != 0.f || (o[i] > mn[i] || o[i] < mx[i]));
+#ifdef MH_EXP_FAST_BBOX_RCP  // timing bound only: approximate reciprocals (not the reference's values)
+        const float rc = __builtin_amdgcn_rcpf(d[i]);
+#else
         const float rc = rcp(d[i]);
+#endif
         const float t1 = (mn[i] - o[i]) * rc, t2 = (mx[i] - o[i]) * rc;
         t1p[i] = fminf(t1, t2);
         t2p[i] = fmaxf(t1, t2);
