@@ -967,7 +967,9 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         float ms = 0.f;
         MH_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
         kernel_ms += ms;
-        for (uint32_t b = 0; b < n_bounces; ++b) {
+        // the fused bounce kernels are timed as one span (launch_wavefront_pass)
+        const uint32_t pairs = wavefront ? (wf_fused(s->S) || L.n_passes > 1 ? 1u : n_bounces) : 0u;
+        for (uint32_t b = 0; b < pairs; ++b) {
             MH_HIP(hipEventElapsedTime(&ms, ev[2 + 2 * b], ev[3 + 2 * b]));
             trace_ms += ms;
         }

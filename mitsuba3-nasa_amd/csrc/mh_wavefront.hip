@@ -750,8 +750,7 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                                              nullptr, st, carry, p, alpha);
         if (e != hipSuccess) return e;
     }
-    if (trace_ev)
-        for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
+    if (trace_ev) (void)hipEventRecord(trace_ev[1], st);  // one span (wf_trace_pairs)
     return hipSuccess;
 }
 
@@ -777,9 +776,11 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
         uint32_t *c = ctr + kCtrStride * b, *cn = ctr + kCtrStride * (b + 1);
         const int cur = (int)(b & 1);
         if (fused) {
-            // timed as one span: an event between two launches costs a ~10 us
-            // gap (measured), so bounce 0 opens the span, the last bounce
-            // closes it and the remaining pairs are recorded empty after it
+            // timed as one span: an event between two launches costs a ~5-10 us
+            // gap (measured), so bounce 0 opens the span and the last bounce
+            // closes it (wf_trace_pairs: the host reads that one pair; the
+            // round-3 build recorded the other 2 n_bounces - 2 events empty
+            // after it, ~75 us of idle GPU per chunk)
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
             if (b == 0)
                 hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), fused_lds_bytes(S), st, S,
@@ -787,8 +788,7 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
             else
                 hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), fused_lds_bytes(S), st,
                                    S, in, lm, seed_value, plane, out, pk, cur, seg_cap, c, cn, n, carry, pass, alpha);
-            if (trace_ev && b + 1 == n_bounces)
-                for (uint32_t k = 1; k < 2 * n_bounces; ++k) (void)hipEventRecord(trace_ev[k], st);
+            if (trace_ev && b + 1 == n_bounces) (void)hipEventRecord(trace_ev[1], st);
             continue;
         }
         if (trace_ev) (void)hipEventRecord(trace_ev[2 * b], st);
