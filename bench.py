@@ -309,6 +309,10 @@ def main():
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
+    # N > 1: the collectives are timed (HIP events around each) so that a
+    # scaling result splits into collective time, rank imbalance and the rest
+    timer = D.CollTimer() if dist_on else None
+    D.set_collective_timer(timer)
     fwd_ms, bwd_ms = [], []
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -319,9 +323,24 @@ def main():
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    elapsed = D.max_over_ranks(elapsed, dev)
+    elapsed_local = time.perf_counter() - t0
+    D.set_collective_timer(None)
+    elapsed = D.max_over_ranks(elapsed_local, dev)
     ms_step = elapsed / args.steps * 1e3
+    multi = None
+    if dist_on:
+        # the barrier-bracketed time above is the same on every rank; a rank's
+        # own work is its step time without the final barrier wait, so the
+        # spread comes from its kernel time (fwd + bwd, HIP events) + collectives
+        colls = timer.summary(args.steps)
+        own = (sum(fwd_ms) + sum(bwd_ms)) / args.steps + sum(c["ms_per_step"] for c in colls.values())
+        coll_max = {k: round(D.max_over_ranks(v["ms_per_step"], dev), 3) for k, v in sorted(colls.items())}
+        multi = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                 "rank_kernel_plus_collective_ms_min": round(D.min_over_ranks(own, dev), 3),
+                 "rank_kernel_plus_collective_ms_max": round(D.max_over_ranks(own, dev), 3),
+                 "collective_ms_per_step_max_over_ranks": coll_max,
+                 "collective_bytes": {k: v["bytes"] for k, v in sorted(colls.items())},
+                 "collective_calls_per_step": {k: round(v["calls_per_step"], 2) for k, v in sorted(colls.items())}}
     samples_step = world * H * W * args.spp
     value = samples_step / (ms_step / 1e3) / 1e6
 
@@ -350,12 +369,19 @@ def main():
         avg_b = (sum(bwd_ms) / len(bwd_ms)) if not args.fwd_only else 0.0
         n_local = H * W * args.spp
         pmc = {}
-        # tools/profile_r2.sh of the latest round's build
-        ppath = next((q for q in (os.path.join(ROOT, "profiles", f"r{r}_pmc.json") for r in (4, 3, 2))
+        # tools/profile_r2.sh of the latest round's build.  These counters are
+        # NOT measured in this run: the line names the file and the build they
+        # come from (traffic_source)
+        ppath = next((q for q in (os.path.join(ROOT, "profiles", f"r{r}_pmc.json") for r in (5, 4, 3, 2))
                       if os.path.exists(q)), "")
+        traffic_source = None
         if os.path.exists(ppath):
             try:
-                pmc = json.load(open(ppath)).get("kernels", {})
+                pj = json.load(open(ppath))
+                pmc = pj.get("kernels", {})
+                traffic_source = (os.path.relpath(ppath, ROOT) + " @ " +
+                                  pj.get("source", "the build committed with that file") +
+                                  " (PMC passes of tools/profile_r2.sh; traffic, valu_issue_frac and clock_ghz are not measured in this run)")
             except Exception:
                 pmc = {}
 
@@ -376,7 +402,8 @@ def main():
             achieved = bytes_launch / (us / 1e6) / 1e9
             traffic, valu, clk = family(kname)
             r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                 "traffic_source": traffic_source if traffic is not None else None, "kernel": kname,
                  "kernel_avg_us": round(us, 1), "algorithmic_bytes_per_launch": round(bytes_launch),
                  # everything the bytes come from, so the line alone reproduces them:
                  # bytes = (2 S (R - N) + b_end N + b_first N) / launches
@@ -440,6 +467,8 @@ def main():
                                            if not args.fwd_only else None),
             "roofline": roofline, "roofline_other": roofline_other, "cpu_baseline": cpu,
         }
+        if multi is not None:
+            line["multi_gpu"] = multi
         print(json.dumps(line), flush=True)
     if dist_on:
         dist.destroy_process_group()

@@ -204,6 +204,31 @@ static WfPacked carve_packed(void *ws, void *ws_ext, uint64_t cap) {
 
 MH_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// Diagnostic build (-DMH_EXP_BPHASE): s_memtime cycles of the fused bounce
+// kernels' phases, summed per wave and added once per wave into g_bph[group]
+// (group: 0 / 1 k_wf_bounce generating / not, 2 / 3 k_wf_bounce_prb
+// generating / not; phases: 0 state load or ray generation, 1 closest-hit
+// packet trace, 2 shade, 3 compaction + state store, 4 shadow packet trace,
+// 5 tail (NEE charge, radiance out), 6 iterations, 7 block prologue).  A
+// phase is charged with the waits that fall in it (a load issued earlier is
+// paid where its value is first used).  Read by mh_exp_bphase.
+#ifdef MH_EXP_BPHASE
+__device__ unsigned long long g_bph[4][8];
+#define MH_BPH_DECL uint64_t bph_t = __builtin_amdgcn_s_memtime(); uint64_t bph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define MH_BPH(k) do { const uint64_t _t = __builtin_amdgcn_s_memtime(); bph[k] += _t - bph_t; bph_t = _t; } while (0)
+#define MH_BPH_ITER() (bph[6] += 1)
+#define MH_BPH_FLUSH(grp)                                                                 \
+    do {                                                                                  \
+        if (lane_id() == 0)                                                               \
+            for (int _k = 0; _k < 8; ++_k) atomicAdd(&g_bph[grp][_k], (unsigned long long)bph[_k]); \
+    } while (0)
+#else
+#define MH_BPH_DECL
+#define MH_BPH(k) do {} while (0)
+#define MH_BPH_ITER() do {} while (0)
+#define MH_BPH_FLUSH(grp) do {} while (0)
+#endif
+
 // segment geometry of a launch: segment of this block, this wave's rank
 // among the segment's waves and the number of waves serving the segment
 struct SegIter {
@@ -506,6 +531,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!block_has_stride_work(it, n)) return;
+    MH_BPH_DECL
     float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
     stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
     const DScene S = stage_tables(S0, lds);
@@ -515,7 +541,9 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
     uint32_t n_shadow = 0;
+    MH_BPH(7);
     for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
+        MH_BPH_ITER();
         const uint32_t i = base + lane_id();
         const bool has = i < n;
         const uint32_t j = sbase + i;
@@ -559,7 +587,9 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             MH_GUARD(pid < n_total, kGuardPathId);
             MH_GUARD(pid < plane, kGuardPlane);
         }
+        MH_BPH(0);
         const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has, recs, dscr);
+        MH_BPH(1);
 #ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
         {
             RayT r2 = ray;
@@ -655,6 +685,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             if (rr_active) tp = tp * rcp(rr_prob);
             alive = active_next && (!rr_active || rr_continue) && tmax != 0.f;
         }
+        MH_BPH(2);
         // ---- compaction: the survivor's next-bounce state leaves registers
         // before the shadow trace (only L and the NEE product stay live across it)
         const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
@@ -669,8 +700,10 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         } else if (has && carry) {
             carry[pid] = rng.state;  // multi-pass: the next pass continues the stream
         }
+        MH_BPH(3);
         // ---- visibility of the NEE sample (scene.cpp:201-210)
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
+        MH_BPH(4);
 #ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
         {
             RayT r2 = sray;
@@ -687,8 +720,10 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         } else if (has) {
             out[pid] = L.x; out[plane + pid] = L.y; out[2 * plane + pid] = L.z;
         }
+        MH_BPH(5);
     }
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
+    MH_BPH_FLUSH(Gen ? 0 : 1);
 }
 
 template <bool InLds, bool Packet, int Eng>
@@ -1211,6 +1246,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!block_has_stride_work(it, n)) return;
+    MH_BPH_DECL
     float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
     stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
     const DScene S = stage_tables(S0, lds);
@@ -1225,7 +1261,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 #pragma unroll
     for (int kk = 0; kk < NR; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
     const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
+    MH_BPH(7);
     for (uint32_t itr = 0; itr < n_iter; ++itr) {
+        MH_BPH_ITER();
         const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
         bool alive = false, shadow = false;
         uint32_t pid = 0, depth = 0;
@@ -1277,7 +1315,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             }
             MH_GUARD(pid < gen.n_total, kGuardPathId);
         }
+        MH_BPH(0);
         const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, i < n, recs, dscr);
+        MH_BPH(1);
         if (i < n) {
             if (Gen) {
                 beta = v3(1.f, 1.f, 1.f);
@@ -1409,6 +1449,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             if (si.valid) depth += 1;
             alive = active_next;
         }
+        MH_BPH(2);
         const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
         MH_GUARD(!alive || slot_n - sbase < seg_cap, kGuardAppendSlot);
         if (alive) {
@@ -1435,7 +1476,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         Hit sh;
         sh.shape = MH_INVALID;
 #else
+        MH_BPH(3);
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
+        MH_BPH(4);
 #endif
         const bool unocc = shadow && sh.shape == MH_INVALID;
         if (unocc) {
@@ -1478,9 +1521,11 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             }
         }
         n_shadow += (uint32_t)__popcll(__ballot(shadow));
+        MH_BPH(5);
     }
     if (lane_id() == 0 && n_shadow) atomicAdd(ctr + it.seg * 32 + 1, n_shadow);  // statistics only
     flush_partial(acc, q);
+    if (!Bm && !Det) MH_BPH_FLUSH(Gen ? 2 : 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -2056,6 +2101,16 @@ hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n
     return hipGetLastError();
 }
 
+#ifdef MH_EXP_BPHASE
+extern "C" int mh_exp_bphase(unsigned long long *out, int reset) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof(g_bph));
+    if (reset) {
+        unsigned long long z[32] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_bph), z, sizeof(z));
+    }
+    return 0;
+}
+#endif
 #ifdef MH_EXP_COUNT
 extern "C" int mh_exp_counters(unsigned long long *out, int reset) {
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_cnt), sizeof(g_exp_cnt));

@@ -48,23 +48,80 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 else None
 
 
-def all_reduce_(t):
+class CollTimer:
+    """Times the step's collectives (bench.py at N > 1, so that a scaling
+    result can be split into collective cost, imbalance and launch tail):
+    per collective its name, its bytes and its duration -- HIP events on the
+    current stream around a device tensor's collective (the stream waits for
+    the collective before it records the second event), host time around a
+    CPU tensor's."""
+
+    def __init__(self):
+        self.records = []  # (name, bytes, start, end, device)
+
+    def run(self, name: str, t, fn):
+        import time
+        import torch
+        if t.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            self.records.append((name, t.numel() * t.element_size(), e0, e1, True))
+        else:
+            t0 = time.perf_counter()
+            fn()
+            self.records.append((name, t.numel() * t.element_size(), t0, time.perf_counter(), False))
+
+    def summary(self, steps: int) -> dict:
+        """{name: {ms_per_step, bytes, calls_per_step}} over the recorded calls; resets."""
+        import torch
+        if any(r[4] for r in self.records):
+            torch.cuda.synchronize()
+        out = {}
+        for name, nb, a, b, dev in self.records:
+            ms = a.elapsed_time(b) if dev else (b - a) * 1e3
+            o = out.setdefault(name, {"ms_per_step": 0.0, "bytes": nb, "calls_per_step": 0.0})
+            o["ms_per_step"] += ms / max(1, steps)
+            o["calls_per_step"] += 1.0 / max(1, steps)
+        self.records = []
+        return out
+
+
+_timer: Optional[CollTimer] = None
+
+
+def set_collective_timer(t: Optional[CollTimer]):
+    """Route every collective of this module through t (None: untimed)."""
+    global _timer
+    _timer = t
+
+
+def _coll(name: str, t, fn):
+    if _timer is not None:
+        _timer.run(name, t, fn)
+    else:
+        fn()
+
+
+def all_reduce_(t, name: str = "all_reduce"):
     """In-place sum over ranks (no-op on one rank)."""
     d = _dist()
     if d is not None:
-        d.all_reduce(t)
+        _coll(name, t, lambda: d.all_reduce(t))
     return t
 
 
-def reduce_to_root_(t):
+def reduce_to_root_(t, name: str = "reduce"):
     """In-place sum onto rank 0 (no-op on one rank); the other ranks' tensor
     is left undefined, as a reduce leaves it."""
     d = _dist()
     if d is not None:
         if t.is_cuda and d.get_backend() == "gloo":
-            d.all_reduce(t)  # gloo reduces device tensors only by all-reduce; rank 0 gets the same sum
+            # gloo reduces device tensors only by all-reduce; rank 0 gets the same sum
+            _coll(name, t, lambda: d.all_reduce(t))
         else:
-            d.reduce(t, dst=0)
+            _coll(name, t, lambda: d.reduce(t, dst=0))
     return t
 
 
@@ -85,18 +142,18 @@ class StepOps:
     packed: Optional[Callable] = None
 
 
-def all_reduce_list_(ts: List) -> List:
+def all_reduce_list_(ts: List, name: str = "all_reduce") -> List:
     """Sum a list of tensors over ranks in ONE collective (concatenated when
     there are several); returns the summed tensors (in place for one)."""
     d = _dist()
     if d is None or not ts:
         return ts
     if len(ts) == 1:
-        d.all_reduce(ts[0])
+        _coll(name, ts[0], lambda: d.all_reduce(ts[0]))
         return ts
     import torch
     flat = torch.cat([t.reshape(-1) for t in ts])
-    d.all_reduce(flat)
+    _coll(name, flat, lambda: d.all_reduce(flat))
     out, o = [], 0
     for t in ts:
         out.append(flat[o:o + t.numel()].view_as(t))
@@ -127,23 +184,23 @@ def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, l
             buf, fv, wv = ops.packed()
             film = ops.render_film(seed, fs.spp_total, fs.begin, fs.end, out=fv)
             w = ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end, out=wv)
-            all_reduce_(buf)  # film + W: one collective
+            all_reduce_(buf, "film+W")  # film + W: one collective
         else:
             film = ops.render_film(seed, fs.spp_total, fs.begin, fs.end)
             w = ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end)
-            film, w = all_reduce_list_([film, w])
+            film, w = all_reduce_list_([film, w], "film+W")
         img = ops.develop(film)
         grads: List = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
-        return img, all_reduce_list_(grads)
+        return img, all_reduce_list_(grads, "gradient")
     film = ops.render_film(seed, fs.spp_total, fs.begin, fs.end)
-    film = reduce_to_root_(film) if film_to_root else all_reduce_(film)
+    film = reduce_to_root_(film, "film") if film_to_root else all_reduce_(film, "film")
     img = ops.develop(film)
     if not with_grad:
         return img, None
     sg = ops.seed_grad(seed)
-    w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end))
+    w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end), "W")
     grads = ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
-    return img, all_reduce_list_(grads)
+    return img, all_reduce_list_(grads, "gradient")
 
 
 def max_over_ranks(x: float, device=None) -> float:
@@ -154,4 +211,15 @@ def max_over_ranks(x: float, device=None) -> float:
     import torch
     t = torch.tensor([x], dtype=torch.float64, device=device)
     d.all_reduce(t, op=d.ReduceOp.MAX)
+    return float(t.item())
+
+
+def min_over_ranks(x: float, device=None) -> float:
+    """Min of a host float over ranks (the per-rank spread of the step time)."""
+    d = _dist()
+    if d is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    d.all_reduce(t, op=d.ReduceOp.MIN)
     return float(t.item())

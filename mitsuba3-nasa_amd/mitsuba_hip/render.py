@@ -404,8 +404,25 @@ def render(scene: Scene, params: Optional[SceneParameters] = None, sensor: int =
 
 
 def render_1(scene: Scene, sensor: int = 0, seed: int = 0, spp: int = 0, integrator: Optional[Integrator] = None):
-    """SamplingIntegrator::render_1 (integrator.cpp:398-743), the fork's
-    radiance-meter loop.  The reference only implements it for monochromatic
-    and spectral variants; in an RGB variant (hip_ad_rgb mirrors llvm_ad_rgb)
-    it raises the same error."""
-    raise A.MitsubaHipError("This render loop only supports monochromatic and spectral modes!")
+    """The fork's radiance-meter loop: every pixel's radiance summed into one
+    Spectrum, normalised by 1 / (W H spp).  In an RGB variant (hip_ad_rgb
+    mirrors llvm_ad_rgb) the two reference implementations differ:
+
+    - the C++ SamplingIntegrator::render_1 (integrator.cpp:398-411), which
+      `path` and `volpath` use, raises;
+    - the Python ADIntegrator.render_1 (ad/integrators/common.py:113-196),
+      which `prb` and `prbvolpath` inherit, renders the primal and then
+      returns Spectrum(0) * nf: its accumulation exists for monochromatic and
+      spectral modes only ("Never use render_1() in RGB mode", :180-181).
+
+    Returns a (3,) float32 tensor on the device for the AD integrators."""
+    integrator = integrator or scene.integrator()
+    if integrator is None or integrator.type not in ("prb", "prbvolpath"):
+        raise A.MitsubaHipError("This render loop only supports monochromatic and spectral modes!")
+    if sensor != 0:
+        raise A.MitsubaHipError("hip_ad_rgb: only sensor index 0 is supported")
+    torch = _torch()
+    spp = spp or scene.sample_count()
+    film = render_film(scene, integrator, seed, spp)  # the primal pass (common.py:141-153)
+    nf = 1.0 / (scene.width * scene.height * spp)
+    return torch.zeros(3, dtype=torch.float32, device=film.device) * nf

@@ -90,3 +90,29 @@ def test_render_1_is_rejected_in_rgb_variants():
     sc = mi.load_dict(mi.cornell_box())
     with pytest.raises(RuntimeError, match="monochromatic and spectral"):
         mi.render_1(sc)
+
+
+def test_render_1_prb_returns_zero_spectrum_in_rgb(monkeypatch):
+    """ADIntegrator.render_1 (ad/integrators/common.py:113-196), which prb and
+    prbvolpath inherit, renders the primal and returns Spectrum(0) * nf in RGB
+    modes instead of raising as the C++ SamplingIntegrator::render_1 of path /
+    volpath does (integrator.cpp:398-411)."""
+    import importlib
+    import torch
+    mi = _mi()
+    R = importlib.import_module("mitsuba_hip.render")  # the module (the package exports the render function)
+    sc = mi.load_dict(mi.cornell_box())
+    calls = []
+
+    def fake_film(scene, integrator=None, seed=0, spp=0, **kw):  # the primal pass (no device here)
+        calls.append((integrator.type, seed, spp))
+        return torch.zeros((scene.height, scene.width, 4))
+    monkeypatch.setattr(R, "render_film", fake_film)
+    for t in ("prb", "prbvolpath"):
+        out = mi.render_1(sc, seed=3, spp=4, integrator=mi.load_dict({"type": t}))
+        assert out.shape == (3,) and out.dtype == torch.float32 and float(out.abs().sum()) == 0.0
+    assert calls == [("prb", 3, 4), ("prbvolpath", 3, 4)]
+    with pytest.raises(RuntimeError, match="monochromatic and spectral"):  # path keeps the C++ behaviour
+        mi.render_1(sc, integrator=mi.load_dict({"type": "path"}))
+    with pytest.raises(RuntimeError, match="monochromatic and spectral"):
+        mi.render_1(sc, integrator=mi.load_dict({"type": "volpath"}))

@@ -59,11 +59,20 @@ def _worker(rank, world, port, out_dir):
     # all-reduce) and the film summed onto rank 0 only
     img2, grads2 = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7, local_weights=True, film_to_root=True)
     # packed: film and W summed in one all-reduce (bench.py's default step)
+    # ... timed as bench.py times it at N > 1 (collective names, bytes, calls)
+    timer = D.CollTimer()
+    D.set_collective_timer(timer)
     img3, grads3 = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7, packed=True)
+    D.set_collective_timer(None)
+    colls = timer.summary(1)
     t = D.max_over_ranks(float(rank) + 0.5)
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), img=img.numpy(), g=grads[0].numpy(), t=t,
+    tmin = D.min_over_ranks(float(rank) + 0.5)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), img=img.numpy(), g=grads[0].numpy(), t=t, tmin=tmin,
              begin=slab.begin, end=slab.end, img2=img2.numpy(), g2=grads2[0].numpy(), img3=img3.numpy(),
-             g3=grads3[0].numpy())
+             g3=grads3[0].numpy(), coll_names=np.array(sorted(colls)),
+             coll_bytes=np.array([colls[k]["bytes"] for k in sorted(colls)]),
+             coll_calls=np.array([colls[k]["calls_per_step"] for k in sorted(colls)]),
+             coll_ms=np.array([colls[k]["ms_per_step"] for k in sorted(colls)]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -90,6 +99,13 @@ def test_gloo_ranks_match_single_process(world, tmp_path):
     per = 8 // world
     assert [(int(r["begin"]), int(r["end"])) for r in rs] == [(i * per, (i + 1) * per) for i in range(world)]
     assert all(float(r["t"]) == world - 0.5 for r in rs)  # max over ranks
+    assert all(float(r["tmin"]) == 0.5 for r in rs)  # min over ranks
+    # the timed packed step: one film + W all-reduce (RGBW film + W image,
+    # concatenated) and one gradient all-reduce (3 floats), once each
+    for r in rs:
+        assert list(r["coll_names"]) == ["film+W", "gradient"]
+        assert list(r["coll_bytes"]) == [24 * 16 * 5 * 4, 12]
+        assert list(r["coll_calls"]) == [1.0, 1.0] and np.all(r["coll_ms"] >= 0)
     r0, r1 = rs[0], rs[-1]
     for r in rs[1:]:
         assert np.array_equal(r0["img"], r["img"]) and np.array_equal(r0["g"], r["g"])

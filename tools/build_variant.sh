@@ -15,4 +15,5 @@ for f in mh_api.hip mh_kernels.hip mh_volwave.hip; do /opt/rocm/bin/hipcc $FLAGS
 /opt/rocm/bin/hipcc $FLAGS -x hip -c mh_comm.cpp -o "$OBJ/mh_comm.o" &
 wait
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$ROOT/gpurun_exp/lib_$NAME.so" "$OBJ"/*.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx -ldl -Wl,-rpath,/opt/rocm/lib
+echo "$*" > "$ROOT/gpurun_exp/$NAME.flags"
 echo "built gpurun_exp/lib_$NAME.so"
