@@ -45,11 +45,20 @@ int set_error(int code, const std::string &msg) {
     return code;
 }
 
+// a wait that failed in comm_wait has already reported why (a collective
+// failed, its deadline passed, the communicator was aborted): MH_HIP keeps
+// that message instead of replacing it by the HIP code's text
+thread_local bool g_keep_error = false;
 #define MH_HIP(expr)                                                                        \
     do {                                                                                    \
         hipError_t _e = (expr);                                                             \
-        if (_e != hipSuccess)                                                               \
+        if (_e != hipSuccess) {                                                             \
+            if (g_keep_error) {                                                             \
+                g_keep_error = false;                                                       \
+                return MH_ERR_HIP;                                                          \
+            }                                                                               \
             return set_error(MH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+        }                                                                                   \
     } while (0)
 
 struct DevBuf {
@@ -789,7 +798,11 @@ static int reduce_result(mh_scene *s, uint32_t flags, float *buf, uint64_t count
 // before issuing its collective returns an error instead of hanging in
 // hipStreamSynchronize; otherwise a plain stream sync.
 static hipError_t wait_stream(mh_scene *s, uint32_t flags, hipStream_t st) {
-    if (wants_reduce(flags) && s->comm) return comm_wait(s->comm, st, "collective call") == MH_OK ? hipSuccess : hipErrorLaunchTimeOut;
+    if (wants_reduce(flags) && s->comm) {
+        if (comm_wait(s->comm, st, "collective call") == MH_OK) return hipSuccess;
+        g_keep_error = true;  // comm_wait's message stands
+        return hipErrorLaunchTimeOut;
+    }
     return hipStreamSynchronize(st);
 }
 #define MH_WAIT(s, flags, st)                                                                         \
@@ -824,6 +837,8 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
     g_call_issued = true;  // past argument validation: a failure from here aborts the communicator
+    // test hook (tests/test_gpu_comm.py): a failure after the call was issued
+    if (getenv("MH_TEST_FAIL_AFTER_ISSUE")) return set_error(MH_ERR_HIP, "MH_TEST_FAIL_AFTER_ISSUE: injected failure");
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
     // film storage: RGBW, or R G B A W for alpha films; the kernels splat into
@@ -1953,12 +1968,22 @@ int mh_trace_shadow(mh_scene *s, uint64_t n, const float *rays, uint32_t *occlud
 static int abort_on_failure(mh_scene *s, uint32_t flags, int rc) {
     const bool issued = g_call_issued;  // argument errors (before any work) leave the communicator usable
     g_call_issued = false;
+    g_keep_error = false;
 #ifdef MH_DEBUG
     // the debug build's device bounds guards (MH_GUARD) fail the call
-    if (rc == MH_OK && issued && s) {
+    // (not for asynchronous calls, whose work is still queued; a call with
+    // collectives in flight waits through comm_wait and its deadline, not a
+    // device-wide sync.  The guard words are per device: concurrent scenes on
+    // one device read each other's counts -- run guard builds one scene at a time)
+    if (rc == MH_OK && issued && s && !(flags & MH_FLAG_NO_SYNC)) {
         (void)hipSetDevice(s->device);
         unsigned long long g[2][kGuardCount] = {};
-        if (hipDeviceSynchronize() != hipSuccess || guard_read_wf(g[0]) != hipSuccess || guard_read_k(g[1]) != hipSuccess)
+        const bool waited = (wants_reduce(flags) && s->comm) ? comm_wait(s->comm, s->stream, "MH_DEBUG guard read") == MH_OK
+                                                             : hipStreamSynchronize(s->stream) == hipSuccess;
+        if (!waited) {
+            if (!(wants_reduce(flags) && s->comm)) rc = set_error(MH_ERR_HIP, "MH_DEBUG: the stream could not be synchronized");
+            else rc = MH_ERR_HIP;  // comm_wait's message stands
+        } else if (guard_read_wf(g[0]) != hipSuccess || guard_read_k(g[1]) != hipSuccess)
             rc = set_error(MH_ERR_HIP, "MH_DEBUG: the device guard counters could not be read");
         static const char *what[kGuardCount] = {"queue item beyond its segment", "path id beyond the chunk",
                                                 "appended slot beyond its segment", "sample-plane index beyond the plane",

@@ -1222,13 +1222,19 @@ hipError_t launch_prb_backward(const DScene &S, const IntegratorParams &in, cons
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipDeviceGetAttribute(&max_wg, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
         (void)hipDeviceGetAttribute(&per_cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+        // the kernel's static LDS (GradCtx's per-wave fixed-point sums,
+        // g_fx_wave) comes on top of the dynamic bytes
+        hipFuncAttributes fa{};
+        const void *fn = S.lds_bytes_bvh ? (fused ? (const void *)k_prb_backward<true, true> : (const void *)k_prb_backward<true, false>)
+                                         : (fused ? (const void *)k_prb_backward<false, true> : (const void *)k_prb_backward<false, false>);
+        const size_t st_lds = hipFuncGetAttributes(&fa, fn) == hipSuccess ? fa.sharedSizeBytes : (size_t)kFxStaticLdsBytes;
         const uint32_t off = (uint32_t)((sh + 15) / 16 * 16);
         const size_t total = off + (size_t)ga.lds_floats * 4;
-        if (total <= (size_t)max_wg) {
+        if (total + st_lds <= (size_t)max_wg) {
             ga.lds_offset = off;
             sh = total;
             const size_t lds_cu = per_cu_lds > 0 ? (size_t)per_cu_lds : (size_t)max_wg;
-            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, lds_cu / sh));
+            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, lds_cu / (sh + st_lds)));
             g = dim3(std::min<uint32_t>(blocks_for(n, bs), (uint32_t)cus * per_cu));
         } else {
             ga.lds_slot = -1;

@@ -1686,6 +1686,9 @@ static_assert(kMaxRgbParams == 4, "GradCtx names four small-slot accumulators");
 // builds a GradCtx does so and flushes it with whole waves.
 constexpr uint32_t kFxWaveWords = 3 * kMaxRgbParams, kFxMaxWaves = 16;  // blocks of up to 1024 threads
 static __shared__ unsigned long long g_fx_wave[kFxMaxWaves * kFxWaveWords];
+// static LDS a kernel holding a GradCtx carries beside its dynamic bytes
+// (host budgets subtract it; hipFuncGetAttributes gives the exact figure)
+constexpr uint32_t kFxStaticLdsBytes = (uint32_t)sizeof(g_fx_wave);
 MH_DEV unsigned long long *fx_wave_sums() { return g_fx_wave + (threadIdx.x >> 6) * kFxWaveWords; }
 // Pass 1 keeps the wave's maxima (the grid's, then each small slot's, as the
 // bits of non-negative floats) in the same LDS words and flushes them with one

@@ -203,24 +203,31 @@ static WfPacked carve_packed(void *ws, void *ws_ext, uint64_t cap) {
 }
 
 MH_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
+// MH_EXP_STATE_L2 (timing experiment, wrong results): the index of a post-trace state load
+#ifdef MH_EXP_STATE_L2
+MH_DEV uint32_t jl_tea(uint32_t j) { return j & 8191u; }
+#else
+MH_DEV uint32_t jl_tea(uint32_t j) { return j; }
+#endif
 
 // Diagnostic build (-DMH_EXP_BPHASE): s_memtime cycles of the fused bounce
 // kernels' phases, summed per wave and added once per wave into g_bph[group]
 // (group: 0 / 1 k_wf_bounce generating / not, 2 / 3 k_wf_bounce_prb
 // generating / not; phases: 0 state load or ray generation, 1 closest-hit
 // packet trace, 2 shade, 3 compaction + state store, 4 shadow packet trace,
-// 5 tail (NEE charge, radiance out), 6 iterations, 7 block prologue).  A
-// phase is charged with the waits that fall in it (a load issued earlier is
-// paid where its value is first used).  Read by mh_exp_bphase.
+// 5 tail (NEE charge, radiance out), 6 iterations, 7 block prologue; 8-11
+// spare).  A phase is charged with the waits that fall in it (a load issued
+// earlier is paid where its value is first used: the state loads issued
+// after the closest trace are paid in shade).  Read by mh_exp_bphase.
 #ifdef MH_EXP_BPHASE
-__device__ unsigned long long g_bph[4][8];
-#define MH_BPH_DECL uint64_t bph_t = __builtin_amdgcn_s_memtime(); uint64_t bph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+__device__ unsigned long long g_bph[4][12];
+#define MH_BPH_DECL uint64_t bph_t = __builtin_amdgcn_s_memtime(); uint64_t bph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define MH_BPH(k) do { const uint64_t _t = __builtin_amdgcn_s_memtime(); bph[k] += _t - bph_t; bph_t = _t; } while (0)
 #define MH_BPH_ITER() (bph[6] += 1)
 #define MH_BPH_FLUSH(grp)                                                                 \
     do {                                                                                  \
         if (lane_id() == 0)                                                               \
-            for (int _k = 0; _k < 8; ++_k) atomicAdd(&g_bph[grp][_k], (unsigned long long)bph[_k]); \
+            for (int _k = 0; _k < 12; ++_k) atomicAdd(&g_bph[grp][_k], (unsigned long long)bph[_k]); \
     } while (0)
 #else
 #define MH_BPH_DECL
@@ -606,7 +613,12 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 prev_pdf = 1.f;
                 rng.state = gen_state;
             } else {
-                const float4 q2 = w.pl(cur, 2)[j], q3 = w.pl(cur, 3)[j], q4 = w.pl(cur, 4)[j];
+#ifdef MH_EXP_STATE_L2  // timing experiment: the post-trace state loads from an L2-resident 8k-path window (wrong results)
+                const uint32_t jl = j & 8191u;
+#else
+                const uint32_t jl = j;
+#endif
+                const float4 q2 = w.pl(cur, 2)[jl], q3 = w.pl(cur, 3)[jl], q4 = w.pl(cur, 4)[jl];
                 tp = v3(q2.x, q2.y, q2.z);
                 prev_pdf = q2.w;
                 prev_p = v3(q3.x, q3.y, q3.z);
@@ -615,7 +627,11 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             }
             eta = 1.f;  // diffuse / null BSDFs: eta stays 1, only the camera vertex is delta
             const bool prev_delta = depth == 0;
+#ifdef MH_EXP_STATE_L2
+            rng.inc = Gen ? gen_inc : (((uint64_t)w.tea(cur)[j & 8191u] << 1) | 1u);
+#else
             rng.inc = Gen ? gen_inc : (((uint64_t)w.tea(cur)[j] << 1) | 1u);
+#endif
             SI si;
             compute_si(S, ray, h, si);
 
@@ -1327,15 +1343,20 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 for (int kk = 0; kk < NR; ++kk) A[kk][0] = A[kk][1] = A[kk][2] = 0.f;
                 rng.state = gen_state;
             } else {
-                beta = v3(w.bx[cur][j], w.by[cur][j], w.bz[cur][j]);
-                prev_p = v3(w.ppx[cur][j], w.ppy[cur][j], w.ppz[cur][j]);
-                prev_pdf = w.ppdf[cur][j];
-                dL = v3(q.dl(cur, 0)[j], q.dl(cur, 1)[j], q.dl(cur, 2)[j]);
+#ifdef MH_EXP_STATE_L2  // timing experiment (see k_wf_bounce)
+                const uint32_t jl = j & 8191u;
+#else
+                const uint32_t jl = j;
+#endif
+                beta = v3(w.bx[cur][jl], w.by[cur][jl], w.bz[cur][jl]);
+                prev_p = v3(w.ppx[cur][jl], w.ppy[cur][jl], w.ppz[cur][jl]);
+                prev_pdf = w.ppdf[cur][jl];
+                dL = v3(q.dl(cur, 0)[jl], q.dl(cur, 1)[jl], q.dl(cur, 2)[jl]);
 #pragma unroll
                 for (int kk = 0; kk < NR; ++kk)
 #pragma unroll
-                    for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[j] : 0.f;
-                rng.state = w.rng[cur][j];
+                    for (int c = 0; c < 3; ++c) A[kk][c] = (uint32_t)kk < n_rgb ? q.A(cur, kk * 3 + c)[jl] : 0.f;
+                rng.state = w.rng[cur][jl];
                 if (Det) {
 #pragma unroll
                     for (int kk = 0; kk < NR; ++kk)
@@ -1349,7 +1370,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             }
             const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
             const float eta = 1.f;
-            rng.inc = Gen ? gen_inc : (((uint64_t)q.tea(cur)[j] << 1) | 1u);
+            rng.inc = Gen ? gen_inc : (((uint64_t)q.tea(cur)[Gen ? j : jl_tea(j)] << 1) | 1u);
             SI si;
             compute_si(S, ray, h, si);
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
@@ -2105,7 +2126,7 @@ hipError_t launch_wf_grad_reduce(const float *partial, uint32_t grid, uint32_t n
 extern "C" int mh_exp_bphase(unsigned long long *out, int reset) {
     hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bph), sizeof(g_bph));
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[48] = {0};
         hipMemcpyToSymbol(HIP_SYMBOL(g_bph), z, sizeof(z));
     }
     return 0;

@@ -305,3 +305,79 @@ def test_render_sharded_with_world1_comm_and_argument_checks():
     with pytest.raises(A.MitsubaHipError, match="spp must be >="):
         render_sharded([scene, other], integ, 2, 1, [f, _film(other, torch)])
     c.close()
+
+
+def test_failed_collective_call_aborts_its_communicator(monkeypatch):
+    """A MH_FLAG_REDUCE call that fails after it was issued aborts the scene's
+    communicator (mh_api.hip abort_on_failure): its error says so, and every
+    later reduce on that communicator fails at once with 'aborted' instead of
+    pairing with a peer's different collective.  The failure is
+    injected by the MH_TEST_FAIL_AFTER_ISSUE hook of mh_render."""
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    from mitsuba_hip.comm import Comm, scene_set_comm
+    scene = _scene(mi)
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    scene_set_comm(scene, comm)
+    film = _film(scene, torch)
+    _render(A, scene, integ, 5, 16, film, A.FLAG_REDUCE)  # healthy first
+    monkeypatch.setenv("MH_TEST_FAIL_AFTER_ISSUE", "1")
+    with pytest.raises(A.MitsubaHipError, match="injected failure.*communicator was aborted"):
+        _render(A, scene, integ, 5, 16, film, A.FLAG_REDUCE)
+    monkeypatch.delenv("MH_TEST_FAIL_AFTER_ISSUE")
+    with pytest.raises(A.MitsubaHipError, match="aborted"):
+        _render(A, scene, integ, 5, 16, film, A.FLAG_REDUCE)
+    # without MH_FLAG_REDUCE the scene still renders
+    ref = _film(scene, torch)
+    _render(A, scene, integ, 5, 16, ref, 0)
+    torch.cuda.synchronize()
+    assert float(ref.sum()) > 0
+    scene_set_comm(scene, None)
+    comm.close()
+
+
+_DEADLINE_SCRIPT = r"""
+import ctypes as C, os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "mitsuba3-nasa_amd"))
+import torch
+import mitsuba_hip as mi
+from mitsuba_hip import _abi as A
+from mitsuba_hip.comm import Comm, scene_set_comm
+mi.set_variant("hip_ad_rgb")
+d = mi.cornell_box()
+d["sensor"]["film"]["width"] = d["sensor"]["film"]["height"] = 512
+scene = mi.load_dict(d)
+integ = mi.load_dict({"type": "path", "max_depth": 8})
+comm = Comm(Comm.unique_id(), 1, 0, 0)
+scene_set_comm(scene, comm)
+film = torch.zeros((512, 512, 4), device="cuda:0")
+ic = integ.c()
+rc = A.lib().mh_render(scene.handle(0), C.byref(ic), 1, 256, 0, 0, C.c_void_p(film.data_ptr()),
+                       A.FLAG_DEVICE_POINTERS | A.FLAG_REDUCE, None)
+msg = A.lib().mh_last_error().decode()
+torch.cuda.synchronize()
+print("RC", rc)
+print("MSG", msg)
+"""
+
+
+def test_collective_wait_deadline_aborts(tmp_path):
+    """comm_wait's deadline (MH_COMM_TIMEOUT_S, read once per process): a
+    REDUCE call whose stream has not drained within it aborts the
+    communicator and returns an error naming the deadline instead of waiting
+    (a peer that never issues its collective would otherwise hang the rank).
+    Here the deadline (1 ms) is shorter than the render (~20 ms)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "deadline.py"
+    script.write_text(_DEADLINE_SCRIPT)
+    env = dict(os.environ, MH_COMM_TIMEOUT_S="0.001")
+    r = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = dict(l.split(" ", 1) for l in r.stdout.splitlines() if l.startswith(("RC ", "MSG ")))
+    assert out["RC"] != "0"
+    assert "did not complete within" in out["MSG"] and "aborted" in out["MSG"], out["MSG"]

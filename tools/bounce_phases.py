@@ -21,6 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mitsuba3-nasa_amd")]
 
 PHASES = ["load/gen", "closest trace", "shade", "store", "shadow trace", "tail"]
+SLOTS = 12  # per group: the 6 phases, iterations, prologue, 4 spare
 GROUPS = ["k_wf_bounce<Gen>", "k_wf_bounce", "k_wf_bounce_prb<Gen>", "k_wf_bounce_prb"]
 
 
@@ -39,7 +40,7 @@ def main():
     w = bench.build_step(a.res, a.spp, 8, 0, 1, dev)
     fn = _abi.lib().mh_exp_bphase
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 32)()
+    buf = (C.c_ulonglong * (4 * SLOTS))()
 
     def step(i):
         return D.fwd_grad_step(w["ops"], w["slab"], i, with_grad=True, packed=True, fwd_slab=w["fwd_slab"])
@@ -53,16 +54,17 @@ def main():
     fn(buf, 1)
     out = {}
     for g, name in enumerate(GROUPS):
-        v = [buf[g * 8 + k] for k in range(8)]
+        v = [buf[g * SLOTS + k] for k in range(SLOTS)]
         tot = sum(v[:6])
         if not tot:
             continue
         iters = max(1, v[6])
         print(f"{name:24s} iterations {iters:9d}  cycles/iteration {tot / iters:8.0f}  prologue {v[7] / max(1, tot + v[7]):.3f}")
-        for k, p in enumerate(PHASES):
-            print(f"    {p:14s} {v[k] / tot:6.3f}  {v[k] / iters:8.0f} cycles/iteration")
+        names, vals = PHASES, v[:6]
+        for p, x in zip(names, vals):
+            print(f"    {p:15s} {x / tot:6.3f}  {x / iters:8.0f} cycles/iteration")
         out[name] = {"iterations": iters, "cycles_per_iteration": tot / iters,
-                     "share": {p: v[k] / tot for k, p in enumerate(PHASES)}}
+                     "share": {p: x / tot for p, x in zip(names, vals)}}
     print(json.dumps(out))
 
 
