@@ -2420,16 +2420,47 @@ struct MEI {
     V3 fs, ft, fn;   // Frame3f(ray.d); wi = (0, 0, -1) local
 };
 
-// Device layout of a density grid: 4x4x4 bricks of 64 floats (256 B), bricks
-// x-fastest, texels x-fastest inside a brick.  The 8 taps of a trilinear
-// lookup then fall in one brick 27/64 of the time (never in more than 8)
-// instead of always spanning 4 rows 1 KiB / 256 KiB apart, and the lookups
-// along a ray walk neighbouring bricks.  Values are unchanged (bit-exact);
-// the host API and gradients keep the reference's linear (z, y, x) layout.
+// Device layout of a density grid (the host API and gradients keep the
+// reference's linear (z, y, x) layout; values are unchanged, so lookups are
+// bit-exact either way).
+//
+// MH_GRID_TILE = 1 (round 5, the default): apron tiles.  The cells of a
+// trilinear lookup (its lower tap corner, clamped to [0, r - 2]) are grouped
+// 3 x 3 x 1, and tile (tx, ty, tz) stores the 4 x 4 x 2 texels x in
+// [3 tx, 3 tx + 4), y in [3 ty, 3 ty + 4), z in [tz, tz + 2) -- every tap of
+// its 9 cells -- as 32 floats, one 128-B cache line, x fastest.  A lookup
+// then touches exactly one line, where the 4^3 bricks below touch 2.34 lines
+// on average (a 2 x 2 x 2 block at a random offset against 4 x 4 x 2 lines),
+// and config 4's k_vol_sched is bound by the lines that miss L2 (twice the
+// lookup lines cost 19 %).  The price is 3.6x the
+// texels (256^3: 236 MB, inside the 256 MB Infinity Cache).
+//
+// MH_GRID_TILE = 0: 4 x 4 x 4 bricks of 64 floats (256 B), bricks x-fastest,
+// texels x-fastest inside a brick.
+#ifndef MH_GRID_TILE
+#define MH_GRID_TILE 1
+#endif
 __host__ __device__ __forceinline__ uint64_t grid_index(int32_t x, int32_t y, int32_t z, int32_t rx, int32_t ry) {
     const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2;
     const uint64_t brick = ((uint64_t)((uint32_t)z >> 2) * nby + ((uint32_t)y >> 2)) * nbx + ((uint32_t)x >> 2);
     return brick * 64u + ((((uint32_t)z & 3u) << 4) | (((uint32_t)y & 3u) << 2) | ((uint32_t)x & 3u));
+}
+// apron tiles per axis: cells 0 .. max(r - 2, 0) in tiles of 3 (x, y) or 1 (z)
+__host__ __device__ __forceinline__ uint32_t grid_tiles_xy(int32_t r) { return ((uint32_t)(r > 2 ? r - 1 : 1) + 2u) / 3u; }
+__host__ __device__ __forceinline__ uint32_t grid_tiles_z(int32_t r) { return (uint32_t)(r > 2 ? r - 1 : 1); }
+__host__ __device__ __forceinline__ uint64_t grid_tiled_size(int32_t rx, int32_t ry, int32_t rz) {
+    return (uint64_t)grid_tiles_xy(rx) * grid_tiles_xy(ry) * grid_tiles_z(rz) * 32u;
+}
+// the texel that float i of the tiled layout holds (the tiles' padding past
+// the grid repeats the last texel; no lookup reads it)
+__host__ __device__ __forceinline__ void grid_tiled_texel(uint64_t i, int32_t rx, int32_t ry, int32_t rz, int32_t &x,
+                                                          int32_t &y, int32_t &z) {
+    const uint64_t tile = i >> 5;
+    const uint32_t w = (uint32_t)(i & 31u), ntx = grid_tiles_xy(rx), nty = grid_tiles_xy(ry);
+    const uint32_t tx = (uint32_t)(tile % ntx), ty = (uint32_t)((tile / ntx) % nty), tz = (uint32_t)(tile / ((uint64_t)ntx * nty));
+    x = min((int32_t)(3u * tx + (w & 3u)), rx - 1);
+    y = min((int32_t)(3u * ty + ((w >> 2) & 3u)), ry - 1);
+    z = min((int32_t)(tz + (w >> 4)), rz - 1);
 }
 
 // [drjit] Texture3f::eval_nonaccel, linear, clamp, 1 channel (grid.cpp:545-558),
@@ -2450,12 +2481,23 @@ MH_DEV void grid_setup(const DMedium &m, V3 p, GridLookup &L) {
     const int32_t x0 = min(max(ix, 0), rx - 1), x1 = min(max(ix + 1, 0), rx - 1);
     const int32_t y0 = min(max(iy, 0), ry - 1), y1 = min(max(iy + 1, 0), ry - 1);
     const int32_t z0 = min(max(iz, 0), rz - 1), z1 = min(max(iz + 1, 0), rz - 1);
+#if MH_GRID_TILE
+    // the lookup's cell, its apron tile and the taps' places in it (32-bit:
+    // mh_scene_create caps a grid's device layout at 2^32 floats)
+    const int32_t cx = min(max(ix, 0), max(rx - 2, 0)), cy = min(max(iy, 0), max(ry - 2, 0)), cz = min(max(iz, 0), max(rz - 2, 0));
+    const uint32_t tx = (uint32_t)cx / 3u, ty = (uint32_t)cy / 3u;
+    const uint32_t base = (((uint32_t)cz * grid_tiles_xy(ry) + ty) * grid_tiles_xy(rx) + tx) * 32u;
+    const uint32_t ox0 = (uint32_t)x0 - 3u * tx, ox1 = (uint32_t)x1 - 3u * tx;
+    const uint32_t oy0 = ((uint32_t)y0 - 3u * ty) << 2, oy1 = ((uint32_t)y1 - 3u * ty) << 2;
+    const uint32_t oz0 = base + (((uint32_t)z0 - (uint32_t)cz) << 4), oz1 = base + (((uint32_t)z1 - (uint32_t)cz) << 4);
+#else
     // grid_index split per axis (brick-major part + texel-in-brick part, the
     // bit fields disjoint), 32-bit (mh_scene_create caps a grid at 2^32 texels)
     const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2, sy = nbx * 64u, sz = sy * nby;
     const uint32_t ox0 = ((uint32_t)x0 >> 2) * 64u + ((uint32_t)x0 & 3u), ox1 = ((uint32_t)x1 >> 2) * 64u + ((uint32_t)x1 & 3u);
     const uint32_t oy0 = ((uint32_t)y0 >> 2) * sy + (((uint32_t)y0 & 3u) << 2), oy1 = ((uint32_t)y1 >> 2) * sy + (((uint32_t)y1 & 3u) << 2);
     const uint32_t oz0 = ((uint32_t)z0 >> 2) * sz + (((uint32_t)z0 & 3u) << 4), oz1 = ((uint32_t)z1 >> 2) * sz + (((uint32_t)z1 & 3u) << 4);
+#endif
     const uint32_t o00 = oy0 + oz0, o10 = oy1 + oz0, o01 = oy0 + oz1, o11 = oy1 + oz1;
     L.o[0] = o00 + ox0; L.o[1] = o00 + ox1; L.o[2] = o10 + ox0; L.o[3] = o10 + ox1;
     L.o[4] = o01 + ox0; L.o[5] = o01 + ox1; L.o[6] = o11 + ox0; L.o[7] = o11 + ox1;
@@ -2473,7 +2515,8 @@ MH_DEV float grid_interp(const GridLookup &L, const float (&v)[8]) {
 // offset, checked at the use: the values are the grid's own, so a match of
 // the cell within the same medium is exact whatever produced the prefetch.
 struct GridPf {
-    uint32_t key;  // ~0u: none
+    uint32_t key, key7;  // the lookup's first and last tap offsets (key ~0u: none); the caller
+                         // checks the medium (k_vol_sched's MH_VS_STEP2: same chain, same medium)
     float v[8];
 };
 MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p, const GridPf *pf = nullptr) {
@@ -2490,7 +2533,7 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p, const GridPf *pf
     }
 #endif
     float v[8];
-    if (pf && pf->key == L.o[0]) {
+    if (pf && pf->key == L.o[0] && pf->key7 == L.o[7]) {
 #ifdef MH_EXP_LOOKUPS
         {
             const unsigned long long ex = __builtin_amdgcn_read_exec();
@@ -2503,6 +2546,18 @@ MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p, const GridPf *pf
 #pragma unroll
         for (int c = 0; c < 8; ++c) v[c] = g[L.o[c]];
     }
+#ifdef MH_EXP_GRIDDEP  // timing experiment: a second, DEPENDENT round trip per lookup (results unchanged)
+    {
+        uint32_t zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+        const uint32_t dep = __float_as_uint(v[0]) & zero;  // 0, but only known after the first loads
+        float u = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) u += g[L.o[c] + dep];
+        asm volatile("" : "+v"(u));
+        return grid_interp(L, v) + (u == 12345.f ? 1.f : 0.f) * 0.f;
+    }
+#endif
 #ifdef MH_EXP_GRID2  // timing experiment: a second lookup's memory traffic (results unchanged)
     {
         float u = 0.f;
@@ -2594,6 +2649,7 @@ MH_DEV void grid_prefetch(const DScene &S, uint32_t med, const RayT &ray, float 
 #pragma unroll
     for (int c = 0; c < 8; ++c) pf.v[c] = g[L.o[c]];
     pf.key = L.o[0];
+    pf.key7 = L.o[7];
 }
 
 MH_DEV V3 mei_to_local(const MEI &m, V3 v) { return v3(dot(v, m.fs), dot(v, m.ft), dot(v, m.fn)); }
@@ -2775,7 +2831,6 @@ struct VolState {
     float pend_w;       // medium: MIS weight applied after the emitted radiance
     DirS ds;
     NeeState ns;
-    GridPf pf;          // k_vol_sched: the next medium sample's taps, loaded a trip ahead (key ~0u: none)
 };
 
 MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT ray, VolState &v) {
@@ -2794,7 +2849,6 @@ MH_DEV void volpath_init(const DScene &S, const IntegratorParams &in, Pcg &rng, 
     v.last_p = v3(0, 0, 0);
     v.last_pdf = 1.f;
     v.mode = kVolPre;
-    v.pf.key = ~0u;
 }
 
 // pre: false when the path ends at the loop head

@@ -680,72 +680,98 @@ MH_DEV uint32_t vs_walk(const DScene &S, Pcg &rng, const DirS &ds, NeeState &ns,
     return vs_walk_post(S, ds, ns, wm, mei);
 }
 
-// k_vol_sched (VolMachine), opt-in: a lane whose next trip is another medium
-// sample issues that sample's 8 grid loads at the end of this trip (GridPf).
-// 79 % of config 4's lookups then come from a prefetch, and the render runs
-// at 191 vs 245 Msamples/s (256 vs 236 VGPRs; the loads left in flight make
-// the other phases' waits wait for them) -- the lookup latency is not what
-// holds the merged trip
-#ifndef MH_VS_PREFETCH
-#define MH_VS_PREFETCH 0
-#endif
 // HEAD and WALK lanes in one trip: both end in a medium sample (a grid
 // lookup, the trip's latency), so the pending lanes of both take it together
 // at one call site instead of one wave trip each.  Per lane the operations
 // and draws are vs_head's / vs_walk's.
+//
+// MH_VS_STEP2 (round 5): a medium sample is usually followed by another one
+// of the same chain -- a null collision continues along its ray, a
+// ratio-tracking step continues its walk -- and the next sample's position
+// depends only on this one's position and the sampler's next draws, not on
+// the density.  So the trip computes the chain's next sample position on a
+// copy of the sampler (for HEAD: vs_med_rest's null draw, vs_head_pre's RR
+// draw, then u; for WALK: u, at remaining = max_dist - (total_dist + t)),
+// issues its lookup's 8 loads beside this sample's 8 (one memory round trip
+// for both), and when this sample's continuation sends the lane to the same
+// phase again it takes that next step in the same trip with those taps.  The
+// speculation is only a cache (GridPf): the second step recomputes its
+// lookup and takes the taps only when its cell and medium match, so per lane
+// the operations and draws stay vs_head's / vs_walk's (bit-identical).
+// (Round 4's one-trip-ahead prefetch, loads left in flight across trips,
+// measured slower: DESIGN.md section 9.)
+#ifndef MH_VS_STEP2
+#define MH_VS_STEP2 0  // measured slower (config 4: 197 vs 249 Msamples/s)
+#endif
+// the ray of a HEAD / WALK lane's medium sample, as values
+MH_DEV RayT vs_medium_ray(const VolState &v, bool head) {
+    const RayT rh = v.ray, rw = v.ns.ray;
+    RayT r;
+    r.o = v3(head ? rh.o.x : rw.o.x, head ? rh.o.y : rw.o.y, head ? rh.o.z : rw.o.z);
+    r.d = v3(head ? rh.d.x : rw.d.x, head ? rh.d.y : rw.d.y, head ? rh.d.z : rw.d.z);
+    r.maxt = head ? rh.maxt : rw.maxt;
+    return r;
+}
 MH_DEV uint32_t vs_medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v, WMei &wm,
                                uint32_t ph) {
     uint32_t nph = kPhFree;
     float u = 0.f;
     const bool head = ph == kPhHead;
     const bool pend = head ? vs_head_pre(S, in, rng, v, nph, u) : vs_walk_pre(S, rng, v.ns, nph, u);
-    if (!pend) {
-#if MH_VS_PREFETCH
-        v.pf.key = ~0u;  // a prefetch lives for one medium trip only
-#endif
-        return nph;
-    }
+    if (!pend) return nph;
     // the request as a select of values (a select of the two fields'
     // addresses would pin the state in scratch)
-    const uint32_t mh = v.medium, mw = v.ns.medium;
-    const RayT rh = v.ray, rw = v.ns.ray;
-    RayT r;
-    r.o = v3(head ? rh.o.x : rw.o.x, head ? rh.o.y : rw.o.y, head ? rh.o.z : rw.o.z);
-    r.d = v3(head ? rh.d.x : rw.d.x, head ? rh.d.y : rw.d.y, head ? rh.d.z : rw.d.z);
-    r.maxt = head ? rh.maxt : rw.maxt;
-    MEI mei;  // the frame only at a real scatter (vs_scatter)
-#if MH_VS_PREFETCH
-    const GridPf pf = v.pf;  // taps this lane loaded at its previous medium trip (if any)
-    v.pf.key = ~0u;
-    sample_interaction<false>(S, head ? mh : mw, r, u, mei, &pf);
-#else
-    sample_interaction<false>(S, head ? mh : mw, r, u, mei);
+    const uint32_t med = head ? v.medium : v.ns.medium;
+    const RayT r = vs_medium_ray(v, head);
+#if MH_VS_STEP2
+    GridPf pf;
+    pf.key = ~0u;
+    {
+        const DMedium &m = S.media[med];
+        float mint1, t1;
+        V3 p1;
+        if (m.type != MH_MEDIUM_HOMOGENEOUS && free_flight(m, r, u, mint1, t1, p1)) {
+            Pcg c = rng;
+            RayT r2;
+            r2.o = p1;
+            r2.d = r.d;
+            float u2;
+            if (head) {
+                (void)c.next_float();  // vs_med_rest: the null / real decision
+                (void)c.next_float();  // vs_head_pre: Russian roulette
+                u2 = c.next_float();
+                r2.maxt = r.maxt;
+            } else {
+                r2.maxt = v.ns.max_dist - (v.ns.total_dist + t1);  // walk_med_rest, then vs_walk_pre
+                u2 = c.next_float();
+            }
+            grid_prefetch(S, med, r2, u2, pf);
+        }
+    }
 #endif
-    if (ph == kPhHead) {
+    MEI mei;  // the frame only at a real scatter (vs_scatter)
+    sample_interaction<false>(S, med, r, u, mei);
+    if (head) {
         v.mei = mei;
         nph = vs_head_post(S, in, rng, v);
     } else {
         nph = vs_walk_post(S, v.ds, v.ns, wm, mei);
     }
-#if MH_VS_PREFETCH
-    // the lane's next trip is a medium sample again (a null collision, a
-    // ratio-tracking step): run that trip's draws on a copy of the sampler
-    // and issue its lookup's loads now (vs_head_pre / vs_walk_pre)
-    if (nph == kPhHead && v.medium != MH_INVALID && v.depth < in.max_depth) {
-        Pcg r2 = rng;
-        bool go = true;
-        if (nonzero(v.throughput)) {
-            const float q = fminf(hmax(v.throughput) * (v.eta * v.eta), 0.95f);
-            go = r2.next_float() < q || !(v.depth > in.rr_depth);
-        }
-        if (go) grid_prefetch(S, v.medium, v.ray, r2.next_float(), v.pf);
-    } else if (nph == kPhWalk && v.ns.medium != MH_INVALID) {
-        const float remaining = v.ns.max_dist - v.ns.total_dist;
-        if (remaining > 0.f) {
-            Pcg r2 = rng;
-            RayT rw2 = v.ns.ray;
-            rw2.maxt = remaining;
-            grid_prefetch(S, v.ns.medium, rw2, r2.next_float(), v.pf);
+#if MH_VS_STEP2
+    if (pf.key != ~0u && nph == ph) {  // the chain goes on: its next trip's step now
+        uint32_t nph2 = kPhFree;
+        float u2 = 0.f;
+        const bool pend2 = head ? vs_head_pre(S, in, rng, v, nph2, u2) : vs_walk_pre(S, rng, v.ns, nph2, u2);
+        if (!pend2) return nph2;
+        const uint32_t med2 = head ? v.medium : v.ns.medium;
+        const RayT r2 = vs_medium_ray(v, head);
+        MEI mei2;
+        sample_interaction<false>(S, med2, r2, u2, mei2, med2 == med ? &pf : nullptr);
+        if (head) {
+            v.mei = mei2;
+            nph = vs_head_post(S, in, rng, v);
+        } else {
+            nph = vs_walk_post(S, v.ds, v.ns, wm, mei2);
         }
     }
 #endif
