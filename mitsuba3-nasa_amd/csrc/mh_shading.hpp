@@ -2424,7 +2424,7 @@ struct MEI {
 // reference's linear (z, y, x) layout; values are unchanged, so lookups are
 // bit-exact either way).
 //
-// MH_GRID_TILE = 1 (round 5, the default): apron tiles.  The cells of a
+// MH_GRID_TILE = 1 (round 5, opt-in): apron tiles.  The cells of a
 // trilinear lookup (its lower tap corner, clamped to [0, r - 2]) are grouped
 // 3 x 3 x 1, and tile (tx, ty, tz) stores the 4 x 4 x 2 texels x in
 // [3 tx, 3 tx + 4), y in [3 ty, 3 ty + 4), z in [tz, tz + 2) -- every tap of
@@ -2432,13 +2432,17 @@ struct MEI {
 // then touches exactly one line, where the 4^3 bricks below touch 2.34 lines
 // on average (a 2 x 2 x 2 block at a random offset against 4 x 4 x 2 lines),
 // and config 4's k_vol_sched is bound by the lines that miss L2 (twice the
-// lookup lines cost 19 %).  The price is 3.6x the
-// texels (256^3: 236 MB, inside the 256 MB Infinity Cache).
+// lookup lines cost 19 %).  The price is 3.6x the texels (256^3: 236 MB,
+// inside the 256 MB Infinity Cache).  Measured: config 4 at 249.3-249.8 vs
+// 247.5-248.9 Msamples/s with the bricks (same box) --
+// within noise, so the lines a lookup misses are not what bounds the trip
+// (the second lookup of that experiment cost its VALU and registers), and
+// the 3.6x footprint is not worth it.
 //
-// MH_GRID_TILE = 0: 4 x 4 x 4 bricks of 64 floats (256 B), bricks x-fastest,
-// texels x-fastest inside a brick.
+// MH_GRID_TILE = 0 (the default): 4 x 4 x 4 bricks of 64 floats (256 B),
+// bricks x-fastest, texels x-fastest inside a brick.
 #ifndef MH_GRID_TILE
-#define MH_GRID_TILE 1
+#define MH_GRID_TILE 0
 #endif
 __host__ __device__ __forceinline__ uint64_t grid_index(int32_t x, int32_t y, int32_t z, int32_t rx, int32_t ry) {
     const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2;

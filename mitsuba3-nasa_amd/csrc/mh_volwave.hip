@@ -1101,15 +1101,54 @@ MH_DEV bool pv_walk_pre(const DScene &S, Pcg &rng, V &v, Hk &hk, uint32_t &nph, 
     nph = pv_walk_fin(S, v, remaining_dist, hk, mei);
     return false;
 }
+// MH_PV_STEP2: the WALK trip's second ratio-tracking step (vs_medium_step's
+// MH_VS_STEP2 for prbvolpath's unmerged WALK phase): the walk's next sample
+// position needs only this sample's position and the next draw, so its
+// lookup's loads go out beside this one's, and a walk that goes on takes its
+// next step in the same trip from those taps (a cache: the step recomputes
+// its lookup and takes the taps only when the cell and medium match)
+#ifndef MH_PV_STEP2
+#define MH_PV_STEP2 0
+#endif
 template <class V, class Hk>
 MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, V &v, Hk &hk) {
     uint32_t nph = kPhPost;
     float u = 0.f;
     if (!pv_walk_pre(S, rng, v, hk, nph, u)) return nph;
+#if MH_PV_STEP2
+    const uint32_t med = v.wmedium;
+    GridPf pf;
+    pf.key = ~0u;
+    {
+        const DMedium &m = S.media[med];
+        float mint1, t1;
+        V3 p1;
+        if (m.type != MH_MEDIUM_HOMOGENEOUS && free_flight(m, v.wray, u, mint1, t1, p1)) {
+            Pcg c = rng;
+            RayT r2;
+            r2.o = p1;
+            r2.d = v.wray.d;
+            r2.maxt = v.ds.dist * (1.f - kShadowEps) - (v.total_dist + t1);  // pv_walk_fin, then pv_remaining
+            grid_prefetch(S, med, r2, c.next_float(), pf);
+        }
+    }
+#endif
     MEI mei;
     pv_walk_mei_init(mei);
     sample_interaction(S, v.wmedium, v.wray, u, mei);
-    return pv_walk_fin(S, v, pv_remaining(v), hk, mei);
+    nph = pv_walk_fin(S, v, pv_remaining(v), hk, mei);
+#if MH_PV_STEP2
+    if (pf.key != ~0u && nph == kPhWalk) {
+        uint32_t nph2 = kPhPost;
+        float u2 = 0.f;
+        if (!pv_walk_pre(S, rng, v, hk, nph2, u2)) return nph2;
+        MEI mei2;
+        pv_walk_mei_init(mei2);
+        sample_interaction(S, v.wmedium, v.wray, u2, mei2, v.wmedium == med ? &pf : nullptr);
+        nph = pv_walk_fin(S, v, pv_remaining(v), hk, mei2);
+    }
+#endif
+    return nph;
 }
 
 // HEAD and WALK lanes in one trip (vs_medium_step's form for prbvolpath)

@@ -324,6 +324,94 @@ MH_DEV bool block_has_range_work(const SegIter &it, uint32_t n) {
     return first_wave * per < n;
 }
 
+// MH_WF_DYN (round 5): persistent fused bounce kernels.  A grid of 30
+// workgroups per CU stages the shading tables and pair records into LDS once
+// per workgroup, i.e. once per ~17 loop iterations of each of its waves: 8-13 %
+// of the bounce kernels' wave cycles went to that prologue
+// (profiles/r5_bounce_phases.txt).  With MH_WF_DYN the grid is the resident
+// workgroups only, and a wave takes 64-path batches of its segment from the
+// segment's grab counter (word 16 of the segment's counter line, zeroed with
+// the counters), then -- its segment drained -- of the other segments, its
+// XCD's first, skipping drained ones by a plain load before any atomic.  The
+// survivors of a batch go to the batch's segment, as before.  Measured slower
+// and kept opt-in: bench 1,703-1,717 (grab at the batch) and 1,810-1,812
+// (grab one batch ahead) vs 1,937-1,952 Msamples/s for the 30-per-CU grid on
+// the same boxes -- the grab state costs the 96-VGPR kernels 3-11 spilled
+// registers, and the prologue the phase timers charge overlaps other blocks'
+// waves on the CU
+#ifndef MH_WF_DYN
+#define MH_WF_DYN 0
+#endif
+constexpr uint32_t kGrabWord = 16;
+struct WfGrab {
+    uint32_t home, k, seg, n;  // wave-uniform: home segment, segments tried, current segment and its length
+    uint32_t next;             // lane 0: the batch grabbed one iteration ahead (its atomic's latency hides
+                               // under the current batch; read with readfirstlane when it is due)
+};
+// the k-th segment a wave of home segment h serves: h's XCD's 8 segments
+// (h mod 8 + 8 j) first, then the next XCD's, ... (a bijection of 0..63)
+MH_DEV uint32_t seg_order(uint32_t h, uint32_t k) {
+    return ((((h >> 3) + k) & 7u) << 3) | (((h & 7u) + (k >> 3)) & 7u);
+}
+MH_DEV uint32_t wf_grab(uint32_t *ctr, uint32_t seg) {
+    uint32_t b = 0;
+    if (lane_id() == 0) b = atomicAdd(ctr + seg * 32u + kGrabWord, 64u);
+    return b;
+}
+template <class CountOf>
+MH_DEV void wf_grab_init(uint32_t *ctr, WfGrab &g, uint32_t home, CountOf count_of) {
+    g.home = g.seg = home;
+    g.k = 0;
+    // (readfirstlane: the values are wave-uniform, and said so they stay in
+    // SGPRs instead of taking VGPRs from the 96-register budget)
+    g.n = (uint32_t)__builtin_amdgcn_readfirstlane(count_of(home));
+    g.next = wf_grab(ctr, home);
+}
+template <class CountOf>
+MH_DEV bool wf_next_batch(uint32_t *ctr, WfGrab &g, CountOf count_of, uint32_t &base) {
+    while (true) {
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane(g.next);
+        if (b < g.n) {
+            base = b;
+            g.next = wf_grab(ctr, g.seg);  // the following batch, due at the next call
+            return true;
+        }
+        // this segment is drained: the next one with work left (a plain load
+        // skips drained ones without an atomic on their counter)
+        while (true) {
+            if (++g.k >= kSeg) return false;
+            g.seg = seg_order(g.home, g.k);
+            g.n = (uint32_t)__builtin_amdgcn_readfirstlane(count_of(g.seg));
+            const uint32_t taken = (uint32_t)__builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(ctr + g.seg * 32u + kGrabWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (taken < g.n) break;
+        }
+        g.next = wf_grab(ctr, g.seg);
+    }
+}
+
+// the grid of a persistent (MH_WF_DYN) fused bounce launch: the workgroups
+// resident at `waves` per SIMD (4 waves per workgroup: `waves` per CU), a
+// whole number per segment, at most the caller's grid (whose per-block
+// gradient partials the PRB kernels fill)
+static uint32_t wf_dyn_grid(uint32_t grid, uint32_t waves) {
+#if MH_WF_DYN
+    static const int cus = [] {
+        int dev = 0, c = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return std::max(1, c);
+    }();
+    uint32_t g = (uint32_t)cus * waves;
+    if (const char *e = getenv("MH_WF_DYN_BPC")) g = (uint32_t)cus * (uint32_t)std::max(1, atoi(e));
+    g = std::max<uint32_t>(kSeg, g / kSeg * kSeg);
+    return std::min(g, grid);
+#else
+    (void)waves;
+    return grid;
+#endif
+}
+
 // contiguous share of a segment for this wave (refill traversal)
 MH_DEV void wave_range(const SegIter &it, uint32_t n, uint32_t &r0, uint32_t &r1) {
     const uint32_t per = (n + it.nwaves - 1) / it.nwaves;
@@ -529,15 +617,22 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             uint64_t *carry, uint32_t pass, int alpha) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
-    uint32_t n;
-    if (Gen) {
-        const uint64_t b0 = (uint64_t)it.seg * seg_cap;
-        n = b0 >= n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, n_total - b0);
-        if (blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
-    } else {
-        n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    auto seg_count = [&](uint32_t sg) -> uint32_t {
+        if (Gen) {
+            const uint64_t b0 = (uint64_t)sg * seg_cap;
+            return b0 >= n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, n_total - b0);
+        }
+        return __hip_atomic_load(ctr + sg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+#if MH_WF_DYN
+    if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = seg_count(it.seg);  // queue statistics
+    WfGrab gb;
+    wf_grab_init(ctr, gb, it.seg, seg_count);
+#else
+    const uint32_t n = seg_count(it.seg);
+    if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
     if (!block_has_stride_work(it, n)) return;
+#endif
     MH_BPH_DECL
     float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
     stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
@@ -545,11 +640,18 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     uint32_t *ws = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(lds) + S0.tab_bytes) +
                    (threadIdx.x >> 6) * S0.stack_size;
     uint8_t *dscr = reinterpret_cast<uint8_t *>(lds) + fused_scratch_offset(S0) + (threadIdx.x >> 6) * kDeferScratch;
-    const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
     uint32_t n_shadow = 0;
     MH_BPH(7);
+#if MH_WF_DYN
+    uint32_t base = 0;
+    while (wf_next_batch(ctr, gb, seg_count, base)) {
+        const uint32_t seg = gb.seg, n = gb.n;
+#else
+    const uint32_t seg = it.seg;
     for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
+#endif
+        const uint32_t sbase = seg * seg_cap;
         MH_BPH_ITER();
         const uint32_t i = base + lane_id();
         const bool has = i < n;
@@ -704,7 +806,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         MH_BPH(2);
         // ---- compaction: the survivor's next-bounce state leaves registers
         // before the shadow trace (only L and the NEE product stay live across it)
-        const uint32_t slot = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        const uint32_t slot = sbase + wave_append(ctr_next + seg * 32, alive);
         MH_GUARD(!alive || slot - sbase < seg_cap, kGuardAppendSlot);
         const float rng_hi = __uint_as_float((uint32_t)(rng.state >> 32));
         if (alive) {
@@ -833,11 +935,12 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
             // round-3 build recorded the other 2 n_bounces - 2 events empty
             // after it, ~75 us of idle GPU per chunk)
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
+            const uint32_t gd = wf_dyn_grid(grid, MH_BOUNCE_WAVES);
             if (b == 0)
-                hipLaunchKernelGGL(k_wf_bounce<true>, dim3(grid), dim3(256), fused_lds_bytes(S), st, S,
+                hipLaunchKernelGGL(k_wf_bounce<true>, dim3(gd), dim3(256), fused_lds_bytes(S), st, S,
                                    in, lm, seed_value, plane, out, pk, cur, seg_cap, c, cn, n, carry, pass, alpha);
             else
-                hipLaunchKernelGGL(k_wf_bounce<false>, dim3(grid), dim3(256), fused_lds_bytes(S), st,
+                hipLaunchKernelGGL(k_wf_bounce<false>, dim3(gd), dim3(256), fused_lds_bytes(S), st,
                                    S, in, lm, seed_value, plane, out, pk, cur, seg_cap, c, cn, n, carry, pass, alpha);
             if (trace_ev && b + 1 == n_bounces) (void)hipEventRecord(trace_ev[1], st);
             continue;
@@ -1253,15 +1356,22 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 int cur, uint32_t seg_cap, uint32_t *ctr, uint32_t *ctr_next, PrbGen gen, WfBmp bm, WfDet det) {
     extern __shared__ uint4 lds[];
     const SegIter it = seg_iter();
-    uint32_t n;
-    if (Gen) {
-        const uint64_t b0 = (uint64_t)it.seg * seg_cap;
-        n = b0 >= gen.n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, gen.n_total - b0);
-        if (blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
-    } else {
-        n = __hip_atomic_load(ctr + it.seg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    auto seg_count = [&](uint32_t sg) -> uint32_t {
+        if (Gen) {
+            const uint64_t b0 = (uint64_t)sg * seg_cap;
+            return b0 >= gen.n_total ? 0u : (uint32_t)std::min<uint64_t>(seg_cap, gen.n_total - b0);
+        }
+        return __hip_atomic_load(ctr + sg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+#if MH_WF_DYN
+    if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = seg_count(it.seg);  // queue statistics
+    WfGrab gb;
+    wf_grab_init(ctr, gb, it.seg, seg_count);
+#else
+    const uint32_t n = seg_count(it.seg);
+    if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
     if (!block_has_stride_work(it, n)) return;
+#endif
     MH_BPH_DECL
     float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
     stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
@@ -1270,17 +1380,25 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                    (threadIdx.x >> 6) * S0.stack_size;
     uint8_t *dscr = reinterpret_cast<uint8_t *>(lds) + fused_scratch_offset(S0) + (threadIdx.x >> 6) * kDeferScratch;
     uint32_t n_shadow = 0;
-    const uint32_t sbase = it.seg * seg_cap;
     const int nxt = cur ^ 1;
     const uint32_t n_rgb = q.n_rgb;
     float acc[NR][3];
 #pragma unroll
     for (int kk = 0; kk < NR; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
-    const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
     MH_BPH(7);
+#if MH_WF_DYN
+    uint32_t base = 0;
+    while (wf_next_batch(ctr, gb, seg_count, base)) {
+        const uint32_t seg = gb.seg, n = gb.n;
+        const uint32_t i = base + lane_id();
+#else
+    const uint32_t seg = it.seg;
+    const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
     for (uint32_t itr = 0; itr < n_iter; ++itr) {
-        MH_BPH_ITER();
         const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
+#endif
+        const uint32_t sbase = seg * seg_cap;
+        MH_BPH_ITER();
         bool alive = false, shadow = false;
         uint32_t pid = 0, depth = 0;
         RayT ray{v3(0, 0, 0), v3(0, 0, 1), -1.f}, sray{v3(0, 0, 0), v3(0, 0, 1), -1.f};
@@ -1471,7 +1589,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             alive = active_next;
         }
         MH_BPH(2);
-        const uint32_t slot_n = sbase + wave_append(ctr_next + it.seg * 32, alive);
+        const uint32_t slot_n = sbase + wave_append(ctr_next + seg * 32, alive);
         MH_GUARD(!alive || slot_n - sbase < seg_cap, kGuardAppendSlot);
         if (alive) {
             w.pd[nxt][slot_n] = pid | (depth << kPidBits);
@@ -2010,8 +2128,9 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     const PrbGen gen{n, grad_in, coalesce};
     if (span) (void)hipEventRecord(span[0], st);
 #define MH_BOUNCE_PRB(NR, GEN, BM, DET)                                                                        \
-    hipLaunchKernelGGL((k_wf_bounce_prb<NR, GEN, BM, DET>), dim3(grid), dim3(256), sh_fused, st, S, in, lm,       \
-                       seed_value, w, q, cur, seg_cap, c, cn, gen, bm, det)
+    hipLaunchKernelGGL((k_wf_bounce_prb<NR, GEN, BM, DET>),                                                    \
+                       dim3(wf_dyn_grid(grid, BM ? MH_BOUNCE_BMP_WAVES : MH_BOUNCE_PRB_WAVES)), dim3(256),      \
+                       sh_fused, st, S, in, lm, seed_value, w, q, cur, seg_cap, c, cn, gen, bm, det)
 #define MH_BOUNCE_PRB_NR(GEN, BM, DET)                                                                         \
     do {                                                                                                       \
         if (n_rgb <= 1) MH_BOUNCE_PRB(1, GEN, BM, DET);                                                        \
