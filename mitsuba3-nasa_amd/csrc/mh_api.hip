@@ -1533,9 +1533,9 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
                 bmp.fx_word = s->bmp_fx.as<uint32_t>();
                 bmp.fx_acc = reinterpret_cast<unsigned long long *>(s->bmp_fx.as<uint8_t>() + 256);
             }
-            const size_t per_wg = std::max<size_t>((size_t)bmp.n_floats * 4, 1);
-            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, (size_t)per_cu_lds / per_wg));
-            bmp.blocks = (uint32_t)cus * per_cu;
+            bmp.wg_lds = (uint32_t)max_wg;
+            bmp.cu_lds = (uint32_t)per_cu_lds;
+            bmp.cus = (uint32_t)cus;
         }
         // MH_FLAG_DETERMINISTIC: rgb slots summed per path and reduced in a
         // fixed order (WfDet); bitmap texels in int64 fixed point (bmp.fx_acc)

@@ -114,7 +114,9 @@ struct WfBitmapArgs {
     float *grad = nullptr;   // the bitmap slots' block of gradient buffers (device)
     uint32_t n_floats = 0;   // that block's floats (texels x channels, padded per slot)
     uint32_t lds_max = 0;    // per-workgroup LDS accumulation when n_floats * 4 <= lds_max
-    uint32_t blocks = 0;     // scatter workgroups (persistent grid)
+    uint32_t wg_lds = 0;     // the device's LDS bytes per workgroup and per CU
+    uint32_t cu_lds = 0;
+    uint32_t cus = 0;        // the scatter's persistent grid: cus x the accumulators a CU holds
     // MH_FLAG_DETERMINISTIC: int64 sums (n_floats) and the max word of the
     // fixed-point scatter (nullptr: float atomics)
     unsigned long long *fx_acc = nullptr;

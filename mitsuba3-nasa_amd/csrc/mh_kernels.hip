@@ -358,7 +358,7 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 
 // The film splat (mode 0) on 4 x 4 tiles of source pixels: a 256-thread
 // workgroup is 16 pixel rows of kSplatLanes lanes, as in k_splat_px, but the
-// rows' footprint sums go to the tile's 8 x 8 film block in LDS (ds_add_f32)
+// rows' footprint sums go to the tile's 8 x 8 film block in LDS (ds_add_f64)
 // and the block is added to the film once, coalesced: 256 lanes, one float
 // each, film rows of 8 pixels x 4 channels contiguous.  k_splat_px issues
 // 100 memory-side atomics per source pixel from 4 lanes of a wave; this
@@ -374,14 +374,15 @@ __global__ void __launch_bounds__(256)
 k_splat_tile(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row_first, uint32_t tiles_x, uint32_t Sn,
              uint32_t n_passes, uint64_t n, uint64_t plane, const float *__restrict__ in, float *__restrict__ film,
              unsigned long long *__restrict__ invalid, uint64_t in_lim, unsigned long long *__restrict__ viol) {
-    __shared__ float tile[kSplatTileFilm * kSplatTileFilm * 4];
+    // double: ds_add_f64 runs ~7x the rate of ds_add_f32 on gfx950 (LdsDouble)
+    __shared__ double tile[kSplatTileFilm * kSplatTileFilm * 4];
     const uint32_t W = S.width, H = S.height;
     const uint32_t tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const uint32_t grp = threadIdx.x / kSplatLanes, g = threadIdx.x % kSplatLanes;
     const uint32_t ti = grp % kSplatTile, tj = grp / kSplatTile;
     const uint32_t px = tx * kSplatTile + ti, py = row_first + ty * kSplatTile + tj;
-    tile[threadIdx.x] = 0.f;
-    if (threadIdx.x < kSplatTileFilm * kSplatTileFilm * 4 - 256) tile[256 + threadIdx.x] = 0.f;
+    tile[threadIdx.x] = 0.0;
+    if (threadIdx.x < kSplatTileFilm * kSplatTileFilm * 4 - 256) tile[256 + threadIdx.x] = 0.0;
     const uint32_t pixel = py * W + px;
     bool live = px < W && py < H && pixel >= pixel_begin && pixel - pixel_begin < n_pix;
     const uint32_t pl = pixel - pixel_begin;
@@ -455,13 +456,14 @@ k_splat_tile(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row_first,
             for (int xs = 0; xs < 5; ++xs)
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    atomicAdd(&tile[((tj + ys) * kSplatTileFilm + (ti + xs)) * 4 + c], acc[ys][xs][c]);
+                    __hip_atomic_fetch_add((LdsDouble *)&tile[((tj + ys) * kSplatTileFilm + (ti + xs)) * 4 + c],
+                                           (double)acc[ys][xs][c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
     // the film block: element e = (row, column, channel) of the tile's 8 x 8 x 4
     const int32_t ox = (int32_t)(tx * kSplatTile) - 2, oy = (int32_t)(row_first + ty * kSplatTile) - 2;
     for (uint32_t e = threadIdx.x; e < kSplatTileFilm * kSplatTileFilm * 4; e += 256) {
-        const float v = tile[e];
+        const float v = (float)tile[e];
         const int32_t x = ox + (int32_t)((e >> 2) % kSplatTileFilm), y = oy + (int32_t)((e >> 2) / kSplatTileFilm);
         if (v != 0.f && x >= 0 && y >= 0 && (uint32_t)x < W && (uint32_t)y < H)
             atomicAdd(film + ((uint64_t)y * W + (uint32_t)x) * 4 + (e & 3u), v);

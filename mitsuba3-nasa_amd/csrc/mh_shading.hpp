@@ -1745,13 +1745,19 @@ MH_DEV V3 acc_get(const GradCtx &g, int32_t k) {
 // ---------------------------------------------------------------------------
 extern "C" __device__ float __ockl_wfred_add_f32(float);
 typedef __attribute__((address_space(3))) float LdsFloat;
+// gfx950 runs a no-return ds_add_f32 at ~190 CU cycles per 64-lane
+// instruction (~3 per active lane; any address pattern), ds_add_f64 at ~26,
+// ds_add_u32 at ~12 (tools/exp_ldsatomic.hip, profiles/r5_lds_atomics.txt):
+// an LDS accumulator that takes many adds is kept in double
+typedef __attribute__((address_space(3))) double LdsDouble;
 #ifndef MH_GROUP_MIN
 #define MH_GROUP_MIN 6
 #endif
 constexpr int kGroupMin = MH_GROUP_MIN, kGroupIters = 4;
 
-template <int C>
-MH_DEV void lds_add_grouped(LdsFloat *acc, uint32_t key, bool on, const float (&v)[C]) {
+template <int C, typename Acc>
+MH_DEV void lds_add_grouped(Acc *acc, uint32_t key, bool on, const float (&v)[C]) {
+    using T = __typeof__(+*acc);
     const uint32_t me = __lane_id();
     for (int it = 0; it < kGroupIters; ++it) {
         const uint64_t m = __ballot(on);
@@ -1766,14 +1772,14 @@ MH_DEV void lds_add_grouped(LdsFloat *acc, uint32_t key, bool on, const float (&
         if (me == leader) {
 #pragma unroll
             for (int c = 0; c < C; ++c)
-                __hip_atomic_fetch_add(acc + kl + c, s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(acc + kl + c, (T)s[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         on = on && !mine;
     }
     if (on) {
 #pragma unroll
         for (int c = 0; c < C; ++c)
-            __hip_atomic_fetch_add(acc + key + c, v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(acc + key + c, (T)v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 

@@ -1892,13 +1892,16 @@ hipError_t launch_wavefront_fwd(const DScene &S, const IntegratorParams &in, con
 
 // Texel gradients of the logged bitmap vertices of one chunk (see WfBmp):
 // adj_k = D_k + dL (L_total - P_k) q_k / pi per record, spread over the
-// bilinear taps (tex_backward's weights).  Lane l of a wave takes path
-// 64 l + c of a 4096-path tile (column c), so the lanes hold paths 64 apart
-// -- 64 different pixels at 64 spp -- instead of the samples of one pixel,
-// whose camera vertices all land on the same texels.  InLds: a
-// persistent grid accumulating into a per-workgroup LDS copy of the texture
-// (grouped ds_add_f32), flushed once with one global atomic per non-zero
-// texel; otherwise global atomics, issued transposed: the wave's records
+// bilinear taps (tex_backward's weights).  InLds: a persistent grid of
+// kScatThreads-wide workgroups accumulating into a per-workgroup LDS copy of
+// the texture, flushed once with one global atomic per non-zero texel; lane l
+// of a wave takes path 64 c + l of a 4096-path tile (column c): coalesced
+// loads, and one pixel's samples, whose camera vertices share texels, fold in
+// lds_add_grouped (round 5, config 3(b): 3.27 -> see DESIGN.md section 9; the
+// lanes 64 paths apart of round 4 re-read each 128-B line 8 times through a
+// thrashed L2: 2.26 ms of the 3.27 were the loads).  Otherwise lane l takes
+// path 64 l + c, 64 different pixels at 64 spp, and adds by global atomics,
+// issued transposed: the wave's records
 // stage (4 tap bases, 12 values) in LDS and the wave adds items (record,
 // tap, channel) 64 at a time, so an instruction carries the two 24-B runs
 // of ~5 records instead of 64 lanes in 64 rows (the float-atomic shape
@@ -1919,15 +1922,32 @@ struct WfBmpTex {
     uint32_t *fx_max;
     double scale;
 };
+// the InLds accumulator: double (ds_add_f64 runs ~7x the rate of ds_add_f32
+// on gfx950, mh_shading.hpp), or float with MH_SCAT_F64=0
+#ifndef MH_SCAT_F64
+#define MH_SCAT_F64 1
+#endif
+#if MH_SCAT_F64
+using ScatT = double;
+using ScatAcc = LdsDouble;
+#else
+using ScatT = float;
+using ScatAcc = LdsFloat;
+#endif
+constexpr uint32_t kScatAccBytes = sizeof(ScatT);
+#ifndef MH_SCAT_THREADS  // InLds: waves sharing one LDS copy of the texture
+#define MH_SCAT_THREADS (MH_SCAT_F64 ? 1024 : 512)
+#endif
+constexpr uint32_t kScatThreads = MH_SCAT_THREADS;
 template <bool InLds, int Fx = 0>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(InLds ? kScatThreads : 256u)
 k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restrict__ grad, uint32_t n_floats) {
     static_assert(!(InLds && Fx), "the fixed-point passes use the global path");
     float fx_mx = 0.f;
     extern __shared__ uint4 lds[];
-    LdsFloat *acc = (LdsFloat *)reinterpret_cast<float *>(lds);
+    ScatAcc *acc = (ScatAcc *)reinterpret_cast<ScatT *>(lds);
     if (InLds) {
-        for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x) acc[i] = 0.f;
+        for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x) acc[i] = (ScatT)0;
         __syncthreads();
     }
     // a workgroup owns whole 4096-path tiles (its waves take the tile's 64
@@ -1935,34 +1955,65 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
     // re-read by the same CU's next columns from its L1 / L2
     const uint32_t n_tiles = (n + 4095u) / 4096u, waves = blockDim.x >> 6, wave = threadIdx.x >> 6,
                    lane = threadIdx.x & 63u;
-    for (uint32_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-      for (uint32_t col = wave; col < 64u; col += waves) {
-        const uint32_t pid = tile * 4096u + lane * 64u + col;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const DTexture tx0 = S.textures[bt.tex[0]];
+#ifndef MH_SCAT_BAL  // float accumulators, 3 workgroups per CU: 2.44 vs 2.23 ms without; double, 1 per CU: 1.36 vs 1.39
+#define MH_SCAT_BAL MH_SCAT_F64
+#endif
+    // InLds: the waves of the grid take 64-path columns in turn, so every
+    // wave gets the same number of columns (+-1) instead of whole tiles
+    const bool bal = InLds && MH_SCAT_BAL;
+    const uint32_t n_outer = bal ? 1u : n_tiles, outer0 = bal ? 0u : blockIdx.x, outer_step = bal ? 1u : gridDim.x;
+    const uint32_t col0 = bal ? blockIdx.x * waves + wave : wave, col_step = bal ? gridDim.x * waves : waves,
+                   n_cols = bal ? (n + 63u) / 64u : 64u;
+    for (uint32_t tile = outer0; tile < n_outer; tile += outer_step) {
+      for (uint32_t col = col0; col < n_cols; col += col_step) {
+        // InLds: lane l takes path 64 c + l (one pixel's samples: the camera
+        // vertices share texels and lds_add_grouped folds them; coalesced
+        // loads); the global path keeps the transposed lanes described above
+        const uint32_t pid = InLds ? tile * 4096u + col * 64u + lane : tile * 4096u + lane * 64u + col;
         uint32_t mask = 0;
-        float4 f0 = make_float4(0.f, 0.f, 0.f, 0.f), f1 = f0;
+        float4 f0 = z4, f1 = z4;
         if (pid < n) {
             f0 = bm.fin[pid];
             mask = __float_as_uint(f0.w);
             if (mask) f1 = bm.fin[bm.stride + pid];
         }
         const V3 Ltot = v3(f0.x, f0.y, f0.z), dL = v3(f1.x, f1.y, f1.z);
-        while (__ballot(mask != 0)) {
-            const bool on = mask != 0;
-            const uint32_t d = on ? (uint32_t)__ffs(mask) - 1u : 0u;
+        // the next record's loads are issued before this record's adds
+        bool on = mask != 0;
+        float4 r0 = z4, r1 = z4, r2 = z4;
+        if (on) {
+            const uint32_t d = (uint32_t)__ffs(mask) - 1u;
+            r0 = bm.r(d, 0)[pid]; r1 = bm.r(d, 1)[pid]; r2 = bm.r(d, 2)[pid];
+        }
+        while (__ballot(on)) {
             mask &= mask - 1u;
+            const bool on_next = mask != 0;
+            float4 q0 = z4, q1 = z4, q2 = z4;
+            if (on_next) {
+                const uint32_t d = (uint32_t)__ffs(mask) - 1u;
+                q0 = bm.r(d, 0)[pid]; q1 = bm.r(d, 1)[pid]; q2 = bm.r(d, 2)[pid];
+            }
             V3 adj = v3(0, 0, 0);
             float uvx = 0.f, uvy = 0.f;
             uint32_t bi = 0;
             if (on) {
-                const float4 r0 = bm.r(d, 0)[pid], r1 = bm.r(d, 1)[pid], r2 = bm.r(d, 2)[pid];
                 const V3 Lsuf = Ltot - v3(r0.x, r0.y, r0.z);  // prb.py: L - Le - Lr_dir
                 adj = v3(r2.x, r2.y, r2.z) + ((dL * Lsuf) * v3(r1.x, r1.y, r1.z)) * kInvPi;
                 uvx = r0.w;
                 uvy = r1.w;
                 bi = min(__float_as_uint(r2.w), (uint32_t)kMaxBitmapParams - 1u);
             }
-            const DTexture tx = S.textures[bt.tex[bi]];
-            const uint32_t goff = bt.off[bi];
+            // a wave whose records all belong to the first bitmap (the common
+            // case) takes its texture from the hoisted scalar copy instead of
+            // five dependent loads per record
+            DTexture tx = tx0;
+            uint32_t goff = bt.off[0];
+            if (__ballot(bi != 0)) {
+                tx = S.textures[bt.tex[bi]];
+                goff = bt.off[bi];
+            }
             Taps tp;
             bitmap_taps(tx, uvx, uvy, tp);
             float w4[4] = {1.f, 0.f, 0.f, 0.f};
@@ -2005,22 +2056,22 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
                     else atomicAdd(grad + base + c, val);
                 }
                 __builtin_amdgcn_wave_barrier();
-                continue;
-            }
+            } else {
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const bool tap = on && k < tp.n;
-                const uint32_t base = goff + (uint32_t)(tp.idx[k] - tx.data_offset);
-                if (tx.channels == 3) {
-                    const float v[3] = {adj.x * w4[k], adj.y * w4[k], adj.z * w4[k]};
-                    if (InLds) lds_add_grouped<3>(acc, base, tap, v);
-                    else if (tap) { atomicAdd(grad + base, v[0]); atomicAdd(grad + base + 1, v[1]); atomicAdd(grad + base + 2, v[2]); }
-                } else {
-                    const float v[1] = {(adj.x + adj.y + adj.z) * w4[k]};
-                    if (InLds) lds_add_grouped<1>(acc, base, tap, v);
-                    else if (tap) atomicAdd(grad + base, v[0]);
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const bool tap = on && k < tp.n;
+                    const uint32_t base = goff + (uint32_t)(tp.idx[k] - tx.data_offset);
+                    if (tx.channels == 3) {
+                        const float v[3] = {adj.x * w4[k], adj.y * w4[k], adj.z * w4[k]};
+                        lds_add_grouped<3>(acc, base, tap, v);
+                    } else {
+                        const float v[1] = {(adj.x + adj.y + adj.z) * w4[k]};
+                        lds_add_grouped<1>(acc, base, tap, v);
+                    }
                 }
             }
+            on = on_next;
+            r0 = q0; r1 = q1; r2 = q2;
         }
       }
     }
@@ -2030,7 +2081,7 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
         if (blockIdx.x == 0)
 #endif
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x)
-            if (acc[i] != 0.f) atomicAdd(grad + i, acc[i]);
+            if (acc[i] != (ScatT)0) atomicAdd(grad + i, (float)acc[i]);
     }
     if constexpr (Fx == 1) {
 #pragma unroll
@@ -2177,8 +2228,10 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
 #undef MH_BOUNCE_PRB_NR
 #undef MH_BOUNCE_PRB
     if (with_bmp) {
-        const bool in_lds = (size_t)bmp->n_floats * 4 <= bmp->lds_max;
-        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->blocks, (uint32_t)((n + 4095) / 4096)));
+        const size_t acc_bytes = std::max<size_t>((size_t)bmp->n_floats * kScatAccBytes, 1);
+        const bool in_lds = (size_t)bmp->n_floats * 4 <= bmp->lds_max && acc_bytes <= bmp->wg_lds;
+        const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, bmp->cu_lds / acc_bytes));
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->cus * per_cu, (uint32_t)((n + 4095) / 4096)));
         WfBmpTex bt;
         for (int b = 0; b < kMaxBitmapParams; ++b) { bt.tex[b] = bmp->tex[b]; bt.off[b] = bmp->off[b]; }
         bt.acc64 = bmp->fx_acc;
@@ -2207,7 +2260,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
                                dim3(256), 0, st, reinterpret_cast<const long long *>(bmp->fx_acc), bmp->grad,
                                bmp->n_floats, std::ldexp(1.0, ex - 31));
         } else if (in_lds)
-            hipLaunchKernelGGL(k_wf_bitmap_scatter<true>, dim3(blocks), dim3(256), (size_t)bmp->n_floats * 4, st, S,
+            hipLaunchKernelGGL(k_wf_bitmap_scatter<true>, dim3(blocks), dim3(kScatThreads), (size_t)bmp->n_floats * kScatAccBytes, st, S,
                                bt, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
         else
             hipLaunchKernelGGL(k_wf_bitmap_scatter<false>, dim3((uint32_t)((n + 4095) / 4096)), dim3(256), 0, st, S,

@@ -1,14 +1,17 @@
 #!/bin/bash
 # SQ stall/issue counters (separate --pmc passes, kernel-trace only) for one
 # forward bench step.  usage: tools/profile_sq.sh <outdir> [bench args...]
+# SQ_PROG=<script relative to the repo> profiles that script instead (its
+# arguments: the bench args, without bench.py's defaults)
 set -o pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=${1:-gpurun_out/sq}; shift
 mkdir -p "$OUT"
 OUT=$(cd "$OUT" && pwd)
 cd /tmp && export TMPDIR=/tmp
-ARGS="--no-cpu --steps 1 --warmup 0 $*"
-run() { timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT" -- python3 "$ROOT/bench.py" $ARGS >> "$OUT/log.txt" 2>&1; }
+PROG=${SQ_PROG:-bench.py}
+if [ -n "$SQ_PROG" ]; then ARGS="$*"; else ARGS="--no-cpu --steps 1 --warmup 0 $*"; fi
+run() { timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT" -- python3 "$ROOT/$PROG" $ARGS >> "$OUT/log.txt" 2>&1; }
 run --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -o sq_a || exit 1
 run --kernel-trace --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS -o sq_b || exit 1
 run --kernel-trace --pmc SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS -o sq_c || exit 1
