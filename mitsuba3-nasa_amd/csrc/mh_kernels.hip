@@ -370,23 +370,29 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 #endif
 constexpr uint32_t kSplatTile = 4;                    // source pixels per tile side
 constexpr uint32_t kSplatTileFilm = kSplatTile + 4;   // film pixels per tile side (the 5 x 5 footprint)
+// Mode 0: the RGBW film from the stored (L, pos); Mode 1: the W image of the
+// PRB weights, its jitter regenerated from the RNG as k_splat_px<1> does
+// (1 channel; round 5: 25 memory-side atomics per source pixel from 4 lanes
+// of a wave were 0.44 ms of the bench step)
+template <int Mode>
 __global__ void __launch_bounds__(256)
 k_splat_tile(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row_first, uint32_t tiles_x, uint32_t Sn,
              uint32_t n_passes, uint64_t n, uint64_t plane, const float *__restrict__ in, float *__restrict__ film,
-             unsigned long long *__restrict__ invalid, uint64_t in_lim, unsigned long long *__restrict__ viol) {
+             unsigned long long *__restrict__ invalid, uint64_t in_lim, unsigned long long *__restrict__ viol,
+             uint32_t seed_value, uint32_t spp_pp, uint32_t s_begin) {
+    constexpr uint32_t NC = Mode == 0 ? 4u : 1u, kTileN = kSplatTileFilm * kSplatTileFilm * NC;
     // double: ds_add_f64 runs ~7x the rate of ds_add_f32 on gfx950 (LdsDouble)
-    __shared__ double tile[kSplatTileFilm * kSplatTileFilm * 4];
+    __shared__ double tile[kTileN];
     const uint32_t W = S.width, H = S.height;
     const uint32_t tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const uint32_t grp = threadIdx.x / kSplatLanes, g = threadIdx.x % kSplatLanes;
     const uint32_t ti = grp % kSplatTile, tj = grp / kSplatTile;
     const uint32_t px = tx * kSplatTile + ti, py = row_first + ty * kSplatTile + tj;
-    tile[threadIdx.x] = 0.0;
-    if (threadIdx.x < kSplatTileFilm * kSplatTileFilm * 4 - 256) tile[256 + threadIdx.x] = 0.0;
+    for (uint32_t e = threadIdx.x; e < kTileN; e += 256) tile[e] = 0.0;
     const uint32_t pixel = py * W + px;
     bool live = px < W && py < H && pixel >= pixel_begin && pixel - pixel_begin < n_pix;
     const uint32_t pl = pixel - pixel_begin;
-    if (live) {  // the bounds guard of k_splat_px: a row that would read past the planes leaves whole
+    if (Mode == 0 && live) {  // the bounds guard of k_splat_px: a row that would read past the planes leaves whole
         const uint64_t last = (uint64_t)(n_passes - 1) * n + (uint64_t)(pl + 1) * Sn - 1 + 4 * plane;
         if (last >= in_lim) {
             if (g == 0) atomicAdd(viol, 1ull);
@@ -395,33 +401,53 @@ k_splat_tile(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row_first,
     }
     __syncthreads();
     uint32_t n_bad = 0;
-    float acc[5][5][4];
+    float acc[5][5][NC];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
 #pragma unroll
         for (int j = 0; j < 5; ++j)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) acc[i][j][c] = 0.f;
+            for (uint32_t c = 0; c < NC; ++c) acc[i][j][c] = 0.f;
     if (live) {
         for (uint32_t pass = 0; pass < n_passes; ++pass) {
             const float *src = in + (uint64_t)pass * n + (uint64_t)pl * Sn;
             float nv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-            if (g < Sn) {
+            if (Mode == 0 && g < Sn) {
 #pragma unroll
                 for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + g];
             }
             for (uint32_t j = g; j < Sn; j += kSplatLanes) {
                 float vals[4] = {nv[0], nv[1], nv[2], 1.f};
-                const float sx = nv[3], sy = nv[4];
-                n_bad += sample_invalid(vals) ? 1u : 0u;
-                const uint32_t jn = j + kSplatLanes;
-                if (jn < Sn) {
+                float sx = nv[3], sy = nv[4];
+                if (Mode == 0) {
+                    n_bad += sample_invalid(vals) ? 1u : 0u;
+                    const uint32_t jn = j + kSplatLanes;
+                    if (jn < Sn) {
 #pragma unroll
-                    for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + jn];
+                        for (int c = 0; c < 5; ++c) nv[c] = src[c * plane + jn];
+                    }
+                } else {
+                    Pcg rng;
+                    rng.seed(seed_value, pixel * spp_pp + s_begin + j);
+                    sx = (float)px + rng.next_float();
+                    sy = (float)py + rng.next_float();
                 }
                 const int32_t fx = (int32_t)floorf(sx), fy = (int32_t)floorf(sy);
                 if (fx != (int32_t)px || fy != (int32_t)py) {  // jitter rounded onto the next pixel
-                    splat_one_atomic(S, film, sx, sy, vals, 4, 0);
+                    if (Mode == 0) {
+                        splat_one_atomic(S, film, sx, sy, vals, 4, 0);
+                    } else {
+                        const int32_t pix = fx - 2, piy = fy - 2;
+                        const float relx = ((float)pix + 0.5f) - sx, rely = ((float)piy + 0.5f) - sy;
+                        for (int ys = 0; ys < 5; ++ys) {
+                            const float wy = gaussian_eval(S.filter_coeff, rely + (float)ys);
+                            for (int xs = 0; xs < 5; ++xs) {
+                                const float wx = gaussian_eval(S.filter_coeff, relx + (float)xs);
+                                const uint32_t xx = (uint32_t)(pix + xs), yy = (uint32_t)(piy + ys);
+                                if (xx < W && yy < H) atomicAdd(film + (uint64_t)yy * W + xx, 1.f * (wx * wy));
+                            }
+                        }
+                    }
                     continue;
                 }
                 const float relx = ((float)(fx - 2) + 0.5f) - sx, rely = ((float)(fy - 2) + 0.5f) - sy;
@@ -436,37 +462,41 @@ k_splat_tile(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t row_first,
 #pragma unroll
                     for (int xs = 0; xs < 5; ++xs) {
                         const float w = wx[xs] * wy[ys];
+                        if (Mode == 0) {
 #pragma unroll
-                        for (int c = 0; c < 4; ++c) acc[ys][xs][c] += vals[c] * w;
+                            for (int c = 0; c < 4; ++c) acc[ys][xs][c] += vals[c] * w;
+                        } else {
+                            acc[ys][xs][0] += 1.f * w;
+                        }
                     }
             }
         }
     }
-    if (invalid && n_bad) atomicAdd(invalid, (unsigned long long)n_bad);  // rare: no reduction
+    if (Mode == 0 && invalid && n_bad) atomicAdd(invalid, (unsigned long long)n_bad);  // rare: no reduction
 #pragma unroll
     for (int ys = 0; ys < 5; ++ys)
 #pragma unroll
         for (int xs = 0; xs < 5; ++xs)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) acc[ys][xs][c] = row16_sum(acc[ys][xs][c]);
+            for (uint32_t c = 0; c < NC; ++c) acc[ys][xs][c] = row16_sum(acc[ys][xs][c]);
     if (live && g == 0) {
 #pragma unroll
         for (int ys = 0; ys < 5; ++ys)
 #pragma unroll
             for (int xs = 0; xs < 5; ++xs)
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    __hip_atomic_fetch_add((LdsDouble *)&tile[((tj + ys) * kSplatTileFilm + (ti + xs)) * 4 + c],
+                for (uint32_t c = 0; c < NC; ++c)
+                    __hip_atomic_fetch_add((LdsDouble *)&tile[((tj + ys) * kSplatTileFilm + (ti + xs)) * NC + c],
                                            (double)acc[ys][xs][c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
-    // the film block: element e = (row, column, channel) of the tile's 8 x 8 x 4
+    // the film block: element e = (row, column, channel) of the tile's 8 x 8 x NC
     const int32_t ox = (int32_t)(tx * kSplatTile) - 2, oy = (int32_t)(row_first + ty * kSplatTile) - 2;
-    for (uint32_t e = threadIdx.x; e < kSplatTileFilm * kSplatTileFilm * 4; e += 256) {
+    for (uint32_t e = threadIdx.x; e < kTileN; e += 256) {
         const float v = (float)tile[e];
-        const int32_t x = ox + (int32_t)((e >> 2) % kSplatTileFilm), y = oy + (int32_t)((e >> 2) / kSplatTileFilm);
+        const int32_t x = ox + (int32_t)((e / NC) % kSplatTileFilm), y = oy + (int32_t)((e / NC) / kSplatTileFilm);
         if (v != 0.f && x >= 0 && y >= 0 && (uint32_t)x < W && (uint32_t)y < H)
-            atomicAdd(film + ((uint64_t)y * W + (uint32_t)x) * 4 + (e & 3u), v);
+            atomicAdd(film + ((uint64_t)y * W + (uint32_t)x) * NC + (e % NC), v);
     }
 }
 
@@ -981,12 +1011,18 @@ hipError_t launch_splat(const DScene &S, const LaneMap &lm, int mode, bool fast,
         if (mode == kSplatFilm && invalid)  // the sample check of the atomic path, counted by the generic kernel's rule
             hipLaunchKernelGGL(k_count_invalid, dim3(blocks_for(n * n_passes, 256)), dim3(256), 0, st, n * n_passes,
                                n, plane, in, invalid);
-    } else if (fast && mode == kSplatFilm && MH_SPLAT_TILE) {
+    } else if (fast && (mode == kSplatFilm || mode == kSplatWeights) && MH_SPLAT_TILE) {
         const uint32_t r_first = lm.pixel_begin / S.width, r_last = (lm.pixel_begin + n_pix - 1) / S.width;
         const uint32_t tiles_x = (S.width + kSplatTile - 1) / kSplatTile;
         const uint32_t tiles_y = (r_last - r_first + 1 + kSplatTile - 1) / kSplatTile;
-        hipLaunchKernelGGL(k_splat_tile, dim3(tiles_x * tiles_y), dim3(256), 0, st, S, lm.pixel_begin, n_pix, r_first,
-                           tiles_x, lm.S, n_passes, n, plane, in, film, invalid, in_floats, viol);
+        if (mode == kSplatFilm)
+            hipLaunchKernelGGL(k_splat_tile<0>, dim3(tiles_x * tiles_y), dim3(256), 0, st, S, lm.pixel_begin, n_pix,
+                               r_first, tiles_x, lm.S, n_passes, n, plane, in, film, invalid, in_floats, viol,
+                               seed_value, lm.spp_pp, lm.s_begin);
+        else
+            hipLaunchKernelGGL(k_splat_tile<1>, dim3(tiles_x * tiles_y), dim3(256), 0, st, S, lm.pixel_begin, n_pix,
+                               r_first, tiles_x, lm.S, n_passes, n, plane, in, film, invalid, in_floats, viol,
+                               seed_value, lm.spp_pp, lm.s_begin);
     } else if (fast) {
         const uint32_t bs = 128;
         const uint64_t lanes = (uint64_t)n_pix * kSplatLanes;
