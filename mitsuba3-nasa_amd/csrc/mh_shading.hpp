@@ -180,17 +180,30 @@ struct LdsBvh {
     uint32_t scap = 0;
     uint32_t *sglb = nullptr;
     uint32_t sgstride = 0;
+    // the LDS column through an LDS-qualified pointer: with the generic one
+    // the compiler merged the two branches into one flat access, and a flat
+    // pop waits for every outstanding load (vmcnt(0) lgkmcnt(0))
+    MH_DEV __attribute__((address_space(3))) uint32_t *lstack() const {
+        return (__attribute__((address_space(3))) uint32_t *)stack;
+    }
     MH_DEV void push(uint32_t sp, uint32_t v) const {
         if (__builtin_expect(sp >= scap, 0)) {
             sglb[(sp - scap) * sgstride] = v;
             return;
         }
-        stack[sp * stride] = v;
+        lstack()[sp * stride] = v;
     }
+    // the LDS read is unconditional (index clamped) and the overflow read a
+    // wave-uniform branch that waits for it inside, so the common pop waits
+    // for its ds_read only, not for the wave's outstanding node loads
     MH_DEV uint32_t pop(uint32_t sp) const {
-        uint32_t v;
-        if (__builtin_expect(sp >= scap, 0)) v = sglb[(sp - scap) * sgstride];
-        else v = stack[sp * stride];
+        uint32_t v = lstack()[min(sp, scap - 1u) * stride];
+        if (__builtin_expect(__ballot(sp >= scap) != 0, 0)) {
+            uint32_t g = 0;
+            if (sp >= scap) g = sglb[(sp - scap) * sgstride];
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, so the join needs none
+            v = sp >= scap ? g : v;
+        }
         return v;
     }
 };
