@@ -39,7 +39,13 @@ struct Box {
     bool valid() const { return lo[0] <= hi[0]; }
 };
 
-constexpr int kBins = 16;
+// SAH bins: 16 for the small (packet-engine) scenes, kBinsLarge otherwise --
+// 1M / 4M-triangle path 586-592 / 492-500 Msamples/s at 16 bins, 605 / 510 at
+// 64, 608-618 / 518-521 at 128 (round 5, same box; build 1.1 -> 1.55 s for 4M)
+#ifndef MH_BVH_BINS
+#define MH_BVH_BINS 128
+#endif
+constexpr int kBinsLarge = MH_BVH_BINS, kBinsSmall = 16, kBinsMax = kBinsLarge > kBinsSmall ? kBinsLarge : kBinsSmall;
 // leaf limits: the per-lane stream engine packs the count in 3 bits (<= 7)
 constexpr uint32_t kMaxDepth = 48;
 
@@ -74,6 +80,7 @@ struct Builder {
     std::vector<uint32_t> order;  // final prim order
     uint32_t max_depth = 0;
     uint32_t kMaxLeaf = 4;
+    int nb = kBinsSmall;     // SAH bins
     float trav_cost = 1.0f;  // SAH traversal cost relative to one primitive test
     Par par;
     uint32_t task_min = 0;            // defer subtrees smaller than this (0: never)
@@ -111,20 +118,20 @@ struct Builder {
         Box cb;
         for (const Box &x : cparts) cb.grow(x);
         // the three axes' bins in one pass
-        struct Bins { Box box[3][kBins]; uint32_t cnt[3][kBins]; };
+        struct Bins { Box box[3][kBinsMax]; uint32_t cnt[3][kBinsMax]; };
         std::vector<Bins> bparts(T);
         par.chunks(b, e, [&](uint32_t t, uint32_t c0, uint32_t c1) {
             Bins &B = bparts[t];
             memset(B.cnt, 0, sizeof(B.cnt));
             for (int a = 0; a < 3; ++a)
-                for (int k = 0; k < kBins; ++k) B.box[a][k] = Box();
+                for (int k = 0; k < nb; ++k) B.box[a][k] = Box();
             for (uint32_t i = c0; i < c1; ++i) {
                 const BuildPrim &q = p[idx[i]];
                 for (int a = 0; a < 3; ++a) {
                     const float ext = cb.hi[a] - cb.lo[a];
                     if (!(ext > 0.f)) continue;
-                    int k = (int)((0.5f * (q.lo[a] + q.hi[a]) - cb.lo[a]) / ext * kBins);
-                    k = std::min(std::max(k, 0), kBins - 1);
+                    int k = (int)((0.5f * (q.lo[a] + q.hi[a]) - cb.lo[a]) / ext * nb);
+                    k = std::min(std::max(k, 0), nb - 1);
                     B.cnt[a][k]++;
                     B.box[a][k].grow(q.lo, q.hi);
                 }
@@ -135,18 +142,18 @@ struct Builder {
         for (int a = 0; a < 3; ++a) {
             float ext = cb.hi[a] - cb.lo[a];
             if (!(ext > 0.f)) continue;
-            Box bin_box[kBins];
-            uint32_t cnt[kBins] = {0};
+            Box bin_box[kBinsMax];
+            uint32_t cnt[kBinsMax] = {0};
             for (uint32_t t = 0; t < T; ++t)
-                for (int k = 0; k < kBins; ++k) {
+                for (int k = 0; k < nb; ++k) {
                     cnt[k] += bparts[t].cnt[a][k];
                     bin_box[k].grow(bparts[t].box[a][k]);
                 }
-            Box lb[kBins], rb[kBins];
-            uint32_t lc[kBins], rc[kBins];
+            Box lb[kBinsMax], rb[kBinsMax];
+            uint32_t lc[kBinsMax], rc[kBinsMax];
             Box acc;
             uint32_t c = 0;
-            for (int k = 0; k < kBins; ++k) {
+            for (int k = 0; k < nb; ++k) {
                 acc.grow(bin_box[k]);
                 c += cnt[k];
                 lb[k] = acc;
@@ -154,13 +161,13 @@ struct Builder {
             }
             acc = Box();
             c = 0;
-            for (int k = kBins - 1; k >= 0; --k) {
+            for (int k = nb - 1; k >= 0; --k) {
                 acc.grow(bin_box[k]);
                 c += cnt[k];
                 rb[k] = acc;
                 rc[k] = c;
             }
-            for (int k = 0; k < kBins - 1; ++k) {
+            for (int k = 0; k < nb - 1; ++k) {
                 if (lc[k] == 0 || rc[k + 1] == 0) continue;
                 float cost = lb[k].area() * lc[k] + rb[k + 1].area() * rc[k + 1];
                 if (cost < best_cost) {
@@ -182,8 +189,8 @@ struct Builder {
         const float ext = cb.hi[a] - cb.lo[a];
         auto left = [&](uint32_t q) {
             float c = 0.5f * (p[q].lo[a] + p[q].hi[a]);
-            int k = (int)((c - cb.lo[a]) / ext * kBins);
-            k = std::min(std::max(k, 0), kBins - 1);
+            int k = (int)((c - cb.lo[a]) / ext * nb);
+            k = std::min(std::max(k, 0), nb - 1);
             return k <= best_bin;
         };
         uint32_t mid;
@@ -292,6 +299,7 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf,
     Builder bld(in, ids);
     bld.kMaxLeaf = std::max<uint32_t>(2, max_leaf);
     bld.trav_cost = trav_cost;
+    bld.nb = n <= 64 ? kBinsSmall : kBinsLarge;  // the mh_scene_create "small" cut
     const uint32_t T = bvh_threads();
     bld.par.threads = T;
     // subtrees below n / 64 primitives (and at least 4096) go to the workers;
@@ -330,6 +338,7 @@ void build_bvh(const std::vector<BuildPrim> &in, BvhOut &out, uint32_t max_leaf,
                     const Pending &pd = bld.pending[k];
                     Builder *sb = new Builder(in, ids);
                     sb->kMaxLeaf = bld.kMaxLeaf;
+                    sb->nb = bld.nb;
                     sb->trav_cost = bld.trav_cost;
                     sb->child(pd.b, pd.e, pd.depth, sub_lo[k], sub_hi[k]);
                     sub[k] = sb;
