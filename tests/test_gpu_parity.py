@@ -582,6 +582,32 @@ def test_prb_bitmap_wavefront_chunks(channels, max_depth, lds, monkeypatch):
         np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max(), err_msg=k)
 
 
+@pytest.mark.parametrize("tex_res", [73, 74])
+def test_prb_bitmap_lds_accumulator_limit(tex_res, monkeypatch):
+    """The largest bitmap the texel scatter accumulates in LDS: 73^2 x 3 =
+    15,987 floats, a 128-KB double accumulator (one 1,024-thread workgroup
+    per CU; round 5), and the first size past it (74^2 x 3: the transposed
+    global atomics).  Gradients vs the oracle over several 4096-path chunks."""
+    monkeypatch.setenv("MH_WF_CHUNK", "4096")
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box_bitmap(tex_res=tex_res, width=40, height=32, spp=16)
+    scene = mi.load_dict(d)
+    integ = mi.load_dict({"type": "prb", "max_depth": 5})
+    params = mi.traverse(scene)
+    keys = ["white.reflectance.data"]
+    gi = np.random.default_rng(9).random((32, 40, 3)).astype(np.float32) / (32 * 40 * 3)
+    st = A.Stats()
+    g = mi.render_backward(scene, params, torch.from_numpy(gi).cuda(), keys, integ, seed=29, spp=16, stats=st)
+    assert st.mode == 1
+    ref = O.render_backward(scene, integ, 29, 16, gi, [params.texture_of(k) for k in keys],
+                            [tuple(params[k].shape) for k in keys])
+    a, b = g[0].cpu().numpy(), ref[0]
+    assert a.shape == b.shape == (tex_res, tex_res, 3) and np.abs(b).max() > 0
+    np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-9 + 2e-4 * np.abs(b).max())
+
+
 @pytest.mark.parametrize("lds", ["1", "0"])
 @pytest.mark.parametrize("red_channels", [3, 1])
 def test_prb_two_bitmaps_wavefront(red_channels, lds, monkeypatch):
