@@ -361,7 +361,7 @@ def main():
         #                    written alike; the first bounce reads the sample's
         #                    grad / W texel (16 B)
         # with R = rays (sum of queue lengths), N = samples: survivors R - N.
-        # traffic / VALU issue from the PMC passes of profiles/r4_pmc.json (r3 / r2 before)
+        # traffic / VALU issue from the PMC passes of the latest profiles/rN_pmc.json
         # (tools/profile_r2.sh: FETCH/WRITE corrected by the calib_fetch factors
         # for the kernel's access width; VALU issue = SQ_INSTS_VALU x 2 cycles /
         # (1024 SIMDs x launch time x measured clock)).
