@@ -762,7 +762,27 @@ MH_DEV F2 pp(const Prim *Q, uint32_t i, uint32_t k) {
 #ifndef MH_RECT_EARLY
 #define MH_RECT_EARLY 1  // wave-level early exit of a rectangle pair after the plane distance
 #endif
-template <bool Shadow>
+// A division-free early exit ahead of the plane distance's two correctly
+// rounded divisions: with lz the ray origin's local z and s1 = lz + ldz *
+// bound its end's, a lane whose lz and s1 have the same sign, both beyond
+// m = 2^-20 (|lz| + |ldz| bound), has no hit: t = -lz / ldz is negative, or
+// exceeds bound by more than the division's rounding, so the exact test below
+// would reject it as well (the bound is m > 2^-23 (|lz| + |ldz| bound), which
+// also covers the rounding of s1).  NaN / inf operands fail the comparisons
+// and take the exact test.  Shadow rays inside a closed room never reach the
+// walls' planes, so their rectangle tests stop here (round 5).
+#ifndef MH_RECT_PRETEST
+#define MH_RECT_PRETEST 1
+#endif
+MH_DEV bool rect_separated(float lz, float ldz, float bound) {
+    const float s1 = __builtin_fmaf(ldz, bound, lz);
+    // (+ 1e-30: |lz| above it keeps -lz / ldz clear of underflow to -0,
+    // which would pass the exact test's t >= 0).  Shadow rays only: a closest
+// ray's bound is its best hit so far, infinite until it has one.
+    const float m = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ldz), bound, __builtin_fabsf(lz)), 0x1p-20f, 1e-30f);
+    return ((lz > m) & (s1 > m)) | ((lz < -m) & (s1 < -m));
+}
+template <bool Shadow, bool Pre = true>
 MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(0);
     MH_CNTL(0, live);
@@ -772,8 +792,11 @@ MH_DEV void rect_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit
     const F2 c0 = pp(Q, pos, 8), c1 = pp(Q, pos, 9), c2 = pp(Q, pos, 10);
     const F2 lz = fma2(c2, oz, fma2(c1, oy, fma2(c0, ox, pp(Q, pos, 11))));
     const F2 ldz = fma2(c2, dz, fma2(c1, dy, c0 * dx));
-    const F2 tt = pair(-lz.x / ldz.x, -lz.y / ldz.y);
     const float bound = Shadow ? r.maxt : h.t;
+    if (Shadow && Pre && MH_RECT_PRETEST &&
+        !wave_any(live & !(rect_separated(lz.x, ldz.x, bound) & rect_separated(lz.y, ldz.y, bound))))
+        return;
+    const F2 tt = pair(-lz.x / ldz.x, -lz.y / ldz.y);
     bool okA = live & (tt.x >= 0.f) & (tt.x <= bound), okB = live & (tt.y >= 0.f) & (tt.y <= bound);
     if (MH_RECT_EARLY && !wave_any(okA | okB)) return;
     MH_CNT(1);
@@ -827,11 +850,12 @@ MH_DEV void tri_pair(const Prim *Q, uint32_t pos, bool live, const RayT r, PHit 
     packet_take<Shadow>(okB, tt.y, u.y, v.y, __float_as_uint(key.y), h);
 }
 
-template <bool Shadow>
+template <bool Shadow, bool Pre = true>
 MH_DEV void rect_one(const Prim *P, uint32_t pos, bool live, const RayT r, PHit &h) {
     MH_CNT(4);
     const float oz = __builtin_fmaf(pf(P, pos, 10), r.o.z, __builtin_fmaf(pf(P, pos, 9), r.o.y, __builtin_fmaf(pf(P, pos, 8), r.o.x, pf(P, pos, 11))));
     const float dz = __builtin_fmaf(pf(P, pos, 10), r.d.z, __builtin_fmaf(pf(P, pos, 9), r.d.y, pf(P, pos, 8) * r.d.x));
+    if (Shadow && Pre && MH_RECT_PRETEST && !wave_any(live & !rect_separated(oz, dz, r.maxt))) return;
     const float tt = -oz / dz;
     bool ok = live & (tt >= 0.f) & (tt <= (Shadow ? r.maxt : h.t));
     if (!wave_any(ok)) return;
@@ -1056,7 +1080,9 @@ MH_DEV void run_deferred(const Defer &df, const RayT r, bool act, PHit &h) {
 // One batch: the wave's 64 rays (act: lanes that hold a ray).  ws: the
 // wave-uniform stack (entry k at ws[k * stride]).  Def: sparse triangle runs
 // are deferred and compacted (dfr: LDS pair records + the wave's scratch).
-template <bool Shadow, bool Def = false>
+// Pre: the rectangle tests' division-free early exit (rect_separated; the
+// non-generating PRB bounce leaves it out: 2 more VGPRs spill there)
+template <bool Shadow, bool Def = false, bool Pre = true>
 MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpairs, const uint2 *key_sp, uint32_t *ws, uint32_t stride,
                         const RayT r, bool act, const float *dfr_recs = nullptr, uint8_t *dfr_scratch = nullptr) {
     const V3 inv = safe_inv_dir(r.d), ood = r.o * inv;
@@ -1079,9 +1105,9 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpai
 #ifdef MH_EXP_SHADOW_NORECT  // timing experiment: shadow queries skip the rectangles (not exact in general)
         if (Shadow) i = nrect;
 #endif
-        for (; i + 1u < nrect; i += 2u) rect_pair<Shadow>(gpairs, c + i, hit & (!Shadow || !ph.occl), r, ph);
+        for (; i + 1u < nrect; i += 2u) rect_pair<Shadow, Pre>(gpairs, c + i, hit & (!Shadow || !ph.occl), r, ph);
         if (i < nrect) {
-            rect_one<Shadow>(gprims, c + i, hit & (!Shadow || !ph.occl), r, ph);
+            rect_one<Shadow, Pre>(gprims, c + i, hit & (!Shadow || !ph.occl), r, ph);
             ++i;
         }
         if (i < cnt) packet_tris<Shadow, Def>(gprims, gpairs, c + i, cnt - i, hit & (!Shadow || !ph.occl), r, ph, df);

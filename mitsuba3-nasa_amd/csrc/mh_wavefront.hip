@@ -1616,7 +1616,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         sh.shape = MH_INVALID;
 #else
         MH_BPH(3);
-        const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
+        const Hit sh = packet_batch<true, true, Gen>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
         MH_BPH(4);
 #endif
         const bool unocc = shadow && sh.shape == MH_INVALID;
