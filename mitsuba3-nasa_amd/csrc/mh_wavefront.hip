@@ -1897,9 +1897,10 @@ hipError_t launch_wavefront_fwd(const DScene &S, const IntegratorParams &in, con
 // the texture, flushed once with one global atomic per non-zero texel; lane l
 // of a wave takes path 64 c + l of a 4096-path tile (column c): coalesced
 // loads, and one pixel's samples, whose camera vertices share texels, fold in
-// lds_add_grouped (round 5, config 3(b): 3.27 -> see DESIGN.md section 9; the
-// lanes 64 paths apart of round 4 re-read each 128-B line 8 times through a
-// thrashed L2: 2.26 ms of the 3.27 were the loads).  Otherwise lane l takes
+// lds_add_grouped (round 5, config 3(b): 3.27 -> 1.37 ms per scatter with the
+// double accumulator below; the lanes 64 paths apart of
+// round 4 re-read each 128-B line 8 times through a thrashed L2: 2.26 ms of
+// the 3.27 were the loads).  Otherwise lane l takes
 // path 64 l + c, 64 different pixels at 64 spp, and adds by global atomics,
 // issued transposed: the wave's records
 // stage (4 tap bases, 12 values) in LDS and the wave adds items (record,
@@ -1950,9 +1951,9 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x) acc[i] = (ScatT)0;
         __syncthreads();
     }
-    // a workgroup owns whole 4096-path tiles (its waves take the tile's 64
-    // columns in turn), so the 64 lines a wave's transposed load touches are
-    // re-read by the same CU's next columns from its L1 / L2
+    // the global path: a workgroup owns whole 4096-path tiles (its waves take
+    // the tile's 64 columns in turn), so the 64 lines a wave's transposed load
+    // touches are re-read by the same CU's next columns from its L1 / L2
     const uint32_t n_tiles = (n + 4095u) / 4096u, waves = blockDim.x >> 6, wave = threadIdx.x >> 6,
                    lane = threadIdx.x & 63u;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
