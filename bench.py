@@ -26,6 +26,14 @@ gradient one AD wavefront of 2^32 samples), max_depth 8, same JSON line.
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5]
        torchrun --nproc-per-node N bench.py --gpus N ...   (the driver)
        torchrun --nproc-per-node 8 bench.py --gpus 8 --config 5
+
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment is
+a launcher: before any GPU call it starts `python -m torch.distributed.run
+--nproc-per-node N ... bench.py <the same arguments>` as a child process
+(rendezvous on 127.0.0.1), lets the ranks' output through (rank 0 prints the
+line) and exits with the child's code.  Under a launcher every rank checks
+that the process group's size equals --gpus; the line's `n_gpus` is the
+process group's size.
 """
 import argparse
 import ctypes as C
@@ -41,9 +49,11 @@ sys.path[:0] = [os.path.join(ROOT, "mitsuba3-nasa_amd"), os.path.join(ROOT, "tes
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU; default: WORLD_SIZE, else 1). N > 1 without WORLD_SIZE launches "
+                        "N ranks through torch.distributed.run")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--res", type=int, default=512)
@@ -66,7 +76,38 @@ def parse():
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' to rehearse "
                         "several ranks on one GPU)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(argv, gpus, env=None):
+    """The child command that runs `gpus` ranks of this script (one process
+    per GPU, torch.distributed.run on 127.0.0.1), or None when this process
+    is itself a rank (WORLD_SIZE set) or a single-GPU run.  Makes no GPU call."""
+    env = os.environ if env is None else env
+    if gpus is None or gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    port = env.get("MASTER_PORT") or str(_free_port())
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def world_from(args, env=None):
+    """(world, rank, local rank) of this process; a rank under a launcher
+    must agree with --gpus."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE is {world}")
+    return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
 
 
 def cpu_info():
@@ -263,9 +304,11 @@ def cpu_single_op(args, scene, integ, res, spp):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cmd = launch_command(sys.argv[1:], args.gpus)
+    if cmd is not None:  # the launcher: no GPU call in this process, the ranks are its child
+        import subprocess
+        raise SystemExit(subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")))
+    world, rank, local = world_from(args)
     import torch
     import torch.distributed as dist
     dist_on = world > 1
@@ -279,6 +322,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(args.backend)
+        world = dist.get_world_size()  # n_gpus comes from the process group, not from a flag
+        if args.gpus is not None and world != args.gpus:
+            raise SystemExit(f"bench.py: process group has {world} ranks, --gpus {args.gpus}")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
