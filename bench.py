@@ -180,6 +180,70 @@ def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
             "cpu_model": model, "nproc": nproc, "affinity": aff, "threads": threads}
 
 
+def _roof(kname, achieved_bytes, us, **extra):
+    """A roofline object: algorithmic bytes of one launch over its average
+    duration (HIP events over the timed region), against the HBM peak."""
+    gbs = achieved_bytes / (us / 1e6) / 1e9 if us > 0 else 0.0
+    r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname, "kernel_avg_us": round(us, 1),
+         "algorithmic_bytes_per_launch": round(achieved_bytes)}
+    r.update(extra)
+    return r
+
+
+def splat_roof(st, n_px):
+    """k_splat_tile of mh_render: 20 B per sample read (L 12 + position 8) and
+    the RGBW film (16 B per pixel) written once per launch."""
+    launches = max(1, st.n_aux_launches)
+    us = st.ms_aux / launches * 1e3
+    b = (20.0 * st.aux_items + 16.0 * n_px * launches) / launches
+    return _roof("k_splat_tile", b, us, launches_per_step=int(st.n_aux_launches), samples=int(st.aux_items),
+                 bytes_formula="(20 samples + 16 pixels launches) / launches",
+                 note="RGBW film L2/MALL-resident; the W image (PRB) rides in the same kernel family")
+
+
+def bitmap_rooflines(st, n_samples, n_floats):
+    """Config 3(b): the PRB bounce family with a bitmap parameter, and the
+    texel scatter (k_wf_bitmap_scatter).  Bounce: per survivor the 100-B path
+    state (pd 4, ray 28, beta 12, prev_p 12, prev_pdf 4, PCG32 state 8, TEA
+    word 4, dL 12, running L 12, record mask 4) read and written; per sample
+    the first bounce's grad/W texel (16 B) and the end record (L_total + mask,
+    dL: 32 B); per bitmap vertex a 48-B record.  Scatter: per sample the end
+    record (32 B, an upper bound: dL is read only for paths with records), per
+    vertex record 48 B, and the texel gradients (4 B per float) once."""
+    launches = max(1, st.n_trace_launches)
+    R, N, V = float(st.rays_closest), float(n_samples), float(st.aux_items)
+    b = (2.0 * 100 * (R - N) + (16.0 + 32.0) * N + 48.0 * V) / launches
+    bounce = _roof("k_wf_bounce_prb", b, st.ms_trace / launches * 1e3, launches_per_step=int(st.n_trace_launches),
+                   rays_closest=int(R), samples=int(N), bitmap_records=int(V), state_bytes=100, first_bytes=16,
+                   end_bytes=32, record_bytes=48,
+                   bytes_formula="(2 state (R - N) + (first + end) N + record V) / launches",
+                   note="includes the Bm instance's vertex-record writes; ms from the bounce span (scatter excluded)")
+    sl = max(1, st.n_aux_launches)
+    sb = (32.0 * N + 48.0 * V) / sl + 4.0 * n_floats
+    scat = _roof("k_wf_bitmap_scatter", sb, st.ms_aux / sl * 1e3, launches_per_step=int(st.n_aux_launches),
+                 samples=int(N), bitmap_records=int(V), texel_floats=int(n_floats),
+                 bytes_formula="(32 N + 48 V) / launches + 4 texel_floats",
+                 note="accumulates in LDS (double); one global add per non-zero texel per workgroup")
+    return bounce, scat
+
+
+def volsched_roofline(st, n_samples, alpha=False):
+    """Config 4: k_vol_sched.  Per device-counted density-grid lookup its 8
+    float taps (32 B: GridVolume::eval's trilinear stencil), per sample the R G
+    B (+ A) W record written (20 B; 24 with alpha).  The medium (64 MiB) is
+    L2/MALL-resident in part, so counter traffic exceeds this figure: see
+    profiles/ for the PMC passes."""
+    launches = max(1, st.n_trace_launches)
+    rec = 24.0 if alpha else 20.0
+    b = (32.0 * st.grid_lookups + rec * n_samples) / launches
+    return _roof("k_vol_sched<VolMachine>", b, st.ms_trace / launches * 1e3, launches_per_step=int(st.n_trace_launches),
+                 grid_lookups=int(st.grid_lookups), lookups_per_sample=round(st.grid_lookups / max(1, n_samples), 3),
+                 samples=int(n_samples), lookup_bytes=32, sample_bytes=int(rec),
+                 bytes_formula="(32 lookups + 20 samples) / launches",
+                 limiter="VALU issue and divergence of the phase machine (DESIGN.md section 3), not HBM")
+
+
 def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     """The bench's hot-path wiring (also driven by tests/test_gpu_multirank.py):
     cornell_box res^2, `path` forward + `prb` backward wrt white's rgb
@@ -431,7 +495,18 @@ def main():
             except Exception:
                 pmc = {}
 
+        # the PMC passes profiled the default workload (config 2: 512^2 @ 256 spp
+        # per rank, max_depth 8); a launch of another workload (config 5's
+        # chunks, another res / spp / depth) does different work per launch, so
+        # its counters are not this launch's: omitted, with a note
+        pmc_applies = (args.config == 2 and args.res == 512 and args.spp == 256 and args.max_depth == 8)
+        pmc_note = (None if pmc_applies else
+                    "traffic / valu_issue_frac omitted: the committed PMC passes profiled config 2's launches "
+                    "(512^2 @ 256 spp, max_depth 8), not this workload's")
+
         def family(kname):
+            if not pmc_applies:
+                return None, None, None
             fam = [v for k, v in pmc.items() if k.startswith(kname + "<") and
                    not (kname == "k_wf_bounce" and k.startswith("k_wf_bounce_prb"))]
             calls = sum(v["calls"] for v in fam)
@@ -455,6 +530,8 @@ def main():
                  # bytes = (2 S (R - N) + b_end N + b_first N) / launches
                  "launches_per_step": launches, "rays_closest": int(R), "samples": int(N),
                  "state_bytes": state_b, "end_bytes": per_death, "first_bytes": per_sample}
+            if pmc_note:
+                r["traffic_note"] = pmc_note
             if valu and clk:
                 r["valu_issue_frac"] = round(valu * 2.0 / (1024 * us * 1e-6 * clk * 1e9), 4)
                 r["valu_insts_per_launch"] = round(valu)
@@ -471,6 +548,10 @@ def main():
         roofs.sort(key=lambda x: -x[0])
         roofline = roofs[0][1] if roofs else None
         roofline_other = roofs[1][1] if len(roofs) > 1 else None
+        # the forward's film splat (k_splat_tile): per sample its L (12 B) and
+        # film position (8 B) read, per launch the RGBW film (16 B per pixel)
+        # added once; timed by HIP events after the bounce span of each chunk
+        roofline_splat = splat_roof(st_f, H * W) if st_f.n_aux_launches else None
         cpu = None
         if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N = 1 only
             cscene = scene
@@ -511,7 +592,8 @@ def main():
                                             if not args.fwd_only else None),
             "rays_shadow_per_sample_prb": (round(st_b.rays_shadow / max(1, n_local), 4)
                                            if not args.fwd_only else None),
-            "roofline": roofline, "roofline_other": roofline_other, "cpu_baseline": cpu,
+            "roofline": roofline, "roofline_other": roofline_other, "roofline_splat": roofline_splat,
+            "cpu_baseline": cpu,
         }
         if multi is not None:
             line["multi_gpu"] = multi
@@ -544,6 +626,20 @@ def main_single_op(args, rank, world, dev, dist_on):
     ms_step = elapsed / args.steps * 1e3
     value = world * res * res * spp / (ms_step / 1e3) / 1e6
     if rank == 0:
+        n_local = res * res * spp
+        roof = roof_other = None
+        if args.config == 3 and st.n_aux_launches:
+            roof, roof_other = bitmap_rooflines(st, n_local, 64 * 64 * 3)  # config 3(b): a 64^2 x 3 bitmap
+        elif args.config == 4 and st.mode == 3 and st.n_trace_launches:
+            roof = volsched_roofline(st, n_local)
+        elif args.config == 1 and st.mode == 2:
+            launches = max(1, st.n_trace_launches)
+            R, N = float(st.rays_closest), float(n_local)
+            roof = _roof("k_wf_bounce", (2.0 * 84 * (R - N) + 20.0 * N) / launches, st.ms_trace / launches * 1e3,
+                         launches_per_step=int(st.n_trace_launches), rays_closest=int(R), samples=int(N),
+                         state_bytes=84, end_bytes=12, first_bytes=8,
+                         bytes_formula="(2 state (R - N) + (end + first) N) / launches")
+            roof_other = splat_roof(st, res * res)
         cpu = None if (args.no_cpu or world > 1) else cpu_single_op(args, scene, integ, res, spp)
         names = {1: "path fwd", 3: "PRB grad (bitmap albedo)", 4: "volpath fwd"}
         line = {
@@ -556,7 +652,7 @@ def main_single_op(args, rank, world, dev, dist_on):
             "kernel_ms": round(sum(kms) / len(kms), 3),
             "rays_closest_per_sample": round(st.rays_closest / max(1, res * res * spp), 4),
             "rays_shadow_per_sample": round(st.rays_shadow / max(1, res * res * spp), 4),
-            "roofline": None, "roofline_note": "rooflines of these kernels: DESIGN.md §3 and profiles/",
+            "roofline": roof, "roofline_other": roof_other,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MH_ABI_VERSION 1u
+#define MH_ABI_VERSION 2u  /* 2: mh_stats gained grid_lookups, aux_items, ms_aux, n_aux_launches */
 #define MH_INVALID 0xffffffffu
 
 /* ----------------------------------------------------------------------- */
@@ -250,12 +250,20 @@ typedef struct mh_stats {
     uint64_t bounces;           /* active lane-bounces */
     double   ms_total;          /* wall time of the call (host clock, ms) */
     double   ms_kernel;         /* device time of the dominant kernel (hipEvents, ms) */
-    double   ms_trace;          /* wavefront: device time of all k_wf_trace (mode 1) / k_wf_bounce (mode 2) launches (ms) */
+    double   ms_trace;          /* wavefront: device time of all k_wf_trace (mode 1) / k_wf_bounce (mode 2) launches (ms);
+                                   volpath on the phase scheduler (mode 3): its k_vol_sched launches */
     uint64_t n_trace_launches;  /* wavefront: number of those launches */
     uint32_t mode;              /* 0 megakernel, 1 wavefront (trace/shade/shadow), 2 wavefront fused bounce kernel,
                                    3 volpath wavefront (main / walk rounds) */
     uint32_t invalid_samples;   /* samples with a non-finite or negative (< -1e-5) radiance channel: the
                                    test of ImageBlock::put's warn_invalid / warn_negative (imageblock.cpp:180-204) */
+    uint64_t grid_lookups;      /* volpath on the phase scheduler: trilinear density-grid lookups (8 taps each,
+                                   GridVolume::eval, grid.cpp:321-384); 0 elsewhere */
+    uint64_t aux_items;         /* items of the secondary kernel: bitmap vertex records the texel scatter read
+                                   (prb with a bitmap parameter), film samples the splat read (mh_render) */
+    double   ms_aux;            /* device time (hipEvents) of the secondary kernel's launches: the bitmap texel
+                                   scatter (mh_render_backward) or the film splat (mh_render, wavefront modes) */
+    uint64_t n_aux_launches;    /* number of those launches (one per chunk) */
 } mh_stats;
 
 typedef struct mh_scene mh_scene;   /* opaque; owns all device buffers */

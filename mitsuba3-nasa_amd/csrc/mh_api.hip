@@ -714,6 +714,10 @@ constexpr int kCtrPvpHead = 30;
 // [kCtrBounds]: rows of the splat kernels that would have read past their
 // input planes (skipped; the call then fails; none in a correct build)
 constexpr int kCtrBounds = 29;
+// [kCtrLookups]: k_vol_sched's density-grid lookups (mh_stats.grid_lookups)
+constexpr int kCtrLookups = 27;
+// [kCtrAuxItems]: bitmap vertex records read by the texel scatter (mh_stats.aux_items)
+constexpr int kCtrAuxItems = 26;
 
 // launch_splat with its bounds contract: hipErrorInvalidValue from the host
 // check becomes a named error instead of a bare HIP code
@@ -831,14 +835,18 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render: spp must be > 0");
     if (int rc = check_reduce_flags(s, flags, "mh_render", true)) return rc;
     double t_start = now_ms();
+    if (stats) *stats = mh_stats{};
     Layout L;
     const bool ad = in->type == MH_INTEGRATOR_PRB || in->type == MH_INTEGRATOR_PRBVOLPATH;
     int rc = make_layout(s, spp, spp_begin, spp_end, L, ad);
     if (rc) return rc;
     MH_HIP(hipSetDevice(s->device));
     g_call_issued = true;  // past argument validation: a failure from here aborts the communicator
-    // test hook (tests/test_gpu_comm.py): a failure after the call was issued
-    if (getenv("MH_TEST_FAIL_AFTER_ISSUE")) return set_error(MH_ERR_HIP, "MH_TEST_FAIL_AFTER_ISSUE: injected failure");
+    // test hook of the communicator's failure semantics (tests/test_gpu_comm.py,
+    // documented in INTEGRATION.md): a reducing call (MH_FLAG_REDUCE) fails
+    // after it was issued.  Calls without a collective never read it.
+    if ((flags & MH_FLAG_REDUCE) && getenv("MH_TEST_FAIL_AFTER_ISSUE"))
+        return set_error(MH_ERR_HIP, "MH_TEST_FAIL_AFTER_ISSUE: injected failure");
     hipStream_t st = s->stream;
     const uint64_t n_px = (uint64_t)L.W * L.H;
     // film storage: RGBW, or R G B A W for alpha films; the kernels splat into
@@ -897,7 +905,7 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     float kernel_ms = 0.f, trace_ms = 0.f;
     const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
     const uint32_t n_bounces = wavefront ? in->max_depth : 0;
-    const size_t ev_per_chunk = 2 + 2 * n_bounces;
+    const size_t ev_per_chunk = 3 + 2 * n_bounces;  // integrator span, bounce spans, splat end
     while (s->evpool.size() < ev_per_chunk * n_chunks) {
         hipEvent_t e;
         MH_HIP(hipEventCreate(&e));
@@ -949,6 +957,7 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         if (alpha)
             MH_SPLAT(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane, s->work.as<float>(), film_a,
                      seed_value, coalesce, st, nullptr, determ, s->work.bytes / 4, n_px, bounds);
+        MH_HIP(hipEventRecord(ev[ev_per_chunk - 1], st));
     }
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     if (int rc = reduce_result(s, flags, film, film_bytes / 4, st, true)) return rc;
@@ -961,7 +970,7 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_WAIT(s, flags, st);
         return check_bounds_counter(s, "mh_render");
     }
-    unsigned long long ctr[2] = {0, 0}, n_invalid = 0;
+    unsigned long long ctr[2] = {0, 0}, n_invalid = 0, n_lookups = 0;
     std::vector<uint32_t> wctr;
     if (wavefront) {
         wctr.resize(ctr_per_chunk * n_chunks);
@@ -972,16 +981,22 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
     unsigned long long iv[2] = {0, 0};  // [kCtrInvalid], [kCtrBounds]
     static_assert(kCtrBounds == kCtrInvalid + 1, "one read-back of both words");
     MH_HIP(hipMemcpyAsync(iv, invalid, sizeof(iv), hipMemcpyDeviceToHost, st));
+    if (volwave && vol_sched_mode())
+        MH_HIP(hipMemcpyAsync(&n_lookups, s->counters.as<unsigned long long>() + kCtrLookups, 8,
+                              hipMemcpyDeviceToHost, st));
     MH_WAIT(s, flags, st);  // the stats counters are read back
     n_invalid = iv[0];
     if (iv[1])
         return set_error(MH_ERR_HIP, "mh_render: " + std::to_string(iv[1]) +
                                          " splat rows would have read past the sample planes (skipped)");
+    float splat_ms = 0.f;
     for (size_t c = 0; c < n_chunks; ++c) {
         hipEvent_t *ev = &s->evpool[ev_per_chunk * c];
         float ms = 0.f;
         MH_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
         kernel_ms += ms;
+        MH_HIP(hipEventElapsedTime(&ms, ev[1], ev[ev_per_chunk - 1]));
+        splat_ms += ms;
         // the fused bounce kernels are timed as one span (launch_wavefront_pass)
         const uint32_t pairs = wavefront ? (wf_fused(s->S) || L.n_passes > 1 ? 1u : n_bounces) : 0u;
         for (uint32_t b = 0; b < pairs; ++b) {
@@ -1027,10 +1042,16 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         stats->bounces = ctr[0];
         stats->ms_total = now_ms() - t_start;
         stats->ms_kernel = kernel_ms;
-        stats->ms_trace = trace_ms;
-        stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces * L.n_passes : 0;
+        // volpath on the phase scheduler: its k_vol_sched launches (one per chunk)
+        const bool sched = volwave && vol_sched_mode();
+        stats->ms_trace = sched ? kernel_ms : trace_ms;
+        stats->n_trace_launches = wavefront ? (uint64_t)n_chunks * n_bounces * L.n_passes : sched ? n_chunks : 0;
         stats->mode = wavefront ? (wf_fused(s->S) ? 2u : 1u) : volwave ? 3u : 0u;
         stats->invalid_samples = (uint32_t)std::min<unsigned long long>(n_invalid, 0xffffffffull);
+        stats->grid_lookups = n_lookups;
+        stats->aux_items = n_px * per_pixel;
+        stats->ms_aux = splat_ms;
+        stats->n_aux_launches = n_chunks;
     }
     return MH_OK;
 }
@@ -1317,6 +1338,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_backward: spp must be > 0");
     if (int rc = check_reduce_flags(s, flags, "mh_render_backward", false)) return rc;
     double t_start = now_ms();
+    if (stats) *stats = mh_stats{};
     Layout L;
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);
     if (rc) return rc;
@@ -1533,6 +1555,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
                 bmp.fx_word = s->bmp_fx.as<uint32_t>();
                 bmp.fx_acc = reinterpret_cast<unsigned long long *>(s->bmp_fx.as<uint8_t>() + 256);
             }
+            bmp.n_rec = s->counters.as<unsigned long long>() + kCtrAuxItems;
             bmp.wg_lds = (uint32_t)max_wg;
             bmp.cu_lds = (uint32_t)per_cu_lds;
             bmp.cus = (uint32_t)cus;
@@ -1544,7 +1567,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
         MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));
         MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, (size_t)grid * kMaxRgbParams * 3 * 4, st));
-        while (s->evpool.size() < 2 * n_chunks) {
+        while (s->evpool.size() < 3 * n_chunks) {
             hipEvent_t e;
             MH_HIP(hipEventCreate(&e));
             s->evpool.push_back(e);
@@ -1556,7 +1579,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
                                         (uint64_t)npx * S_, L.spp_pp >= 4, g_in, w, ga.slot_of_tex, n_rgb,
                                         s->wf_ws.ptr, s->wf_ws_prb.ptr, cap,
                                         s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
-                                        s->wf_partial.as<float>(), st, &s->evpool[2 * chunk],
+                                        s->wf_partial.as<float>(), st, &s->evpool[3 * chunk],
                                         bmp_wf ? &bmp : nullptr, det_grad ? s->wf_ws_det.ptr : nullptr));
         }
         MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
@@ -1704,11 +1727,12 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         MH_WAIT(s, flags, st);
         return check_lost();
     }
-    unsigned long long ctr[2] = {0, 0};
+    unsigned long long ctr[2] = {0, 0}, n_rec = 0;
     std::vector<uint32_t> wctr(wf_ctr_words * wf_chunks);
-    if (wavefront)
+    if (wavefront) {
         MH_HIP(hipMemcpyAsync(wctr.data(), s->wf_ctr.ptr, wctr.size() * 4, hipMemcpyDeviceToHost, st));
-    else
+        MH_HIP(hipMemcpyAsync(&n_rec, s->counters.as<unsigned long long>() + kCtrAuxItems, 8, hipMemcpyDeviceToHost, st));
+    } else
         MH_HIP(hipMemcpyAsync(ctr, s->counters.ptr, sizeof(ctr), hipMemcpyDeviceToHost, st));
     MH_WAIT(s, flags, st);
     if (int rc_lost = check_lost()) return rc_lost;
@@ -1722,12 +1746,19 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
                 }
     }
     if (stats) {
-        float ms = 0.f, trace_ms = 0.f;
+        float ms = 0.f, trace_ms = 0.f, scat_ms = 0.f;
         MH_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         for (size_t c = 0; wavefront && c < wf_chunks; ++c) {
             float t = 0.f;
-            MH_HIP(hipEventElapsedTime(&t, s->evpool[2 * c], s->evpool[2 * c + 1]));
+            MH_HIP(hipEventElapsedTime(&t, s->evpool[3 * c], s->evpool[3 * c + 1]));
             trace_ms += t;
+            MH_HIP(hipEventElapsedTime(&t, s->evpool[3 * c + 1], s->evpool[3 * c + 2]));
+            scat_ms += t;
+        }
+        if (bmp_wf) {  // the texel scatter: one launch per chunk
+            stats->aux_items = n_rec;
+            stats->ms_aux = scat_ms;
+            stats->n_aux_launches = wf_chunks;
         }
         // the bounce-kernel span (fused: k_wf_bounce_prb launches only)
         stats->ms_trace = trace_ms;
@@ -1759,6 +1790,7 @@ static int render_forward_impl(mh_scene *s, const mh_integrator *in, uint32_t se
     if (spp == 0) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_render_forward: spp must be > 0");
     if (int rc = check_reduce_flags(s, flags, "mh_render_forward", true)) return rc;
     const double t_start = now_ms();
+    if (stats) *stats = mh_stats{};
     Layout L;
     int rc = make_layout(s, spp, spp_begin, spp_end, L, true);  // prepare(): one wavefront of <= 2^32
     if (rc) return rc;
@@ -1882,6 +1914,7 @@ static int trace_impl(mh_scene *s, bool shadow, uint64_t n, const float *rays, f
     if (!s || (n && !rays)) return set_error(MH_ERR_INVALID_ARGUMENT, "mh_trace: NULL argument");
     if (n == 0) return MH_OK;
     double t_start = now_ms();
+    if (stats) *stats = mh_stats{};
     MH_HIP(hipSetDevice(s->device));
     hipStream_t st = s->stream;
     const bool dev = flags & MH_FLAG_DEVICE_POINTERS;

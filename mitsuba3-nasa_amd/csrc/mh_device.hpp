@@ -41,11 +41,6 @@ static __device__ unsigned long long g_mh_guard[kGuardCount];
     do {                  \
     } while (0)
 #endif
-#ifdef MH_EXP_LOOKUPS
-// diagnostic build: density-grid lookups of this translation unit's kernels
-static __device__ unsigned long long g_mh_lookups;
-static __device__ unsigned long long g_mh_pf_hits;  // of which served by a prefetch (GridPf)
-#endif
 
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInvPi = 0.31830988618379067154f;

@@ -121,6 +121,7 @@ struct WfBitmapArgs {
     // fixed-point scatter (nullptr: float atomics)
     unsigned long long *fx_acc = nullptr;
     uint32_t *fx_word = nullptr;
+    unsigned long long *n_rec = nullptr;  // += the vertex records the scatter reads (mh_stats.aux_items)
 };
 size_t wf_bmp_workspace_bytes(uint64_t cap, uint32_t n_depth);
 hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, const LaneMap &lm,

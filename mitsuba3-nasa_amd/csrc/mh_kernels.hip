@@ -334,9 +334,6 @@ k_splat_px(DScene S, uint32_t pixel_begin, uint32_t n_pix, uint32_t Sn, uint32_t
 #pragma unroll
             for (int c = (Mode == 0 ? 0 : 3); c < 4; ++c) acc[ys][xs][c] = row16_sum(acc[ys][xs][c]);
     if (g != 0) return;
-#ifdef MH_EXP_SPLAT_NOATOMIC  // timing experiment: the footprint sums are not added (wrong film)
-    if (acc[2][2][3] != 12345.f) return;
-#endif
 #pragma unroll
     for (int ys = 0; ys < 5; ++ys) {
         uint32_t yy = py - 2 + ys;
@@ -1096,50 +1093,28 @@ __global__ void k_accumulate(float *__restrict__ dst, const float *__restrict__ 
     if (i < n) dst[i] += src[i];
 }
 
-// the device layout of a density grid (mh_shading.hpp grid_setup: apron
-// tiles with MH_GRID_TILE, else 4^3 bricks), in floats
+// the device layout of a density grid (mh_shading.hpp grid_setup: 4^3
+// bricks), in floats
 uint64_t grid_bricked_size(const uint32_t res[3]) {
-#if MH_GRID_TILE
-    return grid_tiled_size((int32_t)res[0], (int32_t)res[1], (int32_t)res[2]);
-#else
     return (uint64_t)((res[0] + 3) / 4) * ((res[1] + 3) / 4) * ((res[2] + 3) / 4) * 64u;
-#endif
 }
 
 void grid_to_bricks(const float *src, const uint32_t res[3], float *dst) {
     const int32_t rx = (int32_t)res[0], ry = (int32_t)res[1], rz = (int32_t)res[2];
-#if MH_GRID_TILE
-    const uint64_t m = grid_bricked_size(res);
-    for (uint64_t i = 0; i < m; ++i) {
-        int32_t x, y, z;
-        grid_tiled_texel(i, rx, ry, rz, x, y, z);
-        dst[i] = src[((uint64_t)z * ry + y) * rx + x];
-    }
-#else
     std::fill(dst, dst + grid_bricked_size(res), 0.f);
     for (int32_t z = 0; z < rz; ++z)
         for (int32_t y = 0; y < ry; ++y)
             for (int32_t x = 0; x < rx; ++x)
                 dst[grid_index(x, y, z, rx, ry)] = src[((uint64_t)z * ry + y) * rx + x];
-#endif
 }
 
 __global__ void k_grid_to_bricks(const float *__restrict__ src, int32_t rx, int32_t ry, int32_t rz,
                                  float *__restrict__ dst) {
-#if MH_GRID_TILE
-    const uint64_t n = grid_tiled_size(rx, ry, rz);  // one thread per device float (a gather)
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        int32_t x, y, z;
-        grid_tiled_texel(i, rx, ry, rz, x, y, z);
-        dst[i] = src[((uint64_t)z * ry + y) * rx + x];
-    }
-#else
     const uint64_t n = (uint64_t)rx * ry * rz;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const int32_t x = (int32_t)(i % rx), y = (int32_t)((i / rx) % ry), z = (int32_t)(i / ((uint64_t)rx * ry));
         dst[grid_index(x, y, z, rx, ry)] = src[i];
     }
-#endif
 }
 
 hipError_t launch_grid_to_bricks(const float *src, const uint32_t res[3], float *dst, hipStream_t st) {

@@ -1102,9 +1102,6 @@ MH_DEV Hit packet_batch(const Node *gnodes, const Prim *gprims, const Prim *gpai
         // rectangles [0, nrect) densely (nearly every ray overlaps the room),
         // then the triangle run
         uint32_t i = 0;
-#ifdef MH_EXP_SHADOW_NORECT  // timing experiment: shadow queries skip the rectangles (not exact in general)
-        if (Shadow) i = nrect;
-#endif
         for (; i + 1u < nrect; i += 2u) rect_pair<Shadow, Pre>(gpairs, c + i, hit & (!Shadow || !ph.occl), r, ph);
         if (i < nrect) {
             rect_one<Shadow, Pre>(gprims, c + i, hit & (!Shadow || !ph.occl), r, ph);
@@ -2469,52 +2466,16 @@ struct MEI {
 // reference's linear (z, y, x) layout; values are unchanged, so lookups are
 // bit-exact either way).
 //
-// MH_GRID_TILE = 1 (round 5, opt-in): apron tiles.  The cells of a
-// trilinear lookup (its lower tap corner, clamped to [0, r - 2]) are grouped
-// 3 x 3 x 1, and tile (tx, ty, tz) stores the 4 x 4 x 2 texels x in
-// [3 tx, 3 tx + 4), y in [3 ty, 3 ty + 4), z in [tz, tz + 2) -- every tap of
-// its 9 cells -- as 32 floats, one 128-B cache line, x fastest.  A lookup
-// then touches exactly one line, where the 4^3 bricks below touch 2.34 lines
-// on average (a 2 x 2 x 2 block at a random offset against 4 x 4 x 2 lines),
-// and config 4's k_vol_sched is bound by the lines that miss L2 (twice the
-// lookup lines cost 19 %).  The price is 3.6x the texels (256^3: 236 MB,
-// inside the 256 MB Infinity Cache).  Measured: config 4 at 249.3-249.8 vs
-// 247.5-248.9 Msamples/s with the bricks (same box) --
-// within noise, so the lines a lookup misses are not what bounds the trip
-// (the second lookup of that experiment cost its VALU and registers), and
-// the 3.6x footprint is not worth it.
-//
-// MH_GRID_TILE = 0 (the default): 4 x 4 x 4 bricks of 64 floats (256 B),
-// bricks x-fastest, texels x-fastest inside a brick.
-#ifndef MH_GRID_TILE
-#define MH_GRID_TILE 0
-#endif
+// 4 x 4 x 4 bricks of 64 floats (256 B), bricks x-fastest, texels x-fastest
+// inside a brick.  (Round 5 measured apron tiles -- every lookup in one
+// 128-B line at 3.6x the texels -- as neutral: DESIGN.md section 9.)
 __host__ __device__ __forceinline__ uint64_t grid_index(int32_t x, int32_t y, int32_t z, int32_t rx, int32_t ry) {
     const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2;
     const uint64_t brick = ((uint64_t)((uint32_t)z >> 2) * nby + ((uint32_t)y >> 2)) * nbx + ((uint32_t)x >> 2);
     return brick * 64u + ((((uint32_t)z & 3u) << 4) | (((uint32_t)y & 3u) << 2) | ((uint32_t)x & 3u));
 }
-// apron tiles per axis: cells 0 .. max(r - 2, 0) in tiles of 3 (x, y) or 1 (z)
-__host__ __device__ __forceinline__ uint32_t grid_tiles_xy(int32_t r) { return ((uint32_t)(r > 2 ? r - 1 : 1) + 2u) / 3u; }
-__host__ __device__ __forceinline__ uint32_t grid_tiles_z(int32_t r) { return (uint32_t)(r > 2 ? r - 1 : 1); }
-__host__ __device__ __forceinline__ uint64_t grid_tiled_size(int32_t rx, int32_t ry, int32_t rz) {
-    return (uint64_t)grid_tiles_xy(rx) * grid_tiles_xy(ry) * grid_tiles_z(rz) * 32u;
-}
-// the texel that float i of the tiled layout holds (the tiles' padding past
-// the grid repeats the last texel; no lookup reads it)
-__host__ __device__ __forceinline__ void grid_tiled_texel(uint64_t i, int32_t rx, int32_t ry, int32_t rz, int32_t &x,
-                                                          int32_t &y, int32_t &z) {
-    const uint64_t tile = i >> 5;
-    const uint32_t w = (uint32_t)(i & 31u), ntx = grid_tiles_xy(rx), nty = grid_tiles_xy(ry);
-    const uint32_t tx = (uint32_t)(tile % ntx), ty = (uint32_t)((tile / ntx) % nty), tz = (uint32_t)(tile / ((uint64_t)ntx * nty));
-    x = min((int32_t)(3u * tx + (w & 3u)), rx - 1);
-    y = min((int32_t)(3u * ty + ((w >> 2) & 3u)), ry - 1);
-    z = min((int32_t)(tz + (w >> 4)), rz - 1);
-}
-
 // [drjit] Texture3f::eval_nonaccel, linear, clamp, 1 channel (grid.cpp:545-558),
 // in three parts: the tap offsets and weights, the 8 loads, the interpolation
-// (so that a lookup's loads can be issued ahead of it: GridPf)
 struct GridLookup {
     float w0x, w0y, w0z, w1x, w1y, w1z;
     uint32_t o[8];  // tap (bx, by, bz) at o[bx | by << 1 | bz << 2] in the bricked grid
@@ -2530,23 +2491,12 @@ MH_DEV void grid_setup(const DMedium &m, V3 p, GridLookup &L) {
     const int32_t x0 = min(max(ix, 0), rx - 1), x1 = min(max(ix + 1, 0), rx - 1);
     const int32_t y0 = min(max(iy, 0), ry - 1), y1 = min(max(iy + 1, 0), ry - 1);
     const int32_t z0 = min(max(iz, 0), rz - 1), z1 = min(max(iz + 1, 0), rz - 1);
-#if MH_GRID_TILE
-    // the lookup's cell, its apron tile and the taps' places in it (32-bit:
-    // mh_scene_create caps a grid's device layout at 2^32 floats)
-    const int32_t cx = min(max(ix, 0), max(rx - 2, 0)), cy = min(max(iy, 0), max(ry - 2, 0)), cz = min(max(iz, 0), max(rz - 2, 0));
-    const uint32_t tx = (uint32_t)cx / 3u, ty = (uint32_t)cy / 3u;
-    const uint32_t base = (((uint32_t)cz * grid_tiles_xy(ry) + ty) * grid_tiles_xy(rx) + tx) * 32u;
-    const uint32_t ox0 = (uint32_t)x0 - 3u * tx, ox1 = (uint32_t)x1 - 3u * tx;
-    const uint32_t oy0 = ((uint32_t)y0 - 3u * ty) << 2, oy1 = ((uint32_t)y1 - 3u * ty) << 2;
-    const uint32_t oz0 = base + (((uint32_t)z0 - (uint32_t)cz) << 4), oz1 = base + (((uint32_t)z1 - (uint32_t)cz) << 4);
-#else
     // grid_index split per axis (brick-major part + texel-in-brick part, the
     // bit fields disjoint), 32-bit (mh_scene_create caps a grid at 2^32 texels)
     const uint32_t nbx = (uint32_t)(rx + 3) >> 2, nby = (uint32_t)(ry + 3) >> 2, sy = nbx * 64u, sz = sy * nby;
     const uint32_t ox0 = ((uint32_t)x0 >> 2) * 64u + ((uint32_t)x0 & 3u), ox1 = ((uint32_t)x1 >> 2) * 64u + ((uint32_t)x1 & 3u);
     const uint32_t oy0 = ((uint32_t)y0 >> 2) * sy + (((uint32_t)y0 & 3u) << 2), oy1 = ((uint32_t)y1 >> 2) * sy + (((uint32_t)y1 & 3u) << 2);
     const uint32_t oz0 = ((uint32_t)z0 >> 2) * sz + (((uint32_t)z0 & 3u) << 4), oz1 = ((uint32_t)z1 >> 2) * sz + (((uint32_t)z1 & 3u) << 4);
-#endif
     const uint32_t o00 = oy0 + oz0, o10 = oy1 + oz0, o01 = oy0 + oz1, o11 = oy1 + oz1;
     L.o[0] = o00 + ox0; L.o[1] = o00 + ox1; L.o[2] = o10 + ox0; L.o[3] = o10 + ox1;
     L.o[4] = o01 + ox0; L.o[5] = o01 + ox1; L.o[6] = o11 + ox0; L.o[7] = o11 + ox1;
@@ -2557,64 +2507,13 @@ MH_DEV float grid_interp(const GridLookup &L, const float (&v)[8]) {
     float f0 = __builtin_fmaf(L.w0y, f00, L.w1y * f10), f1 = __builtin_fmaf(L.w0y, f01, L.w1y * f11);
     return __builtin_fmaf(L.w0z, f0, L.w1z * f1);
 }
-// The 8 taps of a medium sample's lookup, loaded a trip ahead (k_vol_sched:
-// a lane that continues a null-collision chain or a ratio-tracking walk
-// issues its next sample's loads at the end of this one, so that the next
-// medium trip finds them in registers).  key = the lookup's first tap
-// offset, checked at the use: the values are the grid's own, so a match of
-// the cell within the same medium is exact whatever produced the prefetch.
-struct GridPf {
-    uint32_t key, key7;  // the lookup's first and last tap offsets (key ~0u: none); the caller
-                         // checks the medium (k_vol_sched's MH_VS_STEP2: same chain, same medium)
-    float v[8];
-};
-MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p, const GridPf *pf = nullptr) {
+MH_DEV float grid_eval(const DScene &S, const DMedium &m, V3 p) {
     GridLookup L;
     grid_setup(m, p, L);
-#ifdef MH_EXP_NOGRID  // timing experiment: no grid memory traffic (wrong results)
-    return L.w0x * 0.3f + L.w1y * 0.2f + L.w0z * 0.1f + (float)(L.o[0] + L.o[7]) * 1e-9f;
-#endif
     const float *g = S.grid + m.grid_offset;
-#ifdef MH_EXP_LOOKUPS  // diagnostic build: count the lookups (one add per wave; results unchanged)
-    {
-        const unsigned long long ex = __builtin_amdgcn_read_exec();
-        if (lane_rank(ex) == 0) atomicAdd(&g_mh_lookups, (unsigned long long)__builtin_popcountll(ex));
-    }
-#endif
     float v[8];
-    if (pf && pf->key == L.o[0] && pf->key7 == L.o[7]) {
-#ifdef MH_EXP_LOOKUPS
-        {
-            const unsigned long long ex = __builtin_amdgcn_read_exec();
-            if (lane_rank(ex) == 0) atomicAdd(&g_mh_pf_hits, (unsigned long long)__builtin_popcountll(ex));
-        }
-#endif
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = pf->v[c];
-    } else {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] = g[L.o[c]];
-    }
-#ifdef MH_EXP_GRIDDEP  // timing experiment: a second, DEPENDENT round trip per lookup (results unchanged)
-    {
-        uint32_t zero;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-        const uint32_t dep = __float_as_uint(v[0]) & zero;  // 0, but only known after the first loads
-        float u = 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) u += g[L.o[c] + dep];
-        asm volatile("" : "+v"(u));
-        return grid_interp(L, v) + (u == 12345.f ? 1.f : 0.f) * 0.f;
-    }
-#endif
-#ifdef MH_EXP_GRID2  // timing experiment: a second lookup's memory traffic (results unchanged)
-    {
-        float u = 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) u += g[L.o[c] ^ 64u];
-        return grid_interp(L, v) + 0.f * u;
-    }
-#endif
+    for (int c = 0; c < 8; ++c) v[c] = g[L.o[c]];
     return grid_interp(L, v);
 }
 
@@ -2626,11 +2525,7 @@ MH_DEV bool bbox_ray_intersect(const float *mn, const float *mx, const RayT &r, 
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         active = active && (d[i] != 0.f || (o[i] > mn[i] || o[i] < mx[i]));
-#ifdef MH_EXP_FAST_BBOX_RCP  // timing bound only: approximate reciprocals (not the reference's values)
-        const float rc = __builtin_amdgcn_rcpf(d[i]);
-#else
         const float rc = rcp(d[i]);
-#endif
         const float t1 = (mn[i] - o[i]) * rc, t2 = (mx[i] - o[i]) * rc;
         t1p[i] = fminf(t1, t2);
         t2p[i] = fmaxf(t1, t2);
@@ -2663,9 +2558,9 @@ MH_DEV bool free_flight(const DMedium &m, const RayT &ray, float u, float &mint_
     p_o = fma3s(ray.d, sampled_t, ray.o);
     return active && sampled_t <= maxt;
 }
+// returns whether the sample looked the density grid up (k_vol_sched counts them)
 template <bool Frame = true>
-MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, float u, MEI &mei,
-                               const GridPf *pf = nullptr) {
+MH_DEV bool sample_interaction(const DScene &S, uint32_t med, const RayT &ray, float u, MEI &mei) {
     const DMedium &m = S.media[med];
     mei.fn = ray.d;
     if (Frame) coordinate_system(ray.d, mei.fs, mei.ft);
@@ -2679,28 +2574,12 @@ MH_DEV void sample_interaction(const DScene &S, uint32_t med, const RayT &ray, f
     mei.mint = mint;
     mei.maj = maj;
     float st = 0.f;
-    if (valid) st = m.type == MH_MEDIUM_HOMOGENEOUS ? m.sigma_t_const * m.scale : m.scale * grid_eval(S, m, mei.p, pf);
+    if (valid) st = m.type == MH_MEDIUM_HOMOGENEOUS ? m.sigma_t_const * m.scale : m.scale * grid_eval(S, m, mei.p);
     mei.sigma_t = st;
     mei.sigma_s = valid ? v3(m.albedo[0], m.albedo[1], m.albedo[2]) * st : v3(0, 0, 0);
     mei.sigma_n = m.type == MH_MEDIUM_HOMOGENEOUS ? 0.f : maj - st;
+    return valid && m.type != MH_MEDIUM_HOMOGENEOUS;
 }
-// the loads of the medium sample a lane will take next (GridPf): the same
-// free flight as sample_interaction's, its 8 taps issued now
-MH_DEV void grid_prefetch(const DScene &S, uint32_t med, const RayT &ray, float u, GridPf &pf) {
-    const DMedium &m = S.media[med];
-    if (m.type == MH_MEDIUM_HOMOGENEOUS) return;
-    float mint, t;
-    V3 p;
-    if (!free_flight(m, ray, u, mint, t, p)) return;
-    GridLookup L;
-    grid_setup(m, p, L);
-    const float *g = S.grid + m.grid_offset;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) pf.v[c] = g[L.o[c]];
-    pf.key = L.o[0];
-    pf.key7 = L.o[7];
-}
-
 MH_DEV V3 mei_to_local(const MEI &m, V3 v) { return v3(dot(v, m.fs), dot(v, m.ft), dot(v, m.fn)); }
 MH_DEV void mei_frame(MEI &m) { coordinate_system(m.fn, m.fs, m.ft); }  // Frame3f(ray.d), as sample_interaction
 MH_DEV V3 mei_to_world(const MEI &m, V3 v) { return fma3s(m.fn, v.z, fma3s(m.ft, v.y, m.fs * v.x)); }
@@ -3141,9 +3020,6 @@ MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8], const 
     for (uint32_t j = 0; j < 8; ++j) {
         const uint32_t t = j * n + r, src = t >> 3, c = t & 7u;
         const uint32_t cc = __float_as_uint(sc[src * 9]);
-#ifdef MH_EXP_NO_SIGMA_ATOMIC  // diagnostic: cost of the grid-gradient scatter (wrong gradients)
-        if (sc[src * 9 + 1 + c] == 12345.f)
-#endif
         if (g.fx_mode == 2) {
             const long long q = __double2ll_rn((double)sc[src * 9 + 1 + c] * g.fx_scale);
             atomicAdd(reinterpret_cast<unsigned long long *>(cb) + (size_t)cc * 8 + c, (unsigned long long)q);
@@ -3202,9 +3078,6 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
             g.fsum += (as * w) * buf[idx];
             continue;
         }
-#ifdef MH_EXP_NO_SIGMA_ATOMIC  // diagnostic: cost of the grid-gradient scatter
-        if (as * w == 12345.f)
-#endif
         unsafeAtomicAdd(buf + idx, as * w);
     }
 }

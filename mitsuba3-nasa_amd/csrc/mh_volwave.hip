@@ -684,25 +684,7 @@ MH_DEV uint32_t vs_walk(const DScene &S, Pcg &rng, const DirS &ds, NeeState &ns,
 // lookup, the trip's latency), so the pending lanes of both take it together
 // at one call site instead of one wave trip each.  Per lane the operations
 // and draws are vs_head's / vs_walk's.
-//
-// MH_VS_STEP2 (round 5): a medium sample is usually followed by another one
-// of the same chain -- a null collision continues along its ray, a
-// ratio-tracking step continues its walk -- and the next sample's position
-// depends only on this one's position and the sampler's next draws, not on
-// the density.  So the trip computes the chain's next sample position on a
-// copy of the sampler (for HEAD: vs_med_rest's null draw, vs_head_pre's RR
-// draw, then u; for WALK: u, at remaining = max_dist - (total_dist + t)),
-// issues its lookup's 8 loads beside this sample's 8 (one memory round trip
-// for both), and when this sample's continuation sends the lane to the same
-// phase again it takes that next step in the same trip with those taps.  The
-// speculation is only a cache (GridPf): the second step recomputes its
-// lookup and takes the taps only when its cell and medium match, so per lane
-// the operations and draws stay vs_head's / vs_walk's (bit-identical).
-// (Round 4's one-trip-ahead prefetch, loads left in flight across trips,
-// measured slower: DESIGN.md section 9.)
-#ifndef MH_VS_STEP2
-#define MH_VS_STEP2 0  // measured slower (config 4: 197 vs 249 Msamples/s)
-#endif
+
 // the ray of a HEAD / WALK lane's medium sample, as values
 MH_DEV RayT vs_medium_ray(const VolState &v, bool head) {
     const RayT rh = v.ray, rw = v.ns.ray;
@@ -713,7 +695,7 @@ MH_DEV RayT vs_medium_ray(const VolState &v, bool head) {
     return r;
 }
 MH_DEV uint32_t vs_medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, VolState &v, WMei &wm,
-                               uint32_t ph) {
+                               uint32_t ph, uint32_t &n_lookups) {
     uint32_t nph = kPhFree;
     float u = 0.f;
     const bool head = ph == kPhHead;
@@ -723,58 +705,14 @@ MH_DEV uint32_t vs_medium_step(const DScene &S, const IntegratorParams &in, Pcg 
     // addresses would pin the state in scratch)
     const uint32_t med = head ? v.medium : v.ns.medium;
     const RayT r = vs_medium_ray(v, head);
-#if MH_VS_STEP2
-    GridPf pf;
-    pf.key = ~0u;
-    {
-        const DMedium &m = S.media[med];
-        float mint1, t1;
-        V3 p1;
-        if (m.type != MH_MEDIUM_HOMOGENEOUS && free_flight(m, r, u, mint1, t1, p1)) {
-            Pcg c = rng;
-            RayT r2;
-            r2.o = p1;
-            r2.d = r.d;
-            float u2;
-            if (head) {
-                (void)c.next_float();  // vs_med_rest: the null / real decision
-                (void)c.next_float();  // vs_head_pre: Russian roulette
-                u2 = c.next_float();
-                r2.maxt = r.maxt;
-            } else {
-                r2.maxt = v.ns.max_dist - (v.ns.total_dist + t1);  // walk_med_rest, then vs_walk_pre
-                u2 = c.next_float();
-            }
-            grid_prefetch(S, med, r2, u2, pf);
-        }
-    }
-#endif
     MEI mei;  // the frame only at a real scatter (vs_scatter)
-    sample_interaction<false>(S, med, r, u, mei);
+    n_lookups += sample_interaction<false>(S, med, r, u, mei) ? 1u : 0u;
     if (head) {
         v.mei = mei;
         nph = vs_head_post(S, in, rng, v);
     } else {
         nph = vs_walk_post(S, v.ds, v.ns, wm, mei);
     }
-#if MH_VS_STEP2
-    if (pf.key != ~0u && nph == ph) {  // the chain goes on: its next trip's step now
-        uint32_t nph2 = kPhFree;
-        float u2 = 0.f;
-        const bool pend2 = head ? vs_head_pre(S, in, rng, v, nph2, u2) : vs_walk_pre(S, rng, v.ns, nph2, u2);
-        if (!pend2) return nph2;
-        const uint32_t med2 = head ? v.medium : v.ns.medium;
-        const RayT r2 = vs_medium_ray(v, head);
-        MEI mei2;
-        sample_interaction<false>(S, med2, r2, u2, mei2, med2 == med ? &pf : nullptr);
-        if (head) {
-            v.mei = mei2;
-            nph = vs_head_post(S, in, rng, v);
-        } else {
-            nph = vs_walk_post(S, v.ds, v.ns, wm, mei2);
-        }
-    }
-#endif
     return nph;
 }
 
@@ -812,8 +750,7 @@ MH_DEV uint32_t vs_trace_hit(const DScene &S, const IntegratorParams &in, Pcg &r
     si_from_hit(S, ray, h, si, si_t);
     return vs_trace_si(S, in, rng, ph, v, wm, si, si_t, n_closest, n_shadow);
 }
-// the continuation of a TRACE lane from its hit's interaction (the trace
-// server's lanes get si / si_t from the server wave)
+// the continuation of a TRACE lane from its hit's interaction
 MH_DEV uint32_t vs_trace_si(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, VolState &v,
                             WMei &wm, const SI &si, float si_t, uint32_t &n_closest, uint32_t &n_shadow) {
     const bool walk = ph == kPhTraceWM || ph == kPhTraceWS;
@@ -1101,53 +1038,15 @@ MH_DEV bool pv_walk_pre(const DScene &S, Pcg &rng, V &v, Hk &hk, uint32_t &nph, 
     nph = pv_walk_fin(S, v, remaining_dist, hk, mei);
     return false;
 }
-// MH_PV_STEP2: the WALK trip's second ratio-tracking step (vs_medium_step's
-// MH_VS_STEP2 for prbvolpath's unmerged WALK phase): the walk's next sample
-// position needs only this sample's position and the next draw, so its
-// lookup's loads go out beside this one's, and a walk that goes on takes its
-// next step in the same trip from those taps (a cache: the step recomputes
-// its lookup and takes the taps only when the cell and medium match)
-#ifndef MH_PV_STEP2
-#define MH_PV_STEP2 0
-#endif
 template <class V, class Hk>
 MH_DEV uint32_t pv_walk(const DScene &S, Pcg &rng, V &v, Hk &hk) {
     uint32_t nph = kPhPost;
     float u = 0.f;
     if (!pv_walk_pre(S, rng, v, hk, nph, u)) return nph;
-#if MH_PV_STEP2
-    const uint32_t med = v.wmedium;
-    GridPf pf;
-    pf.key = ~0u;
-    {
-        const DMedium &m = S.media[med];
-        float mint1, t1;
-        V3 p1;
-        if (m.type != MH_MEDIUM_HOMOGENEOUS && free_flight(m, v.wray, u, mint1, t1, p1)) {
-            Pcg c = rng;
-            RayT r2;
-            r2.o = p1;
-            r2.d = v.wray.d;
-            r2.maxt = v.ds.dist * (1.f - kShadowEps) - (v.total_dist + t1);  // pv_walk_fin, then pv_remaining
-            grid_prefetch(S, med, r2, c.next_float(), pf);
-        }
-    }
-#endif
     MEI mei;
     pv_walk_mei_init(mei);
     sample_interaction(S, v.wmedium, v.wray, u, mei);
     nph = pv_walk_fin(S, v, pv_remaining(v), hk, mei);
-#if MH_PV_STEP2
-    if (pf.key != ~0u && nph == kPhWalk) {
-        uint32_t nph2 = kPhPost;
-        float u2 = 0.f;
-        if (!pv_walk_pre(S, rng, v, hk, nph2, u2)) return nph2;
-        MEI mei2;
-        pv_walk_mei_init(mei2);
-        sample_interaction(S, v.wmedium, v.wray, u2, mei2, v.wmedium == med ? &pf : nullptr);
-        nph = pv_walk_fin(S, v, pv_remaining(v), hk, mei2);
-    }
-#endif
     return nph;
 }
 
@@ -1262,7 +1161,7 @@ MH_DEV uint32_t pv_trace_hit(const DScene &S, const IntegratorParams &in, Pcg &r
     if (ph == kPhTraceM) return pv_med_rest(S, in, rng, v, hk);
     return kPhSurf;
 }
-// the same from the hit's interaction (the trace server's lanes)
+// the same from the hit's interaction
 template <class V, class Hk>
 MH_DEV uint32_t pv_trace_si(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, V &v, const SI &si,
                             float si_t, uint32_t &n_closest, uint32_t &n_shadow, Hk &hk) {
@@ -1331,17 +1230,14 @@ struct VolMachine {
         return vs_surf(S, in, rng, v);
     }
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &wm) { return vs_walk(S, rng, v.ds, v.ns, wm); }
-    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &wm, uint32_t ph) {
-        return vs_medium_step(S, in, rng, v, wm, ph);
+    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &wm, uint32_t ph,
+                                uint32_t &n_lookups) {
+        return vs_medium_step(S, in, rng, v, wm, ph, n_lookups);
     }
     MH_DEV RayT trace_ray(const State &v, uint32_t ph) const { return vs_trace_ray(v, ph); }
     MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &wm,
                               const Hit &h, const RayT &r, uint32_t &nc, uint32_t &ns) {
         return vs_trace_hit(S, in, rng, ph, v, wm, h, r, nc, ns);
-    }
-    MH_DEV uint32_t trace_si(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &wm,
-                             const SI &si, float si_t, uint32_t &nc, uint32_t &ns) {
-        return vs_trace_si(S, in, rng, ph, v, wm, si, si_t, nc, ns);
     }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &, const IntegratorParams &in, Pcg &rng, State &v, uint32_t &) {
         return volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
@@ -1349,275 +1245,6 @@ struct VolMachine {
     MH_DEV void end(const DScene &, const LdsBvh &, const IntegratorParams &, float *out, uint64_t plane,
                     uint32_t pid, const State &v, int alpha, uint32_t &, uint32_t &) {
         vw_write_sample(out, plane, pid, v, alpha);
-    }
-    MH_DEV void finish() {}
-};
-
-// ---------------------------------------------------------------------------
-// VolPkMachine (round 5): VolMachine with its lane state packed by liveness.
-// The scheduler's state is loop-carried through a dynamic phase switch, so
-// the compiler keeps every field of VolState that any phase reads live in
-// every phase (~145 dwords).  But a lane's fields are not all meaningful at
-// once: at a trip boundary the lane's surface interaction (si) and its medium
-// interaction (mei) are never both needed (a trip that samples the medium
-// either consumes mei before it ends or leaves si dead), and the main ray
-// (+ si_t) is dead while an NEE walk runs.  VolPack therefore stores
-//   - the path fields every phase reads (throughput, result, depth, flags ...);
-//   - G[22]: si, or the medium interaction (TraceM, SCATTER, and the walk /
-//     POST of a medium scatter);
-//   - W[42]: the main ray and si_t (HEAD, TraceM, TraceS), or the walk: the
-//     NEE state (its ray, hit, transmittance, emitter value, distances), the
-//     walk's medium sample across its trace (WMei), ds.dist, pend, pend_w,
-//     rho (WALK, TraceWM / WS, POST).
-// Each phase step unpacks a full VolState (overlapping slots alias: a field
-// of the other class reads whatever the slot holds and is never used), runs
-// the unchanged VolMachine step, and packs by the lane's next phase.  Per
-// lane the arithmetic and draws are VolMachine's: bit-identical samples.
-// ---------------------------------------------------------------------------
-// register-demand analysis (compile only): MH_EXP_STUB's bits replace the
-// Srv kernel's phases by a cheap jump to a later phase (1 init, 2 medium
-// trip, 4 trace continuation, 8 scatter, 16 surface, 32 post; 64 / 128 the
-// walk / main-ray part of VolPkMachine's trace continuation)
-#ifndef MH_EXP_STUB
-#define MH_EXP_STUB 0
-#endif
-// machines whose Srv continuation reads the server's LDS result slot itself (trace_res)
-template <class M, class = void>
-struct vs_res_slot : std::false_type {};
-template <class M>
-struct vs_res_slot<M, std::void_t<decltype(M::kResSlot)>> : std::bool_constant<M::kResSlot> {};
-
-struct VolPack {
-    V3 throughput, result, last_p;
-    float last_pdf, eta;
-    uint32_t medium, depth, nee_kind;
-    bool specular_chain, needs_intersection, valid, active, active_medium, active_surface, act_scatter;
-    float g[22], w[42];
-};
-MH_DEV void vp_unpack(const VolPack &P, VolState &v, WMei &wm) {
-    v.throughput = P.throughput; v.result = P.result; v.last_p = P.last_p;
-    v.last_pdf = P.last_pdf; v.eta = P.eta;
-    v.medium = P.medium; v.depth = P.depth; v.nee_kind = P.nee_kind;
-    v.specular_chain = P.specular_chain; v.needs_intersection = P.needs_intersection; v.valid = P.valid;
-    v.active = P.active; v.active_medium = P.active_medium; v.active_surface = P.active_surface;
-    v.act_scatter = P.act_scatter;
-    v.mode = kVolPre;
-    const float *g = P.g, *w = P.w;
-    // G as si
-    v.si.valid = __float_as_uint(g[0]) != 0u;
-    v.si.p = v3(g[1], g[2], g[3]); v.si.n = v3(g[4], g[5], g[6]);
-    v.si.s = v3(g[7], g[8], g[9]); v.si.t_ = v3(g[10], g[11], g[12]); v.si.sn = v3(g[13], g[14], g[15]);
-    v.si.uvx = g[16]; v.si.uvy = g[17];
-    v.si.wi = v3(g[18], g[19], g[20]);
-    v.si.shape = __float_as_uint(g[21]);
-    // G as mei
-    v.mei.valid = __float_as_uint(g[0]) != 0u;
-    v.mei.t = g[1]; v.mei.mint = g[2];
-    v.mei.p = v3(g[3], g[4], g[5]); v.mei.sigma_s = v3(g[6], g[7], g[8]);
-    v.mei.sigma_n = g[9]; v.mei.sigma_t = g[10]; v.mei.maj = g[11];
-    v.mei.fs = v3(g[12], g[13], g[14]); v.mei.ft = v3(g[15], g[16], g[17]); v.mei.fn = v3(g[18], g[19], g[20]);
-    // W as the main ray
-    v.ray.o = v3(w[0], w[1], w[2]); v.ray.d = v3(w[3], w[4], w[5]); v.ray.maxt = w[6];
-    v.si_t = w[7];
-    // W as the walk
-    NeeState &ns = v.ns;
-    ns.ray.o = v3(w[0], w[1], w[2]); ns.ray.d = v3(w[3], w[4], w[5]); ns.ray.maxt = w[6];
-    ns.si_t = w[7];
-    ns.si.valid = __float_as_uint(w[8]) != 0u;
-    ns.si.p = v3(w[9], w[10], w[11]); ns.si.n = v3(w[12], w[13], w[14]);
-    ns.si.shape = __float_as_uint(w[15]);
-    ns.transmittance = v3(w[16], w[17], w[18]); ns.emitter_val = v3(w[19], w[20], w[21]);
-    ns.max_dist = w[22]; ns.total_dist = w[23];
-    ns.medium = __float_as_uint(w[24]); ns.needs_intersection = __float_as_uint(w[25]) != 0u;
-    v.ds.dist = w[26];
-    wm.t = w[27]; wm.mint = w[28]; wm.maj = w[29]; wm.sigma_n = w[30];
-    wm.p = v3(w[31], w[32], w[33]); wm.valid = __float_as_uint(w[34]) != 0u;
-    v.pend = v3(w[35], w[36], w[37]); v.pend_w = w[38]; v.rho = v3(w[39], w[40], w[41]);
-}
-// the fields the lane's next phase reads (see the class comment)
-MH_DEV void vp_pack(uint32_t ph, const VolState &v, const WMei &wm, VolPack &P) {
-    P.throughput = v.throughput; P.result = v.result; P.last_p = v.last_p;
-    P.last_pdf = v.last_pdf; P.eta = v.eta;
-    P.medium = v.medium; P.depth = v.depth; P.nee_kind = v.nee_kind;
-    P.specular_chain = v.specular_chain; P.needs_intersection = v.needs_intersection; P.valid = v.valid;
-    P.active = v.active; P.active_medium = v.active_medium; P.active_surface = v.active_surface;
-    P.act_scatter = v.act_scatter;
-    const bool walk = ph == kPhWalk || ph == kPhTraceWM || ph == kPhTraceWS || ph == kPhPost;
-    const bool gmei = ph == kPhTraceM || ph == kPhScatter || (walk && v.act_scatter);
-    // per-slot selects, not branches: two divergent branches that each write
-    // every slot make the register allocator keep a slot's old and new values
-    // apart (a second copy of the pack)
-    const MEI &m = v.mei;
-    const SI &s = v.si;
-    const float mf[22] = {__uint_as_float(m.valid ? 1u : 0u), m.t, m.mint, m.p.x, m.p.y, m.p.z,
-                          m.sigma_s.x, m.sigma_s.y, m.sigma_s.z, m.sigma_n, m.sigma_t, m.maj,
-                          m.fs.x, m.fs.y, m.fs.z, m.ft.x, m.ft.y, m.ft.z, m.fn.x, m.fn.y, m.fn.z, 0.f};
-    const float sf[22] = {__uint_as_float(s.valid ? 1u : 0u), s.p.x, s.p.y, s.p.z, s.n.x, s.n.y, s.n.z,
-                          s.s.x, s.s.y, s.s.z, s.t_.x, s.t_.y, s.t_.z, s.sn.x, s.sn.y, s.sn.z,
-                          s.uvx, s.uvy, s.wi.x, s.wi.y, s.wi.z, __uint_as_float(s.shape)};
-#pragma unroll
-    for (int k = 0; k < 22; ++k) P.g[k] = gmei ? mf[k] : sf[k];
-    const NeeState &ns = v.ns;
-    const float wf[42] = {ns.ray.o.x, ns.ray.o.y, ns.ray.o.z, ns.ray.d.x, ns.ray.d.y, ns.ray.d.z, ns.ray.maxt,
-                          ns.si_t, __uint_as_float(ns.si.valid ? 1u : 0u), ns.si.p.x, ns.si.p.y, ns.si.p.z,
-                          ns.si.n.x, ns.si.n.y, ns.si.n.z, __uint_as_float(ns.si.shape),
-                          ns.transmittance.x, ns.transmittance.y, ns.transmittance.z,
-                          ns.emitter_val.x, ns.emitter_val.y, ns.emitter_val.z, ns.max_dist, ns.total_dist,
-                          __uint_as_float(ns.medium), __uint_as_float(ns.needs_intersection ? 1u : 0u), v.ds.dist,
-                          wm.t, wm.mint, wm.maj, wm.sigma_n, wm.p.x, wm.p.y, wm.p.z, __uint_as_float(wm.valid ? 1u : 0u),
-                          v.pend.x, v.pend.y, v.pend.z, v.pend_w, v.rho.x, v.rho.y, v.rho.z};
-    const float rf[8] = {v.ray.o.x, v.ray.o.y, v.ray.o.z, v.ray.d.x, v.ray.d.y, v.ray.d.z, v.ray.maxt, v.si_t};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) P.w[k] = walk ? wf[k] : rf[k];
-#pragma unroll
-    for (int k = 8; k < 42; ++k) P.w[k] = wf[k];  // only the walk reads these slots
-}
-struct VolPkMachine {
-    using State = VolPack;
-    static constexpr bool kPrb = false, kWritesPos = true, kDeferEnd = false, kMergeMed = MH_VS_MERGE != 0;
-    MH_DEV VolPkMachine(const VsBwdArgs &, const LaneMap &, uint32_t) {}
-    MH_DEV void init(const DScene &S, const IntegratorParams &in, Pcg &rng, RayT r, State &P, float, float) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        volpath_init(S, in, rng, r, v);
-        vp_pack(kPhHead, v, wm, P);
-    }
-    MH_DEV uint32_t head(const DScene &S, const IntegratorParams &in, Pcg &rng, State &P) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        const uint32_t ph = vs_head(S, in, rng, v);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    template <bool Pk>
-    MH_DEV uint32_t trace(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng,
-                          uint32_t ph, State &P, WMei &, uint32_t &nc, uint32_t &ns) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        ph = vs_trace<Pk>(S, B, in, rng, ph, v, wm, nc, ns);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV uint32_t scatter(const DScene &S, const IntegratorParams &in, Pcg &rng, State &P) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        const uint32_t ph = vs_scatter(S, in, rng, v);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV uint32_t surf(const DScene &S, const IntegratorParams &in, Pcg &rng, State &P) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        const uint32_t ph = vs_surf(S, in, rng, v);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &P, WMei &) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        const uint32_t ph = vs_walk(S, rng, v.ds, v.ns, wm);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &P, WMei &, uint32_t ph) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        ph = vs_medium_step(S, in, rng, v, wm, ph);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV RayT trace_ray(const State &P, uint32_t ph) const {
-        // TraceM / TraceS: the main ray; TraceWM / TraceWS: the walk's ray (the same W slots)
-        RayT r;
-        r.o = v3(P.w[0], P.w[1], P.w[2]);
-        r.d = v3(P.w[3], P.w[4], P.w[5]);
-        r.maxt = P.w[6];
-        return r;
-    }
-    MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &P, WMei &,
-                              const Hit &h, const RayT &r, uint32_t &nc, uint32_t &ns) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        ph = vs_trace_hit(S, in, rng, ph, v, wm, h, r, nc, ns);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV uint32_t trace_si(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &P, WMei &,
-                             const SI &si, float si_t, uint32_t &nc, uint32_t &ns) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        ph = vs_trace_si(S, in, rng, ph, v, wm, si, si_t, nc, ns);
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    // the Srv continuation from the server's result slot r (SoA, srv_put_si):
-    // a main-ray hit reads valid + t first (vs_med_rest needs no more) and
-    // copies the rest of the interaction into G only when the next phase keeps
-    // it, so si and the medium interaction are never both in registers; a walk
-    // hit reads the few fields the walk uses.  Values and order as vs_trace_si.
-    static constexpr bool kResSlot = true;
-    MH_DEV uint32_t trace_res(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &P,
-                              const float *r0, uint32_t &nc, uint32_t &ns) {
-        // volatile: the compiler may not hoist the slot's reads above the
-        // branches that decide whether they are needed (it did, and the
-        // hoisted values set the kernel's register peak)
-        const volatile float *r = r0;
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        // the two kinds as two one-sided branches and ONE pack (not a pack
-        // per branch: see vp_pack)
-        const bool wk = ph == kPhTraceWM || ph == kPhTraceWS;
-        if (wk) {
-            v.ns.si.valid = __float_as_uint(r[0]) != 0u;
-            v.ns.si.p = v3(r[64], r[128], r[192]);
-            v.ns.si.n = v3(r[256], r[320], r[384]);
-            v.ns.si.shape = __float_as_uint(r[1344]);
-            v.ns.si_t = r[1408];
-            ++ns;
-            if (MH_EXP_STUB & 64) ph = (nc & 1u) ? kPhWalk : kPhPost;
-            else if (ph == kPhTraceWM) ph = walk_med_rest(S, v.ds, v.ns, wm) ? kPhWalk : kPhPost;
-            else ph = walk_tail(S, v.ns, false, false, true, true, v.ns.max_dist - v.ns.total_dist) ? kPhWalk : kPhPost;
-        }
-        if (!wk) {
-            v.si.valid = __float_as_uint(r[0]) != 0u;
-            v.si_t = r[1408];
-            ++nc;
-            if (MH_EXP_STUB & 128) ph = (ns & 3u) == 0u ? kPhHead : (ns & 3u) == 1u ? kPhScatter : kPhSurf;
-            else ph = ph == kPhTraceM ? vs_med_rest(S, in, rng, v) : (uint32_t)kPhSurf;
-        }
-        vp_pack(ph, v, wm, P);
-        const bool walk = ph == kPhWalk || ph == kPhTraceWM || ph == kPhTraceWS || ph == kPhPost;
-        const bool gmei = ph == kPhTraceM || ph == kPhScatter || (walk && v.act_scatter);
-        if (!wk && !gmei) {  // the lane keeps the interaction: G = si, straight from the slot
-#pragma unroll
-            for (int k = 0; k < 22; ++k) P.g[k] = r[k * 64];
-        }
-        return ph;
-    }
-    MH_DEV uint32_t post(const DScene &S, const LdsBvh &, const IntegratorParams &in, Pcg &rng, State &P, uint32_t &) {
-        VolState v;
-        WMei wm;
-        vp_unpack(P, v, wm);
-        const uint32_t ph = volpath_post(S, in, rng, v) ? kPhHead : kPhFree;
-        vp_pack(ph, v, wm, P);
-        return ph;
-    }
-    MH_DEV void end(const DScene &, const LdsBvh &, const IntegratorParams &, float *out, uint64_t plane,
-                    uint32_t pid, const State &P, int alpha, uint32_t &, uint32_t &) {
-        out[pid] = P.result.x;
-        out[plane + pid] = P.result.y;
-        out[2 * plane + pid] = P.result.z;
-        if (alpha) out[5 * plane + pid] = P.valid ? 1.f : 0.f;  // aovs[3] (integrator.cpp:1229-1231)
     }
     MH_DEV void finish() {}
 };
@@ -1645,17 +1272,14 @@ struct PvMachine {
         return pv_shade(S, in, rng, v, h);
     }
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, h); }
-    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph) {
+    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph,
+                                uint32_t &) {
         return pv_medium_step(S, in, rng, v, h, ph);
     }
     MH_DEV RayT trace_ray(const State &v, uint32_t ph) const { return pv_trace_ray(v, ph); }
     MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &,
                               const Hit &hh, const RayT &r, uint32_t &nc, uint32_t &ns) {
         return pv_trace_hit(S, in, rng, ph, v, hh, r, nc, ns, h);
-    }
-    MH_DEV uint32_t trace_si(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &,
-                             const SI &si, float si_t, uint32_t &nc, uint32_t &ns) {
-        return pv_trace_si(S, in, rng, ph, v, si, si_t, nc, ns, h);
     }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
                          uint32_t &ns) {
@@ -1718,22 +1342,9 @@ struct PvBwdMachine {
     }
     MH_DEV uint64_t main_base() const { return (uint64_t)t * a.main_cap * 4; }
     MH_DEV uint64_t nee_base() const { return (uint64_t)t * a.nee_cap; }
-    // traffic diagnostics (wrong gradients, timing / byte counts only):
-    // MH_EXP_PVB_MAIN_FIXED / MH_EXP_PVB_NEE_FIXED keep every MainLog / NeeLog
-    // entry of a thread at its entry 0 (cache-resident), so the log's HBM bytes drop out
-#ifdef MH_EXP_PVB_MAIN_FIXED
-    static constexpr uint32_t kMainStep = 0;
-#else
-    static constexpr uint32_t kMainStep = 1;
-#endif
-#ifdef MH_EXP_PVB_NEE_FIXED
-    static constexpr uint32_t kNeeStep = 0;
-#else
-    static constexpr uint32_t kNeeStep = 1;
-#endif
     MH_DEV void log_main(State &v, float4 q0, float4 q1, float4 q2, float4 q3) {
         if (v.ml_n >= a.main_cap) { v.ml_over = true; return; }
-        float4 *e = a.main_log + main_base() + (uint64_t)4 * v.ml_n * kMainStep;
+        float4 *e = a.main_log + main_base() + (uint64_t)4 * v.ml_n;
         e[0] = q0;
         e[1] = q1;
         e[2] = q2;
@@ -1775,7 +1386,7 @@ struct PvBwdMachine {
     }
     MH_DEV void walk_step(State &v, V3 p, float coef) {
         if (v.nl_n < a.nee_cap && (v.nl_n == 0 || v.nl_med == v.wmedium)) {
-            a.nee_log[nee_base() + v.nl_n * kNeeStep] = make_float4(p.x, p.y, p.z, coef);
+            a.nee_log[nee_base() + v.nl_n] = make_float4(p.x, p.y, p.z, coef);
             v.nl_med = v.wmedium;
             ++v.nl_n;
         } else {
@@ -1840,17 +1451,14 @@ struct PvBwdMachine {
         return pv_shade(S, in, rng, v, *this);
     }
     MH_DEV uint32_t walk(const DScene &S, Pcg &rng, State &v, WMei &) { return pv_walk(S, rng, v, *this); }
-    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph) {
+    MH_DEV uint32_t medium_step(const DScene &S, const IntegratorParams &in, Pcg &rng, State &v, WMei &, uint32_t ph,
+                                uint32_t &) {
         return pv_medium_step(S, in, rng, v, *this, ph);
     }
     MH_DEV RayT trace_ray(const State &v, uint32_t ph) const { return pv_trace_ray(v, ph); }
     MH_DEV uint32_t trace_hit(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &,
                               const Hit &hh, const RayT &r, uint32_t &nc, uint32_t &ns) {
         return pv_trace_hit(S, in, rng, ph, v, hh, r, nc, ns, *this);
-    }
-    MH_DEV uint32_t trace_si(const DScene &S, const IntegratorParams &in, Pcg &rng, uint32_t ph, State &v, WMei &,
-                             const SI &si, float si_t, uint32_t &nc, uint32_t &ns) {
-        return pv_trace_si(S, in, rng, ph, v, si, si_t, nc, ns, *this);
     }
     MH_DEV uint32_t post(const DScene &S, const LdsBvh &B, const IntegratorParams &in, Pcg &rng, State &v,
                          uint32_t &ns) {
@@ -1884,7 +1492,7 @@ struct PvBwdMachine {
             const float Ko = __shfl(K, (int)o);
             const uint32_t mo = (uint32_t)__shfl((int)med, (int)o);
             if (valid) {
-                const float4 q = a.nee_log[(t0 + o) * a.nee_cap + e * kNeeStep];
+                const float4 q = a.nee_log[(t0 + o) * a.nee_cap + e];
                 sigma_t_backward(S, mo, v3(q.x, q.y, q.z), q.w * Ko, g);
             }
         });
@@ -1896,7 +1504,7 @@ struct PvBwdMachine {
         wave_flat(cnt, flat_scratch(), [&](uint32_t o, uint32_t e, bool valid) {
             const V3 L = v3(__shfl(v.L.x, (int)o), __shfl(v.L.y, (int)o), __shfl(v.L.z, (int)o));
             if (valid) {  // MainLog entry e of thread t0 + o: float4 (t * main_cap + e) * 4
-                const float4 *q = a.main_log + ((t0 + o) * a.main_cap + e * kMainStep) * 4u;
+                const float4 *q = a.main_log + ((t0 + o) * a.main_cap + e) * 4u;
                 pvp_log_entry(S, q[0], q[1], q[2], q[3], L, g);
             }
         });
@@ -1906,6 +1514,7 @@ struct PvBwdMachine {
 #ifndef MH_VS_WAVES
 #define MH_VS_WAVES 2
 #endif
+constexpr uint32_t kVsCtrLookups = 27;  // mh_api.hip kCtrLookups: the density-grid lookups of the launch
 // TRACE as one wave-wide packet traversal with sparse-run deferral (packet scenes)
 #ifndef MH_VS_DEFER
 #define MH_VS_DEFER 1
@@ -1934,170 +1543,13 @@ __host__ __device__ inline uint32_t vs_defer_bytes(const DScene &S) {
 __host__ __device__ inline uint32_t vs_media_bytes(const DScene &S) { return (S.n_media * (uint32_t)sizeof(DMedium) + 15u) & ~15u; }
 __host__ __device__ inline uint32_t vs_tab_bytes(const DScene &S) { return ((S.tab_bytes + 15u) & ~15u) + vs_media_bytes(S); }
 
-// ---------------------------------------------------------------------------
-// The trace server (Srv, round 5).  The packet traversal and the hit's
-// surface interaction were the register peak of the persistent kernel: the
-// whole machine state (VolState, 127 dwords) stayed live across them, so the
-// kernel needed ~236 VGPRs and ran 2 waves per SIMD.  With Srv a workgroup is
-// kSrvM machine waves and kSrvT server waves.  A machine wave never traces: it
-// posts its TRACE lanes' rays to its LDS mailbox and goes on with its other
-// lanes' phases; a server wave packs the posted rays of several machine waves
-// into one 64-lane packet (a packet of incoherent rays costs about the same
-// with 20 or 60 lanes: it enters nearly every leaf either way), traces it,
-// computes each hit's interaction (compute_si) and posts SI + t back.  The
-// two roles are separate branches of the kernel, so its register demand is
-// the larger of the two, not their sum.  Per lane the operations and draws
-// are unchanged (the same traversal and compute_si on the same ray).
-//
-// Mailbox protocol (one word per machine wave, workgroup-scope atomics in
-// LDS): 0 idle -> the machine writes its rays (slot = rank among the posting
-// lanes), the count, then 1 -> a server claims it (3 when several servers)
-// and writes the results, then 2 -> the machine reads its lanes' results in
-// the same slot order and sets 0.  A machine wave has one request in flight;
-// lanes that reach TRACE meanwhile wait for the next.  Waves that leave count
-// into the `finished` word; servers leave when every machine wave has.
-// ---------------------------------------------------------------------------
-#ifndef MH_VS_SRV_M
-#define MH_VS_SRV_M 5  // machine waves per workgroup
-#endif
-#ifndef MH_VS_SRV_T
-#define MH_VS_SRV_T 1  // server waves per workgroup
-#endif
-#ifndef MH_VS_SRV_WAVES
-#define MH_VS_SRV_WAVES 3  // waves per SIMD the Srv kernel is built for
-#endif
-// TRACE weights of the Srv machine: posting a request (cheap) / taking its results
-#ifndef MH_VS_SRV_WP
-#define MH_VS_SRV_WP 8
-#endif
-#ifndef MH_VS_SRV_WC
-#define MH_VS_SRV_WC 64
-#endif
-constexpr uint32_t kSrvM = MH_VS_SRV_M, kSrvT = MH_VS_SRV_T, kSrvThreads = 64u * (kSrvM + kSrvT);
-static_assert(kSrvM >= 1 && kSrvM <= 15 && kSrvT >= 1 && kSrvM + kSrvT <= 16, "trace server workgroup shape");
-constexpr uint32_t kSrvRayDw = 7, kSrvResDw = 23;  // RayT; SI (22 dwords) + si_t
-constexpr uint32_t kPhWaitBit = 0x40u;             // a TRACE lane whose ray is posted
-// LDS after the tables: the servers' packet stacks, the pair records, one
-// deferral scratch per server wave, the mailboxes (flag[16], cnt[15],
-// finished), then per machine wave its posted rays and their results (SoA:
-// dword k of slot s at k * 64 + s)
-struct SrvLayout {
-    uint32_t stack, recs, dscr, box, req, res, end;
-};
-__host__ __device__ inline SrvLayout srv_layout(const DScene &S, uint32_t base) {
-    SrvLayout L;
-    L.stack = align16(base);
-    L.recs = align16(L.stack + 4u * S.stack_size * kSrvT);
-    L.dscr = L.recs + align16(S.n_prims * kPairRecFloats * 4u);
-    L.box = L.dscr + kSrvT * kDeferScratch;
-    L.req = L.box + 128u;
-    L.res = L.req + kSrvM * kSrvRayDw * 64u * 4u;
-    L.end = L.res + kSrvM * kSrvResDw * 64u * 4u;
-    return L;
-}
-MH_DEV void srv_put_si(float *r, const SI &si, float si_t) {
-    const float f[kSrvResDw] = {__uint_as_float(si.valid ? 1u : 0u), si.p.x, si.p.y, si.p.z, si.n.x, si.n.y, si.n.z,
-                                si.s.x, si.s.y, si.s.z, si.t_.x, si.t_.y, si.t_.z, si.sn.x, si.sn.y, si.sn.z,
-                                si.uvx, si.uvy, si.wi.x, si.wi.y, si.wi.z, __uint_as_float(si.shape), si_t};
-#pragma unroll
-    for (uint32_t k = 0; k < kSrvResDw; ++k) r[k * 64u] = f[k];
-}
-MH_DEV void srv_get_si(const float *r, SI &si, float &si_t) {
-    si.valid = __float_as_uint(r[0]) != 0u;
-    si.p = v3(r[64], r[128], r[192]);
-    si.n = v3(r[256], r[320], r[384]);
-    si.s = v3(r[448], r[512], r[576]);
-    si.t_ = v3(r[640], r[704], r[768]);
-    si.sn = v3(r[832], r[896], r[960]);
-    si.uvx = r[1024];
-    si.uvy = r[1088];
-    si.wi = v3(r[1152], r[1216], r[1280]);
-    si.shape = __float_as_uint(r[1344]);
-    si_t = r[1408];
-}
-MH_DEV uint32_t srv_load(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-MH_DEV void srv_store(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); }
-
-// a server wave: until every machine wave of the workgroup has left, take the
-// posted requests that fit one packet, trace them and post the interactions
-template <bool Def>
-MH_DEV void vs_serve(const DScene &S, uint8_t *lb, const SrvLayout &L, uint32_t t) {
-    uint32_t *box = reinterpret_cast<uint32_t *>(lb + L.box);
-    const float *req = reinterpret_cast<const float *>(lb + L.req);
-    float *res = reinterpret_cast<float *>(lb + L.res);
-    uint32_t *ws = reinterpret_cast<uint32_t *>(lb + L.stack) + t * S.stack_size;
-    const float *recs = reinterpret_cast<const float *>(lb + L.recs);
-    uint8_t *dscr = lb + L.dscr + t * kDeferScratch;
-    const uint32_t lane = threadIdx.x & 63u;
-    uint32_t rot = t % kSrvM;  // the first mailbox a scan looks at (rotates: no machine wave starves)
-    while (true) {
-        const uint32_t f = lane < kSrvM ? srv_load(box + lane) : 0u;
-        const uint64_t pend = __builtin_amdgcn_ballot_w64(lane < kSrvM && f == 1u);
-        if (pend == 0) {
-            if (__builtin_amdgcn_readfirstlane(srv_load(box + 31)) >= kSrvM) break;
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        const uint32_t c = ((pend >> lane) & 1u) ? box[16 + lane] : 0u;
-        uint32_t tot = 0, take = 0, myw = 0, myslot = 0;
-        bool act = false;
-        for (uint32_t j = 0; j < kSrvM; ++j) {
-            uint32_t w = rot + j;
-            if (w >= kSrvM) w -= kSrvM;
-            if (!((pend >> w) & 1u)) continue;
-            const uint32_t cw = __builtin_amdgcn_readlane(c, w);
-            if (tot + cw > 64u) continue;
-            if (kSrvT > 1) {  // claim it against the other servers
-                uint32_t ok = 0;
-                if (lane == 0) {
-                    uint32_t e = 1u;
-                    ok = __hip_atomic_compare_exchange_strong(box + w, &e, 3u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
-                }
-                if (!__builtin_amdgcn_readfirstlane(ok)) continue;
-            }
-            take |= 1u << w;
-            if (lane >= tot && lane < tot + cw) {
-                myw = w;
-                myslot = lane - tot;
-                act = true;
-            }
-            tot += cw;
-        }
-        rot = rot + 1u == kSrvM ? 0u : rot + 1u;
-        RayT r{v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 1.f), -1.f};
-        if (act) {
-            const float *q = req + myw * (kSrvRayDw * 64u) + myslot;
-            r.o = v3(q[0], q[64], q[128]);
-            r.d = v3(q[192], q[256], q[320]);
-            r.maxt = q[384];
-        }
-        Hit h;
-        if (Def) h = packet_batch<false, true>(S.nodes, S.prims, S.prim_pairs, S.key_sp, ws, 1u, r, act, recs, dscr);
-        else h = packet_batch<false>(S.nodes, S.prims, S.prim_pairs, S.key_sp, ws, 1u, r, act);
-        if (act) {
-            SI si;
-            float si_t;
-            si_from_hit(S, r, h, si, si_t);
-            srv_put_si(res + myw * (kSrvResDw * 64u) + myslot, si, si_t);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane < kSrvM && ((take >> lane) & 1u)) srv_store(box + lane, 2u);
-    }
-}
-
-#define MH_EXP_STUBBED(b) (Srv && (MH_EXP_STUB & (b)) != 0)
-// dynamic LDS of a Srv launch: the staged tables, then the server's region
-__host__ __device__ inline uint32_t vs_srv_lds_bytes(const DScene &S) { return srv_layout(S, vs_tab_bytes(S)).end; }
-
-template <class M, bool InLds, bool Pk, bool Tab, bool Srv = false>
-__global__ void __launch_bounds__(Srv ? kSrvThreads : 256u, Srv ? MH_VS_SRV_WAVES : MH_VS_WAVES)
+template <class M, bool InLds, bool Pk, bool Tab>
+__global__ void __launch_bounds__(256u, MH_VS_WAVES)
 k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uint64_t n, uint64_t plane,
             float *__restrict__ out, unsigned long long *__restrict__ counters, unsigned long long *__restrict__ work,
             int alpha, VsBwdArgs bw) {
     // samples are handed out in batches of 64 from one device counter (work)
     extern __shared__ uint4 lds[];
-    static_assert(!Srv || (Pk && !M::kDeferEnd), "the trace server runs the packet engine for the primal machines");
     DScene S = S0;
     uint32_t tab = 0;
     if (Tab) {
@@ -2109,26 +1561,8 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         S.media = reinterpret_cast<const DMedium *>(mb);
         tab = vs_tab_bytes(S0) / 16u;
     }
-    uint8_t *const lb = reinterpret_cast<uint8_t *>(lds);
-    SrvLayout SL{};
-    uint32_t *box = nullptr;
-    float *sreq = nullptr, *sres = nullptr;
-    const uint32_t mw = threadIdx.x >> 6;  // this wave of the workgroup
-    if constexpr (Srv) {
-        SL = srv_layout(S0, tab * 16u);
-        if (MH_VS_DEFER) stage_pair_records(S0, reinterpret_cast<float *>(lb + SL.recs));
-        box = reinterpret_cast<uint32_t *>(lb + SL.box);
-        if (threadIdx.x < 32u) box[threadIdx.x] = 0u;
-        __syncthreads();
-        if (mw >= kSrvM) {
-            vs_serve<MH_VS_DEFER != 0>(S, lb, SL, mw - kSrvM);
-            return;
-        }
-        sreq = reinterpret_cast<float *>(lb + SL.req) + mw * (kSrvRayDw * 64u);
-        sres = reinterpret_cast<float *>(lb + SL.res) + mw * (kSrvResDw * 64u);
-    }
-    LdsBvh B = stage_bvh<InLds && !Srv>(S0, lds + tab);
-    if (Pk && MH_VS_DEFER && !Srv) {  // pair records + deferral scratch after the stacks (vs_defer_bytes)
+    LdsBvh B = stage_bvh<InLds>(S0, lds + tab);
+    if (Pk && MH_VS_DEFER) {  // pair records + deferral scratch after the stacks (vs_defer_bytes)
         const uint32_t off = (tab * 16u + S0.lds_bytes_bvh + S0.stack_size * blockDim.x * 4u + 15u) & ~15u;
         float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + off);
         stage_pair_records(S0, recs);
@@ -2142,7 +1576,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     for (uint32_t k = 0; k < kNGroups; ++k) W[k] = (M::kMergeMed && k == kGHead) ? (uint32_t)MH_VS_MERGE_W : W0[k];
     constexpr uint32_t NG = M::kDeferEnd ? kNGroups : kGEnd;  // groups this machine uses
     const float sw = S.inv_width, sh = S.inv_height;
-    uint32_t n_closest = 0, n_shadow = 0;
+    uint32_t n_closest = 0, n_shadow = 0, n_lookups = 0;
     M mc(bw, lm, seed_value);
     typename M::State v;
     WMei wm;
@@ -2181,16 +1615,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 #endif
     while (true) {
         uint32_t cnt[kNGroups];
-        uint32_t g = (M::kMergeMed && ph == kPhWalk) ? (uint32_t)kGHead : ph_group(ph & ~kPhWaitBit);
-        uint32_t fl = 0;  // Srv: this wave's mailbox (0 idle, 1 / 3 posted, 2 results ready)
-        if constexpr (Srv) {
-            fl = __builtin_amdgcn_readfirstlane(srv_load(box + mw));
-            // TRACE lanes post when the mailbox is idle; posted lanes take their
-            // results when they are ready; otherwise both wait (g = kNGroups)
-            if (ph & kPhWaitBit) g = fl == 2u ? (uint32_t)kGTrace : (uint32_t)kNGroups;
-            else if (g == kGTrace && fl != 0u) g = kNGroups;
-            W[kGTrace] = fl == 2u ? (uint32_t)MH_VS_SRV_WC : (uint32_t)MH_VS_SRV_WP;
-        }
+        const uint32_t g = (M::kMergeMed && ph == kPhWalk) ? (uint32_t)kGHead : ph_group(ph);
 #pragma unroll
         for (uint32_t k = 0; k < NG; ++k) cnt[k] = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(g == k));
         if (drained && next >= end) cnt[kGFree] = 0;
@@ -2198,14 +1623,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 #pragma unroll
         for (uint32_t k = 0; k < NG; ++k)
             if (cnt[k] * W[k] > best) { best = cnt[k] * W[k]; sel = k; }
-        if (sel == kNGroups) {
-            // Srv: lanes waiting on the server (or on the mailbox) hold paths
-            if (Srv && __builtin_amdgcn_ballot_w64(g == kNGroups) != 0) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            break;  // no lane holds a path and the range is done
-        }
+        if (sel == kNGroups) break;  // no lane holds a path and the range is done
 #ifdef MH_EXP_VSCNT  // diagnostic build: wave trips, lanes and shader cycles per phase (in registers)
 #pragma unroll
         for (uint32_t k = 0; k < kNGroups; ++k)
@@ -2244,54 +1662,20 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                         out[3 * plane + k] = sx;
                         out[4 * plane + k] = sy;
                     }
-                    if (!MH_EXP_STUBBED(1)) mc.init(S, in, rng, r, v, sx, sy);
+                    mc.init(S, in, rng, r, v, sx, sy);
                     ph = kPhHead;
                 }
             }
             next = std::min<uint64_t>(end, next + (uint64_t)__popcll(m));
         } else if (sel == kGHead) {
-            if (MH_EXP_STUBBED(2)) { if (g == kGHead) ph = (pid & 3u) == 0u ? kPhTraceM : (pid & 3u) == 1u ? kPhScatter : (pid & 3u) == 2u ? kPhSurf : kPhTraceWM; }
-            else if constexpr (M::kMergeMed) {
-                if (g == kGHead) { ph = mc.medium_step(S, in, rng, v, wm, ph); ended = ph == kPhFree; }
+            if constexpr (M::kMergeMed) {
+                if (g == kGHead) { ph = mc.medium_step(S, in, rng, v, wm, ph, n_lookups); ended = ph == kPhFree; }
             } else if (ph == kPhHead) {
                 ph = mc.head(S, in, rng, v);
                 ended = ph == kPhFree;
             }
         } else if (sel == kGTrace) {
-            if constexpr (Srv) {
-                const bool act = g == kGTrace;
-                const uint64_t m = __builtin_amdgcn_ballot_w64(act);
-                const uint32_t slot = (uint32_t)__popcll(m & ((1ull << vw_lane()) - 1ull));
-                if (fl == 0u) {  // post the TRACE lanes' rays
-                    if (act) {
-                        const RayT r = mc.trace_ray(v, ph);
-                        float *q = sreq + slot;
-                        q[0] = r.o.x; q[64] = r.o.y; q[128] = r.o.z;
-                        q[192] = r.d.x; q[256] = r.d.y; q[320] = r.d.z;
-                        q[384] = r.maxt;
-                        ph |= kPhWaitBit;
-                    }
-                    if (vw_lane() == 0) box[16 + mw] = (uint32_t)__popcll(m);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (vw_lane() == 0) srv_store(box + mw, 1u);
-                } else {  // fl == 2: the posted lanes continue from their hits
-                    if (MH_EXP_STUBBED(4)) { if (act) ph = (pid & 3u) == 0u ? kPhHead : (pid & 3u) == 1u ? kPhScatter : (pid & 3u) == 2u ? kPhSurf : kPhWalk; }
-                    else if (act) {
-                        ph &= ~kPhWaitBit;
-                        if constexpr (vs_res_slot<M>::value) {  // reads the interaction from LDS as it needs it
-                            ph = mc.trace_res(S, in, rng, ph, v, sres + slot, n_closest, n_shadow);
-                        } else {
-                            SI si;
-                            float si_t;
-                            srv_get_si(sres + slot, si, si_t);
-                            ph = mc.trace_si(S, in, rng, ph, v, wm, si, si_t, n_closest, n_shadow);
-                        }
-                        ended = ph == kPhFree;
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (vw_lane() == 0) srv_store(box + mw, 0u);
-                }
-            } else if constexpr (Pk && MH_VS_DEFER) {
+            if constexpr (Pk && MH_VS_DEFER) {
                 // every lane of the wave in the traversal (the deferral hands
                 // sparse leaves' (ray, pair) items to all 64 lanes); TRACE lanes
                 // carry their rays, the others ride along inactive
@@ -2309,16 +1693,13 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 ended = ph == kPhFree;
             }
         } else if (sel == kGScatter) {
-            if (MH_EXP_STUBBED(8)) { if (ph == kPhScatter) ph = (pid & 1u) ? kPhWalk : kPhPost; }
-            else if (ph == kPhScatter) { ph = mc.scatter(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhScatter) { ph = mc.scatter(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGSurf) {
-            if (MH_EXP_STUBBED(16)) { if (ph == kPhSurf) ph = (pid & 1u) ? kPhWalk : kPhPost; }
-            else if (ph == kPhSurf) { ph = mc.surf(S, in, rng, v); ended = ph == kPhFree; }
+            if (ph == kPhSurf) { ph = mc.surf(S, in, rng, v); ended = ph == kPhFree; }
         } else if (sel == kGWalk) {
             if (ph == kPhWalk) ph = mc.walk(S, rng, v, wm);
         } else if (sel == kGPost) {
-            if (MH_EXP_STUBBED(32)) { if (ph == kPhPost) ph = (pid & 2u) ? kPhHead : kPhFree; }
-            else if (ph == kPhPost) { ph = mc.post(S, B, in, rng, v, n_shadow); ended = ph == kPhFree; }
+            if (ph == kPhPost) { ph = mc.post(S, B, in, rng, v, n_shadow); ended = ph == kPhFree; }
             if constexpr (M::kDeferEnd) mc.post_wave(S);
         } else if (M::kDeferEnd) {
             if (ph == kPhEnd) {
@@ -2340,12 +1721,11 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         }
 #endif
     }
-    if constexpr (Srv)  // the servers leave once every machine wave has
-        if (vw_lane() == 0) __hip_atomic_fetch_add(box + 31, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     mc.finish();
     if (counters) {
         wave_count(&counters[0], n_closest);
         wave_count(&counters[1], n_shadow);
+        wave_count(&counters[kVsCtrLookups], n_lookups);
     }
 #ifdef MH_EXP_VSCNT
     if (vw_lane() == 0 && counters)
@@ -2410,44 +1790,12 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
     unsigned long long *work = counters + 32;  // the 8 queue heads of this launch (128 B apart)
     hipError_t e = hipMemsetAsync(work, 0, 8 * 128, st);
     if (e != hipSuccess) return e;
-#ifdef MH_EXP_LOOKUPS
-    const unsigned long long zero = 0;
-    if ((e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mh_lookups), &zero, 8, 0, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
-    if ((e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mh_pf_hits), &zero, 8, 0, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
-#endif
-    // the trace server (packet scenes with staged tables), opt-in: MH_VS_SRV=1
-    // (volpath: VolPkMachine; prbvolpath's primal with MH_PV_SRV=1 as well).
-    // Measured slower than the 2-wave kernel: at 3 waves per SIMD the machine
-    // still spills
-    const char *se = getenv("MH_VS_SRV"), *pe = getenv("MH_PV_SRV");
-    const bool srv = pk && tab && se && !strcmp(se, "1") && vs_srv_lds_bytes(S) <= 160u * 1024u &&
-                     (in.type != MH_INTEGRATOR_PRBVOLPATH || (pe && !strcmp(pe, "1")));
-    if (srv) {
-        // grid: the workgroups of kSrvM + kSrvT waves that fill the CUs at MH_VS_SRV_WAVES per SIMD
-        const uint32_t cus = std::max<uint32_t>(1u, grid / (uint32_t)MH_VS_WAVES);
-        const uint32_t g2 = cus * std::max<uint32_t>(1u, (4u * MH_VS_SRV_WAVES) / (kSrvM + kSrvT));
-        if (in.type == MH_INTEGRATOR_PRBVOLPATH)
-            hipLaunchKernelGGL((k_vol_sched<PvMachine, false, true, true, true>), dim3(g2), dim3(kSrvThreads),
-                               vs_srv_lds_bytes(S), st, S, in, lm, seed_value, n, plane, out, counters, work, alpha, VsBwdArgs{});
-        else
-            hipLaunchKernelGGL((k_vol_sched<VolPkMachine, false, true, true, true>), dim3(g2), dim3(kSrvThreads),
-                               vs_srv_lds_bytes(S), st, S, in, lm, seed_value, n, plane, out, counters, work, alpha, VsBwdArgs{});
-    } else if (pk && tab) MH_VS(false, true, true);
+    if (pk && tab) MH_VS(false, true, true);
     else if (pk) MH_VS(false, true, false);
     else if (lds) MH_VS(true, false, false);
     else MH_VS(false, false, false);
 #undef MH_VS
 #undef MH_VS1
-#ifdef MH_EXP_LOOKUPS
-    {
-        unsigned long long nl = 0, nh = 0;
-        if ((e = hipMemcpyFromSymbolAsync(&nl, HIP_SYMBOL(g_mh_lookups), 8, 0, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-            (e = hipMemcpyFromSymbolAsync(&nh, HIP_SYMBOL(g_mh_pf_hits), 8, 0, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-            (e = hipStreamSynchronize(st)) != hipSuccess)
-            return e;
-        fprintf(stderr, "MH_LOOKUPS k_vol_sched samples %llu lookups %llu prefetched %llu\n", (unsigned long long)n, nl, nh);
-    }
-#endif
     return hipGetLastError();
 }
 

@@ -203,12 +203,6 @@ static WfPacked carve_packed(void *ws, void *ws_ext, uint64_t cap) {
 }
 
 MH_DEV uint32_t lane_id() { return threadIdx.x & 63u; }
-// MH_EXP_STATE_L2 (timing experiment, wrong results): the index of a post-trace state load
-#ifdef MH_EXP_STATE_L2
-MH_DEV uint32_t jl_tea(uint32_t j) { return j & 8191u; }
-#else
-MH_DEV uint32_t jl_tea(uint32_t j) { return j; }
-#endif
 
 // Diagnostic build (-DMH_EXP_BPHASE): s_memtime cycles of the fused bounce
 // kernels' phases, summed per wave and added once per wave into g_bph[group]
@@ -322,94 +316,6 @@ MH_DEV bool block_has_range_work(const SegIter &it, uint32_t n) {
     const uint32_t first_wave = (blockIdx.x / kSeg) * (blockDim.x / 64u);
     const uint32_t per = (n + it.nwaves - 1) / it.nwaves;
     return first_wave * per < n;
-}
-
-// MH_WF_DYN (round 5): persistent fused bounce kernels.  A grid of 30
-// workgroups per CU stages the shading tables and pair records into LDS once
-// per workgroup, i.e. once per ~17 loop iterations of each of its waves: 8-13 %
-// of the bounce kernels' wave cycles went to that prologue
-// (profiles/r5_bounce_phases.txt).  With MH_WF_DYN the grid is the resident
-// workgroups only, and a wave takes 64-path batches of its segment from the
-// segment's grab counter (word 16 of the segment's counter line, zeroed with
-// the counters), then -- its segment drained -- of the other segments, its
-// XCD's first, skipping drained ones by a plain load before any atomic.  The
-// survivors of a batch go to the batch's segment, as before.  Measured slower
-// and kept opt-in: bench 1,703-1,717 (grab at the batch) and 1,810-1,812
-// (grab one batch ahead) vs 1,937-1,952 Msamples/s for the 30-per-CU grid on
-// the same boxes -- the grab state costs the 96-VGPR kernels 3-11 spilled
-// registers, and the prologue the phase timers charge overlaps other blocks'
-// waves on the CU
-#ifndef MH_WF_DYN
-#define MH_WF_DYN 0
-#endif
-constexpr uint32_t kGrabWord = 16;
-struct WfGrab {
-    uint32_t home, k, seg, n;  // wave-uniform: home segment, segments tried, current segment and its length
-    uint32_t next;             // lane 0: the batch grabbed one iteration ahead (its atomic's latency hides
-                               // under the current batch; read with readfirstlane when it is due)
-};
-// the k-th segment a wave of home segment h serves: h's XCD's 8 segments
-// (h mod 8 + 8 j) first, then the next XCD's, ... (a bijection of 0..63)
-MH_DEV uint32_t seg_order(uint32_t h, uint32_t k) {
-    return ((((h >> 3) + k) & 7u) << 3) | (((h & 7u) + (k >> 3)) & 7u);
-}
-MH_DEV uint32_t wf_grab(uint32_t *ctr, uint32_t seg) {
-    uint32_t b = 0;
-    if (lane_id() == 0) b = atomicAdd(ctr + seg * 32u + kGrabWord, 64u);
-    return b;
-}
-template <class CountOf>
-MH_DEV void wf_grab_init(uint32_t *ctr, WfGrab &g, uint32_t home, CountOf count_of) {
-    g.home = g.seg = home;
-    g.k = 0;
-    // (readfirstlane: the values are wave-uniform, and said so they stay in
-    // SGPRs instead of taking VGPRs from the 96-register budget)
-    g.n = (uint32_t)__builtin_amdgcn_readfirstlane(count_of(home));
-    g.next = wf_grab(ctr, home);
-}
-template <class CountOf>
-MH_DEV bool wf_next_batch(uint32_t *ctr, WfGrab &g, CountOf count_of, uint32_t &base) {
-    while (true) {
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane(g.next);
-        if (b < g.n) {
-            base = b;
-            g.next = wf_grab(ctr, g.seg);  // the following batch, due at the next call
-            return true;
-        }
-        // this segment is drained: the next one with work left (a plain load
-        // skips drained ones without an atomic on their counter)
-        while (true) {
-            if (++g.k >= kSeg) return false;
-            g.seg = seg_order(g.home, g.k);
-            g.n = (uint32_t)__builtin_amdgcn_readfirstlane(count_of(g.seg));
-            const uint32_t taken = (uint32_t)__builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(ctr + g.seg * 32u + kGrabWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (taken < g.n) break;
-        }
-        g.next = wf_grab(ctr, g.seg);
-    }
-}
-
-// the grid of a persistent (MH_WF_DYN) fused bounce launch: the workgroups
-// resident at `waves` per SIMD (4 waves per workgroup: `waves` per CU), a
-// whole number per segment, at most the caller's grid (whose per-block
-// gradient partials the PRB kernels fill)
-static uint32_t wf_dyn_grid(uint32_t grid, uint32_t waves) {
-#if MH_WF_DYN
-    static const int cus = [] {
-        int dev = 0, c = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-        return std::max(1, c);
-    }();
-    uint32_t g = (uint32_t)cus * waves;
-    if (const char *e = getenv("MH_WF_DYN_BPC")) g = (uint32_t)cus * (uint32_t)std::max(1, atoi(e));
-    g = std::max<uint32_t>(kSeg, g / kSeg * kSeg);
-    return std::min(g, grid);
-#else
-    (void)waves;
-    return grid;
-#endif
 }
 
 // contiguous share of a segment for this wave (refill traversal)
@@ -624,15 +530,9 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         }
         return __hip_atomic_load(ctr + sg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-#if MH_WF_DYN
-    if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = seg_count(it.seg);  // queue statistics
-    WfGrab gb;
-    wf_grab_init(ctr, gb, it.seg, seg_count);
-#else
     const uint32_t n = seg_count(it.seg);
     if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
     if (!block_has_stride_work(it, n)) return;
-#endif
     MH_BPH_DECL
     float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
     stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
@@ -643,14 +543,8 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     const int nxt = cur ^ 1;
     uint32_t n_shadow = 0;
     MH_BPH(7);
-#if MH_WF_DYN
-    uint32_t base = 0;
-    while (wf_next_batch(ctr, gb, seg_count, base)) {
-        const uint32_t seg = gb.seg, n = gb.n;
-#else
     const uint32_t seg = it.seg;
     for (uint32_t base = it.wave * 64u; base < n; base += it.nwaves * 64u) {
-#endif
         const uint32_t sbase = seg * seg_cap;
         MH_BPH_ITER();
         const uint32_t i = base + lane_id();
@@ -699,14 +593,6 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         MH_BPH(0);
         const Hit h = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, ray, has, recs, dscr);
         MH_BPH(1);
-#ifdef MH_EXP_TRACE2  // timing experiment: a second closest-hit trace of the same rays
-        {
-            RayT r2 = ray;
-            asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<false, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, has, recs, dscr);
-            asm volatile("" ::"v"(h2.t), "v"(h2.prim), "v"(h2.u));
-        }
-#endif
         if (has) {
             if (Gen) {
                 tp = v3(1.f, 1.f, 1.f);
@@ -715,11 +601,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 prev_pdf = 1.f;
                 rng.state = gen_state;
             } else {
-#ifdef MH_EXP_STATE_L2  // timing experiment: the post-trace state loads from an L2-resident 8k-path window (wrong results)
-                const uint32_t jl = j & 8191u;
-#else
                 const uint32_t jl = j;
-#endif
                 const float4 q2 = w.pl(cur, 2)[jl], q3 = w.pl(cur, 3)[jl], q4 = w.pl(cur, 4)[jl];
                 tp = v3(q2.x, q2.y, q2.z);
                 prev_pdf = q2.w;
@@ -729,11 +611,7 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
             }
             eta = 1.f;  // diffuse / null BSDFs: eta stays 1, only the camera vertex is delta
             const bool prev_delta = depth == 0;
-#ifdef MH_EXP_STATE_L2
-            rng.inc = Gen ? gen_inc : (((uint64_t)w.tea(cur)[j & 8191u] << 1) | 1u);
-#else
             rng.inc = Gen ? gen_inc : (((uint64_t)w.tea(cur)[j] << 1) | 1u);
-#endif
             SI si;
             compute_si(S, ray, h, si);
 
@@ -822,14 +700,6 @@ k_wf_bounce(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         // ---- visibility of the NEE sample (scene.cpp:201-210)
         const Hit sh = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
         MH_BPH(4);
-#ifdef MH_EXP_SHADOW2  // timing experiment: a second shadow trace of the same rays
-        {
-            RayT r2 = sray;
-            asm volatile("" : "+v"(r2.maxt));
-            const Hit h2 = packet_batch<true, true>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, r2, shadow, recs, dscr);
-            asm volatile("" ::"v"(h2.shape));
-        }
-#endif
         if (shadow && sh.shape == MH_INVALID) L = fma3(a_nee, b_nee, L);
         n_shadow += (uint32_t)__popcll(__ballot(shadow));
         // ---- radiance: survivors carry it on, finished paths -> sample planes
@@ -935,7 +805,7 @@ static hipError_t launch_wavefront_pass(const DScene &S, const IntegratorParams 
             // round-3 build recorded the other 2 n_bounces - 2 events empty
             // after it, ~75 us of idle GPU per chunk)
             if (trace_ev && b == 0) (void)hipEventRecord(trace_ev[0], st);
-            const uint32_t gd = wf_dyn_grid(grid, MH_BOUNCE_WAVES);
+            const uint32_t gd = grid;
             if (b == 0)
                 hipLaunchKernelGGL(k_wf_bounce<true>, dim3(gd), dim3(256), fused_lds_bytes(S), st, S,
                                    in, lm, seed_value, plane, out, pk, cur, seg_cap, c, cn, n, carry, pass, alpha);
@@ -1363,15 +1233,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
         }
         return __hip_atomic_load(ctr + sg * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-#if MH_WF_DYN
-    if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = seg_count(it.seg);  // queue statistics
-    WfGrab gb;
-    wf_grab_init(ctr, gb, it.seg, seg_count);
-#else
     const uint32_t n = seg_count(it.seg);
     if (Gen && blockIdx.x < kSeg && threadIdx.x == 0) ctr[it.seg * 32] = n;  // queue statistics
     if (!block_has_stride_work(it, n)) return;
-#endif
     MH_BPH_DECL
     float *recs = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(lds) + fused_pairs_offset(S0));
     stage_pair_records(S0, recs);  // made visible by stage_tables' barrier
@@ -1386,17 +1250,10 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
 #pragma unroll
     for (int kk = 0; kk < NR; ++kk) acc[kk][0] = acc[kk][1] = acc[kk][2] = 0.f;
     MH_BPH(7);
-#if MH_WF_DYN
-    uint32_t base = 0;
-    while (wf_next_batch(ctr, gb, seg_count, base)) {
-        const uint32_t seg = gb.seg, n = gb.n;
-        const uint32_t i = base + lane_id();
-#else
     const uint32_t seg = it.seg;
     const uint32_t n_iter = (n + it.nwaves * 64u - 1) / (it.nwaves * 64u);  // wave-uniform
     for (uint32_t itr = 0; itr < n_iter; ++itr) {
         const uint32_t i = (itr * it.nwaves + it.wave) * 64u + lane_id();
-#endif
         const uint32_t sbase = seg * seg_cap;
         MH_BPH_ITER();
         bool alive = false, shadow = false;
@@ -1430,15 +1287,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                                  __builtin_fmaf(sy, S0.inv_height, -0.f));
                 gen_state = g.state;
                 gen_inc = g.inc;  // the TEA of this lane, reused below
-#ifdef MH_EXP_NO_GATHER  // diagnostic: cost of the first bounce's dL gather
-                { const float4 g = reinterpret_cast<const float4 *>(gen.grad_in)[px + py * S0.width]; dL = v3(g.x, g.y, g.z); }
-#else
-#ifdef MH_EXP_SGPR_GATHER  // the scalar-cache gather (taps in SGPRs)
-                dL = gather_dL_wave(S0, gen.coalesce, gen.grad_in, sx, sy);
-#else
                 dL = gather_dL_wave_lds(S0, gen.coalesce, gen.grad_in, sx, sy, dscr);
-#endif
-#endif
             } else {
                 const uint32_t pd = w.pd[cur][j];
                 pid = pd & kPidMask;
@@ -1461,11 +1310,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 for (int kk = 0; kk < NR; ++kk) A[kk][0] = A[kk][1] = A[kk][2] = 0.f;
                 rng.state = gen_state;
             } else {
-#ifdef MH_EXP_STATE_L2  // timing experiment (see k_wf_bounce)
-                const uint32_t jl = j & 8191u;
-#else
                 const uint32_t jl = j;
-#endif
                 beta = v3(w.bx[cur][jl], w.by[cur][jl], w.bz[cur][jl]);
                 prev_p = v3(w.ppx[cur][jl], w.ppy[cur][jl], w.ppz[cur][jl]);
                 prev_pdf = w.ppdf[cur][jl];
@@ -1488,7 +1333,7 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
             }
             const bool prev_delta = depth == 0;  // diffuse / null BSDFs: only the camera vertex is delta
             const float eta = 1.f;
-            rng.inc = Gen ? gen_inc : (((uint64_t)q.tea(cur)[Gen ? j : jl_tea(j)] << 1) | 1u);
+            rng.inc = Gen ? gen_inc : (((uint64_t)q.tea(cur)[j] << 1) | 1u);
             SI si;
             compute_si(S, ray, h, si);
             const uint32_t b = si.valid ? S.shapes[si.shape].bsdf : MH_INVALID;
@@ -1611,14 +1456,9 @@ k_wf_bounce_prb(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value,
                 }
         }
         // ---- visibility of the NEE sample; the record is charged if unoccluded
-#ifdef MH_EXP_NO_SHADOW  // timing experiment: no shadow traversal (every NEE sample unoccluded; wrong gradients)
-        Hit sh;
-        sh.shape = MH_INVALID;
-#else
         MH_BPH(3);
         const Hit sh = packet_batch<true, true, Gen>(S0.nodes, S0.prims, S0.prim_pairs, S0.key_sp, ws, 1u, sray, shadow, recs, dscr);
         MH_BPH(4);
-#endif
         const bool unocc = shadow && sh.shape == MH_INVALID;
         if (unocc) {
             float (&ga)[NR][3] = Det ? Pp : acc;
@@ -1922,6 +1762,7 @@ struct WfBmpTex {
     unsigned long long *acc64;
     uint32_t *fx_max;
     double scale;
+    unsigned long long *n_rec;  // += records read (nullptr: not counted)
 };
 // the InLds accumulator: double (ds_add_f64 runs ~7x the rate of ds_add_f32
 // on gfx950, mh_shading.hpp), or float with MH_SCAT_F64=0
@@ -1958,6 +1799,7 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
                    lane = threadIdx.x & 63u;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     const DTexture tx0 = S.textures[bt.tex[0]];
+    uint32_t n_recs = 0;  // this lane's records (mh_stats.aux_items)
 #ifndef MH_SCAT_BAL  // float accumulators, 3 workgroups per CU: 2.44 vs 2.23 ms without; double, 1 per CU: 1.36 vs 1.39
 #define MH_SCAT_BAL MH_SCAT_F64
 #endif
@@ -1980,6 +1822,7 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
             mask = __float_as_uint(f0.w);
             if (mask) f1 = bm.fin[bm.stride + pid];
         }
+        n_recs += (uint32_t)__popc(mask);
         const V3 Ltot = v3(f0.x, f0.y, f0.z), dL = v3(f1.x, f1.y, f1.z);
         // the next record's loads are issued before this record's adds
         bool on = mask != 0;
@@ -2076,11 +1919,9 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
         }
       }
     }
+    if (bt.n_rec && Fx != 1) wave_count(bt.n_rec, n_recs);
     if (InLds) {
         __syncthreads();
-#ifdef MH_EXP_NO_FLUSH  // diagnostic: cost of the per-workgroup flush
-        if (blockIdx.x == 0)
-#endif
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x)
             if (acc[i] != (ScatT)0) atomicAdd(grad + i, (float)acc[i]);
     }
@@ -2181,7 +2022,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     if (span) (void)hipEventRecord(span[0], st);
 #define MH_BOUNCE_PRB(NR, GEN, BM, DET)                                                                        \
     hipLaunchKernelGGL((k_wf_bounce_prb<NR, GEN, BM, DET>),                                                    \
-                       dim3(wf_dyn_grid(grid, BM ? MH_BOUNCE_BMP_WAVES : MH_BOUNCE_PRB_WAVES)), dim3(256),      \
+                       dim3(grid), dim3(256),      \
                        sh_fused, st, S, in, lm, seed_value, w, q, cur, seg_cap, c, cn, gen, bm, det)
 #define MH_BOUNCE_PRB_NR(GEN, BM, DET)                                                                         \
     do {                                                                                                       \
@@ -2228,16 +2069,28 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
     }
 #undef MH_BOUNCE_PRB_NR
 #undef MH_BOUNCE_PRB
+    if (span) (void)hipEventRecord(span[1], st);  // the bounce span; span[1] -> span[2]: the scatter
     if (with_bmp) {
         const size_t acc_bytes = std::max<size_t>((size_t)bmp->n_floats * kScatAccBytes, 1);
         const bool in_lds = (size_t)bmp->n_floats * 4 <= bmp->lds_max && acc_bytes <= bmp->wg_lds;
-        const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(8, bmp->cu_lds / acc_bytes));
+        // accumulators per CU: as many as its LDS holds, at most the workgroups
+        // of kScatThreads that are resident at once (more would only zero and
+        // flush extra LDS copies)
+        static int resident = 0;
+        if (!resident && hipOccupancyMaxActiveBlocksPerMultiprocessor(&resident, k_wf_bitmap_scatter<true>, kScatThreads,
+                                                                      0) != hipSuccess) {
+            (void)hipGetLastError();
+            resident = 0;
+        }
+        const uint32_t per_cu = (uint32_t)std::max<size_t>(
+            1, std::min<size_t>(resident > 0 ? (size_t)resident : 8u, std::min<size_t>(8, bmp->cu_lds / acc_bytes)));
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->cus * per_cu, (uint32_t)((n + 4095) / 4096)));
         WfBmpTex bt;
         for (int b = 0; b < kMaxBitmapParams; ++b) { bt.tex[b] = bmp->tex[b]; bt.off[b] = bmp->off[b]; }
         bt.acc64 = bmp->fx_acc;
         bt.fx_max = bmp->fx_word;
         bt.scale = 0.0;
+        bt.n_rec = bmp->n_rec;
         const dim3 g_all((uint32_t)((n + 4095) / 4096));
         if (bmp->fx_acc) {  // deterministic: max pass, then int64 pass, then fold (this chunk's own scale)
             e = hipMemsetAsync(bmp->fx_word, 0, 4, st);
@@ -2267,7 +2120,7 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
             hipLaunchKernelGGL(k_wf_bitmap_scatter<false>, dim3((uint32_t)((n + 4095) / 4096)), dim3(256), 0, st, S,
                                bt, bm, (uint32_t)n, bmp->grad, bmp->n_floats);
     }
-    if (span) (void)hipEventRecord(span[1], st);
+    if (span) (void)hipEventRecord(span[2], st);
     if (det_on) {
         hipLaunchKernelGGL(k_wf_det_sum, dim3(kDetBlocks), dim3(256), 0, st, det, (uint32_t)(seg_cap * kSeg), n_rgb * 3);
         hipLaunchKernelGGL(k_wf_det_fold, dim3(1), dim3(64), 0, st, det, n_rgb * 3, partial);

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 INVALID = 0xFFFFFFFF
 
 # status codes
@@ -126,7 +126,8 @@ class Integrator(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("samples", u64), ("rays_closest", u64), ("rays_shadow", u64), ("bounces", u64),
                 ("ms_total", f64), ("ms_kernel", f64), ("ms_trace", f64), ("n_trace_launches", u64),
-                ("mode", u32), ("invalid_samples", u32)]
+                ("mode", u32), ("invalid_samples", u32), ("grid_lookups", u64), ("aux_items", u64),
+                ("ms_aux", f64), ("n_aux_launches", u64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

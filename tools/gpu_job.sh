@@ -16,6 +16,7 @@
 #   rocprof <out> [bench args]    rocprofv3 --kernel-trace --stats of bench.py
 #   vol [args]                    tools/bench_volpath.py (config 4) with the given args
 #   mesh [args]                   tools/bench_mesh.py --tris 1000000,4000000 (large-mesh path)
+#   gloo2                         bench.py --gpus 2 --backend gloo: the launcher starts 2 ranks on the one GPU
 # Outputs go to gpurun_out/job_<job>_*.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -69,6 +70,9 @@ rocprof)
     ;;
 vol)
     timeout -k 10 300 python tools/bench_volpath.py --no-cpu "$@" > gpurun_out/job_vol.json 2> gpurun_out/job_vol.err || exit 1
+    ;;
+gloo2)
+    timeout -k 10 400 python bench.py --gpus 2 --backend gloo --no-cpu --steps 3 --warmup 1 > gpurun_out/job_gloo2.json 2> gpurun_out/job_gloo2.err || exit 1
     ;;
 mesh)
     timeout -k 10 300 python tools/bench_mesh.py --tris 1000000,4000000 --steps 3 "$@" > gpurun_out/job_mesh.txt 2>&1 || exit 1

@@ -2,10 +2,8 @@
 """Roofline line of k_vol_sched (config 4 volpath) from one profile directory.
 
 Inputs (written by tools/profile_volsched.sh on the GPU box):
-  <dir>/lookups.err  -- `MH_LOOKUPS k_vol_sched samples N lookups L` lines of the
-                        MH_EXP_LOOKUPS diagnostic build (device-counted density-grid
-                        lookups per launch; results are bit-identical to the release
-                        build, so the count is the release kernel's too)
+  <dir>/lookups.json -- bench.py --config 4's line: its roofline carries the release
+                        kernel's device-counted density-grid lookups (mh_stats.grid_lookups)
   <dir>/pmc.json     -- tools/make_pmc.py over the release build's rocprofv3 passes
                         (average launch duration, calibrated FETCH x2 + WRITE bytes)
 
@@ -14,18 +12,15 @@ Algorithmic bytes per launch = L x 32 B (the 8 float taps of a trilinear lookup)
 """
 import json
 import os
-import re
 import sys
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
 def main(d):
-    lines = [ln for ln in open(os.path.join(d, "lookups.err")) if ln.startswith("MH_LOOKUPS")]
-    if not lines:
-        sys.exit("no MH_LOOKUPS line (was the diagnostic library loaded?)")
-    m = re.search(r"samples (\d+) lookups (\d+)", lines[-1])
-    n, lookups = int(m.group(1)), int(m.group(2))
+    line = json.loads(open(os.path.join(d, "lookups.json")).read().strip().splitlines()[-1])
+    rf = line["roofline"]
+    n, lookups = int(rf["samples"]) // max(1, int(rf["launches_per_step"])), int(rf["grid_lookups"]) // max(1, int(rf["launches_per_step"]))
     pmc = json.load(open(os.path.join(d, "pmc.json")))["kernels"]
     name = next(k for k in pmc if k.startswith("k_vol_sched<VolMachine"))
     k = pmc[name]
