@@ -42,6 +42,21 @@ static __device__ unsigned long long g_mh_guard[kGuardCount];
     } while (0)
 #endif
 
+// Atomic adds to device (global) memory through a generic pointer, emitted as
+// global_atomic_*.  For a pointer it cannot prove global (loaded from a
+// struct or a pointer table) the compiler emits flat_atomic_*, and a flat
+// operation counts in lgkmcnt as well as vmcnt: every later LDS wait of the
+// wave then waits for the atomic's round trip to memory (round 6: the
+// prbvolpath backward's corner scatters, the bitmap / film scatters).
+typedef __attribute__((address_space(1))) float g_float;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+MH_DEV void gatomic_add(float *p, float v) {
+    __hip_atomic_fetch_add((g_float *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+MH_DEV void gatomic_add(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_fetch_add((g_u64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInvPi = 0.31830988618379067154f;
 constexpr float kRayEps = 1500.0f * 5.9604644775390625e-08f;  // core/math.h:18-23

@@ -818,7 +818,7 @@ k_prb_backward(DScene S, IntegratorParams in, LaneMap lm, uint32_t seed_value, u
         __syncthreads();
         float *dst = ga.bufs[ga.lds_slot];
         for (uint32_t i = threadIdx.x; i < ga.lds_floats; i += blockDim.x)
-            if (tex_acc[i] != 0.f) atomicAdd(dst + i, tex_acc[i]);
+            if (tex_acc[i] != 0.f) gatomic_add(dst + i, tex_acc[i]);
     }
     flush_small_slots(g, ga);
     if (counters) {

@@ -779,7 +779,11 @@ MH_DEV bool rect_separated(float lz, float ldz, float bound) {
     // (+ 1e-30: |lz| above it keeps -lz / ldz clear of underflow to -0,
     // which would pass the exact test's t >= 0).  Shadow rays only: a closest
 // ray's bound is its best hit so far, infinite until it has one.
-    const float m = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ldz), bound, __builtin_fabsf(lz)), 0x1p-20f, 1e-30f);
+    // the margin takes the bound as at least FLT_MIN: |lz| > m >= |ldz| 2^-146
+    // keeps |lz / ldz| above 2^-146, so the exact test's quotient cannot
+    // underflow to a (passing) -0 when the bound is subnormal
+    const float m = __builtin_fmaf(__builtin_fmaf(__builtin_fabsf(ldz), __builtin_fmaxf(bound, 0x1p-126f),
+                                                  __builtin_fabsf(lz)), 0x1p-20f, 1e-30f);
     return ((lz > m) & (s1 > m)) | ((lz < -m) & (s1 < -m));
 }
 template <bool Shadow, bool Pre = true>
@@ -1754,7 +1758,7 @@ MH_DEV void bmp_add_fx(const GradCtx &g, int32_t k, const float *dst, float v) {
         return;
     }
     const double sc = reinterpret_cast<const double *>(reinterpret_cast<const uint8_t *>(g.fx_max) + 64)[k];
-    atomicAdd(reinterpret_cast<unsigned long long *>(g.fx_i64 + (dst - g.fx_f32)),
+    gatomic_add(reinterpret_cast<unsigned long long *>(g.fx_i64 + (dst - g.fx_f32)),
               (unsigned long long)__double2ll_rn((double)v * sc));
 }
 MH_DEV void acc_add(GradCtx &g, int32_t k, V3 a) {
@@ -1896,11 +1900,11 @@ MH_DEV void tex_backward(const DScene &S, uint32_t tex, float uvx, float uvy, V3
             continue;
         }
         if (tx.channels == 3) {
-            atomicAdd(buf + base + 0, adj.x * w[j]);
-            atomicAdd(buf + base + 1, adj.y * w[j]);
-            atomicAdd(buf + base + 2, adj.z * w[j]);
+            gatomic_add(buf + base + 0, adj.x * w[j]);
+            gatomic_add(buf + base + 1, adj.y * w[j]);
+            gatomic_add(buf + base + 2, adj.z * w[j]);
         } else {
-            atomicAdd(buf + base, (adj.x + adj.y + adj.z) * w[j]);
+            gatomic_add(buf + base, (adj.x + adj.y + adj.z) * w[j]);
         }
     }
 }
@@ -3022,9 +3026,9 @@ MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8], const 
         const uint32_t cc = __float_as_uint(sc[src * 9]);
         if (g.fx_mode == 2) {
             const long long q = __double2ll_rn((double)sc[src * 9 + 1 + c] * g.fx_scale);
-            atomicAdd(reinterpret_cast<unsigned long long *>(cb) + (size_t)cc * 8 + c, (unsigned long long)q);
+            gatomic_add(reinterpret_cast<unsigned long long *>(cb) + (size_t)cc * 8 + c, (unsigned long long)q);
         } else {
-            unsafeAtomicAdd(cb + (size_t)cc * 8 + c, sc[src * 9 + 1 + c]);
+            gatomic_add(cb + (size_t)cc * 8 + c, sc[src * 9 + 1 + c]);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -3078,7 +3082,7 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
             g.fsum += (as * w) * buf[idx];
             continue;
         }
-        unsafeAtomicAdd(buf + idx, as * w);
+        gatomic_add(buf + idx, as * w);
     }
 }
 
@@ -3584,7 +3588,7 @@ MH_DEV void flush_small_slots(GradCtx &g, const GradArgs &ga) {
         if (j < 3u * ga.n_rgb) {
             const unsigned long long v = fx_wave_sums()[j];
             unsigned long long *w = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(g.fx_max) + 192);
-            if (v) atomicAdd(w + j, v);
+            if (v) gatomic_add(w + j, v);
         }
         return;
     }
@@ -3596,7 +3600,7 @@ MH_DEV void flush_small_slots(GradCtx &g, const GradArgs &ga) {
             float v = c == 0 ? a.x : c == 1 ? a.y : a.z;
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(ga.bufs[slot] + c, v);
+            if ((threadIdx.x & 63) == 0 && v != 0.f) gatomic_add(ga.bufs[slot] + c, v);
         }
     }
 }

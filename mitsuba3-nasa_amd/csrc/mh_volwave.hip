@@ -1317,8 +1317,28 @@ struct PvBwdState : PvState {
     bool ml_over, nl_over;
 };
 
+#ifdef MH_EXP_VSCNT
+// diagnostic build: PvBwdMachine's POST / END sub-phases (s_memtime cycles per
+// wave, summed over the waves; read by mh_exp_vs_sub):
+//   [0] POST per-lane code (pv_post)      [1] POST wave loop (post_wave)
+//   [2]   its NeeLog entry loads           [3]   its sigma_t scatters
+//   [4]   NeeLog entries charged           [5] END per-lane code (end)
+//   [6] END wave loop (end_wave)           [7]   its MainLog entry loads
+//   [8]   its log-entry charges            [9]   MainLog entries charged
+//   [10] post_wave loop steps              [11] end_wave loop steps
+__device__ unsigned long long g_vs_sub[16];
+#define MH_VS_SUB_DECL uint64_t sub[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define MH_VS_SUB(k, v) (sub[k] += (uint64_t)(v))
+#define MH_VS_T() __builtin_amdgcn_s_memtime()
+#define MH_VS_SUB_AT(m, k, v) ((m).sub[k] += (uint64_t)(v))
+#else
+#define MH_VS_SUB_DECL
+#define MH_VS_SUB(k, v) ((void)0)
+#define MH_VS_T() 0ull
+#endif
 struct PvBwdMachine {
     using State = PvBwdState;
+    MH_VS_SUB_DECL
     // the end-of-path log application is a phase of its own (kPhEnd): run
     // when a path ends, it would hold the wave for the few lanes that ended
     static constexpr bool kPrb = true, kWritesPos = false, kDeferEnd = true, kMergeMed = MH_PVB_MERGE != 0;
@@ -1491,10 +1511,21 @@ struct PvBwdMachine {
         wave_flat(cnt, flat_scratch(), [&](uint32_t o, uint32_t e, bool valid) {
             const float Ko = __shfl(K, (int)o);
             const uint32_t mo = (uint32_t)__shfl((int)med, (int)o);
+            const uint64_t ta = MH_VS_T();
             if (valid) {
                 const float4 q = a.nee_log[(t0 + o) * a.nee_cap + e];
+#ifdef MH_EXP_VSCNT
+                asm volatile("" ::"v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w));  // the load's wait here
+                MH_VS_SUB(2, MH_VS_T() - ta);
+#endif
+                const uint64_t tb = MH_VS_T();
                 sigma_t_backward(S, mo, v3(q.x, q.y, q.z), q.w * Ko, g);
+                MH_VS_SUB(3, MH_VS_T() - tb);
+                (void)tb;
             }
+            MH_VS_SUB(4, __popcll(__ballot(valid)));
+            MH_VS_SUB(10, 1);
+            (void)ta;
         });
     }
     MH_DEV void end_wave(const DScene &S, const State &v) {
@@ -1503,12 +1534,31 @@ struct PvBwdMachine {
         pend_main = 0;
         wave_flat(cnt, flat_scratch(), [&](uint32_t o, uint32_t e, bool valid) {
             const V3 L = v3(__shfl(v.L.x, (int)o), __shfl(v.L.y, (int)o), __shfl(v.L.z, (int)o));
+            const uint64_t ta = MH_VS_T();
             if (valid) {  // MainLog entry e of thread t0 + o: float4 (t * main_cap + e) * 4
                 const float4 *q = a.main_log + ((t0 + o) * a.main_cap + e) * 4u;
+#ifdef MH_EXP_VSCNT
+                const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+                asm volatile("" ::"v"(q0.x), "v"(q1.x), "v"(q2.x), "v"(q3.x), "v"(q3.w));
+                MH_VS_SUB(7, MH_VS_T() - ta);
+                const uint64_t tb = MH_VS_T();
+                pvp_log_entry(S, q0, q1, q2, q3, L, g);
+                MH_VS_SUB(8, MH_VS_T() - tb);
+#else
                 pvp_log_entry(S, q[0], q[1], q[2], q[3], L, g);
+#endif
             }
+            MH_VS_SUB(9, __popcll(__ballot(valid)));
+            MH_VS_SUB(11, 1);
+            (void)ta;
         });
     }
+#ifdef MH_EXP_VSCNT
+    MH_DEV void sub_flush() {
+        if ((threadIdx.x & 63u) == 0)
+            for (int k = 0; k < 12; ++k) atomicAdd(&g_vs_sub[k], sub[k]);
+    }
+#endif
 };
 
 #ifndef MH_VS_WAVES
@@ -1699,14 +1749,38 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         } else if (sel == kGWalk) {
             if (ph == kPhWalk) ph = mc.walk(S, rng, v, wm);
         } else if (sel == kGPost) {
+#ifdef MH_EXP_VSCNT
+            const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+#endif
             if (ph == kPhPost) { ph = mc.post(S, B, in, rng, v, n_shadow); ended = ph == kPhFree; }
-            if constexpr (M::kDeferEnd) mc.post_wave(S);
+            if constexpr (M::kDeferEnd) {
+#ifdef MH_EXP_VSCNT
+                const uint64_t tp1 = __builtin_amdgcn_s_memtime();
+                mc.post_wave(S);
+                MH_VS_SUB_AT(mc, 0, tp1 - tp0);
+                MH_VS_SUB_AT(mc, 1, __builtin_amdgcn_s_memtime() - tp1);
+#else
+                mc.post_wave(S);
+#endif
+            }
         } else if (M::kDeferEnd) {
+#ifdef MH_EXP_VSCNT
+            const uint64_t te0 = __builtin_amdgcn_s_memtime();
+#endif
             if (ph == kPhEnd) {
                 mc.end(S, B, in, out, plane, pid, v, alpha, n_closest, n_shadow);
                 ph = kPhFree;
             }
-            if constexpr (M::kDeferEnd) mc.end_wave(S, v);
+            if constexpr (M::kDeferEnd) {
+#ifdef MH_EXP_VSCNT
+                const uint64_t te1 = __builtin_amdgcn_s_memtime();
+                mc.end_wave(S, v);
+                MH_VS_SUB_AT(mc, 5, te1 - te0);
+                MH_VS_SUB_AT(mc, 6, __builtin_amdgcn_s_memtime() - te1);
+#else
+                mc.end_wave(S, v);
+#endif
+            }
         }
         if (ended) {
             if (M::kDeferEnd) ph = kPhEnd;
@@ -1722,6 +1796,9 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
 #endif
     }
     mc.finish();
+#ifdef MH_EXP_VSCNT
+    if constexpr (M::kDeferEnd) mc.sub_flush();
+#endif
     if (counters) {
         wave_count(&counters[0], n_closest);
         wave_count(&counters[1], n_shadow);
@@ -1798,6 +1875,17 @@ hipError_t launch_vol_sched(const DScene &S, const IntegratorParams &in, const L
 #undef MH_VS1
     return hipGetLastError();
 }
+
+#ifdef MH_EXP_VSCNT
+extern "C" int mh_exp_vs_sub(unsigned long long *out, int reset) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_vs_sub), sizeof(g_vs_sub));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        hipMemcpyToSymbol(HIP_SYMBOL(g_vs_sub), z, sizeof(z));
+    }
+    return 0;
+}
+#endif
 
 // prbvolpath's single-pass backward on the phase scheduler: n samples of the
 // lane map, gradients into bw.ga's slot buffers (k_prbvol_backward's Mode 2)

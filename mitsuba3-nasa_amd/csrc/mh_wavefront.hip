@@ -1896,8 +1896,8 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
                     const float val = st[src * 16 + 4 + k * 3 + c];
                     if constexpr (Fx == 1) fx_mx = fmaxf(fx_mx, fabsf(val));
                     else if constexpr (Fx == 2)
-                        atomicAdd(bt.acc64 + base + c, (unsigned long long)__double2ll_rn((double)val * bt.scale));
-                    else atomicAdd(grad + base + c, val);
+                        gatomic_add(bt.acc64 + base + c, (unsigned long long)__double2ll_rn((double)val * bt.scale));
+                    else gatomic_add(grad + base + c, val);
                 }
                 __builtin_amdgcn_wave_barrier();
             } else {
@@ -1923,7 +1923,7 @@ k_wf_bitmap_scatter(DScene S, WfBmpTex bt, WfBmp bm, uint32_t n, float *__restri
     if (InLds) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < n_floats; i += blockDim.x)
-            if (acc[i] != (ScatT)0) atomicAdd(grad + i, (float)acc[i]);
+            if (acc[i] != (ScatT)0) gatomic_add(grad + i, (float)acc[i]);
     }
     if constexpr (Fx == 1) {
 #pragma unroll

@@ -403,7 +403,9 @@ def render(scene: Scene, params: Optional[SceneParameters] = None, sensor: int =
     return _render_op().apply(scene, params, keys, integrator, (seed, seed_grad), (spp, spp_grad), *values)
 
 
-def render_1(scene: Scene, sensor: int = 0, seed: int = 0, spp: int = 0, integrator: Optional[Integrator] = None):
+def render_1(scene: Scene, params: Optional[SceneParameters] = None, sensor: int = 0,
+             integrator: Optional[Integrator] = None, seed: int = 0, seed_grad: int = 0,
+             spp: int = 0, spp_grad: int = 0):
     """The fork's radiance-meter loop: every pixel's radiance summed into one
     Spectrum, normalised by 1 / (W H spp).  In an RGB variant (hip_ad_rgb
     mirrors llvm_ad_rgb) the two reference implementations differ:
@@ -415,12 +417,24 @@ def render_1(scene: Scene, sensor: int = 0, seed: int = 0, spp: int = 0, integra
       returns Spectrum(0) * nf: its accumulation exists for monochromatic and
       spectral modes only ("Never use render_1() in RGB mode", :180-181).
 
+    The signature and argument checks are mi.render_1's (util.py:627-669):
+    (scene, params, sensor, integrator, seed, seed_grad, spp, spp_grad).
     Returns a (3,) float32 tensor on the device for the AD integrators."""
+    if params is not None and not isinstance(params, SceneParameters):
+        raise A.MitsubaHipError("params should be an instance of mi.SceneParameter!")
     integrator = integrator or scene.integrator()
-    if integrator is None or integrator.type not in ("prb", "prbvolpath"):
-        raise A.MitsubaHipError("This render loop only supports monochromatic and spectral modes!")
+    if integrator is None:
+        raise A.MitsubaHipError("No integrator specified! Add an integrator in the scene "
+                                "description or provide an integrator directly as argument.")
+    if not isinstance(sensor, int):
+        raise A.MitsubaHipError("hip_ad_rgb: the sensor is given by its index (only sensor 0 exists)")
     if sensor != 0:
         raise A.MitsubaHipError("hip_ad_rgb: only sensor index 0 is supported")
+    if seed_grad != 0 and seed_grad == seed:
+        raise A.MitsubaHipError("The primal and differential seed should be different to ensure "
+                                "unbiased gradient computation!")
+    if integrator.type not in ("prb", "prbvolpath"):
+        raise A.MitsubaHipError("This render loop only supports monochromatic and spectral modes!")
     torch = _torch()
     spp = spp or scene.sample_count()
     film = render_film(scene, integrator, seed, spp)  # the primal pass (common.py:141-153)

@@ -111,7 +111,18 @@ def test_render_1_prb_returns_zero_spectrum_in_rgb(monkeypatch):
     for t in ("prb", "prbvolpath"):
         out = mi.render_1(sc, seed=3, spp=4, integrator=mi.load_dict({"type": t}))
         assert out.shape == (3,) and out.dtype == torch.float32 and float(out.abs().sum()) == 0.0
-    assert calls == [("prb", 3, 4), ("prbvolpath", 3, 4)]
+    assert calls[:2] == [("prb", 3, 4), ("prbvolpath", 3, 4)]
+    # mi.render_1's own signature (util.py:627-634): params second, positionally
+    params = mi.traverse(sc)
+    out = mi.render_1(sc, params, 0, mi.load_dict({"type": "prb"}), 5, 0, 8, 8)
+    assert out.shape == (3,) and float(out.abs().sum()) == 0.0
+    assert calls[-1] == ("prb", 5, 8)
+    out = mi.render_1(sc, params=params, integrator=mi.load_dict({"type": "prb"}), seed=1, seed_grad=2, spp_grad=4)
+    assert calls[-1] == ("prb", 1, sc.sample_count())
+    with pytest.raises(RuntimeError, match="should be different"):
+        mi.render_1(sc, params, integrator=mi.load_dict({"type": "prb"}), seed=3, seed_grad=3)
+    with pytest.raises(RuntimeError, match="SceneParameter"):
+        mi.render_1(sc, {"a": 1}, integrator=mi.load_dict({"type": "prb"}))
     with pytest.raises(RuntimeError, match="monochromatic and spectral"):  # path keeps the C++ behaviour
         mi.render_1(sc, integrator=mi.load_dict({"type": "path"}))
     with pytest.raises(RuntimeError, match="monochromatic and spectral"):

@@ -19,7 +19,8 @@ def fma32(a, b, c):
 
 def separated(lz, ldz, bound):
     s1 = fma32(ldz, bound, lz)
-    m = fma32(fma32(np.abs(ldz), bound, np.abs(lz)), np.full_like(lz, 2.0 ** -20), np.full_like(lz, 1e-30))
+    m = fma32(fma32(np.abs(ldz), np.maximum(bound, F(2.0 ** -126)), np.abs(lz)), np.full_like(lz, 2.0 ** -20),
+              np.full_like(lz, 1e-30))
     return ((lz > m) & (s1 > m)) | ((lz < -m) & (s1 < -m))
 
 
@@ -48,6 +49,16 @@ def test_random_triples_over_wide_exponents():
     assert 0.2 < sep.mean() < 0.9  # the test is not vacuous
 
 
+def test_subnormal_and_tiny_bounds():
+    rng = np.random.default_rng(7)
+    n = 1_000_000
+    mag = lambda lo, hi: F(10.0) ** rng.uniform(lo, hi, n).astype(F)
+    lz = (rng.choice([-1, 1], n) * mag(-38, 0)).astype(F)
+    ldz = (rng.choice([-1, 1], n) * mag(0, 38)).astype(F)
+    bound = mag(-45, -30)
+    _check(lz, ldz, bound)
+
+
 def test_segments_ending_just_short_of_the_plane():
     # t = -lz / ldz just above bound: the adversarial side of the pretest
     rng = np.random.default_rng(6)
@@ -65,6 +76,8 @@ def test_segments_ending_just_short_of_the_plane():
     (1e-30, 1e8, 1.0), (1.5e-30, 1e8, 1.0), (1e-38, 1.0, 1.0), (1.0, 0.0, 1.0), (-1.0, 0.0, 1.0),
     (1.0, -0.0, np.inf), (1.0, -1.0, np.inf), (np.nan, 1.0, 1.0), (1.0, np.nan, 1.0), (0.0, 1.0, 1.0),
     (-0.0, -1.0, 1.0), (1.0, -1.0, 1.0), (1.0, -1.0000001, 1.0), (3.0, -1.0, 3.0000002),
+    # subnormal bounds: -lz / ldz underflows to -0, which the exact test accepts
+    (1e-12, 3e38, 1.4e-45), (-1e-12, -3e38, 1.4e-45), (1e-30, 1e20, 1e-40), (1e-25, 3e38, 2 ** -126),
 ])
 def test_edge_values(lz, ldz, bound):
     _check([lz], [ldz], [bound])

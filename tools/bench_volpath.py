@@ -70,6 +70,20 @@ def main():
     print(json.dumps(out), flush=True)
 
 
+def vs_sub(A):
+    """MH_EXP_VSCNT builds: PvBwdMachine's POST / END sub-phase cycles summed
+    over the calls since the library loaded (mh_exp_vs_sub); None otherwise."""
+    import ctypes as C
+    f = getattr(A.lib(), "mh_exp_vs_sub", None)
+    if f is None:
+        return None
+    buf = (C.c_ulonglong * 16)()
+    f(buf, 0)
+    names = ["post_lane", "post_wave", "post_wave_load", "post_wave_scatter", "nee_entries", "end_lane",
+             "end_wave", "end_wave_load", "end_wave_charge", "main_entries", "post_wave_steps", "end_wave_steps"]
+    return {k: int(buf[i]) for i, k in enumerate(names)}
+
+
 def bench_prbvolpath(a, mi, A, scene, t_load):
     import torch
     params = mi.traverse(scene)
@@ -94,11 +108,12 @@ def bench_prbvolpath(a, mi, A, scene, t_load):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     n = a.res * a.res * a.spp
+    sub = vs_sub(A)
     out = {"metric": "Msamples/s prbvolpath fwd + grad (sigma_t grid, albedo)", "value": round(n / dt / 1e6, 2),
            "unit": "Msamples/s", "ms_per_step": round(dt * 1e3, 3),
            "fwd_kernel_ms": round(sum(kf) / len(kf), 3), "bwd_kernel_ms": round(sum(kb) / len(kb), 3),
            "grad_sigma_t_abs_sum": float(g[0].abs().sum()), "grad_albedo": [float(x) for x in g[1]],
-           "deterministic": a.deterministic,
+           "deterministic": a.deterministic, "bwd_subphases": sub,
            "fwd_rays_closest_per_sample": round(sf.rays_closest / n, 3),
            "fwd_rays_shadow_per_sample": round(sf.rays_shadow / n, 3),
            "config": {"film": f"{a.res}x{a.res}", "spp": a.spp, "grid": f"{a.grid}^3 fBm",
