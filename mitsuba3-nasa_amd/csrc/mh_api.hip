@@ -1320,6 +1320,19 @@ static hipError_t upload_slots(mh_scene *s, Slots &P, hipStream_t st, std::vecto
     bool any_corner = false;
     for (float *c : P.corner) any_corner = any_corner || c;
     ga.corner = any_corner ? reinterpret_cast<float *const *>(mb + o_cor) : nullptr;
+    ga.hot_med = ga.hot_sigma = ga.hot_albedo = -1;
+    ga.hot_buf = ga.hot_corner = nullptr;
+    for (size_t m = 0; m < P.sigma_slot.size() && P.n_medium_params; ++m) {
+        if (P.sigma_slot[m] < 0 && P.albedo_slot[m] < 0) continue;
+        ga.hot_med = (int32_t)m;
+        ga.hot_sigma = P.sigma_slot[m];
+        ga.hot_albedo = P.albedo_slot[m];
+        if (ga.hot_sigma >= 0) {
+            ga.hot_buf = bufs[ga.hot_sigma];
+            ga.hot_corner = P.corner[ga.hot_sigma];
+        }
+        break;
+    }
     return hipSuccess;
 }
 

@@ -45,6 +45,15 @@ struct GradArgs {
     // element i of the slot block (s->tmp_c) at fx_i64[i] (fx_f32 = the block)
     long long *fx_i64 = nullptr;
     const float *fx_f32 = nullptr;
+    // the first medium with a parameter, its slots and buffers as values
+    // (prbvolpath): the scatter loops of its gradient read them from
+    // registers instead of loading sigma_slot / corner / bufs entries, whose
+    // vector loads waited (vmcnt) for the loop's outstanding atomics
+    int32_t hot_med = -1;      // medium index (-1: none)
+    int32_t hot_sigma = -1;    // its sigma_t slot (-1: none)
+    int32_t hot_albedo = -1;   // its albedo slot (-1: none)
+    float *hot_buf = nullptr;    // bufs[hot_sigma]
+    float *hot_corner = nullptr; // corner[hot_sigma] (nullptr: atomics into hot_buf)
 };
 
 // ---- BVH builder (host, binned SAH) --------------------------------------

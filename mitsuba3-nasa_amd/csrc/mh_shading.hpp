@@ -1712,6 +1712,8 @@ struct GradCtx {
     // scattering -- with dL = e_c that is the channel-c tangent radiance
     bool fwd;
     float fsum;
+    int32_t hot_med, hot_sigma, hot_albedo;  // GradArgs::hot_* (the first medium with a parameter)
+    float *hot_buf, *hot_corner;
 };
 
 // register accumulator of a small (rgb / scalar) parameter slot
@@ -3036,14 +3038,14 @@ MH_DEV void corner_scatter(float *cb, uint32_t cell, const float (&v)[8], const 
 
 // adjoint of sigma_t(p) = scale * Texture3f(grid).eval(p) (heterogeneous.cpp:192)
 // or scale * sigma_t (homogeneous.cpp:158); adj = d loss / d sigma_t(p)
-MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, GradCtx &g) {
-    if (!g.sigma_slot) return;
-    const int32_t k = g.sigma_slot[med];
-    if (k < 0) return;
+// the scatter of one sigma_t adjoint into slot k (buffer buf, corner block
+// cb or nullptr)
+MH_DEV void sigma_t_backward_at(const DScene &S, uint32_t med, V3 p, float adj, GradCtx &g, int32_t k, float *buf,
+                                float *cb) {
     const DMedium &m = S.media[med];
     const float as = adj * m.scale;
     if (m.type == MH_MEDIUM_HOMOGENEOUS) {
-        if (g.fwd) g.fsum += as * g.bufs[k][0];
+        if (g.fwd) g.fsum += as * buf[0];
         else acc_add(g, k, v3(as, 0.f, 0.f));
         return;
     }
@@ -3057,20 +3059,17 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
     const int32_t xs[2] = {min(max(ix, 0), rx - 1), min(max(ix + 1, 0), rx - 1)};
     const int32_t ys[2] = {min(max(iy, 0), ry - 1), min(max(iy + 1, 0), ry - 1)};
     const int32_t zs[2] = {min(max(iz, 0), rz - 1), min(max(iz + 1, 0), rz - 1)};
-    float *buf = g.bufs[k];
-    if (!g.fwd && g.corner) {
-        if (float *cb = g.corner[k]) {
-            float v[8];
+    if (!g.fwd && cb) {
+        float v[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
-                v[c] = as * (((bz ? w1z : w0z) * (by ? w1y : w0y)) * (bx ? w1x : w0x));
-            }
-            const uint32_t cx = (uint32_t)(min(max(ix, -1), rx - 1) + 1), cy = (uint32_t)(min(max(iy, -1), ry - 1) + 1),
-                           cz = (uint32_t)(min(max(iz, -1), rz - 1) + 1);
-            corner_scatter(cb, (cz * (uint32_t)(ry + 1) + cy) * (uint32_t)(rx + 1) + cx, v, g);
-            return;
+        for (int c = 0; c < 8; ++c) {
+            const int bx = c & 1, by = (c >> 1) & 1, bz = c >> 2;
+            v[c] = as * (((bz ? w1z : w0z) * (by ? w1y : w0y)) * (bx ? w1x : w0x));
         }
+        const uint32_t cx = (uint32_t)(min(max(ix, -1), rx - 1) + 1), cy = (uint32_t)(min(max(iy, -1), ry - 1) + 1),
+                       cz = (uint32_t)(min(max(iz, -1), rz - 1) + 1);
+        corner_scatter(cb, (cz * (uint32_t)(ry + 1) + cy) * (uint32_t)(rx + 1) + cx, v, g);
+        return;
     }
     const uint64_t sy = (uint64_t)rx, sz = (uint64_t)rx * (uint64_t)ry;
 #pragma unroll
@@ -3085,10 +3084,25 @@ MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, Gra
         gatomic_add(buf + idx, as * w);
     }
 }
+// The hot medium (GradArgs::hot_*) takes its slot, buffer and corner block
+// from registers, in a branch of its own: a vector load of a slot table entry
+// waits (vmcnt, issue order) for every atomic the wave issued before it, so a
+// load whose value merged into the scatter made each scatter wait for the
+// previous one's atomics to complete.
+MH_DEV void sigma_t_backward(const DScene &S, uint32_t med, V3 p, float adj, GradCtx &g) {
+    if (!g.sigma_slot) return;
+    if ((int32_t)med == g.hot_med) {
+        if (g.hot_sigma >= 0) sigma_t_backward_at(S, med, p, adj, g, g.hot_sigma, g.hot_buf, g.hot_corner);
+        return;
+    }
+    const int32_t k = g.sigma_slot[med];
+    if (k < 0) return;
+    sigma_t_backward_at(S, med, p, adj, g, k, g.bufs[k], g.corner ? g.corner[k] : nullptr);
+}
 
 MH_DEV void albedo_backward(uint32_t med, V3 adj, GradCtx &g) {
     if (!g.albedo_slot) return;
-    const int32_t k = g.albedo_slot[med];
+    const int32_t k = (int32_t)med == g.hot_med ? g.hot_albedo : g.albedo_slot[med];
     if (k < 0) return;
     if (g.fwd) g.fsum += (adj.x * g.bufs[k][0] + adj.y * g.bufs[k][1]) + adj.z * g.bufs[k][2];
     else acc_add(g, k, adj);
@@ -3628,6 +3642,11 @@ MH_DEV GradCtx make_grad_ctx(const GradArgs &ga) {
     g.fwd = false;
     g.fsum = 0.f;
     g.acc0 = g.acc1 = g.acc2 = g.acc3 = v3(0.f, 0.f, 0.f);
+    g.hot_med = ga.hot_med;
+    g.hot_sigma = ga.hot_sigma;
+    g.hot_albedo = ga.hot_albedo;
+    g.hot_buf = ga.hot_buf;
+    g.hot_corner = ga.hot_corner;
     return g;
 }
 
