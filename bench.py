@@ -482,7 +482,7 @@ def main():
         # tools/profile_r2.sh of the latest round's build.  These counters are
         # NOT measured in this run: the line names the file and the build they
         # come from (traffic_source)
-        ppath = next((q for q in (os.path.join(ROOT, "profiles", f"r{r}_pmc.json") for r in (5, 4, 3, 2))
+        ppath = next((q for q in (os.path.join(ROOT, "profiles", f"r{r}_pmc.json") for r in (6, 5, 4, 3, 2))
                       if os.path.exists(q)), "")
         traffic_source = None
         if os.path.exists(ppath):

@@ -2186,6 +2186,31 @@ MH_DEV V3 gather_dL_wave_lds(const DScene &S, int coalesce, const float *__restr
              wd = gaussian_eval2(S.filter_coeff, pair(rely + 1.f, rely + 2.f)),
              we = gaussian_eval2(S.filter_coeff, pair(rely + 3.f, rely + 4.f));
     const float wxs[5] = {wa.x, wa.y, wb.x, wb.y, wc.x}, wys[5] = {wc.y, wd.x, wd.y, we.x, we.y};
+    if (pix >= 0 && piy >= 0 && (uint32_t)pix + 4u < W && (uint32_t)piy + 4u < H) {
+        // interior footprint (wave-uniform): a row's 5 taps read back at once
+        // (one LDS wait per row, not per tap), the r / g channels on packed
+        // pairs; per channel the same products and sums in the same order as
+        // the general loop below (bit-identical dL)
+        typedef float F4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) F4 LdsF4;
+        const LdsF4 *t4 = (const LdsF4 *)taps;
+        F2 o01 = sp2(0.f);
+        float o2 = 0.f;
+#pragma unroll
+        for (int32_t ys = 0; ys < 5; ++ys) {
+            F4 t[5];
+#pragma unroll
+            for (int32_t xs = 0; xs < 5; ++xs) t[xs] = t4[ys * 5 + xs];
+            const float wy = wys[ys];
+#pragma unroll
+            for (int32_t xs = 0; xs < 5; ++xs) {
+                const float w = wy * wxs[xs];
+                o01 = o01 + pair(t[xs].x, t[xs].y) * sp2(w);
+                o2 += t[xs].z * w;
+            }
+        }
+        return v3(o01.x, o01.y, o2);
+    }
     float o0 = 0.f, o1 = 0.f, o2 = 0.f;
 #pragma unroll
     for (int32_t ys = 0; ys < 5; ++ys) {
