@@ -197,7 +197,7 @@ def splat_roof(st, n_px):
     launches = max(1, st.n_aux_launches)
     us = st.ms_aux / launches * 1e3
     b = (20.0 * st.aux_items + 16.0 * n_px * launches) / launches
-    return _roof("k_splat_tile", b, us, launches_per_step=int(st.n_aux_launches), samples=int(st.aux_items),
+    return _roof("k_splat_tile<0>", b, us, launches_per_step=int(st.n_aux_launches), samples=int(st.aux_items),
                  bytes_formula="(20 samples + 16 pixels launches) / launches",
                  note="RGBW film L2/MALL-resident; the W image (PRB) rides in the same kernel family")
 
