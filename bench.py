@@ -180,6 +180,13 @@ def cpu_baseline(scene, fwd, prb, key, spp_gpu, budget_s, fwd_only):
             "cpu_model": model, "nproc": nproc, "affinity": aff, "threads": threads}
 
 
+def pmc_applies(args):
+    """The committed PMC passes (tools/profile_r2.sh) profiled the default
+    workload: config 2, 512^2 @ 256 spp per rank, max_depth 8.  Their per-launch
+    counters describe launches of that workload only."""
+    return args.config == 2 and args.res == 512 and args.spp == 256 and args.max_depth == 8
+
+
 def _roof(kname, achieved_bytes, us, **extra):
     """A roofline object: algorithmic bytes of one launch over its average
     duration (HIP events over the timed region), against the HBM peak."""
@@ -499,13 +506,13 @@ def main():
         # per rank, max_depth 8); a launch of another workload (config 5's
         # chunks, another res / spp / depth) does different work per launch, so
         # its counters are not this launch's: omitted, with a note
-        pmc_applies = (args.config == 2 and args.res == 512 and args.spp == 256 and args.max_depth == 8)
-        pmc_note = (None if pmc_applies else
+        applies = pmc_applies(args)
+        pmc_note = (None if applies else
                     "traffic / valu_issue_frac omitted: the committed PMC passes profiled config 2's launches "
                     "(512^2 @ 256 spp, max_depth 8), not this workload's")
 
         def family(kname):
-            if not pmc_applies:
+            if not applies:
                 return None, None, None
             fam = [v for k, v in pmc.items() if k.startswith(kname + "<") and
                    not (kname == "k_wf_bounce" and k.startswith("k_wf_bounce_prb"))]

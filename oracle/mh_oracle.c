@@ -1438,6 +1438,14 @@ static inline float medium_majorant(const mh_medium *m) {
     return m->scale * m->max_density;
 }
 
+/* density-grid lookups since the last oracle_grid_lookups(1): the check of the
+   device's mh_stats.grid_lookups (test infrastructure, like the rest of the oracle) */
+static uint64_t g_grid_lookups;
+uint64_t oracle_grid_lookups(int reset) {
+    return reset ? __atomic_exchange_n(&g_grid_lookups, 0, __ATOMIC_RELAXED)
+                 : __atomic_load_n(&g_grid_lookups, __ATOMIC_RELAXED);
+}
+
 static void sample_interaction(const mh_scene_desc *d, uint32_t med, const ray3 *ray, float u,
                                uint32_t channel, med_int *mei) {
     const mh_medium *m = &d->media[med];
@@ -1467,6 +1475,7 @@ static void sample_interaction(const mh_scene_desc *d, uint32_t med, const ray3 
     float st = 0.f;
     if (valid) st = m->type == MH_MEDIUM_HOMOGENEOUS ? m->sigma_t_const * m->scale
                                                       : m->scale * grid_eval(d, m, mei->p);
+    if (valid && m->type != MH_MEDIUM_HOMOGENEOUS) __atomic_fetch_add(&g_grid_lookups, 1, __ATOMIC_RELAXED);
     mei->sigma_t = st;
     mei->sigma_s = vscale(vload(m->albedo), st);
     if (!valid) mei->sigma_s = V3(0, 0, 0);

@@ -62,6 +62,9 @@ int oracle_sample_range(const mh_scene_desc *desc, const mh_integrator *integ, u
 
 /* Full render into an RGBW film (H*W*4, overwritten).  spp_begin/end select
  * a sample slab of every pixel (0,0 = all).  n_threads >= 1.              */
+/* density-grid lookups (valid heterogeneous medium samples) of every render
+   since the last call with reset = 1 (the check of mh_stats.grid_lookups) */
+uint64_t oracle_grid_lookups(int reset);
 int oracle_render(const mh_scene_desc *desc, const mh_integrator *integ, uint32_t seed,
                   uint32_t spp, uint32_t spp_begin, uint32_t spp_end, int n_threads,
                   float *film_rgbw);

@@ -62,6 +62,8 @@ def lib():
     L.oracle_spiral_order.restype = C.c_uint32
     L.oracle_spiral_order.argtypes = [C.c_uint32, C.c_uint32, vp, vp]
     L.oracle_last_error.restype = C.c_char_p
+    L.oracle_grid_lookups.restype = C.c_uint64
+    L.oracle_grid_lookups.argtypes = [C.c_int]
     _lib = L
     return L
 
@@ -194,3 +196,9 @@ def render_forward(scene, integrator, seed, spp, param_ids, tangents, spp_begin=
     check(lib().oracle_render_forward(C.byref(scene.desc), C.byref(ic), seed, spp, spp_begin, spp_end,
                                       len(tans), _p(ids), ptrs, threads or nthreads(), _p(film)))
     return film
+
+
+def grid_lookups(reset=True):
+    """Density-grid lookups of the oracle's renders since the last reset
+    (the check of mh_stats.grid_lookups)."""
+    return int(lib().oracle_grid_lookups(1 if reset else 0))
