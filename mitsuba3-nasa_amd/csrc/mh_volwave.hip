@@ -1326,6 +1326,7 @@ struct PvBwdState : PvState {
 //   [6] END wave loop (end_wave)           [7]   its MainLog entry loads
 //   [8]   its log-entry charges            [9]   MainLog entries charged
 //   [10] post_wave loop steps              [11] end_wave loop steps
+//   [12] TRACE trips' packet traversal     [13] TRACE trips' hit continuations (every machine)
 __device__ unsigned long long g_vs_sub[16];
 #define MH_VS_SUB_DECL uint64_t sub[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define MH_VS_SUB(k, v) (sub[k] += (uint64_t)(v))
@@ -1662,6 +1663,7 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
     bool drained = false;        // wave-uniform: every queue is exhausted
 #ifdef MH_EXP_VSCNT
     unsigned long long d_trips[kNGroups] = {}, d_lanes[kNGroups] = {}, d_ticks[kNGroups] = {};
+    unsigned long long d_trace[2] = {0, 0};  // TRACE trips: the packet traversal, the hits' continuations
 #endif
     while (true) {
         uint32_t cnt[kNGroups];
@@ -1732,12 +1734,23 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
                 const bool act = g == kGTrace;
                 RayT r{v3(0.f, 0.f, 0.f), v3(0.f, 0.f, 1.f), -1.f};
                 if (act) r = mc.trace_ray(v, ph);
+#ifdef MH_EXP_VSCNT
+                const uint64_t tt0 = __builtin_amdgcn_s_memtime();
+#endif
                 const Hit h = packet_batch<false, true>(S.nodes, S.prims, S.prim_pairs, S.key_sp,
                                                         B.stack - (threadIdx.x & 63u), B.stride, r, act, B.recs, B.dscr);
+#ifdef MH_EXP_VSCNT
+                asm volatile("" ::"v"(h.t), "v"(h.prim));  // the traversal's results are in
+                const uint64_t tt1 = __builtin_amdgcn_s_memtime();
+                d_trace[0] += tt1 - tt0;
+#endif
                 if (act) {
                     ph = mc.trace_hit(S, in, rng, ph, v, wm, h, r, n_closest, n_shadow);
                     ended = ph == kPhFree;
                 }
+#ifdef MH_EXP_VSCNT
+                d_trace[1] += __builtin_amdgcn_s_memtime() - tt1;
+#endif
             } else if (g == kGTrace) {
                 ph = mc.template trace<Pk>(S, B, in, rng, ph, v, wm, n_closest, n_shadow);
                 ended = ph == kPhFree;
@@ -1805,6 +1818,10 @@ k_vol_sched(DScene S0, IntegratorParams in, LaneMap lm, uint32_t seed_value, uin
         wave_count(&counters[kVsCtrLookups], n_lookups);
     }
 #ifdef MH_EXP_VSCNT
+    if (vw_lane() == 0) {
+        atomicAdd(&g_vs_sub[12], d_trace[0]);
+        atomicAdd(&g_vs_sub[13], d_trace[1]);
+    }
     if (vw_lane() == 0 && counters)
         for (uint32_t k = 0; k < kNGroups; ++k) {
             atomicAdd(&counters[2 + k], d_trips[k]);

@@ -67,6 +67,9 @@ def main():
         tc = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": round(a.res * a.res * a.cpu_spp / tc / 1e6, 3), "unit": "Msamples/s",
                                "cores": thr, "kind": "port", "sample": f"{a.res}^2 @ {a.cpu_spp} spp, {tc:.1f} s"}
+    sub = vs_sub(A)
+    if sub is not None:
+        out["vs_subphases"] = sub
     print(json.dumps(out), flush=True)
 
 
@@ -80,7 +83,8 @@ def vs_sub(A):
     buf = (C.c_ulonglong * 16)()
     f(buf, 0)
     names = ["post_lane", "post_wave", "post_wave_load", "post_wave_scatter", "nee_entries", "end_lane",
-             "end_wave", "end_wave_load", "end_wave_charge", "main_entries", "post_wave_steps", "end_wave_steps"]
+             "end_wave", "end_wave_load", "end_wave_charge", "main_entries", "post_wave_steps", "end_wave_steps",
+             "trace_traversal", "trace_continuation"]
     return {k: int(buf[i]) for i, k in enumerate(names)}
 
 
