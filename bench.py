@@ -639,6 +639,17 @@ def main_single_op(args, rank, world, dev, dist_on):
             roof, roof_other = bitmap_rooflines(st, n_local, 64 * 64 * 3)  # config 3(b): a 64^2 x 3 bitmap
         elif args.config == 4 and st.mode == 3 and st.n_trace_launches:
             roof = volsched_roofline(st, n_local)
+            # config 4's own PMC passes (tools/profile_volsched.sh): traffic and
+            # VALU issue of the same launch shape (one k_vol_sched per render)
+            pc = os.path.join(ROOT, "profiles", "r6_pmc_config4.json")
+            if os.path.exists(pc):
+                pj = json.load(open(pc))
+                k = next((v for n_, v in pj.get("kernels", {}).items() if n_.startswith("k_vol_sched<VolMachine")), None)
+                if k:
+                    roof["traffic"] = round(k["hbm_bytes_per_call"])
+                    roof["valu_issue_frac"] = round(k["valu_issue_frac"], 4)
+                    roof["traffic_source"] = ("profiles/r6_pmc_config4.json @ " + pj.get("source", "") +
+                                              " (not measured in this run)")
         elif args.config == 1 and st.mode == 2:
             launches = max(1, st.n_trace_launches)
             R, N = float(st.rays_closest), float(n_local)
