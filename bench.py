@@ -14,9 +14,18 @@ max-over-ranks step time.  Inputs (the scene) are resident in HBM before the
 timed region; the timed region ends with the image and gradients on the
 device.
 
-Per step two collectives (packed, the default): the film and the W image
-(which depends only on the gradient seed's jitters) are summed in ONE
-all-reduce, the gradients in another (mitsuba_hip.distributed.fwd_grad_step).
+The step is overlapped (the default since round 6): the forward and the
+gradient pass are independent (the backward's seed is TEA(seed, 1); it needs
+the W image, not the film), so the forward runs on its own scene handle,
+HIP stream and host thread while this thread computes the W image,
+all-reduces it and runs render_backward; the film and the gradients are then
+summed in ONE all-reduce (two collectives per step: W, film + gradient;
+mitsuba_hip.distributed.fwd_grad_step(overlap=True)).  --serial runs the
+round-5 step instead: forward, then gradient pass, the film and the W image
+in one packed all-reduce, the gradients in another.  The kernel rooflines of
+an overlapped run come from 2 serial steps right after the timed region (the
+launches of the timed steps share the chip with the other pass:
+`roofline_overlapped`).
 
 --config 5 is BASELINE.json configs[4]: cornell_box 2048x2048 @ 1024 spp
 TOTAL (strong scaling: rank r takes samples [1024 r / N, 1024 (r + 1) / N) of
@@ -72,7 +81,11 @@ def parse(argv=None):
                         "1: path 256^2 @ 16 (CPU leg: the scalar_rgb restatement); 3: prb gradient wrt a 64^2x3 "
                         "albedo bitmap, 512^2 @ 64; 4: volpath, 256^3 fBm medium + HG, 256^2 @ 64")
     p.add_argument("--unpacked", action="store_true",
-                   help="separate film and W collectives (3 per step) instead of one packed film + W all-reduce")
+                   help="serial step, separate film and W collectives (3 per step) instead of one packed film + W "
+                        "all-reduce")
+    p.add_argument("--serial", action="store_true",
+                   help="forward, then gradient pass (the round-5 step: film + W in one packed all-reduce) instead "
+                        "of the two running concurrently on two streams")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' to rehearse "
                         "several ranks on one GPU)")
@@ -257,7 +270,11 @@ def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     reflectance, the rank's sample slab of a spp * world render, through the
     HIP C-ABI wrappers of mitsuba_hip.  fwd_passes: the forward's passes
     (integrator.cpp:281-295; its slab counts lanes of one pass).  One device
-    buffer holds the film and the W image (StepOps.packed)."""
+    buffer holds the film and the W image (StepOps.packed).  The forward
+    renders through its own handle of the scene (scene_fwd: the same scene
+    description, its own device copy, scratch and stream), so that the
+    overlapped step (StepOps.concurrent) can run it alongside the gradient
+    pass."""
     import torch
     import mitsuba_hip as mi
     from mitsuba_hip import _abi as A
@@ -267,6 +284,7 @@ def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     d["sensor"]["film"]["width"] = res
     d["sensor"]["film"]["height"] = res
     scene = mi.load_dict(d)
+    scene_fwd = mi.load_dict(d)
     fwd = mi.load_dict({"type": "path", "max_depth": max_depth})
     prb = mi.load_dict({"type": "prb", "max_depth": max_depth})
     params = mi.traverse(scene)
@@ -278,14 +296,16 @@ def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     views = (packed, packed[:res * res * 4].view(res, res, 4), packed[res * res * 4:].view(res, res))
     ops = D.StepOps(
         render_film=lambda seed, spp_, b, e, out=None: mi.render_film(
-            scene, fwd, seed=seed, spp=spp_, spp_begin=b, spp_end=e, film=film if out is None else out, stats=st_f),
+            scene_fwd, fwd, seed=seed, spp=spp_, spp_begin=b, spp_end=e, film=film if out is None else out,
+            stats=st_f),
         develop=lambda f: mi.develop(scene, f),
         prb_weights=lambda seed, spp_, b, e, out=None: mi.prb_weights(scene, seed, spp_, b, e, out=out),
         render_backward=lambda seed, spp_, b, e, w: mi.render_backward(
             scene, params, grad_in, [key], prb, seed=seed, spp=spp_, spp_begin=b, spp_end=e, weights=w,
             stats=st_b),
         seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0],
-        packed=lambda: views)
+        packed=lambda: views,
+        concurrent=D.PairRunner((torch.cuda.Stream(dev), torch.cuda.Stream(dev)), dev))
     slab = D.sample_slab(rank, world, spp)
     fs = D.sample_slab(rank, world, spp // fwd_passes)
     fwd_slab = D.Slab(slab.spp_total, fs.begin, fs.end)
@@ -414,11 +434,13 @@ def main():
         w[k] for k in ("scene", "fwd", "prb", "key", "ops", "slab", "fwd_slab", "st_f", "st_b"))
     H = W = args.res
     spp_total = args.spp * world
-    packed = not (args.unpacked or args.local_weights or args.fwd_only)
+    overlap = not (args.serial or args.unpacked or args.fwd_only)
+    packed = not (overlap or args.unpacked or args.local_weights or args.fwd_only)
 
     def step(i):
         return D.fwd_grad_step(ops, slab, i, with_grad=not args.fwd_only, local_weights=args.local_weights,
-                               film_to_root=not args.film_all_reduce, packed=packed, fwd_slab=fwd_slab)
+                               film_to_root=not args.film_all_reduce, packed=packed, fwd_slab=fwd_slab,
+                               overlap=overlap)
 
     for i in range(args.warmup):
         step(1000 + i)
@@ -450,7 +472,12 @@ def main():
         # own work is its step time without the final barrier wait, so the
         # spread comes from its kernel time (fwd + bwd, HIP events) + collectives
         colls = timer.summary(args.steps)
-        own = (sum(fwd_ms) + sum(bwd_ms)) / args.steps + sum(c["ms_per_step"] for c in colls.values())
+        cms = {k: c["ms_per_step"] for k, c in colls.items()}
+        if overlap:  # the forward runs alongside W + its all-reduce + the backward
+            own = (max(sum(fwd_ms) / args.steps, sum(bwd_ms) / args.steps + cms.get("W", 0.0)) +
+                   cms.get("film+gradient", 0.0))
+        else:
+            own = (sum(fwd_ms) + sum(bwd_ms)) / args.steps + sum(cms.values())
         coll_max = {k: round(D.max_over_ranks(v["ms_per_step"], dev), 3) for k, v in sorted(colls.items())}
         multi = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
                  "rank_kernel_plus_collective_ms_min": round(D.min_over_ranks(own, dev), 3),
@@ -460,6 +487,23 @@ def main():
                  "collective_calls_per_step": {k: round(v["calls_per_step"], 2) for k, v in sorted(colls.items())}}
     samples_step = world * H * W * args.spp
     value = samples_step / (ms_step / 1e3) / 1e6
+    # the timed steps overlap the forward and the gradient pass, so a bounce
+    # launch shares the chip with the other pass's launches for most of its
+    # duration: its HIP-event time there is not the kernel's own.  The kernel
+    # rooflines come from a roofline pass of serial steps right after the timed
+    # region (same workload, the kernels alone on the chip; the timed region's
+    # figures are reported beside them as roofline_overlapped)
+    st_f_timed, st_b_timed = A.Stats.from_buffer_copy(st_f), A.Stats.from_buffer_copy(st_b)
+    fwd_ms_serial = bwd_ms_serial = None
+    if overlap:
+        fs_ms, bs_ms = [], []
+        for i in range(2):
+            D.fwd_grad_step(ops, slab, 2000 + i, local_weights=args.local_weights,
+                            film_to_root=not args.film_all_reduce, packed=not args.local_weights, fwd_slab=fwd_slab)
+            fs_ms.append(st_f.ms_kernel)
+            bs_ms.append(st_b.ms_kernel)
+        torch.cuda.synchronize()
+        fwd_ms_serial, bwd_ms_serial = sum(fs_ms) / 2, sum(bs_ms) / 2
 
     if rank == 0:
         # ---- rooflines of the two bounce-kernel families, the dominant one as
@@ -555,6 +599,24 @@ def main():
         roofs.sort(key=lambda x: -x[0])
         roofline = roofs[0][1] if roofs else None
         roofline_other = roofs[1][1] if len(roofs) > 1 else None
+        roofline_overlapped = None
+        if overlap and roofline is not None:
+            for r in (roofline, roofline_other):
+                r["measured"] = ("roofline pass: 2 serial steps right after the timed region (forward, then "
+                                 "gradient pass; the kernel alone on the chip), HIP events on the kernel's stream")
+            # the timed (overlapped) steps: the same launches sharing the chip
+            # with the other pass.  chip_*: both bounce families' algorithmic
+            # bytes of a step / the step time (what the chip moved for them)
+            sts = {"k_wf_bounce": (st_f_timed, 84.0, 12.0, 8.0), "k_wf_bounce_prb": (st_b_timed, 108.0, 0.0, 16.0)}
+            ro = roof(roofline["kernel"], *sts[roofline["kernel"]])
+            chip = sum(r["algorithmic_bytes_per_launch"] * r["launches_per_step"] for r in (roofline, roofline_other))
+            chip_gbs = chip / (ms_step / 1e3) / 1e9  # one rank's bytes over its step time
+            roofline_overlapped = {k: ro[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us",
+                                                      "launches_per_step", "algorithmic_bytes_per_launch")}
+            roofline_overlapped.update(
+                measured="the timed region (forward || gradient pass): each launch shares the chip",
+                chip_bounce_bytes_per_step=round(chip), chip_achieved=round(chip_gbs, 1),
+                chip_frac=round(chip_gbs / HBM_PEAK_GBS, 4))
         # the forward's film splat (k_splat_tile): per sample its L (12 B) and
         # film position (8 B) read, per launch the RGBW film (16 B per pixel)
         # added once; timed by HIP events after the bounce span of each chunk
@@ -569,7 +631,11 @@ def main():
                 cscene = mi.load_dict(d)
             cpu = cpu_baseline(cscene, fwd, prb, key, args.spp, args.cpu_seconds, args.fwd_only)
         coll = ("RCCL" if args.backend == "nccl" else args.backend)
-        if packed:
+        if overlap:
+            par = (f"sample-slab x{world}; forward || gradient pass (two scene handles, two HIP streams); {coll}" +
+                   (" local W" if args.local_weights else " all-reduce (W)") +
+                   " + all-reduce (film + gradient, one buffer)")
+        elif packed:
             par = f"sample-slab x{world} + {coll} all-reduce (film + W, one packed buffer) + all-reduce (gradient)"
         else:
             par = (f"sample-slab x{world} + {coll}" +
@@ -588,11 +654,17 @@ def main():
                                    + ("" if args.fwd_only else f" + prb backward wrt '{key}'"),
                        "film": f"{W}x{H}", "spp_per_gpu": args.spp, "spp_total": spp_total,
                        "parallelism": par,
-                       "collectives_per_step": (2 if packed else (1 if args.fwd_only else (2 if args.local_weights else 3))),
-                       "collective_bytes": ({"film+W": H * W * 20, "gradient": 12} if packed else
+                       "step": ("overlapped" if overlap else "serial"),
+                       "collectives_per_step": ((1 if args.local_weights else 2) if overlap else
+                                                2 if packed else (1 if args.fwd_only else (2 if args.local_weights else 3))),
+                       "collective_bytes": (dict(({} if args.local_weights else {"W": H * W * 4}),
+                                                 **{"film+gradient": H * W * 16 + 12}) if overlap else
+                                            {"film+W": H * W * 20, "gradient": 12} if packed else
                                             {"film": H * W * 16, "W": 0 if args.local_weights else H * W * 4,
                                              "gradient": 12})},
             "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
+            "fwd_kernel_ms_serial": None if fwd_ms_serial is None else round(fwd_ms_serial, 3),
+            "bwd_kernel_ms_serial": None if bwd_ms_serial is None else round(bwd_ms_serial, 3),
             "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
             "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),
             "rays_closest_per_sample_prb": (round(st_b.rays_closest / max(1, n_local), 4)
@@ -600,6 +672,7 @@ def main():
             "rays_shadow_per_sample_prb": (round(st_b.rays_shadow / max(1, n_local), 4)
                                            if not args.fwd_only else None),
             "roofline": roofline, "roofline_other": roofline_other, "roofline_splat": roofline_splat,
+            "roofline_overlapped": roofline_overlapped,
             "cpu_baseline": cpu,
         }
         if multi is not None:

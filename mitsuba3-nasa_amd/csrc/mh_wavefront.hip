@@ -2076,12 +2076,16 @@ hipError_t launch_wavefront_prb(const DScene &S, const IntegratorParams &in, con
         // accumulators per CU: as many as its LDS holds, at most the workgroups
         // of kScatThreads that are resident at once (more would only zero and
         // flush extra LDS copies)
-        static int resident = 0;
-        if (!resident && hipOccupancyMaxActiveBlocksPerMultiprocessor(&resident, k_wf_bitmap_scatter<true>, kScatThreads,
-                                                                      0) != hipSuccess) {
-            (void)hipGetLastError();
-            resident = 0;
-        }
+        // (a thread-safe one-time query: calls on distinct scenes may run concurrently)
+        static const int resident = [] {
+            int r = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&r, k_wf_bitmap_scatter<true>, kScatThreads, 0) !=
+                hipSuccess) {
+                (void)hipGetLastError();
+                r = 0;
+            }
+            return r;
+        }();
         const uint32_t per_cu = (uint32_t)std::max<size_t>(
             1, std::min<size_t>(resident > 0 ? (size_t)resident : 8u, std::min<size_t>(8, bmp->cu_lds / acc_bytes)));
         const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>(bmp->cus * per_cu, (uint32_t)((n + 4095) / 4096)));

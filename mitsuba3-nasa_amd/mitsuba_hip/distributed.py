@@ -20,6 +20,12 @@ gradients (12 B per rgb parameter) per step.  Unpacked, the film is reduced
 (or all-reduced) and W all-reduced separately, or W is computed locally on
 every rank (local_weights: no W exchange, N times the W splat).
 
+Overlapped (`overlap`, the default of bench.py since round 6): the forward
+and the gradient pass are independent, so they run concurrently on two scene
+handles and two streams (PairRunner); the W image is all-reduced inside the
+gradient side, and the film and the gradients are summed in one all-reduce
+after both (W: 1 MiB, film + gradient: 4 MiB + 12 B at 512²).
+
 One process per GPU; torch.distributed with backend "nccl" (= RCCL over xGMI
 on ROCm), or "gloo" for the CPU tests.  No collective sits inside a kernel
 loop.
@@ -140,6 +146,61 @@ class StepOps:
     # output view), so the packed exchange needs no copy.  None: the packed
     # step concatenates the two.
     packed: Optional[Callable] = None
+    # optional: (fwd, bwd) -> (fwd(), bwd()) with the two running concurrently
+    # (a PairRunner; on a GPU render_film then uses its own scene handle and
+    # stream).  None: the overlapped step runs them one after the other.
+    concurrent: Optional[Callable] = None
+
+
+class PairRunner:
+    """Runs `fwd` on a worker thread concurrently with `bwd` on the calling
+    thread and returns (fwd(), bwd()).  The C-ABI calls release the GIL, so
+    the forward's and the backward's kernels overlap on the device (distinct
+    scene handles may be used concurrently, include/mitsuba_hip.h).
+
+    streams = (stream_fwd, stream_bwd) on `device`: each side runs with its
+    stream current; both wait for the caller's current stream first, the
+    caller's stream waits for both on return, and returned device tensors are
+    marked as used on the caller's stream (the caching allocator must not
+    reuse them early).  None: host threads only (the CPU tests)."""
+
+    def __init__(self, streams=None, device=None):
+        from concurrent.futures import ThreadPoolExecutor
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mh-fwd")
+        self.streams, self.device = streams, device
+
+    def __call__(self, fwd: Callable, bwd: Callable):
+        if self.streams is None:
+            fut = self.pool.submit(fwd)
+            try:
+                b = bwd()
+            finally:
+                fut.exception()  # joins the forward whatever the backward did
+            return fut.result(), b
+        import torch
+        sa, sb = self.streams
+        cur = torch.cuda.current_stream(self.device)
+        sa.wait_stream(cur)
+        sb.wait_stream(cur)
+
+        def run_fwd():
+            torch.cuda.set_device(self.device)  # the current device is per host thread
+            with torch.cuda.stream(sa):
+                return fwd()
+
+        fut = self.pool.submit(run_fwd)
+        try:
+            with torch.cuda.stream(sb):
+                b = bwd()
+        finally:
+            fut.exception()  # joins the forward whatever the backward did
+        a = fut.result()
+        cur.wait_stream(sa)
+        cur.wait_stream(sb)
+        for t in ([a] if torch.is_tensor(a) else list(a or [])) + ([b] if torch.is_tensor(b) else list(b or [])):
+            if torch.is_tensor(t) and t.is_cuda:
+                t.record_stream(cur)
+        return a, b
 
 
 def all_reduce_list_(ts: List, name: str = "all_reduce") -> List:
@@ -162,10 +223,18 @@ def all_reduce_list_(ts: List, name: str = "all_reduce") -> List:
 
 
 def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, local_weights: bool = False,
-                  film_to_root: bool = False, packed: bool = False, fwd_slab: Optional[Slab] = None):
+                  film_to_root: bool = False, packed: bool = False, fwd_slab: Optional[Slab] = None,
+                  overlap: bool = False):
     """One benchmark step: forward render of the rank's slab + film
     all-reduce + develop; then (with_grad) PRB render_backward of the slab
     with the globally all-reduced W image and an all-reduced gradient.
+
+    overlap: the forward and the gradient pass are independent (the
+    backward's seed is TEA(seed, 1); it needs the W image, not the film), so
+    they run concurrently (ops.concurrent): the forward on one side, the W
+    image + its all-reduce + render_backward on the other; then the film and
+    the gradients are summed in ONE all-reduce (two collectives per step: W,
+    film + gradient; one with local_weights).  film_to_root does not apply.
 
     packed: the W image of the gradient seed is computed before the forward
     exchange and summed together with the film in one all-reduce (two
@@ -178,6 +247,17 @@ def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, l
     fwd_slab: the forward's slab when it differs from the gradient's (a
     multi-pass forward counts its slab in lanes of one pass)."""
     fs = fwd_slab or slab
+    if with_grad and overlap:
+        sg = ops.seed_grad(seed)
+
+        def grad_pass():
+            w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end), "W")
+            return ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
+
+        run = ops.concurrent or (lambda f, g: (f(), g()))
+        film, grads = run(lambda: ops.render_film(seed, fs.spp_total, fs.begin, fs.end), grad_pass)
+        summed = all_reduce_list_([film] + list(grads), "film+gradient")
+        return ops.develop(summed[0]), summed[1:]
     if with_grad and packed and not local_weights:
         sg = ops.seed_grad(seed)
         if ops.packed is not None:

@@ -33,11 +33,14 @@ def main():
     # bench.py's default: film + W in one packed all-reduce (StepOps.packed views)
     img3, grads3 = D.fwd_grad_step(w["ops"], w["slab"], seed=11, packed=True, fwd_slab=w["fwd_slab"])
     img3, g3 = img3.clone(), grads3[0].clone()
+    # bench.py's default since round 6: forward || gradient pass on two scene
+    # handles and streams, W all-reduce, film + gradient in one all-reduce
+    img4, grads4 = D.fwd_grad_step(w["ops"], w["slab"], seed=11, overlap=True, fwd_slab=w["fwd_slab"])
     torch.cuda.synchronize()
     t = D.max_over_ranks(float(rank) + 0.25, torch.device("cuda:0"))
     np.savez(os.path.join(out, f"r{rank}.npz"), img=img.cpu().numpy(), g=grads[0].cpu().numpy(), t=t,
              begin=w["slab"].begin, end=w["slab"].end, img2=img2.cpu().numpy(), g2=grads2[0].cpu().numpy(),
-             img3=img3.cpu().numpy(), g3=g3.cpu().numpy())
+             img3=img3.cpu().numpy(), g3=g3.cpu().numpy(), img4=img4.cpu().numpy(), g4=grads4[0].cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
 

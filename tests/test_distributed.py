@@ -65,6 +65,14 @@ def _worker(rank, world, port, out_dir):
     img3, grads3 = D.fwd_grad_step(_ops(mi, O, scene, torch), slab, seed=7, packed=True)
     D.set_collective_timer(None)
     colls = timer.summary(1)
+    # overlapped (bench.py's default): forward on a worker thread alongside
+    # W + W all-reduce + backward, then film + gradient in one all-reduce
+    ops = _ops(mi, O, scene, torch)
+    ops.concurrent = D.PairRunner()
+    D.set_collective_timer(timer)
+    img4, grads4 = D.fwd_grad_step(ops, slab, seed=7, overlap=True)
+    D.set_collective_timer(None)
+    colls4 = timer.summary(1)
     t = D.max_over_ranks(float(rank) + 0.5)
     tmin = D.min_over_ranks(float(rank) + 0.5)
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), img=img.numpy(), g=grads[0].numpy(), t=t, tmin=tmin,
@@ -72,7 +80,9 @@ def _worker(rank, world, port, out_dir):
              g3=grads3[0].numpy(), coll_names=np.array(sorted(colls)),
              coll_bytes=np.array([colls[k]["bytes"] for k in sorted(colls)]),
              coll_calls=np.array([colls[k]["calls_per_step"] for k in sorted(colls)]),
-             coll_ms=np.array([colls[k]["ms_per_step"] for k in sorted(colls)]))
+             coll_ms=np.array([colls[k]["ms_per_step"] for k in sorted(colls)]), img4=img4.numpy(),
+             g4=grads4[0].numpy(), coll4_names=np.array(sorted(colls4)),
+             coll4_bytes=np.array([colls4[k]["bytes"] for k in sorted(colls4)]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -123,6 +133,26 @@ def test_gloo_ranks_match_single_process(world, tmp_path):
     for r in rs:
         np.testing.assert_allclose(r["img3"], img.numpy(), rtol=2e-6, atol=1e-7)
         np.testing.assert_allclose(r["g3"], grads[0].numpy(), rtol=1e-5, atol=1e-9)
+    # overlapped: W all-reduce, then film + gradient (4 + 16 B per pixel + 12 B) in one
+    for r in rs:
+        assert list(r["coll4_names"]) == ["W", "film+gradient"]
+        assert list(r["coll4_bytes"]) == [24 * 16 * 4, 24 * 16 * 16 + 12]
+        np.testing.assert_allclose(r["img4"], img.numpy(), rtol=2e-6, atol=1e-7)
+        np.testing.assert_allclose(r["g4"], grads[0].numpy(), rtol=1e-5, atol=1e-9)
+
+
+def test_pair_runner_runs_both_and_propagates_errors():
+    import threading
+    from mitsuba_hip import distributed as D
+    run = D.PairRunner()
+    names = []
+    a, b = run(lambda: names.append(threading.current_thread().name) or 1,
+               lambda: names.append(threading.current_thread().name) or 2)
+    assert (a, b) == (1, 2) and len(set(names)) == 2  # the forward ran on the worker thread
+    with pytest.raises(ZeroDivisionError):
+        run(lambda: 1 // 0, lambda: 2)
+    with pytest.raises(KeyError):
+        run(lambda: 1, lambda: {}["x"])
 
 
 def test_all_reduce_list_single_rank():

@@ -69,3 +69,11 @@ def test_two_ranks_on_one_gpu_match_single_process(tmp_path):
     for r in (r0, r1):
         np.testing.assert_allclose(r["img3"], img, rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(r["g3"], g, rtol=1e-4)
+    # the overlapped step (bench.py's default): forward || gradient pass
+    for r in (r0, r1):
+        np.testing.assert_allclose(r["img4"], img, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(r["g4"], g, rtol=1e-4)
+    # ... and on one process: the same image and gradient as the serial step
+    img5, grads5 = D.fwd_grad_step(w["ops"], w["slab"], seed=11, overlap=True)
+    np.testing.assert_allclose(img5.cpu().numpy(), img, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(grads5[0].cpu().numpy(), g, rtol=1e-4)

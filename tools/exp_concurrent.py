@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Experiment (round 6): the bench step's forward render and PRB backward are
+independent (different seeds; the backward needs only the W image), so they
+can run concurrently on two scene handles, two streams and two host threads
+(the C-ABI calls release the GIL; concurrent handles on distinct scenes are
+allowed, include/mitsuba_hip.h).  Prints the sequential and the concurrent
+step time of cornell_box 512^2 @ 256 spp fwd + PRB grad (one MI355X)."""
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "mitsuba3-nasa_amd")]
+
+
+def main():
+    import torch
+    import mitsuba_hip as mi
+    mi.set_variant("hip_ad_rgb")
+    res, spp, steps = 512, 256, int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"] = d["sensor"]["film"]["height"] = res
+    sa, sb = mi.load_dict(d), mi.load_dict(d)
+    fwd = mi.load_dict({"type": "path", "max_depth": 8})
+    prb = mi.load_dict({"type": "prb", "max_depth": 8})
+    key = "white.reflectance.value"
+    pa, pb = mi.traverse(sa), mi.traverse(sb)
+    gi = torch.full((res, res, 3), 1.0 / (res * res * 3), device="cuda")
+    st_a, st_b = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def fwd_call(scene, seed, stream):
+        with torch.cuda.stream(stream):
+            mi.render_film(scene, fwd, seed=seed, spp=spp)
+
+    def bwd_call(scene, params, seed, w, stream):
+        with torch.cuda.stream(stream):
+            mi.render_backward(scene, params, gi, [key], prb, seed=seed, spp=spp, weights=w)
+
+    def step_seq(i):
+        sg = mi.sample_tea_32(i, 1)[0]
+        fwd_call(sa, i, st_a)
+        with torch.cuda.stream(st_a):
+            w = mi.prb_weights(sa, sg, spp)
+        bwd_call(sa, pa, sg, w, st_a)
+
+    def step_conc(i):
+        sg = mi.sample_tea_32(i, 1)[0]
+        with torch.cuda.stream(st_b):
+            w = mi.prb_weights(sb, sg, spp)
+        t1 = threading.Thread(target=fwd_call, args=(sa, i, st_a))
+        t2 = threading.Thread(target=bwd_call, args=(sb, pb, sg, w, st_b))
+        t1.start(); t2.start(); t1.join(); t2.join()
+
+    out = {}
+    for name, fn in (("sequential", step_seq), ("concurrent", step_conc), ("sequential_2", step_seq),
+                     ("concurrent_2", step_conc)):
+        for i in range(2):
+            fn(1000 + i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        out[name] = {"ms_per_step": round(ms, 3), "msamples_s": round(res * res * spp / ms / 1e3, 1)}
+    # the gradients of both modes agree (same seeds; float atomics: order only)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
