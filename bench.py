@@ -494,16 +494,30 @@ def main():
     # region (same workload, the kernels alone on the chip; the timed region's
     # figures are reported beside them as roofline_overlapped)
     st_f_timed, st_b_timed = A.Stats.from_buffer_copy(st_f), A.Stats.from_buffer_copy(st_b)
-    fwd_ms_serial = bwd_ms_serial = None
+    fwd_ms_serial = bwd_ms_serial = serial = None
     if overlap:
+        # (timed too: the serial step is what a loss whose grad_in depends on
+        # the image would run -- this benchmark's grad_in, d mean(image), does not)
         fs_ms, bs_ms = [], []
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         for i in range(2):
             D.fwd_grad_step(ops, slab, 2000 + i, local_weights=args.local_weights,
                             film_to_root=not args.film_all_reduce, packed=not args.local_weights, fwd_slab=fwd_slab)
             fs_ms.append(st_f.ms_kernel)
             bs_ms.append(st_b.ms_kernel)
         torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        s_ms = D.max_over_ranks(time.perf_counter() - t1, dev) / 2 * 1e3
         fwd_ms_serial, bwd_ms_serial = sum(fs_ms) / 2, sum(bs_ms) / 2
+        serial = {"ms_per_step": round(s_ms, 3), "value": round(samples_step / (s_ms / 1e3) / 1e6, 2), "steps": 2,
+                  "note": "the roofline pass: the same step with forward, then gradient pass (bench.py --serial); "
+                          "the timed steps overlap them because this benchmark's grad_in (d mean(image)) does not "
+                          "depend on the image"}
 
     if rank == 0:
         # ---- rooflines of the two bounce-kernel families, the dominant one as
@@ -672,7 +686,7 @@ def main():
             "rays_shadow_per_sample_prb": (round(st_b.rays_shadow / max(1, n_local), 4)
                                            if not args.fwd_only else None),
             "roofline": roofline, "roofline_other": roofline_other, "roofline_splat": roofline_splat,
-            "roofline_overlapped": roofline_overlapped,
+            "roofline_overlapped": roofline_overlapped, "serial_step": serial,
             "cpu_baseline": cpu,
         }
         if multi is not None:

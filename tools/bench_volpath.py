@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--no-nee", action="store_true", help="medium sample_emitters = false (diagnostic)")
     ap.add_argument("--deterministic", action="store_true",
                     help="prbvolpath: MH_FLAG_DETERMINISTIC backward (int64 fixed-point grid + albedo gradients)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="prbvolpath: forward || backward on two scene handles and streams (grad_in is constant)")
     a = ap.parse_args()
     import torch
     import mitsuba_hip as mi
@@ -94,12 +96,20 @@ def bench_prbvolpath(a, mi, A, scene, t_load):
     keys = ["medium1.sigma_t.data", "medium1.albedo.value"]
     gi = torch.full((a.res, a.res, 3), 1.0 / (a.res * a.res * 3), device="cuda")
     sf, sb = A.Stats(), A.Stats()
+    scene_f, run = scene, None
+    if a.overlap:
+        from mitsuba_hip import distributed as D
+        d = mi.volume_cube(a.res, a.res, a.spp, grid=mi.fbm_grid(a.grid))
+        d["integrator"]["type"] = a.integrator
+        scene_f = mi.load_dict(d)  # the forward's own handle
+        dev = torch.device("cuda:0")
+        run = D.PairRunner((torch.cuda.Stream(dev), torch.cuda.Stream(dev)), dev)
 
     def step(seed):
-        film = mi.render_film(scene, seed=seed, spp=a.spp, stats=sf)
-        g = mi.render_backward(scene, params, gi, keys, seed=seed + 1, spp=a.spp, stats=sb,
-                               deterministic=a.deterministic)
-        return film, g
+        fwd = lambda: mi.render_film(scene_f, seed=seed, spp=a.spp, stats=sf)
+        bwd = lambda: mi.render_backward(scene, params, gi, keys, seed=seed + 1, spp=a.spp, stats=sb,
+                                         deterministic=a.deterministic)
+        return run(fwd, bwd) if run else (fwd(), bwd())
 
     step(100)
     torch.cuda.synchronize()
@@ -117,7 +127,7 @@ def bench_prbvolpath(a, mi, A, scene, t_load):
            "unit": "Msamples/s", "ms_per_step": round(dt * 1e3, 3),
            "fwd_kernel_ms": round(sum(kf) / len(kf), 3), "bwd_kernel_ms": round(sum(kb) / len(kb), 3),
            "grad_sigma_t_abs_sum": float(g[0].abs().sum()), "grad_albedo": [float(x) for x in g[1]],
-           "deterministic": a.deterministic, "bwd_subphases": sub,
+           "deterministic": a.deterministic, "overlap": a.overlap, "bwd_subphases": sub,
            "fwd_rays_closest_per_sample": round(sf.rays_closest / n, 3),
            "fwd_rays_shadow_per_sample": round(sf.rays_shadow / n, 3),
            "config": {"film": f"{a.res}x{a.res}", "spp": a.spp, "grid": f"{a.grid}^3 fBm",
