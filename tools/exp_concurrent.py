@@ -28,7 +28,11 @@ def main():
     key = "white.reflectance.value"
     pa, pb = mi.traverse(sa), mi.traverse(sb)
     gi = torch.full((res, res, 3), 1.0 / (res * res * 3), device="cuda")
-    st_a, st_b = torch.cuda.Stream(), torch.cuda.Stream()
+    hi = torch.cuda.Stream.priority_range()[1]  # the highest priority
+    pairs = {"": (torch.cuda.Stream(), torch.cuda.Stream()),
+             "_bwd_hi": (torch.cuda.Stream(), torch.cuda.Stream(priority=hi)),
+             "_fwd_hi": (torch.cuda.Stream(priority=hi), torch.cuda.Stream())}
+    st_a, st_b = pairs[""]
 
     def fwd_call(scene, seed, stream):
         with torch.cuda.stream(stream):
@@ -45,7 +49,8 @@ def main():
             w = mi.prb_weights(sa, sg, spp)
         bwd_call(sa, pa, sg, w, st_a)
 
-    def step_conc(i):
+    def step_conc(i, st_a=None, st_b=None):
+        st_a, st_b = st_a or pairs[""][0], st_b or pairs[""][1]
         sg = mi.sample_tea_32(i, 1)[0]
         with torch.cuda.stream(st_b):
             w = mi.prb_weights(sb, sg, spp)
@@ -54,8 +59,11 @@ def main():
         t1.start(); t2.start(); t1.join(); t2.join()
 
     out = {}
-    for name, fn in (("sequential", step_seq), ("concurrent", step_conc), ("sequential_2", step_seq),
-                     ("concurrent_2", step_conc)):
+    runs = [("sequential", step_seq)]
+    for r in range(2):
+        for k, (a_, b_) in pairs.items():
+            runs.append((f"concurrent{k}_{r}", lambda i, a_=a_, b_=b_: step_conc(i, a_, b_)))
+    for name, fn in runs:
         for i in range(2):
             fn(1000 + i)
         torch.cuda.synchronize()
