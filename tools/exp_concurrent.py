@@ -3,8 +3,11 @@
 independent (different seeds; the backward needs only the W image), so they
 can run concurrently on two scene handles, two streams and two host threads
 (the C-ABI calls release the GIL; concurrent handles on distinct scenes are
-allowed, include/mitsuba_hip.h).  Prints the sequential and the concurrent
-step time of cornell_box 512^2 @ 256 spp fwd + PRB grad (one MI355X)."""
+allowed, include/mitsuba_hip.h).  Prints the step time of cornell_box
+512^2 @ 256 spp fwd + PRB grad (one MI355X): sequential; concurrent on two
+streams; and four-way (each pass split into two sample slabs on four handles
+and streams).  DESIGN.md §9 round 6 records the results (stream priorities
+were measured with an earlier version of this script)."""
 import json
 import os
 import sys
@@ -58,11 +61,40 @@ def main():
         t2 = threading.Thread(target=bwd_call, args=(sb, pb, sg, w, st_b))
         t1.start(); t2.start(); t1.join(); t2.join()
 
+    # 4-way: the forward and the gradient pass each split into two sample
+    # slabs (the multi-GPU slab decomposition) on four handles and streams
+    s4 = [mi.load_dict(d) for _ in range(4)]
+    p4 = [mi.traverse(x) for x in s4]
+    st4 = [torch.cuda.Stream() for _ in range(4)]
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(3)
+
+    def step_4way(i):
+        sg = mi.sample_tea_32(i, 1)[0]
+        with torch.cuda.stream(st4[2]):
+            w = mi.prb_weights(s4[2], sg, spp)
+        torch.cuda.current_stream().synchronize()
+        h = spp // 2
+
+        def f(k):
+            torch.cuda.set_device(0)
+            with torch.cuda.stream(st4[k]):
+                if k < 2:
+                    mi.render_film(s4[k], fwd, seed=i, spp=spp, spp_begin=k * h, spp_end=(k + 1) * h)
+                else:
+                    b = (k - 2) * h
+                    mi.render_backward(s4[k], p4[k], gi, [key], prb, seed=sg, spp=spp, spp_begin=b, spp_end=b + h,
+                                       weights=w)
+        futs = [pool.submit(f, k) for k in range(3)]
+        f(3)
+        for x in futs:
+            x.result()
+
     out = {}
     runs = [("sequential", step_seq)]
     for r in range(2):
-        for k, (a_, b_) in pairs.items():
-            runs.append((f"concurrent{k}_{r}", lambda i, a_=a_, b_=b_: step_conc(i, a_, b_)))
+        runs.append((f"concurrent_{r}", step_conc))
+        runs.append((f"four_way_{r}", step_4way))
     for name, fn in runs:
         for i in range(2):
             fn(1000 + i)
