@@ -264,6 +264,23 @@ def volsched_roofline(st, n_samples, alpha=False):
                  limiter="VALU issue and divergence of the phase machine (DESIGN.md section 3), not HBM")
 
 
+def overlapped_roofline(timed, serial_roofs, ms_step):
+    """`roofline_overlapped` of an overlapped bench line: the dominant
+    kernel's figures from the timed steps (`timed`, a roofline dict of the
+    same kernel, each launch sharing the chip with the other pass), and
+    chip_*: both bounce families' algorithmic bytes per step (launches x
+    bytes per launch of the serial rooflines) over the step time, one rank's
+    bytes over its own step."""
+    chip = sum(r["algorithmic_bytes_per_launch"] * r["launches_per_step"] for r in serial_roofs if r)
+    gbs = chip / (ms_step / 1e3) / 1e9
+    out = {k: timed[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us", "launches_per_step",
+                                 "algorithmic_bytes_per_launch")}
+    out.update(measured="the timed region (forward || gradient pass): each launch shares the chip",
+               chip_bounce_bytes_per_step=round(chip), chip_achieved=round(gbs, 1),
+               chip_frac=round(gbs / HBM_PEAK_GBS, 4))
+    return out
+
+
 def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     """The bench's hot-path wiring (also driven by tests/test_gpu_multirank.py):
     cornell_box res^2, `path` forward + `prb` backward wrt white's rgb
@@ -622,15 +639,8 @@ def main():
             # with the other pass.  chip_*: both bounce families' algorithmic
             # bytes of a step / the step time (what the chip moved for them)
             sts = {"k_wf_bounce": (st_f_timed, 84.0, 12.0, 8.0), "k_wf_bounce_prb": (st_b_timed, 108.0, 0.0, 16.0)}
-            ro = roof(roofline["kernel"], *sts[roofline["kernel"]])
-            chip = sum(r["algorithmic_bytes_per_launch"] * r["launches_per_step"] for r in (roofline, roofline_other))
-            chip_gbs = chip / (ms_step / 1e3) / 1e9  # one rank's bytes over its step time
-            roofline_overlapped = {k: ro[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us",
-                                                      "launches_per_step", "algorithmic_bytes_per_launch")}
-            roofline_overlapped.update(
-                measured="the timed region (forward || gradient pass): each launch shares the chip",
-                chip_bounce_bytes_per_step=round(chip), chip_achieved=round(chip_gbs, 1),
-                chip_frac=round(chip_gbs / HBM_PEAK_GBS, 4))
+            roofline_overlapped = overlapped_roofline(roof(roofline["kernel"], *sts[roofline["kernel"]]),
+                                                      (roofline, roofline_other), ms_step)
         # the forward's film splat (k_splat_tile): per sample its L (12 B) and
         # film position (8 B) read, per launch the RGBW film (16 B per pixel)
         # added once; timed by HIP events after the bounce span of each chunk

@@ -82,3 +82,22 @@ def test_splat_roofline_from_stats():
 def test_pmc_counters_attach_to_the_profiled_workload_only(argv, applies):
     a = bench.parse(argv)
     assert bench.pmc_applies(a) == applies
+
+
+def test_overlapped_roofline_recomputes_from_the_line():
+    # the round-6 final line's figures (profiles/r6_bench_line_2.txt): the
+    # PRB bounce's timed-region launches and both families' serial rooflines
+    timed = {"kernel": "k_wf_bounce_prb", "achieved": 1502.0, "frac": 0.1877, "kernel_avg_us": 1922.2,
+             "launches_per_step": 16, "algorithmic_bytes_per_launch": 2887105140, "traffic": None}
+    prb = {"algorithmic_bytes_per_launch": 2887130263, "launches_per_step": 16}
+    fwd = {"algorithmic_bytes_per_launch": 2041861558, "launches_per_step": 16}
+    r = bench.overlapped_roofline(timed, (prb, fwd), 32.392)
+    assert r["kernel"] == "k_wf_bounce_prb" and r["kernel_avg_us"] == 1922.2 and "traffic" not in r
+    chip = 16 * (2887130263 + 2041861558)
+    assert r["chip_bounce_bytes_per_step"] == chip == 78863869136  # the line's value
+    assert (r["chip_achieved"], r["chip_frac"]) == (2434.7, 0.3043)
+    assert r["chip_achieved"] == pytest.approx(chip / 32.392e-3 / 1e9, abs=0.1)
+    assert r["chip_frac"] == pytest.approx(r["chip_achieved"] / bench.HBM_PEAK_GBS, abs=1e-4)
+    assert 0.29 < r["chip_frac"] < 0.31
+    # a missing second family (forward-only rooflines) counts nothing
+    assert bench.overlapped_roofline(timed, (prb, None), 32.392)["chip_bounce_bytes_per_step"] == 16 * 2887130263
