@@ -17,9 +17,10 @@ device.
 The step is overlapped (the default since round 6): the forward and the
 gradient pass are independent (the backward's seed is TEA(seed, 1); it needs
 the W image, not the film), so the forward runs on its own scene handle,
-HIP stream and host thread while this thread computes the W image,
-all-reduces it and runs render_backward; the film and the gradients are then
-summed in ONE all-reduce (two collectives per step: W, film + gradient;
+HIP stream and host thread while this thread runs render_backward (after
+the W image and its all-reduce, so that no collective runs beside the
+passes); the film and the gradients are then summed in ONE all-reduce (two
+collectives per step: W, film + gradient;
 mitsuba_hip.distributed.fwd_grad_step(overlap=True)).  --serial runs the
 round-5 step instead: forward, then gradient pass, the film and the W image
 in one packed all-reduce, the gradients in another.  The kernel rooflines of
@@ -490,8 +491,8 @@ def main():
         # spread comes from its kernel time (fwd + bwd, HIP events) + collectives
         colls = timer.summary(args.steps)
         cms = {k: c["ms_per_step"] for k, c in colls.items()}
-        if overlap:  # the forward runs alongside W + its all-reduce + the backward
-            own = (max(sum(fwd_ms) / args.steps, sum(bwd_ms) / args.steps + cms.get("W", 0.0)) +
+        if overlap:  # W and its all-reduce, then the forward alongside the backward
+            own = (cms.get("W", 0.0) + max(sum(fwd_ms) / args.steps, sum(bwd_ms) / args.steps) +
                    cms.get("film+gradient", 0.0))
         else:
             own = (sum(fwd_ms) + sum(bwd_ms)) / args.steps + sum(cms.values())

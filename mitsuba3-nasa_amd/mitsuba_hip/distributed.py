@@ -22,9 +22,9 @@ every rank (local_weights: no W exchange, N times the W splat).
 
 Overlapped (`overlap`, the default of bench.py since round 6): the forward
 and the gradient pass are independent, so they run concurrently on two scene
-handles and two streams (PairRunner); the W image is all-reduced inside the
-gradient side, and the film and the gradients are summed in one all-reduce
-after both (W: 1 MiB, film + gradient: 4 MiB + 12 B at 512²).
+handles and two streams (PairRunner), after the W image and its
+all-reduce; the film and the gradients are summed in one all-reduce after
+both (W: 1 MiB, film + gradient: 4 MiB + 12 B at 512²).
 
 One process per GPU; torch.distributed with backend "nccl" (= RCCL over xGMI
 on ROCm), or "gloo" for the CPU tests.  No collective sits inside a kernel
@@ -231,10 +231,11 @@ def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, l
 
     overlap: the forward and the gradient pass are independent (the
     backward's seed is TEA(seed, 1); it needs the W image, not the film), so
-    they run concurrently (ops.concurrent): the forward on one side, the W
-    image + its all-reduce + render_backward on the other; then the film and
-    the gradients are summed in ONE all-reduce (two collectives per step: W,
-    film + gradient; one with local_weights).  film_to_root does not apply.
+    after the W image and its all-reduce they run concurrently
+    (ops.concurrent): the forward on one side, render_backward on the other;
+    then the film and the gradients are summed in ONE all-reduce (two
+    collectives per step: W, film + gradient; one with local_weights).
+    film_to_root does not apply.
 
     packed: the W image of the gradient seed is computed before the forward
     exchange and summed together with the film in one all-reduce (two
@@ -249,13 +250,14 @@ def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, l
     fs = fwd_slab or slab
     if with_grad and overlap:
         sg = ops.seed_grad(seed)
-
-        def grad_pass():
-            w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end), "W")
-            return ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w)
-
+        # W and its all-reduce first, so that no collective runs while the two
+        # passes share the device (an RCCL kernel queued behind the forward's
+        # launches would hold its peers' kernels spinning); the W splat fills
+        # the chip by itself
+        w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end), "W")
         run = ops.concurrent or (lambda f, g: (f(), g()))
-        film, grads = run(lambda: ops.render_film(seed, fs.spp_total, fs.begin, fs.end), grad_pass)
+        film, grads = run(lambda: ops.render_film(seed, fs.spp_total, fs.begin, fs.end),
+                          lambda: ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w))
         summed = all_reduce_list_([film] + list(grads), "film+gradient")
         return ops.develop(summed[0]), summed[1:]
     if with_grad and packed and not local_weights:
