@@ -710,6 +710,7 @@ def main():
 def main_single_op(args, rank, world, dev, dist_on):
     import torch
     import torch.distributed as dist
+    from mitsuba_hip import _abi as A
     from mitsuba_hip import distributed as D
     scene, integ, res, spp, work, step, st = single_op(args, rank, world, dev)
     for i in range(args.warmup):
@@ -730,11 +731,36 @@ def main_single_op(args, rank, world, dev, dist_on):
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
     ms_step = elapsed / args.steps * 1e3
     value = world * res * res * spp / (ms_step / 1e3) / 1e6
+    # config 3: mh_render_backward runs the bitmap wavefront's two chunks on
+    # two streams (mh_api.hip fork_stream), so a timed launch shares the chip
+    # with the other chunk's; the rooflines come from 2 one-stream steps
+    # (MH_WF_STREAMS=1) right after the timed region, the timed figures sit
+    # beside them (roofline_two_streams)
+    st_timed = A.Stats.from_buffer_copy(st)
+    if args.config == 3:
+        old = os.environ.get("MH_WF_STREAMS")
+        os.environ["MH_WF_STREAMS"] = "1"
+        try:
+            for i in range(2):
+                step(3000 + i)
+            torch.cuda.synchronize()
+        finally:
+            if old is None:
+                os.environ.pop("MH_WF_STREAMS", None)
+            else:
+                os.environ["MH_WF_STREAMS"] = old
     if rank == 0:
         n_local = res * res * spp
-        roof = roof_other = None
+        roof = roof_other = two = None
         if args.config == 3 and st.n_aux_launches:
             roof, roof_other = bitmap_rooflines(st, n_local, 64 * 64 * 3)  # config 3(b): a 64^2 x 3 bitmap
+            note = "one-stream pass: 2 steps with MH_WF_STREAMS=1 right after the timed region"
+            roof["measured"] = roof_other["measured"] = note
+            if st_timed.n_aux_launches > st.n_aux_launches:  # the timed steps ran the two-stream pipeline
+                tb, ts = bitmap_rooflines(st_timed, n_local, 64 * 64 * 3)
+                two = {"measured": "the timed region: the two chunks on two streams, each launch sharing the chip",
+                       "kernels": [{k: r[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us",
+                                                      "launches_per_step")} for r in (tb, ts)]}
         elif args.config == 4 and st.mode == 3 and st.n_trace_launches:
             roof = volsched_roofline(st, n_local)
             # config 4's own PMC passes (tools/profile_volsched.sh): traffic and
@@ -771,6 +797,8 @@ def main_single_op(args, rank, world, dev, dist_on):
             "roofline": roof, "roofline_other": roof_other,
             "cpu_baseline": cpu,
         }
+        if two:
+            line["roofline_two_streams"] = two
         print(json.dumps(line), flush=True)
     if dist_on:
         dist.destroy_process_group()

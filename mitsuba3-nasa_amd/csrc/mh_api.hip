@@ -137,6 +137,11 @@ struct mh_scene {
     uint32_t bvh_nodes = 0, bvh_prims = 0, bvh_depth = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::vector<hipEvent_t> evpool;  // per-chunk timing events of mh_render
+    // two-stream chunk pipeline of the bitmap PRB wavefront (fork_stream): odd
+    // chunks run on stream2 with their own workspace
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    DevBuf wf_ws2, wf_ws_prb2, wf_ws_bmp2, wf_partial2;
 };
 
 extern "C" {
@@ -546,8 +551,15 @@ int mh_scene_destroy(mh_scene *s) {
                       &s->emitters, &s->positions, &s->normals, &s->texcoords, &s->faces, &s->texels,
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word, &s->bmp_fx,
-                      &s->shard_w, &s->shard_tmp, &s->shard_g})
+                      &s->shard_w, &s->shard_tmp, &s->shard_g, &s->replay_fx, &s->wf_ws2, &s->wf_ws_prb2,
+                      &s->wf_ws_bmp2, &s->wf_partial2})
         b->release();
+    if (s->stream2) {
+        (void)hipStreamSynchronize(s->stream2);
+        (void)hipStreamDestroy(s->stream2);
+    }
+    if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+    if (s->ev_join) (void)hipEventDestroy(s->ev_join);
     for (hipEvent_t e : s->evpool) (void)hipEventDestroy(e);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -822,6 +834,38 @@ static hipError_t wait_stream(mh_scene *s, uint32_t flags, hipStream_t st) {
 // back to the host, so the call returns with its work enqueued on the stream
 static bool async_call(uint32_t flags, const mh_stats *stats) {
     return (flags & MH_FLAG_DEVICE_POINTERS) && (flags & MH_FLAG_NO_SYNC) && !stats;
+}
+
+// Two-stream chunk pipeline of the fused PRB wavefront with a bitmap
+// parameter: chunk c runs on the scene's stream (c even) or on stream2 (c
+// odd), each with its own workspace, so one chunk's texel scatter and late
+// bounces -- a few paths each, the chip mostly idle -- overlap the next
+// chunk's launches.  Only where the chunks share nothing but atomically
+// updated outputs: the fused (packet, LDS-stack) kernels and the
+// non-deterministic gradient paths.  A single-chunk call of at least
+// kTwoStreamMinSamples samples is split into two chunks.  MH_WF_STREAMS=1
+// keeps one stream (measurements, A/B).
+constexpr uint64_t kTwoStreamMinSamples = 1ull << 19;
+static bool chunk_streams_enabled() {
+    const char *e = getenv("MH_WF_STREAMS");
+    return !(e && !strcmp(e, "1"));
+}
+// stream2 (created on first use, on the scene's device) waits for the work
+// enqueued on st so far
+static hipError_t fork_stream(mh_scene *s, hipStream_t st) {
+    hipError_t e = hipSuccess;
+    if (!s->stream2) e = hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking);
+    if (e == hipSuccess && !s->ev_fork) e = hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess && !s->ev_join) e = hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(s->ev_fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s->stream2, s->ev_fork, 0);
+    return e;
+}
+// st waits for everything enqueued on stream2
+static hipError_t join_stream(mh_scene *s, hipStream_t st) {
+    hipError_t e = hipEventRecord(s->ev_join, s->stream2);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, s->ev_join, 0);
+    return e;
 }
 
 static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint32_t spp, uint32_t spp_begin,
@@ -1535,16 +1579,30 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         const uint32_t n_depth = std::max<uint32_t>(1, in->max_depth - 1);
         if (bmp_wf)  // vertex records: 48 B per path and depth; at most 8 GiB of them per chunk
             max_samples = std::min<uint64_t>(max_samples, std::max<uint64_t>(1 << 16, (8ull << 30) / (48ull * n_depth)));
-        const uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
+        uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
+        // two-stream chunk pipeline (fork_stream): a bitmap parameter's texel
+        // scatter overlaps the other chunk's bounces (config 3: 8.01 -> 7.83
+        // ms; without a bitmap, and on the forward, it measured slower: DESIGN
+        // §9 round 6).  Float gradients only: per-stream block partials,
+        // atomic texel scatter
+        const bool two_ok = bmp_wf && wf_fused(s->S) && !deterministic(flags) && chunk_streams_enabled();
+        if (two_ok && chunk_px >= n_px && n_px >= 2 && n_px * S_ >= kTwoStreamMinSamples)
+            chunk_px = (uint32_t)((n_px + 1) / 2);
+        const bool two = two_ok && chunk_px < n_px;
         const uint64_t cap = (uint64_t)chunk_px * S_;
         const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
         const uint32_t n_bounces = in->max_depth;
         const size_t ctr_per_chunk = wf_counter_words(n_bounces);
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(cap)));
         MH_HIP(s->wf_ws_prb.alloc(wf_prb_workspace_bytes(cap)));
+        if (two) {
+            MH_HIP(s->wf_ws2.alloc(wf_workspace_bytes(cap)));
+            MH_HIP(s->wf_ws_prb2.alloc(wf_prb_workspace_bytes(cap)));
+        }
         WfBitmapArgs bmp;
         if (bmp_wf) {
             MH_HIP(s->wf_ws_bmp.alloc(wf_bmp_workspace_bytes(cap, n_depth)));
+            if (two) MH_HIP(s->wf_ws_bmp2.alloc(wf_bmp_workspace_bytes(cap, n_depth)));
             int max_wg = 64 << 10, per_cu_lds = 160 << 10;
             (void)hipDeviceGetAttribute(&max_wg, hipDeviceAttributeMaxSharedMemoryPerBlock, s->device);
             (void)hipDeviceGetAttribute(&per_cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, s->device);
@@ -1578,24 +1636,37 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         const bool det_grad = deterministic(flags) && n_rgb > 0;
         if (det_grad) MH_HIP(s->wf_ws_det.alloc(wf_det_workspace_bytes(cap)));
         MH_HIP(s->wf_ctr.alloc(ctr_per_chunk * n_chunks * 4));
-        MH_HIP(s->wf_partial.alloc((size_t)grid * kMaxRgbParams * 3 * 4));
-        MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, (size_t)grid * kMaxRgbParams * 3 * 4, st));
+        const size_t partial_bytes = (size_t)grid * kMaxRgbParams * 3 * 4;
+        MH_HIP(s->wf_partial.alloc(partial_bytes));
+        MH_HIP(hipMemsetAsync(s->wf_partial.ptr, 0, partial_bytes, st));
+        if (two) {
+            MH_HIP(s->wf_partial2.alloc(partial_bytes));
+            MH_HIP(hipMemsetAsync(s->wf_partial2.ptr, 0, partial_bytes, st));
+        }
         while (s->evpool.size() < 3 * n_chunks) {
             hipEvent_t e;
             MH_HIP(hipEventCreate(&e));
             s->evpool.push_back(e);
         }
+        if (two) MH_HIP(fork_stream(s, st));
         size_t chunk = 0;
         for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
             const uint32_t npx = (uint32_t)std::min<uint64_t>(chunk_px, n_px - p0);
+            // the chunk's stream and buffers (two: odd chunks on stream2)
+            const bool odd = two && (chunk & 1);
+            WfBitmapArgs bc = bmp;
+            if (odd) bc.ws = s->wf_ws_bmp2.ptr;
             MH_HIP(launch_wavefront_prb(s->S, *in, lane_map(L, (uint32_t)p0), s->S.sampler_seed + seed,
                                         (uint64_t)npx * S_, L.spp_pp >= 4, g_in, w, ga.slot_of_tex, n_rgb,
-                                        s->wf_ws.ptr, s->wf_ws_prb.ptr, cap,
+                                        (odd ? s->wf_ws2 : s->wf_ws).ptr, (odd ? s->wf_ws_prb2 : s->wf_ws_prb).ptr, cap,
                                         s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
-                                        s->wf_partial.as<float>(), st, &s->evpool[3 * chunk],
-                                        bmp_wf ? &bmp : nullptr, det_grad ? s->wf_ws_det.ptr : nullptr));
+                                        (odd ? s->wf_partial2 : s->wf_partial).as<float>(), odd ? s->stream2 : st,
+                                        &s->evpool[3 * chunk], bmp_wf ? &bc : nullptr,
+                                        det_grad ? s->wf_ws_det.ptr : nullptr));
         }
+        if (two) MH_HIP(join_stream(s, st));
         MH_HIP(launch_wf_grad_reduce(s->wf_partial.as<float>(), grid, n_rgb, ga.bufs, st));
+        if (two) MH_HIP(launch_wf_grad_reduce(s->wf_partial2.as<float>(), grid, n_rgb, ga.bufs, st));
         wf_ctr_words = ctr_per_chunk;
         wf_chunks = n_chunks;
     } else if (vol && !(env_pvl && !strcmp(env_pvl, "0"))) {

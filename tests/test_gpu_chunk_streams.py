@@ -1,0 +1,99 @@
+"""The two-stream chunk pipeline of the fused PRB wavefront with a bitmap
+parameter (mh_api.hip fork_stream): odd chunks run on a second stream with
+their own workspace, and a single-chunk call of >= 2^19 samples is split in
+two.  The samples are the same as on one stream (the chunking changes which
+launch renders a pixel, not its lanes), so the bitmap gradient equals the
+one-stream call up to float-atomic summation order (MH_WF_STREAMS=1 keeps one
+stream).  The forward and the rgb-only backward keep one stream (the
+pipeline measured slower there)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mi():
+    import mitsuba_hip as mi
+    if not mi.is_available():
+        pytest.fail("no HIP device / native library: the GPU tests need an MI355X")
+    mi.set_variant("hip_ad_rgb")
+    return mi
+
+
+def _both(fn):
+    """fn() with the two-stream pipeline (default) and with one stream."""
+    old = os.environ.pop("MH_WF_STREAMS", None)
+    try:
+        a = fn()
+        os.environ["MH_WF_STREAMS"] = "1"
+        b = fn()
+    finally:
+        os.environ.pop("MH_WF_STREAMS", None)
+        if old is not None:
+            os.environ["MH_WF_STREAMS"] = old
+    return a, b
+
+
+def test_forward_keeps_one_stream():
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"], d["sensor"]["film"]["height"] = 256, 255  # odd pixel count: unequal halves
+    s = mi.load_dict(d)
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+
+    def run():
+        st = A.Stats()
+        f = mi.render_film(s, integ, seed=5, spp=16, stats=st).cpu().numpy()
+        return f, st.n_aux_launches, st.rays_closest
+
+    (f2, n2, r2), (f1, n1, r1) = _both(run)
+    assert (n2, n1) == (1, 1) and r2 == r1  # the forward is not split: one chunk, one stream
+    np.testing.assert_allclose(f2, f1, rtol=2e-5, atol=1e-6)
+
+
+def test_rgb_prb_keeps_one_stream():
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"], d["sensor"]["film"]["height"] = 192, 160
+    s = mi.load_dict(d)
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(s)
+    keys = ["white.reflectance.value", "red.reflectance.value"]
+    gi = torch.full((160, 192, 3), 1.0 / (160 * 192 * 3), device="cuda")
+
+    def run():
+        st = A.Stats()
+        g = mi.render_backward(s, params, gi, keys, integ, seed=9, spp=32, stats=st)
+        return [x.cpu().numpy() for x in g], st.n_trace_launches, st.rays_closest
+
+    (g2, n2, r2), (g1, n1, r1) = _both(run)
+    assert (n2, n1) == (6, 6) and r2 == r1  # rgb keys only: not split
+    for a, b in zip(g2, g1):
+        assert np.abs(b).min() > 0
+        np.testing.assert_allclose(a, b, rtol=1e-4)
+
+
+def test_bitmap_two_streams_equal_one():
+    mi = _mi()
+    import torch
+    from mitsuba_hip import _abi as A
+    s = mi.load_dict(mi.cornell_box_bitmap(16, 160, 128, 32))
+    integ = mi.load_dict({"type": "prb", "max_depth": 6})
+    params = mi.traverse(s)
+    key = "white.reflectance.data"
+    gi = torch.full((128, 160, 3), 1.0 / (128 * 160 * 3), device="cuda")
+
+    def run():
+        st = A.Stats()
+        (g,) = mi.render_backward(s, params, gi, [key], integ, seed=4, spp=32, stats=st)
+        return g.cpu().numpy(), st.n_aux_launches, st.aux_items
+
+    (g2, n2, a2), (g1, n1, a1) = _both(run)
+    assert (n2, n1) == (2, 1) and a2 == a1  # the same vertex records, in two scatters
+    assert np.abs(g1).max() > 0
+    np.testing.assert_allclose(g2, g1, rtol=1e-4, atol=1e-6 * np.abs(g1).max())
