@@ -199,3 +199,24 @@ def test_config4_grid_update_bricks(config4):
     c = mi.render_film(scene, seed=1, spp=8).cpu().numpy()
     np.testing.assert_allclose(c, a, rtol=1e-5, atol=1e-7)
     assert np.abs(a - b).max() > 1e-3
+
+
+def test_bench_step_overlapped_equals_serial():
+    """bench.py's step at its full size (cornell_box 512^2 @ 256 spp, max_depth
+    8): the overlapped step (forward || gradient pass on two scene handles and
+    streams, mitsuba_hip.distributed.PairRunner) renders the same samples as
+    the serial step, so image and gradient agree up to float-atomic order."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from mitsuba_hip import distributed as D
+    w = bench.build_step(512, 256, 8, 0, 1, torch.device("cuda:0"))
+    img_s, g_s = D.fwd_grad_step(w["ops"], w["slab"], seed=21, packed=True, fwd_slab=w["fwd_slab"])
+    img_s, g_s = img_s.cpu().numpy(), g_s[0].cpu().numpy()
+    img_o, g_o = D.fwd_grad_step(w["ops"], w["slab"], seed=21, overlap=True, fwd_slab=w["fwd_slab"])
+    img_o, g_o = img_o.cpu().numpy(), g_o[0].cpu().numpy()
+    assert img_s.mean() > 0 and np.abs(g_s).min() > 0
+    np.testing.assert_allclose(img_o, img_s, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(g_o, g_s, rtol=1e-5)
