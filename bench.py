@@ -313,17 +313,17 @@ def build_step(res, spp, max_depth, rank, world, dev, fwd_passes=1):
     packed = torch.empty(res * res * 5, dtype=torch.float32, device=dev)  # film (RGBW) | W image
     views = (packed, packed[:res * res * 4].view(res, res, 4), packed[res * res * 4:].view(res, res))
     ops = D.StepOps(
-        render_film=lambda seed, spp_, b, e, out=None: mi.render_film(
+        render_film=lambda seed, spp_, b, e, out=None, shared=False: mi.render_film(
             scene_fwd, fwd, seed=seed, spp=spp_, spp_begin=b, spp_end=e, film=film if out is None else out,
-            stats=st_f),
+            stats=st_f, shared=shared),
         develop=lambda f: mi.develop(scene, f),
         prb_weights=lambda seed, spp_, b, e, out=None: mi.prb_weights(scene, seed, spp_, b, e, out=out),
-        render_backward=lambda seed, spp_, b, e, w: mi.render_backward(
+        render_backward=lambda seed, spp_, b, e, w, shared=False: mi.render_backward(
             scene, params, grad_in, [key], prb, seed=seed, spp=spp_, spp_begin=b, spp_end=e, weights=w,
-            stats=st_b),
+            stats=st_b, shared=shared),
         seed_grad=lambda seed: mi.sample_tea_32(seed, 1)[0],
         packed=lambda: views,
-        concurrent=D.PairRunner((torch.cuda.Stream(dev), torch.cuda.Stream(dev)), dev))
+        concurrent=D.PairRunner((torch.cuda.Stream(dev), torch.cuda.Stream(dev)), dev), shared_hint=True)
     slab = D.sample_slab(rank, world, spp)
     fs = D.sample_slab(rank, world, spp // fwd_passes)
     fwd_slab = D.Slab(slab.spp_total, fs.begin, fs.end)

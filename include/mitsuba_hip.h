@@ -126,9 +126,13 @@ enum {
     MH_FLAG_REDUCE          = 1u << 7,  /* all ranks receive the sum */
     MH_FLAG_REDUCE_ROOT     = 1u << 8,  /* films: only rank 0 receives the sum (a reduce, not an all-reduce);
                                            the other ranks' film is left undefined */
-    MH_FLAG_LOCAL_WEIGHTS   = 1u << 9   /* mh_render_backward with weights == NULL and MH_FLAG_REDUCE: every rank
+    MH_FLAG_LOCAL_WEIGHTS   = 1u << 9,  /* mh_render_backward with weights == NULL and MH_FLAG_REDUCE: every rank
                                            computes the whole W image itself (all spp of every pixel) instead
                                            of its slab's W + an all-reduce */
+    MH_FLAG_SHARED_DEVICE   = 1u << 10  /* a performance hint, results unchanged: the caller runs another call on
+                                           the same device at the same time (e.g. a forward beside a gradient
+                                           pass, on two scene handles and streams), so the wavefront launches
+                                           take a share of the CUs' slots and the two calls' launches interleave */
 };
 
 /* ----------------------------------------------------------------------- */

@@ -49,6 +49,7 @@ int set_error(int code, const std::string &msg) {
 // failed, its deadline passed, the communicator was aborted): MH_HIP keeps
 // that message instead of replacing it by the HIP code's text
 thread_local bool g_keep_error = false;
+
 #define MH_HIP(expr)                                                                        \
     do {                                                                                    \
         hipError_t _e = (expr);                                                             \
@@ -980,7 +981,8 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         if (wavefront) {
             MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
                                     s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
-                                    n_bounces, wf_blocks(cus), ev + 2, st, L.n_passes,
+                                    n_bounces, wf_blocks(cus, (flags & MH_FLAG_SHARED_DEVICE) != 0), ev + 2, st,
+                                    L.n_passes,
                                     L.n_passes > 1 ? s->wf_carry.as<uint64_t>() : nullptr, alpha));
         } else if (volwave && vol_sched_mode()) {
             MH_HIP(launch_vol_sched(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), vs_blocks(cus),
@@ -1572,7 +1574,8 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
     if (wavefront) {
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
-        const uint32_t grid = wf_grid(wf_blocks(cus));
+        // MH_FLAG_SHARED_DEVICE: another call runs beside this one (wf_blocks)
+        const uint32_t grid = wf_grid(wf_blocks(cus, (flags & MH_FLAG_SHARED_DEVICE) != 0));
         const char *ec = getenv("MH_WF_CHUNK");
         uint64_t max_samples = std::min<uint64_t>(
             wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());

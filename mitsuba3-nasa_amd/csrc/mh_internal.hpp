@@ -108,7 +108,7 @@ hipError_t launch_wavefront(const DScene &S, const IntegratorParams &in, const L
                             int alpha = 0);              // alpha: write the validity plane (plane 5)
 size_t wf_prb_workspace_bytes(uint64_t cap);
 uint32_t wf_grid(uint32_t grid);
-uint32_t wf_blocks(int cus);  // wavefront workgroups for a device of `cus` CUs
+uint32_t wf_blocks(int cus, bool shared = false);  // wavefront workgroups for a device of `cus` CUs (shared: another call runs beside)
 uint32_t wf_packet_max_prims();  // largest scene (primitives) the packet engine traces
 bool wf_fused(const DScene &S);  // launch_wavefront runs the fused bounce kernel  // grid rounded to whole queue segments
 // One bitmap parameter on the fused PRB wavefront: the bounce kernel logs a

@@ -2139,8 +2139,14 @@ uint32_t wf_grid(uint32_t grid) { return std::max<uint32_t>(kSeg, grid / kSeg * 
 // (stride loop), and a CU holds 5 bounce workgroups at a time, so a grid of a
 // few resident rounds leaves CUs idle in its last round; many small rounds
 // even the tail out (MH_WF_BPC overrides for experiments: tools/exp_bpc.sh).
-uint32_t wf_blocks(int cus) {
-    uint32_t bpc = 30;  // measured: 8 -> 54.6, 20 -> 51.4, 30 -> 51.2, 60 -> 52.3 ms per bench step
+// shared: another call runs on the device at the same time
+// (MH_FLAG_SHARED_DEVICE): each launch then takes a smaller share of the CUs' slots, so
+// the two calls' launches interleave instead of queueing behind each other --
+// the overlapped bench step (forward || gradient pass), 3 runs per point:
+// 30 -> 2,074-2,094, 20 -> 2,098-2,106, 12 -> 2,105-2,129, 8 -> 2,105-2,117,
+// 6 -> 2,070-2,082 Msamples/s (alone, 12 would cost 6 %: 1,824 vs 1,946)
+uint32_t wf_blocks(int cus, bool shared) {
+    uint32_t bpc = shared ? 12 : 30;  // measured alone: 8 -> 54.6, 20 -> 51.4, 30 -> 51.2, 60 -> 52.3 ms per bench step
     if (const char *e = getenv("MH_WF_BPC")) bpc = std::max(1, atoi(e));
     return (uint32_t)cus * bpc;
 }

@@ -62,6 +62,7 @@ FLAG_DETERMINISTIC = 1 << 6
 FLAG_REDUCE = 1 << 7
 FLAG_REDUCE_ROOT = 1 << 8
 FLAG_LOCAL_WEIGHTS = 1 << 9
+FLAG_SHARED_DEVICE = 1 << 10  # performance hint: another call runs on the device at the same time
 COMM_ID_BYTES = 128
 
 u32, u64, f32, f64 = C.c_uint32, C.c_uint64, C.c_float, C.c_double

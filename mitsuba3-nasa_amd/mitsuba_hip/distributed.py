@@ -150,6 +150,10 @@ class StepOps:
     # (a PairRunner; on a GPU render_film then uses its own scene handle and
     # stream).  None: the overlapped step runs them one after the other.
     concurrent: Optional[Callable] = None
+    # render_film / render_backward take shared=True: the overlapped step passes
+    # the MH_FLAG_SHARED_DEVICE hint (each call's launches sized for a share
+    # of the device)
+    shared_hint: bool = False
 
 
 class PairRunner:
@@ -256,8 +260,9 @@ def fwd_grad_step(ops: StepOps, slab: Slab, seed: int, with_grad: bool = True, l
         # the chip by itself
         w = None if local_weights else all_reduce_(ops.prb_weights(sg, slab.spp_total, slab.begin, slab.end), "W")
         run = ops.concurrent or (lambda f, g: (f(), g()))
-        film, grads = run(lambda: ops.render_film(seed, fs.spp_total, fs.begin, fs.end),
-                          lambda: ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w))
+        kw = {"shared": True} if (ops.shared_hint and ops.concurrent is not None) else {}
+        film, grads = run(lambda: ops.render_film(seed, fs.spp_total, fs.begin, fs.end, **kw),
+                          lambda: ops.render_backward(sg, slab.spp_total, slab.begin, slab.end, w, **kw))
         summed = all_reduce_list_([film] + list(grads), "film+gradient")
         return ops.develop(summed[0]), summed[1:]
     if with_grad and packed and not local_weights:

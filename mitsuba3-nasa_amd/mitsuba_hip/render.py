@@ -179,12 +179,15 @@ def traverse(scene: Scene, device=None) -> SceneParameters:
 # ---------------------------------------------------------------------------
 def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                 spp_begin: int = 0, spp_end: int = 0, device=None, film=None, accumulate=False,
-                stats: Optional[A.Stats] = None, mode: str = "auto", deterministic: bool = False):
+                stats: Optional[A.Stats] = None, mode: str = "auto", deterministic: bool = False,
+                shared: bool = False):
     """Integrator::render(develop=False): RGBW film (H, W, 4) on the device.
     mode: 'auto' (wavefront for `path`), 'mega' (per-lane megakernel) or 'wavefront'.
     deterministic: splat as a fixed-order gather (bit-reproducible film) instead
     of float atomics.  stats.invalid_samples counts samples with a non-finite
-    or negative channel (ImageBlock::put's warn_invalid / warn_negative test)."""
+    or negative channel (ImageBlock::put's warn_invalid / warn_negative test).
+    shared: another call runs on the device at the same time
+    (MH_FLAG_SHARED_DEVICE, a performance hint; the result is unchanged)."""
     torch = _torch()
     dev = _device_index(device)
     integrator = integrator or scene.integrator()
@@ -198,6 +201,7 @@ def render_film(scene: Scene, integrator: Optional[Integrator] = None, seed: int
     flags = A.FLAG_DEVICE_POINTERS | _NO_SYNC | (A.FLAG_ACCUMULATE if accumulate else 0)
     flags |= {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "wavefront": A.FLAG_WAVEFRONT}[mode]
     flags |= A.FLAG_DETERMINISTIC if deterministic else 0
+    flags |= A.FLAG_SHARED_DEVICE if shared else 0
     ic = integrator.c()
     A.check(A.lib().mh_render(h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(film), flags,
                               C.byref(stats) if stats is not None else None))
@@ -262,7 +266,8 @@ def _grad_to_rgb(scene: Scene, grad_in):
 def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[str],
                     integrator: Optional[Integrator] = None, seed: int = 0, spp: int = 0,
                     spp_begin: int = 0, spp_end: int = 0, weights=None,
-                    stats: Optional[A.Stats] = None, mode: str = "auto", deterministic: bool = False):
+                    stats: Optional[A.Stats] = None, mode: str = "auto", deterministic: bool = False,
+                    shared: bool = False):
     """RBIntegrator.render_backward (ad/integrators/common.py:828-983).
     Returns a list of gradient tensors (one per key, same shape as the param).
     mode: 'auto' (wavefront single-traversal kernels when the keys are rgb
@@ -272,7 +277,10 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
     single traversal) or 'replay' (per-lane primal + adjoint replay, the
     reference's own two-pass structure).
     deterministic: bit-reproducible rgb gradients on the fused wavefront (each
-    path's sum reduced in a fixed order) and a fixed-order W splat."""
+    path's sum reduced in a fixed order) and a fixed-order W splat.
+    shared: another call runs on the device at the same time
+    (MH_FLAG_SHARED_DEVICE, a performance hint; the result is unchanged up to
+    float summation order)."""
     torch = _torch()
     integrator = integrator or scene.integrator()
     if integrator.type not in ("prb", "prbvolpath"):
@@ -289,7 +297,7 @@ def render_backward(scene: Scene, params: SceneParameters, grad_in, keys: List[s
         h, C.byref(ic), seed, spp, spp_begin, spp_end, _ptr(grad_in),
         _ptr(weights) if weights is not None else None, len(keys), tex, ptrs,
         A.FLAG_DEVICE_POINTERS | _NO_SYNC | {"auto": 0, "mega": A.FLAG_MEGAKERNEL, "replay": A.FLAG_PRB_REPLAY}[mode]
-        | (A.FLAG_DETERMINISTIC if deterministic else 0),
+        | (A.FLAG_DETERMINISTIC if deterministic else 0) | (A.FLAG_SHARED_DEVICE if shared else 0),
         C.byref(stats) if stats is not None else None))
     return outs
 

@@ -88,7 +88,7 @@ def test_flags_match_header():
     from mitsuba_hip import _abi as A
     src = open(HEADER).read()
     for name in ("DEVICE_POINTERS", "ACCUMULATE", "NO_SYNC", "MEGAKERNEL", "WAVEFRONT", "PRB_REPLAY", "DETERMINISTIC", "REDUCE",
-                 "REDUCE_ROOT", "LOCAL_WEIGHTS"):
+                 "REDUCE_ROOT", "LOCAL_WEIGHTS", "SHARED_DEVICE"):
         m = re.search(rf"MH_FLAG_{name}\s*=\s*1u << (\d+)", src)
         assert m, name
         assert getattr(A, "FLAG_" + name) == 1 << int(m.group(1))
