@@ -1574,8 +1574,6 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
     if (wavefront) {
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device);
-        // MH_FLAG_SHARED_DEVICE: another call runs beside this one (wf_blocks)
-        const uint32_t grid = wf_grid(wf_blocks(cus, (flags & MH_FLAG_SHARED_DEVICE) != 0));
         const char *ec = getenv("MH_WF_CHUNK");
         uint64_t max_samples = std::min<uint64_t>(
             wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
@@ -1592,6 +1590,10 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         if (two_ok && chunk_px >= n_px && n_px >= 2 && n_px * S_ >= kTwoStreamMinSamples)
             chunk_px = (uint32_t)((n_px + 1) / 2);
         const bool two = two_ok && chunk_px < n_px;
+        // MH_FLAG_SHARED_DEVICE (another call runs beside this one) or the two
+        // chunk streams: the launches take a share of the CUs' slots (wf_blocks;
+        // config 3 with two streams: 12 per CU 2,215-2,225 vs 30 2,157-2,173)
+        const uint32_t grid = wf_grid(wf_blocks(cus, two || (flags & MH_FLAG_SHARED_DEVICE) != 0));
         const uint64_t cap = (uint64_t)chunk_px * S_;
         const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);
         const uint32_t n_bounces = in->max_depth;
