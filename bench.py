@@ -14,19 +14,16 @@ max-over-ranks step time.  Inputs (the scene) are resident in HBM before the
 timed region; the timed region ends with the image and gradients on the
 device.
 
-The step is overlapped (the default since round 6): the forward and the
-gradient pass are independent (the backward's seed is TEA(seed, 1); it needs
-the W image, not the film), so the forward runs on its own scene handle,
-HIP stream and host thread while this thread runs render_backward (after
-the W image and its all-reduce, so that no collective runs beside the
-passes); the film and the gradients are then summed in ONE all-reduce (two
-collectives per step: W, film + gradient;
-mitsuba_hip.distributed.fwd_grad_step(overlap=True)).  --serial runs the
-round-5 step instead: forward, then gradient pass, the film and the W image
-in one packed all-reduce, the gradients in another.  The kernel rooflines of
-an overlapped run come from 2 serial steps right after the timed region (the
-launches of the timed steps share the chip with the other pass:
-`roofline_overlapped`).
+Per step two collectives (packed): the film and the W image (which depends
+only on the gradient seed's jitters) are summed in ONE all-reduce, the
+gradients in another (mitsuba_hip.distributed.fwd_grad_step).  Inside each
+call the library runs the fused wavefront's chunks on two streams (mh_api.hip
+fork_stream), so the kernel rooflines come from 2 steps with one stream
+(MH_WF_STREAMS=1) right after the timed region -- a timed launch shares the
+chip with the other chunk's (`roofline_timed`).  --overlap runs the forward
+and the gradient pass of a step concurrently instead (two scene handles,
+streams and host threads; valid here because grad_in = d mean(image) does
+not depend on the image).
 
 --config 5 is BASELINE.json configs[4]: cornell_box 2048x2048 @ 1024 spp
 TOTAL (strong scaling: rank r takes samples [1024 r / N, 1024 (r + 1) / N) of
@@ -84,9 +81,11 @@ def parse(argv=None):
     p.add_argument("--unpacked", action="store_true",
                    help="serial step, separate film and W collectives (3 per step) instead of one packed film + W "
                         "all-reduce")
-    p.add_argument("--serial", action="store_true",
-                   help="forward, then gradient pass (the round-5 step: film + W in one packed all-reduce) instead "
-                        "of the two running concurrently on two streams")
+    p.add_argument("--overlap", action="store_true",
+                   help="run the forward and the gradient pass of a step concurrently (two scene handles and "
+                        "streams; W all-reduce first, film + gradient in one all-reduce after) instead of one after "
+                        "the other")
+    p.add_argument("--serial", action="store_true", help="(the default) forward, then gradient pass")
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' to rehearse "
                         "several ranks on one GPU)")
@@ -265,18 +264,18 @@ def volsched_roofline(st, n_samples, alpha=False):
                  limiter="VALU issue and divergence of the phase machine (DESIGN.md section 3), not HBM")
 
 
-def overlapped_roofline(timed, serial_roofs, ms_step):
-    """`roofline_overlapped` of an overlapped bench line: the dominant
-    kernel's figures from the timed steps (`timed`, a roofline dict of the
-    same kernel, each launch sharing the chip with the other pass), and
-    chip_*: both bounce families' algorithmic bytes per step (launches x
-    bytes per launch of the serial rooflines) over the step time, one rank's
-    bytes over its own step."""
+def overlapped_roofline(timed, serial_roofs, ms_step, measured="the timed region: each launch shares the chip"):
+    """`roofline_timed` of a bench line: the dominant kernel's figures from
+    the timed steps (`timed`, a roofline dict of the same kernel, each launch
+    sharing the chip with the other chunk's or pass's), and chip_*: both
+    bounce families' algorithmic bytes per step (launches x bytes per launch
+    of the one-stream rooflines) over the step time, one rank's bytes over its
+    own step."""
     chip = sum(r["algorithmic_bytes_per_launch"] * r["launches_per_step"] for r in serial_roofs if r)
     gbs = chip / (ms_step / 1e3) / 1e9
     out = {k: timed[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us", "launches_per_step",
                                  "algorithmic_bytes_per_launch")}
-    out.update(measured="the timed region (forward || gradient pass): each launch shares the chip",
+    out.update(measured=measured,
                chip_bounce_bytes_per_step=round(chip), chip_achieved=round(gbs, 1),
                chip_frac=round(gbs / HBM_PEAK_GBS, 4))
     return out
@@ -452,7 +451,7 @@ def main():
         w[k] for k in ("scene", "fwd", "prb", "key", "ops", "slab", "fwd_slab", "st_f", "st_b"))
     H = W = args.res
     spp_total = args.spp * world
-    overlap = not (args.serial or args.unpacked or args.fwd_only)
+    overlap = args.overlap and not (args.unpacked or args.fwd_only)
     packed = not (overlap or args.unpacked or args.local_weights or args.fwd_only)
 
     def step(i):
@@ -505,25 +504,26 @@ def main():
                  "collective_calls_per_step": {k: round(v["calls_per_step"], 2) for k, v in sorted(colls.items())}}
     samples_step = world * H * W * args.spp
     value = samples_step / (ms_step / 1e3) / 1e6
-    # the timed steps overlap the forward and the gradient pass, so a bounce
-    # launch shares the chip with the other pass's launches for most of its
-    # duration: its HIP-event time there is not the kernel's own.  The kernel
-    # rooflines come from a roofline pass of serial steps right after the timed
-    # region (same workload, the kernels alone on the chip; the timed region's
-    # figures are reported beside them as roofline_overlapped)
+    # in the timed steps a bounce launch shares the chip with the other
+    # chunk's launches (the library's two chunk streams) or with the other
+    # pass's (--overlap) for most of its duration: its HIP-event time there is
+    # not the kernel's own.  The kernel rooflines come from a roofline pass of
+    # 2 serial steps with one stream (MH_WF_STREAMS=1) right after the timed
+    # region (same workload, each launch alone on the chip; the timed region's
+    # figures are reported beside them as roofline_timed)
     st_f_timed, st_b_timed = A.Stats.from_buffer_copy(st_f), A.Stats.from_buffer_copy(st_b)
-    fwd_ms_serial = bwd_ms_serial = serial = None
-    if overlap:
-        # (timed too: the serial step is what a loss whose grad_in depends on
-        # the image would run -- this benchmark's grad_in, d mean(image), does not)
-        fs_ms, bs_ms = [], []
+    fs_ms, bs_ms = [], []
+    old_streams = os.environ.get("MH_WF_STREAMS")
+    os.environ["MH_WF_STREAMS"] = "1"
+    try:
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for i in range(2):
-            D.fwd_grad_step(ops, slab, 2000 + i, local_weights=args.local_weights,
-                            film_to_root=not args.film_all_reduce, packed=not args.local_weights, fwd_slab=fwd_slab)
+            D.fwd_grad_step(ops, slab, 2000 + i, with_grad=not args.fwd_only, local_weights=args.local_weights,
+                            film_to_root=not args.film_all_reduce, packed=not (args.local_weights or args.fwd_only),
+                            fwd_slab=fwd_slab)
             fs_ms.append(st_f.ms_kernel)
             bs_ms.append(st_b.ms_kernel)
         torch.cuda.synchronize()
@@ -531,11 +531,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         s_ms = D.max_over_ranks(time.perf_counter() - t1, dev) / 2 * 1e3
-        fwd_ms_serial, bwd_ms_serial = sum(fs_ms) / 2, sum(bs_ms) / 2
-        serial = {"ms_per_step": round(s_ms, 3), "value": round(samples_step / (s_ms / 1e3) / 1e6, 2), "steps": 2,
-                  "note": "the roofline pass: the same step with forward, then gradient pass (bench.py --serial); "
-                          "the timed steps overlap them because this benchmark's grad_in (d mean(image)) does not "
-                          "depend on the image"}
+    finally:
+        if old_streams is None:
+            os.environ.pop("MH_WF_STREAMS", None)
+        else:
+            os.environ["MH_WF_STREAMS"] = old_streams
+    fwd_ms_serial, bwd_ms_serial = sum(fs_ms) / 2, sum(bs_ms) / 2
+    serial = {"ms_per_step": round(s_ms, 3), "value": round(samples_step / (s_ms / 1e3) / 1e6, 2), "steps": 2,
+              "note": "the roofline pass: the same work as a serial step with one stream per call "
+                      "(MH_WF_STREAMS=1: no chunk pipelining, no forward || gradient overlap)"}
 
     if rank == 0:
         # ---- rooflines of the two bounce-kernel families, the dominant one as
@@ -631,17 +635,22 @@ def main():
         roofs.sort(key=lambda x: -x[0])
         roofline = roofs[0][1] if roofs else None
         roofline_other = roofs[1][1] if len(roofs) > 1 else None
-        roofline_overlapped = None
-        if overlap and roofline is not None:
+        roofline_timed = None
+        if roofline is not None:
             for r in (roofline, roofline_other):
-                r["measured"] = ("roofline pass: 2 serial steps right after the timed region (forward, then "
-                                 "gradient pass; the kernel alone on the chip), HIP events on the kernel's stream")
-            # the timed (overlapped) steps: the same launches sharing the chip
-            # with the other pass.  chip_*: both bounce families' algorithmic
-            # bytes of a step / the step time (what the chip moved for them)
+                if r:
+                    r["measured"] = ("roofline pass: 2 serial steps with one stream per call (MH_WF_STREAMS=1) "
+                                     "right after the timed region, each launch alone on the chip; HIP events on "
+                                     "the kernel's stream")
+            # the timed steps: the same kind of launches sharing the chip with
+            # the other chunk's (two chunk streams) or pass's (--overlap).
+            # chip_*: both bounce families' algorithmic bytes of a step / the
+            # step time (what the chip moved for them)
             sts = {"k_wf_bounce": (st_f_timed, 84.0, 12.0, 8.0), "k_wf_bounce_prb": (st_b_timed, 108.0, 0.0, 16.0)}
-            roofline_overlapped = overlapped_roofline(roof(roofline["kernel"], *sts[roofline["kernel"]]),
-                                                      (roofline, roofline_other), ms_step)
+            roofline_timed = overlapped_roofline(
+                roof(roofline["kernel"], *sts[roofline["kernel"]]), (roofline, roofline_other), ms_step,
+                "the timed region: " + ("forward || gradient pass" if overlap else "each call's chunks on two streams")
+                + ", each launch sharing the chip")
         # the forward's film splat (k_splat_tile): per sample its L (12 B) and
         # film position (8 B) read, per launch the RGBW film (16 B per pixel)
         # added once; timed by HIP events after the bounce span of each chunk
@@ -679,7 +688,9 @@ def main():
                                    + ("" if args.fwd_only else f" + prb backward wrt '{key}'"),
                        "film": f"{W}x{H}", "spp_per_gpu": args.spp, "spp_total": spp_total,
                        "parallelism": par,
-                       "step": ("overlapped" if overlap else "serial"),
+                       "step": ("overlapped: forward || gradient pass" if overlap else
+                                "serial: forward, then gradient pass; each call's fused-wavefront chunks on two "
+                                "streams (mh_api.hip fork_stream)"),
                        "collectives_per_step": ((1 if args.local_weights else 2) if overlap else
                                                 2 if packed else (1 if args.fwd_only else (2 if args.local_weights else 3))),
                        "collective_bytes": (dict(({} if args.local_weights else {"W": H * W * 4}),
@@ -688,8 +699,8 @@ def main():
                                             {"film": H * W * 16, "W": 0 if args.local_weights else H * W * 4,
                                              "gradient": 12})},
             "fwd_kernel_ms": round(avg_f, 3), "bwd_kernel_ms": round(avg_b, 3),
-            "fwd_kernel_ms_serial": None if fwd_ms_serial is None else round(fwd_ms_serial, 3),
-            "bwd_kernel_ms_serial": None if bwd_ms_serial is None else round(bwd_ms_serial, 3),
+            "fwd_kernel_ms_one_stream": round(fwd_ms_serial, 3),
+            "bwd_kernel_ms_one_stream": round(bwd_ms_serial, 3) if not args.fwd_only else None,
             "rays_closest_per_sample": round(st_f.rays_closest / max(1, n_local), 4),
             "rays_shadow_per_sample": round(st_f.rays_shadow / max(1, n_local), 4),
             "rays_closest_per_sample_prb": (round(st_b.rays_closest / max(1, n_local), 4)
@@ -697,7 +708,7 @@ def main():
             "rays_shadow_per_sample_prb": (round(st_b.rays_shadow / max(1, n_local), 4)
                                            if not args.fwd_only else None),
             "roofline": roofline, "roofline_other": roofline_other, "roofline_splat": roofline_splat,
-            "roofline_overlapped": roofline_overlapped, "serial_step": serial,
+            "roofline_timed": roofline_timed, "one_stream_step": serial,
             "cpu_baseline": cpu,
         }
         if multi is not None:
@@ -731,13 +742,13 @@ def main_single_op(args, rank, world, dev, dist_on):
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
     ms_step = elapsed / args.steps * 1e3
     value = world * res * res * spp / (ms_step / 1e3) / 1e6
-    # config 3: mh_render_backward runs the bitmap wavefront's two chunks on
-    # two streams (mh_api.hip fork_stream), so a timed launch shares the chip
-    # with the other chunk's; the rooflines come from 2 one-stream steps
+    # configs 1 / 3: the fused wavefront runs the call's two chunks on two
+    # streams (mh_api.hip fork_stream), so a timed launch shares the chip with
+    # the other chunk's; the rooflines come from 2 one-stream steps
     # (MH_WF_STREAMS=1) right after the timed region, the timed figures sit
     # beside them (roofline_two_streams)
     st_timed = A.Stats.from_buffer_copy(st)
-    if args.config == 3:
+    if args.config in (1, 3):
         old = os.environ.get("MH_WF_STREAMS")
         os.environ["MH_WF_STREAMS"] = "1"
         try:
@@ -775,13 +786,22 @@ def main_single_op(args, rank, world, dev, dist_on):
                     roof["traffic_source"] = ("profiles/r6_pmc_config4.json @ " + pj.get("source", "") +
                                               " (not measured in this run)")
         elif args.config == 1 and st.mode == 2:
-            launches = max(1, st.n_trace_launches)
-            R, N = float(st.rays_closest), float(n_local)
-            roof = _roof("k_wf_bounce", (2.0 * 84 * (R - N) + 20.0 * N) / launches, st.ms_trace / launches * 1e3,
-                         launches_per_step=int(st.n_trace_launches), rays_closest=int(R), samples=int(N),
-                         state_bytes=84, end_bytes=12, first_bytes=8,
-                         bytes_formula="(2 state (R - N) + (end + first) N) / launches")
-            roof_other = splat_roof(st, res * res)
+            def c1_roofs(s):
+                launches = max(1, s.n_trace_launches)
+                R, N = float(s.rays_closest), float(n_local)
+                return (_roof("k_wf_bounce", (2.0 * 84 * (R - N) + 20.0 * N) / launches, s.ms_trace / launches * 1e3,
+                              launches_per_step=int(s.n_trace_launches), rays_closest=int(R), samples=int(N),
+                              state_bytes=84, end_bytes=12, first_bytes=8,
+                              bytes_formula="(2 state (R - N) + (end + first) N) / launches"),
+                        splat_roof(s, res * res))
+            roof, roof_other = c1_roofs(st)
+            note = "one-stream pass: 2 steps with MH_WF_STREAMS=1 right after the timed region"
+            roof["measured"] = roof_other["measured"] = note
+            if st_timed.n_aux_launches > st.n_aux_launches:  # the timed steps ran the two-stream pipeline
+                tb, ts = c1_roofs(st_timed)
+                two = {"measured": "the timed region: the two chunks on two streams, each launch sharing the chip",
+                       "kernels": [{k: r[k] for k in ("kernel", "achieved", "frac", "kernel_avg_us",
+                                                      "launches_per_step")} for r in (tb, ts)]}
         cpu = None if (args.no_cpu or world > 1) else cpu_single_op(args, scene, integ, res, spp)
         names = {1: "path fwd", 3: "PRB grad (bitmap albedo)", 4: "volpath fwd"}
         line = {

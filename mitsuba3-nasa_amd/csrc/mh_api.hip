@@ -142,7 +142,7 @@ struct mh_scene {
     // chunks run on stream2 with their own workspace
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    DevBuf wf_ws2, wf_ws_prb2, wf_ws_bmp2, wf_partial2;
+    DevBuf wf_ws2, wf_ws_prb2, wf_ws_bmp2, wf_partial2, work2, wf_carry2;
 };
 
 extern "C" {
@@ -553,7 +553,7 @@ int mh_scene_destroy(mh_scene *s) {
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word, &s->bmp_fx,
                       &s->shard_w, &s->shard_tmp, &s->shard_g, &s->replay_fx, &s->wf_ws2, &s->wf_ws_prb2,
-                      &s->wf_ws_bmp2, &s->wf_partial2})
+                      &s->wf_ws_bmp2, &s->wf_partial2, &s->work2, &s->wf_carry2})
         b->release();
     if (s->stream2) {
         (void)hipStreamSynchronize(s->stream2);
@@ -837,20 +837,23 @@ static bool async_call(uint32_t flags, const mh_stats *stats) {
     return (flags & MH_FLAG_DEVICE_POINTERS) && (flags & MH_FLAG_NO_SYNC) && !stats;
 }
 
-// Two-stream chunk pipeline of the fused PRB wavefront with a bitmap
-// parameter: chunk c runs on the scene's stream (c even) or on stream2 (c
-// odd), each with its own workspace, so one chunk's texel scatter and late
-// bounces -- a few paths each, the chip mostly idle -- overlap the next
-// chunk's launches.  Only where the chunks share nothing but atomically
+// Two-stream chunk pipeline of the fused wavefront (mh_render and
+// mh_render_backward): chunk c runs on the scene's stream (c even) or on
+// stream2 (c odd), each with its own workspace, and the launches take the
+// shared-device grid (wf_blocks), so one chunk's late bounces -- a few paths
+// each, the chip mostly idle -- and its splat / texel scatter overlap the
+// other chunk's launches.  Only where the chunks share nothing but atomically
 // updated outputs: the fused (packet, LDS-stack) kernels and the
-// non-deterministic gradient paths.  A single-chunk call of at least
-// kTwoStreamMinSamples samples is split into two chunks.  MH_WF_STREAMS=1
-// keeps one stream (measurements, A/B).
+// non-deterministic splat / gradient paths; not with MH_FLAG_SHARED_DEVICE
+// (the caller already runs another call beside this one).  A single-chunk
+// call of at least kTwoStreamMinSamples samples is split into two chunks.
+// MH_WF_STREAMS=1 keeps one stream (measurements, the bench's roofline pass).
 constexpr uint64_t kTwoStreamMinSamples = 1ull << 19;
 static bool chunk_streams_enabled() {
     const char *e = getenv("MH_WF_STREAMS");
     return !(e && !strcmp(e, "1"));
 }
+
 // stream2 (created on first use, on the scene's device) waits for the work
 // enqueued on st so far
 static hipError_t fork_stream(mh_scene *s, hipStream_t st) {
@@ -938,8 +941,14 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         max_samples = std::min<uint64_t>(wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
     }
     uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
+    const bool two_ok = wavefront && wf_fused(s->S) && !deterministic(flags) && !(flags & MH_FLAG_SHARED_DEVICE) &&
+                        chunk_streams_enabled();
+    if (two_ok && chunk_px >= n_px && n_px >= 2 && n_px * per_pixel >= kTwoStreamMinSamples)
+        chunk_px = (uint32_t)((n_px + 1) / 2);
+    const bool two = two_ok && chunk_px < n_px;
     const uint64_t plane = (uint64_t)chunk_px * per_pixel;
     MH_HIP(s->work.alloc(plane * (alpha ? 6 : 5) * sizeof(float)));
+    if (two) MH_HIP(s->work2.alloc(plane * (alpha ? 6 : 5) * sizeof(float)));
     const bool fast_splat = L.spp_pp >= 4 && s->S.rfilter == MH_RFILTER_GAUSSIAN &&
                             s->S.rfilter_radius > 1.5f && s->S.rfilter_radius <= 2.5f;
     const int coalesce = L.spp_pp >= 4;
@@ -964,7 +973,12 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         MH_HIP(s->wf_ws.alloc(wf_workspace_bytes(plane)));
         MH_HIP(s->wf_ctr.alloc(std::max<size_t>(16, ctr_per_chunk * n_chunks * 4)));
         if (L.n_passes > 1) MH_HIP(s->wf_carry.alloc((size_t)chunk_px * S_ * 8));
+        if (two) {
+            MH_HIP(s->wf_ws2.alloc(wf_workspace_bytes(plane)));
+            if (L.n_passes > 1) MH_HIP(s->wf_carry2.alloc((size_t)chunk_px * S_ * 8));
+        }
     }
+    if (two) MH_HIP(fork_stream(s, st));
     if (volwave && !vol_sched_mode()) {
         MH_HIP(s->wf_ws.alloc(vw_workspace_bytes(plane)));
         MH_HIP(s->wf_ctr.alloc((size_t)vw_counter_words(vw_rounds(*in)) * 4));
@@ -975,15 +989,20 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         LaneMap lm = lane_map(L, (uint32_t)p0);
         uint64_t n = (uint64_t)npx * S_;
         hipEvent_t *ev = &s->evpool[ev_per_chunk * chunk];
-        MH_HIP(hipEventRecord(ev[0], st));
+        const bool odd = two && (chunk & 1);
+        const hipStream_t cs = odd ? s->stream2 : st;
+        DevBuf &work = odd ? s->work2 : s->work;
+        MH_HIP(hipEventRecord(ev[0], cs));
         {
         ScopedPhase sample_("SamplingIntegratorSample");
         if (wavefront) {
-            MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(),
-                                    s->wf_ws.ptr, plane, s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
-                                    n_bounces, wf_blocks(cus, (flags & MH_FLAG_SHARED_DEVICE) != 0), ev + 2, st,
+            MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, work.as<float>(),
+                                    (odd ? s->wf_ws2 : s->wf_ws).ptr, plane,
+                                    s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
+                                    n_bounces, wf_blocks(cus, two || (flags & MH_FLAG_SHARED_DEVICE) != 0), ev + 2, cs,
                                     L.n_passes,
-                                    L.n_passes > 1 ? s->wf_carry.as<uint64_t>() : nullptr, alpha));
+                                    L.n_passes > 1 ? (odd ? s->wf_carry2 : s->wf_carry).as<uint64_t>() : nullptr,
+                                    alpha));
         } else if (volwave && vol_sched_mode()) {
             MH_HIP(launch_vol_sched(s->S, *in, lm, seed_value, n, plane, s->work.as<float>(), vs_blocks(cus),
                                     s->counters.as<unsigned long long>(), st, alpha));
@@ -996,15 +1015,16 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
                                  s->counters.as<unsigned long long>(), st, alpha));
         }
         }
-        MH_HIP(hipEventRecord(ev[1], st));
+        MH_HIP(hipEventRecord(ev[1], cs));
         ScopedPhase put_("ImageBlockPut");
-        MH_SPLAT(s->S, lm, kSplatFilm, fast_splat, npx, L.n_passes, n, plane, s->work.as<float>(), film4,
-                 seed_value, coalesce, st, invalid, determ, s->work.bytes / 4, n_px * 4, bounds);
+        MH_SPLAT(s->S, lm, kSplatFilm, fast_splat, npx, L.n_passes, n, plane, work.as<float>(), film4,
+                 seed_value, coalesce, cs, invalid, determ, work.bytes / 4, n_px * 4, bounds);
         if (alpha)
-            MH_SPLAT(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane, s->work.as<float>(), film_a,
-                     seed_value, coalesce, st, nullptr, determ, s->work.bytes / 4, n_px, bounds);
-        MH_HIP(hipEventRecord(ev[ev_per_chunk - 1], st));
+            MH_SPLAT(s->S, lm, kSplatAlpha, fast_splat, npx, L.n_passes, n, plane, work.as<float>(), film_a,
+                     seed_value, coalesce, cs, nullptr, determ, work.bytes / 4, n_px, bounds);
+        MH_HIP(hipEventRecord(ev[ev_per_chunk - 1], cs));
     }
+    if (two) MH_HIP(join_stream(s, st));
     if (alpha) MH_HIP(launch_film_rgbaw(n_px, film4, film_a, film, st));
     if (int rc = reduce_result(s, flags, film, film_bytes / 4, st, true)) return rc;
     if (!(flags & MH_FLAG_DEVICE_POINTERS))
@@ -1581,18 +1601,15 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         if (bmp_wf)  // vertex records: 48 B per path and depth; at most 8 GiB of them per chunk
             max_samples = std::min<uint64_t>(max_samples, std::max<uint64_t>(1 << 16, (8ull << 30) / (48ull * n_depth)));
         uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
-        // two-stream chunk pipeline (fork_stream): a bitmap parameter's texel
-        // scatter overlaps the other chunk's bounces (config 3: 8.01 -> 7.83
-        // ms; without a bitmap, and on the forward, it measured slower: DESIGN
-        // §9 round 6).  Float gradients only: per-stream block partials,
-        // atomic texel scatter
-        const bool two_ok = bmp_wf && wf_fused(s->S) && !deterministic(flags) && chunk_streams_enabled();
+        // two-stream chunk pipeline (fork_stream): float gradients only
+        // (per-stream block partials, atomic texel scatter)
+        const bool two_ok = wf_fused(s->S) && !deterministic(flags) && !(flags & MH_FLAG_SHARED_DEVICE) &&
+                            chunk_streams_enabled();
         if (two_ok && chunk_px >= n_px && n_px >= 2 && n_px * S_ >= kTwoStreamMinSamples)
             chunk_px = (uint32_t)((n_px + 1) / 2);
         const bool two = two_ok && chunk_px < n_px;
         // MH_FLAG_SHARED_DEVICE (another call runs beside this one) or the two
-        // chunk streams: the launches take a share of the CUs' slots (wf_blocks;
-        // config 3 with two streams: 12 per CU 2,215-2,225 vs 30 2,157-2,173)
+        // chunk streams: the launches take a share of the CUs' slots (wf_blocks)
         const uint32_t grid = wf_grid(wf_blocks(cus, two || (flags & MH_FLAG_SHARED_DEVICE) != 0));
         const uint64_t cap = (uint64_t)chunk_px * S_;
         const size_t n_chunks = (size_t)((n_px + chunk_px - 1) / chunk_px);

@@ -1,11 +1,11 @@
-"""The two-stream chunk pipeline of the fused PRB wavefront with a bitmap
-parameter (mh_api.hip fork_stream): odd chunks run on a second stream with
-their own workspace, and a single-chunk call of >= 2^19 samples is split in
-two.  The samples are the same as on one stream (the chunking changes which
-launch renders a pixel, not its lanes), so the bitmap gradient equals the
-one-stream call up to float-atomic summation order (MH_WF_STREAMS=1 keeps one
-stream).  The forward and the rgb-only backward keep one stream (the
-pipeline measured slower there)."""
+"""The two-stream chunk pipeline of the fused wavefront (mh_api.hip
+fork_stream): odd chunks of mh_render / mh_render_backward run on a second
+stream with their own workspace, and a single-chunk call of >= 2^19 samples
+is split in two.  The samples are the same as on one stream (the chunking
+changes which launch renders a pixel, not its lanes), so the film, the rgb
+gradient and the bitmap gradient equal the one-stream call up to float
+summation order (MH_WF_STREAMS=1 keeps one stream; MH_FLAG_SHARED_DEVICE
+calls keep one too)."""
 import os
 
 import numpy as np
@@ -36,7 +36,7 @@ def _both(fn):
     return a, b
 
 
-def test_forward_keeps_one_stream():
+def test_forward_two_streams_equal_one():
     mi = _mi()
     from mitsuba_hip import _abi as A
     d = mi.cornell_box()
@@ -50,11 +50,11 @@ def test_forward_keeps_one_stream():
         return f, st.n_aux_launches, st.rays_closest
 
     (f2, n2, r2), (f1, n1, r1) = _both(run)
-    assert (n2, n1) == (1, 1) and r2 == r1  # the forward is not split: one chunk, one stream
+    assert (n2, n1) == (2, 1) and r2 == r1  # 256 * 255 * 16 >= 2^19 samples: split in two, the same paths
     np.testing.assert_allclose(f2, f1, rtol=2e-5, atol=1e-6)
 
 
-def test_rgb_prb_keeps_one_stream():
+def test_rgb_prb_two_streams_equal_one():
     mi = _mi()
     import torch
     from mitsuba_hip import _abi as A
@@ -72,7 +72,7 @@ def test_rgb_prb_keeps_one_stream():
         return [x.cpu().numpy() for x in g], st.n_trace_launches, st.rays_closest
 
     (g2, n2, r2), (g1, n1, r1) = _both(run)
-    assert (n2, n1) == (6, 6) and r2 == r1  # rgb keys only: not split
+    assert (n2, n1) == (2 * 6, 6) and r2 == r1
     for a, b in zip(g2, g1):
         assert np.abs(b).min() > 0
         np.testing.assert_allclose(a, b, rtol=1e-4)
@@ -97,3 +97,17 @@ def test_bitmap_two_streams_equal_one():
     assert (n2, n1) == (2, 1) and a2 == a1  # the same vertex records, in two scatters
     assert np.abs(g1).max() > 0
     np.testing.assert_allclose(g2, g1, rtol=1e-4, atol=1e-6 * np.abs(g1).max())
+
+
+def test_shared_device_flag_keeps_one_stream():
+    mi = _mi()
+    from mitsuba_hip import _abi as A
+    d = mi.cornell_box()
+    d["sensor"]["film"]["width"], d["sensor"]["film"]["height"] = 256, 255
+    s = mi.load_dict(d)
+    integ = mi.load_dict({"type": "path", "max_depth": 6})
+    st, st2 = A.Stats(), A.Stats()
+    f = mi.render_film(s, integ, seed=5, spp=16, stats=st, shared=True).cpu().numpy()
+    g = mi.render_film(s, integ, seed=5, spp=16, stats=st2).cpu().numpy()
+    assert (st.n_aux_launches, st2.n_aux_launches) == (1, 2)  # the hint: another call runs beside, one stream
+    np.testing.assert_allclose(f, g, rtol=2e-5, atol=1e-6)

@@ -664,7 +664,9 @@ def test_multipass_config5_slab_parity(b, e):
     from mitsuba_hip import _abi as A
     st = A.Stats()
     film = mi.render_film(scene, integ, seed=2, spp=1024, spp_begin=b, spp_end=e, stats=st).cpu().numpy()
-    assert st.mode == 2 and st.n_trace_launches == 2 * 8  # one chunk x 2 passes x 8 bounces
+    # the single chunk is split in two for the two-stream chunk pipeline
+    # (mh_api.hip fork_stream): 2 chunks x 2 passes x 8 bounces
+    assert st.mode == 2 and st.n_trace_launches == 2 * 2 * 8
     ref = O.render(scene, integ, seed=2, spp=1024, spp_begin=b, spp_end=e)
     assert ref[..., 3].sum() > 0
     ok, frac = _film_close(film, ref)
@@ -730,7 +732,7 @@ def test_multipass_wavefront_matches_megakernel():
     st = A.Stats()
     wf = mi.render_film(scene, integ, seed=3, spp=1024, spp_begin=4, spp_end=6, mode="wavefront",
                         stats=st).cpu().numpy()
-    assert st.mode == 2 and st.n_trace_launches == 2 * 8  # one chunk, two passes of 8 bounces
+    assert st.mode == 2 and st.n_trace_launches == 2 * 2 * 8  # two chunks (two-stream split), two passes of 8 bounces
     mega = mi.render_film(scene, integ, seed=3, spp=1024, spp_begin=4, spp_end=6, mode="mega").cpu().numpy()
     assert mega[..., 3].sum() > 0
     ok, frac = _film_close(wf, mega)

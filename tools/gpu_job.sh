@@ -33,10 +33,10 @@ final)
     for i in 1 2; do timeout -k 10 300 python bench.py > gpurun_out/job_${tag}_c2_$i.json 2> gpurun_out/job_${tag}_c2_$i.err || exit 1; done
     for c in 1 3 4; do timeout -k 10 300 python bench.py --config $c > gpurun_out/job_${tag}_c$c.json 2> gpurun_out/job_${tag}_c$c.err || exit 1; done
     timeout -k 10 300 python bench.py --config 5 --steps 2 --warmup 1 > gpurun_out/job_${tag}_c5.json 2> gpurun_out/job_${tag}_c5.err || exit 1
-    # the PMC passes and the kernel trace on the serial step: the line's
-    # rooflines come from its serial roofline pass, and an overlapped launch's
-    # duration is shared with the other pass's launches
-    bash tools/profile_r2.sh gpurun_out/job_${tag}_prof --serial > gpurun_out/job_${tag}_prof.log 2>&1 || exit 1
+    # the PMC passes and the kernel trace with one stream per call: the line's
+    # rooflines come from its one-stream roofline pass (MH_WF_STREAMS=1), and a
+    # two-stream launch's duration is shared with the other chunk's launches
+    MH_WF_STREAMS=1 bash tools/profile_r2.sh gpurun_out/job_${tag}_prof > gpurun_out/job_${tag}_prof.log 2>&1 || exit 1
     ;;
 ab)
     runs=$1; shift
