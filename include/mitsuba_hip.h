@@ -267,9 +267,9 @@ typedef struct mh_stats {
                                    (prb with a bitmap parameter), film samples the splat read (mh_render) */
     double   ms_aux;            /* device time (hipEvents) of the secondary kernel's launches: the bitmap texel
                                    scatter (mh_render_backward) or the film splat (mh_render, wavefront modes) */
-    uint64_t n_aux_launches;    /* number of those launches (one per chunk).  A prb backward with a bitmap
-                                   parameter runs its chunks on two streams: ms_trace / ms_aux then sum
-                                   spans that overlap in time (MH_WF_STREAMS=1: one stream) */
+    uint64_t n_aux_launches;    /* number of those launches (one per chunk).  The fused wavefront runs a
+                                   call's chunks on two streams: ms_trace / ms_aux then sum spans that
+                                   overlap in time (MH_WF_STREAMS=1: one stream) */
 } mh_stats;
 
 typedef struct mh_scene mh_scene;   /* opaque; owns all device buffers */
