@@ -143,6 +143,7 @@ struct mh_scene {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     DevBuf wf_ws2, wf_ws_prb2, wf_ws_bmp2, wf_partial2, work2, wf_carry2;
+    DevBuf stack_ovf2;  // the stream engine's stack overflow columns of stream2's launches
 };
 
 extern "C" {
@@ -553,7 +554,7 @@ int mh_scene_destroy(mh_scene *s) {
                       &s->media, &s->grid, &s->work, &s->film_tmp, &s->film4, &s->alpha_px, &s->counters, &s->grad_meta, &s->tmp_a, &s->tmp_b,
                       &s->tmp_c, &s->tmp_d, &s->tmp_e, &s->weights_tmp, &s->wf_ws, &s->wf_ctr, &s->wf_ws_prb, &s->wf_partial, &s->gw, &s->wf_carry, &s->wf_ws_bmp, &s->wf_ws_det, &s->pvp_log, &s->pvp_main, &s->pvp_ovf, &s->grid_corner, &s->fx_word, &s->bmp_fx,
                       &s->shard_w, &s->shard_tmp, &s->shard_g, &s->replay_fx, &s->wf_ws2, &s->wf_ws_prb2,
-                      &s->wf_ws_bmp2, &s->wf_partial2, &s->work2, &s->wf_carry2})
+                      &s->wf_ws_bmp2, &s->wf_partial2, &s->work2, &s->wf_carry2, &s->stack_ovf2})
         b->release();
     if (s->stream2) {
         (void)hipStreamSynchronize(s->stream2);
@@ -837,14 +838,14 @@ static bool async_call(uint32_t flags, const mh_stats *stats) {
     return (flags & MH_FLAG_DEVICE_POINTERS) && (flags & MH_FLAG_NO_SYNC) && !stats;
 }
 
-// Two-stream chunk pipeline of the fused wavefront (mh_render and
+// Two-stream chunk pipeline of the wavefront (mh_render and
 // mh_render_backward): chunk c runs on the scene's stream (c even) or on
-// stream2 (c odd), each with its own workspace, and the launches take the
+// stream2 (c odd), each with its own workspace (and, for the stream engine of
+// large meshes, its own stack overflow columns), and the launches take the
 // shared-device grid (wf_blocks), so one chunk's late bounces -- a few paths
 // each, the chip mostly idle -- and its splat / texel scatter overlap the
 // other chunk's launches.  Only where the chunks share nothing but atomically
-// updated outputs: the fused (packet, LDS-stack) kernels and the
-// non-deterministic splat / gradient paths; not with MH_FLAG_SHARED_DEVICE
+// updated outputs: the non-deterministic splat / gradient paths; not with MH_FLAG_SHARED_DEVICE
 // (the caller already runs another call beside this one).  A single-chunk
 // call of at least kTwoStreamMinSamples samples is split into two chunks.
 // MH_WF_STREAMS=1 keeps one stream (measurements, the bench's roofline pass).
@@ -941,7 +942,9 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         max_samples = std::min<uint64_t>(wf_max_chunk(), ec ? std::max<uint64_t>(1024, strtoull(ec, nullptr, 10)) : wf_max_chunk());
     }
     uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / per_pixel));
-    const bool two_ok = wavefront && wf_fused(s->S) && !deterministic(flags) && !(flags & MH_FLAG_SHARED_DEVICE) &&
+    // (the unfused stream-engine kernels of large meshes too: stream2's launches
+    // get their own stack overflow columns, S2 below)
+    const bool two_ok = wavefront && !deterministic(flags) && !(flags & MH_FLAG_SHARED_DEVICE) &&
                         chunk_streams_enabled();
     if (two_ok && chunk_px >= n_px && n_px >= 2 && n_px * per_pixel >= kTwoStreamMinSamples)
         chunk_px = (uint32_t)((n_px + 1) / 2);
@@ -978,6 +981,11 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
             if (L.n_passes > 1) MH_HIP(s->wf_carry2.alloc((size_t)chunk_px * S_ * 8));
         }
     }
+    DScene S2 = s->S;  // stream2's scene view: its own stack overflow columns
+    if (two && s->S.stack_ovf) {
+        MH_HIP(s->stack_ovf2.alloc(s->stack_ovf.bytes));
+        S2.stack_ovf = s->stack_ovf2.as<uint32_t>();
+    }
     if (two) MH_HIP(fork_stream(s, st));
     if (volwave && !vol_sched_mode()) {
         MH_HIP(s->wf_ws.alloc(vw_workspace_bytes(plane)));
@@ -996,7 +1004,7 @@ static int render_impl(mh_scene *s, const mh_integrator *in, uint32_t seed, uint
         {
         ScopedPhase sample_("SamplingIntegratorSample");
         if (wavefront) {
-            MH_HIP(launch_wavefront(s->S, *in, lm, seed_value, n, plane, work.as<float>(),
+            MH_HIP(launch_wavefront(odd ? S2 : s->S, *in, lm, seed_value, n, plane, work.as<float>(),
                                     (odd ? s->wf_ws2 : s->wf_ws).ptr, plane,
                                     s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk,
                                     n_bounces, wf_blocks(cus, two || (flags & MH_FLAG_SHARED_DEVICE) != 0), ev + 2, cs,
@@ -1603,8 +1611,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
         uint32_t chunk_px = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_px, max_samples / S_));
         // two-stream chunk pipeline (fork_stream): float gradients only
         // (per-stream block partials, atomic texel scatter)
-        const bool two_ok = wf_fused(s->S) && !deterministic(flags) && !(flags & MH_FLAG_SHARED_DEVICE) &&
-                            chunk_streams_enabled();
+        const bool two_ok = !deterministic(flags) && !(flags & MH_FLAG_SHARED_DEVICE) && chunk_streams_enabled();
         if (two_ok && chunk_px >= n_px && n_px >= 2 && n_px * S_ >= kTwoStreamMinSamples)
             chunk_px = (uint32_t)((n_px + 1) / 2);
         const bool two = two_ok && chunk_px < n_px;
@@ -1670,6 +1677,11 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
             MH_HIP(hipEventCreate(&e));
             s->evpool.push_back(e);
         }
+        DScene S2 = s->S;  // stream2's scene view: its own stack overflow columns (stream-engine scenes)
+        if (two && s->S.stack_ovf) {
+            MH_HIP(s->stack_ovf2.alloc(s->stack_ovf.bytes));
+            S2.stack_ovf = s->stack_ovf2.as<uint32_t>();
+        }
         if (two) MH_HIP(fork_stream(s, st));
         size_t chunk = 0;
         for (uint64_t p0 = 0; p0 < n_px; p0 += chunk_px, ++chunk) {
@@ -1678,7 +1690,7 @@ static int render_backward_impl(mh_scene *s, const mh_integrator *in, uint32_t s
             const bool odd = two && (chunk & 1);
             WfBitmapArgs bc = bmp;
             if (odd) bc.ws = s->wf_ws_bmp2.ptr;
-            MH_HIP(launch_wavefront_prb(s->S, *in, lane_map(L, (uint32_t)p0), s->S.sampler_seed + seed,
+            MH_HIP(launch_wavefront_prb(odd ? S2 : s->S, *in, lane_map(L, (uint32_t)p0), s->S.sampler_seed + seed,
                                         (uint64_t)npx * S_, L.spp_pp >= 4, g_in, w, ga.slot_of_tex, n_rgb,
                                         (odd ? s->wf_ws2 : s->wf_ws).ptr, (odd ? s->wf_ws_prb2 : s->wf_ws_prb).ptr, cap,
                                         s->wf_ctr.as<uint32_t>() + ctr_per_chunk * chunk, n_bounces, grid,
